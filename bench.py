@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""bench.py -- DEFLATE encode throughput on MI355X (BASELINE.json metric).
+
+One "step" = one full encode of the rank's resident input (HBM -> HBM zlib stream),
+i.e. all five kernels of the hot path.  N = 1 workload: config C3 (enwik8-sized
+enwik-style text, 100 000 000 B, 3 052 blocks of 32 KiB).  N > 1 (one process per GPU
+under torch.distributed.run): weak scaling, every rank encodes its own 100 MB shard
+(per-rank seed) framed as a shard of one stream, and the compressed chunks are
+gathered to rank 0 over RCCL (point-to-point over xGMI) inside the timed region.
+
+Prints ONE JSON line on rank 0 (see DESIGN.md §6 for the roofline accounting).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+import zlib
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
+
+WORKLOADS = {
+    # name: (bytes per rank, generator, seed, description)
+    "text": (100_000_000, "text", 0xE5818, "C3: enwik8-sized enwik-style wiki text (seeded generator)"),
+    "zeros": (1 << 30, "zeros", 0, "1 GiB of 0x00 (zero-entropy run, C2 scaled up)"),
+    "random": (1 << 30, "random", 0x5EED, "C4: 1 GiB splitmix64 bytes (stored-block path)"),
+    "enwik9": (1_000_000_000, "text", 0xE5819, "C5: 1 GB enwik9-style text split across the ranks (strong)"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_input(kind: str, n: int, seed: int):
+    import numpy as np
+    import deflate_compression_amd as D
+    if kind == "text":
+        return D.gen_text(n, seed)
+    if kind == "random":
+        return D.gen_random(n, seed)
+    return np.zeros(n, dtype=np.uint8)
+
+
+def cpu_baseline(data, max_chain: int, budget_s: float):
+    """Time the CPU side on rank 0: the reference encoder itself (oracle/_ref, built
+    from /root/reference's own sources; one process per 32 KiB block, as it is only
+    correct for one window) if that binary is present, plus our C port of the
+    reference parse + emitter (oracle/dmx_oracle.c).  Bounded samples, 1 core each."""
+    import numpy as np
+    from oracle import oracle as O
+    out = {}
+    # port: whole blocks until the budget is used
+    t0 = time.perf_counter()
+    done = 0
+    blk = 1 << 20
+    while done < data.size and time.perf_counter() - t0 < budget_s:
+        O.compress(data[done:done + blk], max_chain=max_chain)
+        done += min(blk, data.size - done)
+    dt = time.perf_counter() - t0
+    out["port"] = {"value": done / dt / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
+                   "sample": f"first {done} B of the workload, oracle/dmx_oracle.c compress "
+                             f"(reference parse, max_chain={max_chain}, + Huffman/emitter), 1 thread"}
+    if O.ref_available():
+        t0 = time.perf_counter()
+        done = 0
+        while done < data.size and time.perf_counter() - t0 < budget_s:
+            O.ref_stats(data[done:done + 32768].tobytes())
+            done += min(32768, data.size - done)
+        dt = time.perf_counter() - t0
+        out["reference"] = {"value": done / dt / 1e9, "unit": "GB/s", "cores": 1, "kind": "reference",
+                            "sample": f"first {done} B of the workload in 32 KiB blocks through the reference "
+                                      "encoder (src/deflate_compress.c + aht.c + h_tree.c, oracle/_ref), "
+                                      "1 process at a time, incl. its per-token estimator"}
+    return out
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="text", choices=sorted(WORKLOADS))
+    ap.add_argument("--bytes", type=int, default=0, help="override bytes per rank")
+    ap.add_argument("--max-chain", type=int, default=int(os.environ.get("DMX_MAX_CHAIN", "0")))
+    ap.add_argument("--gather", default="root", choices=["root", "all", "none"])
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds per CPU baseline leg (0 = skip)")
+    ap.add_argument("--traffic-csv", default="", help="rocprofv3 counter CSV (FETCH_SIZE/WRITE_SIZE) for roofline.traffic")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import deflate_compression_amd as D
+    from deflate_compression_amd import shard as S
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device(f"cuda:{local}")
+
+    per_rank, gen, seed, desc = WORKLOADS[args.workload]
+    strong = args.workload == "enwik9"
+    if args.bytes:
+        per_rank = args.bytes
+    if strong:
+        total = per_rank
+        full = make_input(gen, total, seed)
+        lo, hi = S.shard_range(total, rank, world)
+        host = np.ascontiguousarray(full[lo:hi])
+        del full
+    else:
+        host = make_input(gen, per_rank, seed + rank)
+    n = int(host.size)
+    flags = D.DMX_ZLIB if world == 1 else S.shard_flags(rank, world)
+    enc = D.Encoder(local, n, 32768, args.max_chain, flags)
+    d_in = torch.from_numpy(host).to(dev)
+    cap = D.max_compressed(n)
+    d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        enc.encode_async(d_in.data_ptr(), n, d_out.data_ptr(), cap, stream)
+        if world > 1 and args.gather != "none":
+            r = enc.result(stream)   # chunk length (device -> host) before the exchange
+            S.gather_chunks(d_out, int(r.out_len), root=0 if args.gather == "root" else None)
+
+    # correctness of the measured configuration (outside the timed region)
+    enc.encode_async(d_in.data_ptr(), n, d_out.data_ptr(), cap, stream)
+    res = enc.result(stream)
+    out_len = int(res.out_len)
+    ok = True
+    if world == 1:
+        z = d_out[:out_len].cpu().numpy().tobytes()
+        ok = zlib.decompress(z) == host.tobytes()
+        if not ok:
+            log("ERROR: stream does not inflate to the input")
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    enc.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    stage_ms, nstage = enc.stage_times()
+    enc.set_timing(False)
+    dt = t1 - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+        nn = torch.tensor([n, out_len], dtype=torch.int64, device=dev)
+        dist.all_reduce(nn)
+        tot_in, tot_out = int(nn[0].item()), int(nn[1].item())
+    else:
+        tot_in, tot_out = n, out_len
+
+    if rank == 0:
+        ms_step = dt / args.steps * 1e3
+        value = tot_in * args.steps / dt / 1e9
+        dom = max(stage_ms, key=stage_ms.get)
+        dom_ms = stage_ms[dom]
+        algo_bytes = n + out_len   # per launch on this rank: input read + stream written
+        achieved = algo_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+        traffic = None
+        if args.traffic_csv and os.path.exists(args.traffic_csv):
+            try:
+                from tools.pmc import traffic_per_launch
+                traffic = traffic_per_launch(args.traffic_csv, f"dmx_{dom}_kernel")
+            except Exception as e:  # pragma: no cover
+                log("traffic csv unreadable:", e)
+        cpu = {}
+        if world == 1 and args.cpu_budget > 0:
+            cpu = cpu_baseline(host, args.max_chain, args.cpu_budget)
+        base = cpu.get("reference") or cpu.get("port")
+        line = {
+            "metric": "encode GB/s (uncompressed in) + compression ratio vs CPU ref, 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong" if strong else "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {
+                "workload": desc,
+                "bytes_per_rank": n,
+                "block": 32768,
+                "parse": "exhaustive (reference semantics)" if args.max_chain == 0 else f"max_chain={args.max_chain}",
+                "parallelism": f"blocks sharded over {world} GPU(s)" + (f", gather={args.gather}" if world > 1 else ""),
+            },
+            "ratio": round(out_len / n, 5),
+            "compressed_bytes_rank0": out_len,
+            "inflate_ok": ok,
+            "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
+            "roofline": {
+                "bound": "hbm",
+                "kernel": f"dmx_{dom}_kernel",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": algo_bytes,
+                "launch_ms": round(dom_ms, 4),
+                "launches_timed": nstage,
+            },
+            "cpu_baseline": base,
+            "cpu_baseline_port": cpu.get("port") if base is not cpu.get("port") else None,
+            "host": {"cpu": platform.processor() or platform.machine(), "nproc": os.cpu_count()},
+        }
+        if base:
+            line["gpu_over_cpu"] = round(value / base["value"], 1) if base["value"] else None
+        print(json.dumps(line), flush=True)
+    enc.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

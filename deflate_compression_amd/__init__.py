@@ -1,0 +1,299 @@
+"""deflate_compression_amd -- MI355X-native DEFLATE encoder (host mirror of the
+reference's codec API, src/include/deflate_ext.h of mparker97/deflate_compression).
+
+The compute path is libdmx.so (hand-written HIP kernels for gfx950 behind a C ABI,
+include/dmx.h).  This module is a thin ctypes layer:
+
+    deflate_compress(fd_in, fd_out, fd_stats=-1, sw=32768, ops=0) -> int
+        deflate_ext.h:17 / deflate_compress.c:362 -- 0 or -E_* (no exceptions, like C)
+    deflate_decompress(data, ops=0) -> bytes
+        deflate_ext.h:16 -- raises DeflateError(code) on a negative return
+    compress(data, sw=32768, max_chain=0) -> bytes        host buffer convenience
+    Encoder                                               device-resident encodes
+
+There is no CPU fallback: if libdmx.so is missing the import of this module fails,
+and on a machine without an MI355X every encode fails with -E_NEXIST.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import struct
+
+__all__ = [
+    "DeflateError", "Opts", "Result", "Encoder", "lib", "compress", "deflate_compress",
+    "deflate_decompress", "max_compressed", "adler32_combine", "gen_text", "gen_random",
+    "COMPRESS_STATS", "E", "DMX_F_HEADER", "DMX_F_TRAILER", "DMX_F_FINAL", "DMX_ZLIB",
+]
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdmx.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "dmx.h")
+
+DEFLATE_NULLTERM = 1
+DMX_F_HEADER, DMX_F_TRAILER, DMX_F_FINAL = 1, 2, 4
+DMX_ZLIB = 7
+_M = 1 << 24
+# global_errors.h:64-75 and deflate_errors.h:134-147
+E = {
+    "E_LEN": 1, "E_MALLOC": 2, "E_FORK": 3, "E_PIPE": 4, "E_CRC": 5, "E_SZ": 6, "E_EXIST": 7,
+    "E_NEXIST": 8, "E_NONULL": 9, "E_RANGE": 10, "E_INVAL": 11, "E_RESERV": 12,
+    "E_HUFAMB": _M + 1, "E_HUFINV": _M + 2, "E_HUFVAL": _M + 3, "E_HUFDIS": _M + 4,
+    "E_ZADL32": _M + 5, "E_ZHEAD": _M + 6, "E_ZFCHCK": _M + 7, "E_ZCMPMT": _M + 8,
+    "E_ZSLWIN": _M + 9, "E_ZPDICT": _M + 10, "E_ZBSZ": _M + 11, "E_ZNLEN": _M + 12,
+    "E_ZINV": _M + 13, "E_ZBTYPE": _M + 14, "E_DEVICE": _M + 64,
+}
+_ENAME = {v: k for k, v in E.items()}
+
+# struct compress_stats (deflate_ext.h:19-31): six little-endian int32
+COMPRESS_STATS = struct.Struct("<6i")
+
+
+class DeflateError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        super().__init__(f"{what or 'dmx'} failed: -{_ENAME.get(-code, str(-code))} ({code})")
+
+
+class Opts(ctypes.Structure):
+    _fields_ = [("sw", ctypes.c_int32), ("max_chain", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("reserved", ctypes.c_int32)]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("out_len", ctypes.c_uint64), ("end_bits", ctypes.c_uint64), ("n", ctypes.c_uint64),
+                ("ntokens", ctypes.c_uint64), ("adler", ctypes.c_uint32), ("status", ctypes.c_int32),
+                ("nblocks", ctypes.c_uint32), ("nstored", ctypes.c_uint32), ("nfixed", ctypes.c_uint32),
+                ("ndynamic", ctypes.c_uint32), ("pad", ctypes.c_uint32 * 2)]
+
+
+class _StringLen(ctypes.Structure):
+    _fields_ = [("str", ctypes.POINTER(ctypes.c_ubyte)), ("len", ctypes.c_size_t)]
+
+
+_lib = None
+_libc = ctypes.CDLL(None)
+_libc.free.argtypes = [ctypes.c_void_p]
+_libc.free.restype = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libdmx.so (built by __graft_entry__.build() / `make -C deflate_compression_amd/csrc`)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                          "g.build()'` (the encoder has no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, i32, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint32
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    sig = {
+        "deflate_compress": ([ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_ushort, ctypes.c_int], ctypes.c_int),
+        "deflate_decompress": ([ctypes.POINTER(_StringLen), ctypes.POINTER(_StringLen), ctypes.c_int], ctypes.c_int),
+        "spawn_deflate_compr_t": ([], vp),
+        "deflate_compr_init": ([vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_ushort], None),
+        "deflate_compr_deinit": ([vp], None),
+        "dmx_ctx_create": ([ctypes.c_int, u64, ctypes.POINTER(vp)], ctypes.c_int),
+        "dmx_ctx_destroy": ([vp], None),
+        "dmx_ctx_reserve": ([vp, u64, i32], ctypes.c_int),
+        "dmx_max_compressed": ([u64, i32], u64),
+        "dmx_encode_async": ([vp, vp, u64, vp, u64, ctypes.POINTER(Opts), vp], ctypes.c_int),
+        "dmx_encode_result": ([vp, ctypes.POINTER(Result), vp], ctypes.c_int),
+        "dmx_encode_host": ([vp, u64, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(Opts)], ctypes.c_int),
+        "dmx_last_blocks": ([vp, u32p, u8p, u32p, u32], ctypes.c_int),
+        "dmx_last_tokens": ([vp, u32, u32p, u32], ctypes.c_int),
+        "dmx_last_code_lengths": ([vp, u32, u8p], ctypes.c_int),
+        "dmx_ctx_set_timing": ([vp, ctypes.c_int], ctypes.c_int),
+        "dmx_ctx_stage_times": ([vp, ctypes.POINTER(ctypes.c_double), u32p], ctypes.c_int),
+        "dmx_adler32_combine": ([u32, u32, u64], u32),
+        "dmx_gen_text": ([vp, u64, u64], None),
+        "dmx_gen_random": ([vp, u64, u64], None),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def _check(r: int, what: str) -> None:
+    if r != 0:
+        raise DeflateError(r, what)
+
+
+def _buf(data):
+    """(ctypes pointer, length, keepalive) for bytes / bytearray / memoryview / numpy."""
+    try:
+        import numpy as np
+        if isinstance(data, np.ndarray):
+            a = np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+            return ctypes.c_void_p(a.ctypes.data), a.size, a
+    except ImportError:  # pragma: no cover
+        pass
+    b = bytes(data)
+    cb = ctypes.create_string_buffer(b, len(b) or 1)
+    return ctypes.cast(cb, ctypes.c_void_p), len(b), cb
+
+
+def max_compressed(n: int, sw: int = 32768) -> int:
+    return int(lib().dmx_max_compressed(n, sw))
+
+
+def compress(data, sw: int = 32768, max_chain: int = 0, flags: int = DMX_ZLIB) -> bytes:
+    """Encode a host buffer on the GPU; returns the zlib stream (or raw DEFLATE with flags)."""
+    L = lib()
+    p, n, keep = _buf(data)
+    cap = max_compressed(n, sw)
+    out = ctypes.create_string_buffer(cap)
+    olen = ctypes.c_uint64(0)
+    o = Opts(sw, max_chain, flags, 0)
+    _check(L.dmx_encode_host(p, n, out, cap, ctypes.byref(olen), ctypes.byref(o)), "dmx_encode_host")
+    del keep
+    return out.raw[:olen.value]
+
+
+def deflate_compress(fd_in: int, fd_out: int, fd_stats: int = -1, sw: int = 32768, ops: int = 0) -> int:
+    """deflate_ext.h:17 -- returns 0 or -E_* exactly like the C entry point."""
+    return int(lib().deflate_compress(fd_in, fd_out, fd_stats, sw & 0xFFFF, ops))
+
+
+def deflate_decompress(data, ops: int = 0) -> bytes:
+    """deflate_ext.h:16 -- inflate a zlib stream; raises DeflateError on -E_*."""
+    L = lib()
+    b = bytes(data)
+    src = (ctypes.c_ubyte * max(len(b), 1)).from_buffer_copy(b or b"\0")
+    cin = _StringLen(ctypes.cast(src, ctypes.POINTER(ctypes.c_ubyte)), len(b))
+    cout = _StringLen()
+    r = L.deflate_decompress(ctypes.byref(cout), ctypes.byref(cin), ops)
+    if r != 0:
+        raise DeflateError(r, "deflate_decompress")
+    n = cout.len + (1 if ops & DEFLATE_NULLTERM else 0)
+    res = ctypes.string_at(cout.str, n)
+    _libc.free(ctypes.cast(cout.str, ctypes.c_void_p))
+    return res
+
+
+def adler32_combine(a: int, b: int, len_b: int) -> int:
+    return int(lib().dmx_adler32_combine(a, b, len_b))
+
+
+def gen_text(n: int, seed: int = 0xE5818):
+    import numpy as np
+    a = np.empty(n, dtype=np.uint8)
+    lib().dmx_gen_text(ctypes.c_void_p(a.ctypes.data), n, seed)
+    return a
+
+
+def gen_random(n: int, seed: int = 0x5EED):
+    import numpy as np
+    a = np.empty(n, dtype=np.uint8)
+    lib().dmx_gen_random(ctypes.c_void_p(a.ctypes.data), n, seed)
+    return a
+
+
+class Encoder:
+    """Device-resident encoder on one GPU (a dmx_ctx: own HIP stream + HBM workspace).
+
+    encode_async(d_in, n, d_out, cap, stream=None) takes raw device pointers (ints),
+    e.g. torch tensors' .data_ptr(); nothing is allocated or synchronised per call.
+    """
+
+    def __init__(self, device: int = 0, max_input: int = 1 << 20, sw: int = 32768, max_chain: int = 0,
+                 flags: int = DMX_ZLIB):
+        self._L = lib()
+        self.device = device
+        self.opts = Opts(sw, max_chain, flags, 0)
+        self._ctx = ctypes.c_void_p()
+        _check(self._L.dmx_ctx_create(device, max_input, ctypes.byref(self._ctx)), "dmx_ctx_create")
+
+    def close(self) -> None:
+        if self._ctx:
+            self._L.dmx_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reserve(self, n: int, sw: int = 32768) -> None:
+        _check(self._L.dmx_ctx_reserve(self._ctx, n, sw), "dmx_ctx_reserve")
+
+    def encode_async(self, d_in: int, n: int, d_out: int, cap: int, stream: int | None = None,
+                     opts: Opts | None = None) -> None:
+        o = opts or self.opts
+        _check(self._L.dmx_encode_async(self._ctx, ctypes.c_void_p(d_in), n, ctypes.c_void_p(d_out), cap,
+                                        ctypes.byref(o), ctypes.c_void_p(stream or 0)), "dmx_encode_async")
+
+    def result(self, stream: int | None = None) -> Result:
+        r = Result()
+        _check(self._L.dmx_encode_result(self._ctx, ctypes.byref(r), ctypes.c_void_p(stream or 0)),
+               "dmx_encode_result")
+        if r.status:
+            raise DeflateError(r.status, "encode")
+        return r
+
+    # -- introspection of the last encode (tests / stats) --
+    def blocks(self, nblk: int):
+        import numpy as np
+        nt = np.zeros(nblk, np.uint32)
+        bt = np.zeros(nblk, np.uint8)
+        hb = np.zeros(nblk, np.uint32)
+        r = self._L.dmx_last_blocks(self._ctx, nt.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                    bt.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                    hb.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), nblk)
+        if r < 0:
+            raise DeflateError(r, "dmx_last_blocks")
+        return nt[:r], bt[:r], hb[:r]
+
+    def tokens(self, blk: int):
+        import numpy as np
+        t = np.zeros(32768, np.uint32)
+        r = self._L.dmx_last_tokens(self._ctx, blk, t.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), 32768)
+        if r < 0:
+            raise DeflateError(r, "dmx_last_tokens")
+        return t[:r].copy()
+
+    def code_lengths(self, blk: int):
+        import numpy as np
+        ln = np.zeros(316, np.uint8)
+        _check(self._L.dmx_last_code_lengths(self._ctx, blk, ln.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))),
+               "dmx_last_code_lengths")
+        return ln
+
+    def set_timing(self, on: bool) -> None:
+        self._L.dmx_ctx_set_timing(self._ctx, 1 if on else 0)
+
+    def stage_times(self):
+        ms = (ctypes.c_double * 5)()
+        cnt = ctypes.c_uint32(0)
+        self._L.dmx_ctx_stage_times(self._ctx, ms, ctypes.byref(cnt))
+        return dict(zip(["chain", "match", "huff", "scan", "pack"], list(ms))), cnt.value
+
+    # -- host convenience on this context via torch tensors --
+    def compress_tensor(self, t_in, stream=None, opts: Opts | None = None):
+        """Encode a uint8 CUDA tensor; returns (uint8 CUDA tensor of the stream, Result)."""
+        import torch
+        o = opts or self.opts
+        n = t_in.numel()
+        cap = max_compressed(n, o.sw)
+        out = torch.empty(cap, dtype=torch.uint8, device=t_in.device)
+        s = stream if stream is not None else torch.cuda.current_stream(t_in.device).cuda_stream
+        self.encode_async(t_in.data_ptr() if n else out.data_ptr(), n, out.data_ptr(), cap, s, o)
+        r = self.result(s)
+        return out[:r.out_len], r
+
+    def compress_bytes(self, data, sw: int = 32768, max_chain: int = 0, flags: int = DMX_ZLIB):
+        """Host bytes -> HBM -> encode -> host bytes, on this context (keeps introspection)."""
+        import numpy as np
+        import torch
+        a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        t = torch.from_numpy(a.copy()).to(f"cuda:{self.device}") if a.size else \
+            torch.empty(0, dtype=torch.uint8, device=f"cuda:{self.device}")
+        self.reserve(a.size, sw)
+        out, r = self.compress_tensor(t, opts=Opts(sw, max_chain, flags, 0))
+        return out.cpu().numpy().tobytes(), r

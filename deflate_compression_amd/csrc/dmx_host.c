@@ -1,0 +1,194 @@
+/*
+ * dmx_host.c -- host C side of libdmx: the reference's public codec API
+ * (src/include/deflate_ext.h) on top of the HIP layer (dmx_kernels.hip).
+ *
+ *   deflate_compress(fd_in, fd_out, fd_stats, sw, ops)   deflate_compress.c:362-376
+ *   spawn_deflate_compr_t / deflate_compr_init / _deinit  deflate_compress.c:83-112
+ *   struct compress_stats stream                         deflate_compress.c:290-309
+ *
+ * Errors are returned as -E_* (global_errors.h / deflate_errors.h codes); nothing
+ * longjmps.  There is no CPU encode path: the encode runs on the GPU or fails.
+ */
+#include <errno.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include "../../include/dmx.h"
+#include "dmx_internal.h"
+
+/* from dmx_kernels.hip */
+dmx_ctx* dmx_cached_ctx(int device, uint64_t max_input, int* err);
+
+struct deflate_compr {
+    int fd_in, fd_out, fd_stats;
+    swi sw;
+};
+
+deflate_compr_t* spawn_deflate_compr_t(void) { return (deflate_compr_t*)calloc(1, sizeof(deflate_compr_t)); }
+
+void deflate_compr_init(deflate_compr_t* com, int fd_in, int fd_out, int fd_stats, swi sw) {
+    if (!com) return;
+    com->fd_in = fd_in;
+    com->fd_out = fd_out;
+    com->fd_stats = fd_stats;
+    com->sw = sw;
+}
+
+void deflate_compr_deinit(deflate_compr_t* com) {
+    if (com) memset(com, 0, sizeof(*com));
+}
+
+static int read_all(int fd, uint8_t** buf, uint64_t* n) {
+    uint64_t cap = 1 << 20, len = 0;
+    uint8_t* b = (uint8_t*)malloc(cap);
+    if (!b) return -E_MALLOC;
+    for (;;) {
+        if (len == cap) {
+            uint8_t* nb = (uint8_t*)realloc(b, cap * 2);
+            if (!nb) { free(b); return -E_MALLOC; }
+            b = nb;
+            cap *= 2;
+        }
+        ssize_t r = read(fd, b + len, cap - len);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            free(b);
+            return -E_NEXIST;
+        }
+        if (r == 0) break;
+        len += (uint64_t)r;
+    }
+    *buf = b;
+    *n = len;
+    return 0;
+}
+
+static int write_all(int fd, const void* p, uint64_t n) {
+    const uint8_t* c = (const uint8_t*)p;
+    while (n) {
+        ssize_t w = write(fd, c, n);
+        if (w < 0) {
+            if (errno == EINTR) continue;
+            return -E_PIPE;
+        }
+        c += w;
+        n -= (uint64_t)w;
+    }
+    return 0;
+}
+
+/* RFC 1951 §3.2.5 symbol + extra bits (host copy, used only to format stats) */
+static void h_len_sym(int len, int* sym, int* eb) {
+    static const int base[] = {11, 13, 15, 17, 19, 23, 27, 31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227};
+    if (len == 258) { *sym = 285; *eb = 0; return; }
+    if (len <= 10) { *sym = 254 + len; *eb = 0; return; }
+    int k = 19;
+    while (base[k] > len) k--;
+    *sym = 265 + k;
+    *eb = 1 + k / 4;
+}
+static void h_dist_sym(int dist, int* sym, int* eb) {
+    int x = dist - 1, e = 0;
+    if (x < 4) { *sym = x; *eb = 0; return; }
+    while ((x >> (e + 1)) != 0) e++;
+    *sym = 2 * e + ((x >> (e - 1)) & 1);
+    *eb = e - 1;
+}
+
+/* One compress_stats record per token (deflate_compress.c:290-309) with exact costs:
+ * tree_bits = header bits of the token's block, ll_bits/d_bits = running lit/len and
+ * distance bits inside the block. */
+static int write_stats(dmx_ctx* c, int fd, uint64_t n, int sw) {
+    const uint32_t nblk = (uint32_t)((n + (uint64_t)sw - 1) / (uint64_t)sw);
+    if (!nblk) return 0;
+    uint32_t* ntok = (uint32_t*)malloc(sizeof(uint32_t) * nblk);
+    uint8_t* bt = (uint8_t*)malloc(nblk);
+    uint32_t* hb = (uint32_t*)malloc(sizeof(uint32_t) * nblk);
+    uint32_t* tok = (uint32_t*)malloc(sizeof(uint32_t) * DMX_BLK);
+    struct compress_stats* rec = (struct compress_stats*)malloc(sizeof(struct compress_stats) * DMX_BLK);
+    int r = 0;
+    if (!ntok || !bt || !hb || !tok || !rec) r = -E_MALLOC;
+    if (!r && dmx_last_blocks(c, ntok, bt, hb, nblk) != (int)nblk) r = -E_DEVICE;
+    for (uint32_t b = 0; !r && b < nblk; b++) {
+        uint8_t lens[316];
+        int nt = dmx_last_tokens(c, b, tok, DMX_BLK);
+        if (nt < 0) { r = nt; break; }
+        if (dmx_last_code_lengths(c, b, lens)) { r = -E_DEVICE; break; }
+        int ll_bits = 0, d_bits = 0;
+        uint64_t pos = (uint64_t)b * (uint64_t)sw;
+        for (int k = 0; k < nt; k++) {
+            uint32_t t = tok[k];
+            struct compress_stats* cs = rec + k;
+            cs->bytes = (int)(pos + 1);
+            cs->tree_bits = bt[b] == 2 ? (int)hb[b] : 3;
+            if ((t >> 9) == 0) {
+                cs->ll = (int)(t & 0xFF);
+                cs->d = 0;
+                ll_bits += bt[b] == 0 ? 8 : lens[t & 0xFF];
+                pos += 1;
+            } else {
+                int len = (int)(t & 0x1FF), dist = (int)(t >> 9), s, eb;
+                cs->ll = len;
+                cs->d = dist;
+                if (bt[b] == 0) {          /* stored block: the bytes themselves */
+                    ll_bits += 8 * len;
+                } else {
+                    h_len_sym(len, &s, &eb);
+                    ll_bits += lens[s] + eb;
+                    h_dist_sym(dist, &s, &eb);
+                    d_bits += lens[DMX_DIST0 + s] + eb;
+                }
+                pos += (uint64_t)len;
+            }
+            cs->ll_bits = ll_bits;
+            cs->d_bits = d_bits;
+        }
+        r = write_all(fd, rec, sizeof(struct compress_stats) * (uint64_t)nt);
+    }
+    free(ntok); free(bt); free(hb); free(tok); free(rec);
+    return r;
+}
+
+int deflate_compress(int fd_in, int fd_out, int fd_stats, swi sw, int ops) {
+    (void)ops; /* unused by the reference's compress too */
+    int swv = sw == 0 ? DMX_BLK : (int)sw;
+    if (swv > DMX_BLK) return -E_RANGE;
+    const char* mc = getenv("DMX_MAX_CHAIN");
+    dmx_opts o;
+    o.sw = swv;
+    o.max_chain = mc ? atoi(mc) : 0;
+    o.flags = DMX_ZLIB;
+    o.reserved = 0;
+    uint8_t* in = NULL;
+    uint64_t n = 0;
+    int r = read_all(fd_in, &in, &n);
+    if (r) return r;
+    uint64_t cap = dmx_max_compressed(n, swv);
+    uint8_t* out = (uint8_t*)malloc(cap);
+    if (!out) { free(in); return -E_MALLOC; }
+    uint64_t out_len = 0;
+    r = dmx_encode_host(in, n, out, cap, &out_len, &o);
+    if (!r && fd_out >= 0) r = write_all(fd_out, out, out_len);
+    if (!r && fd_stats >= 0) {
+        const char* dev_s = getenv("DMX_DEVICE");
+        int err = 0;
+        dmx_ctx* c = dmx_cached_ctx(dev_s ? atoi(dev_s) : 0, n, &err);
+        r = c ? write_stats(c, fd_stats, n, swv) : err;
+    }
+    free(in);
+    free(out);
+    return r;
+}
+
+/* Adler-32 of A||B from adler(A), adler(B) and len(B) (RFC 1950 §8.2 arithmetic). */
+uint32_t dmx_adler32_combine(uint32_t a, uint32_t b, uint64_t len_b) {
+    const uint64_t M = 65521;
+    const uint64_t rem = len_b % M;
+    uint64_t s1 = a & 0xFFFF, s2 = (rem * s1) % M;
+    s1 = (s1 + (b & 0xFFFF) + M - 1) % M;
+    s2 = (s2 + ((a >> 16) & 0xFFFF) + ((b >> 16) & 0xFFFF) + M - rem) % M;
+    return (uint32_t)(s1 | (s2 << 16));
+}

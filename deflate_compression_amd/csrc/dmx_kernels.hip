@@ -1,0 +1,1241 @@
+// dmx_kernels.hip -- the MI355X (gfx950 / CDNA4) hot path of the DEFLATE encoder.
+//
+// The input is cut into independent sw-byte blocks (sw <= 32768 = the window).
+// Per encode, five launches on one HIP stream:
+//   K1a dmx_chain_kernel  one wave per block: builds the hash chains prev[] of
+//                         deflate_compress.c:312-319 (every position at the head of
+//                         its bucket) in position order, 64 positions per step,
+//                         in-wave conflicts resolved with ballots; prev[] -> HBM.
+//   K1b dmx_match_kernel  one 1024-thread workgroup per block, block + chains in
+//                         LDS: the longest match of EVERY position (chain walk of
+//                         deflate_compress.c:243-264, newest first, strict >),
+//                         then the greedy path 0 -> i + max(len,1) (:265-288) by
+//                         speculative 32-position segments + two fix-up levels,
+//                         token compaction (block scan) and lit/len + dist
+//                         histograms.  Tokens -> HBM.
+//   K2  dmx_huff_kernel   one wave per block: length-limited canonical Huffman
+//                         codes, RFC 1951 §3.2.7 header, exact stored/fixed/
+//                         dynamic cost, BTYPE choice (replaces the reference's
+//                         per-token estimators aht.c / h_tree.c).
+//   K3  dmx_scan_kernel   one workgroup: bit offsets of all blocks (a scan over an
+//                         associative "stored blocks re-align" monoid), Adler-32
+//                         combine, zlib header / flush / trailer, boundary words.
+//   K4  dmx_pack_kernel   one 256-thread workgroup per block: bit-packs header +
+//                         tokens (or the stored bytes) at the block's absolute bit
+//                         offset in LDS, then coalesced 32-bit stores to HBM.
+// Token encoding: t = byte (literal) | (dist << 9) | len  (DESIGN.md §2).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "dmx_internal.h"
+#include "../../include/dmx.h"
+
+#define MAXLEN 258
+
+// ------------------------------------------------------------------------------------
+// small device helpers
+// ------------------------------------------------------------------------------------
+
+__device__ __forceinline__ uint32_t dmx_hash(uint32_t tri) { return (tri * 0x9E3779B1u) >> DMX_HASH_SHIFT; }
+
+// RFC 1951 §3.2.5 length -> symbol 257..285, extra-bit count, extra value
+__device__ __forceinline__ void len_sym(uint32_t len, uint32_t& sym, uint32_t& eb, uint32_t& ev) {
+    if (len == 258) { sym = 285; eb = 0; ev = 0; }
+    else if (len <= 10) { sym = 254 + len; eb = 0; ev = 0; }
+    else {
+        uint32_t l = len - 3;
+        uint32_t e = 31 - __clz(l) - 2;
+        sym = 261 + 4 * e + ((l >> e) - 4);
+        eb = e;
+        ev = l & ((1u << e) - 1);
+    }
+}
+
+// RFC 1951 §3.2.5 distance -> symbol 0..29, extra-bit count, extra value
+__device__ __forceinline__ void dist_sym(uint32_t dist, uint32_t& sym, uint32_t& eb, uint32_t& ev) {
+    uint32_t x = dist - 1;
+    if (x < 4) { sym = x; eb = 0; ev = 0; }
+    else {
+        uint32_t e = 31 - __clz(x);
+        eb = e - 1;
+        sym = 2 * e + ((x >> (e - 1)) & 1);
+        ev = x & ((1u << eb) - 1);
+    }
+}
+
+__device__ __forceinline__ uint32_t len_eb_of_sym(uint32_t s) {  // s in 257..285
+    return (s >= 265 && s < 285) ? (s - 261) / 4 : 0;
+}
+__device__ __forceinline__ uint32_t dist_eb_of_sym(uint32_t s) { return s < 4 ? 0 : s / 2 - 1; }
+__device__ __forceinline__ uint32_t fixed_len(uint32_t s) { return s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8; }
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// ------------------------------------------------------------------------------------
+// K1a: hash chains
+// ------------------------------------------------------------------------------------
+
+__global__ __launch_bounds__(64) void dmx_chain_kernel(const uint8_t* __restrict__ in, uint64_t n,
+                                                       uint32_t sw, uint16_t* __restrict__ prev_g) {
+    __shared__ uint64_t head64[DMX_NBUCKET / 4];
+    uint16_t* head = reinterpret_cast<uint16_t*>(head64);
+    const uint32_t lane = threadIdx.x;
+    const uint64_t off = (uint64_t)blockIdx.x * sw;
+    const uint32_t bn = (uint32_t)((n - off) < sw ? (n - off) : sw);
+    const uint8_t* d = in + off;
+    uint16_t* pg = prev_g + (uint64_t)blockIdx.x * DMX_BLK;
+
+    for (uint32_t k = lane; k < DMX_NBUCKET / 4; k += 64) head64[k] = ~0ull;
+    __syncthreads();
+
+    const uint32_t nsteps = (bn + 63) >> 6;
+    uint32_t c0 = lane < bn ? d[lane] : 0;
+    uint32_t cx = (lane < 2 && 64 + lane < bn) ? d[64 + lane] : 0;
+    for (uint32_t s = 0; s < nsteps; s++) {
+        const uint32_t base = s << 6;
+        const uint32_t b0 = c0, bx = cx;
+        {   // prefetch the next step's bytes while this one is hashed
+            const uint32_t np = base + 64 + lane;
+            c0 = np < bn ? d[np] : 0;
+            cx = (lane < 2 && np + 64 < bn) ? d[np + 64] : 0;
+        }
+        uint32_t b1 = __shfl_down(b0, 1);
+        uint32_t b2 = __shfl_down(b0, 2);
+        const uint32_t x0 = __shfl(bx, 0), x1 = __shfl(bx, 1);
+        if (lane == 63) { b1 = x0; b2 = x1; }
+        else if (lane == 62) { b2 = x0; }
+        const uint32_t p = base + lane;
+        const bool valid = p + 2 < bn;
+        const uint32_t h = dmx_hash(b0 | (b1 << 8) | (b2 << 16));
+        uint64_t eq = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < 14; bit++) {
+            const bool hb = (h >> bit) & 1;
+            const uint64_t m = __ballot(hb);
+            eq &= hb ? m : ~m;
+        }
+        uint16_t pv = DMX_NONE16;
+        if (valid) {
+            const uint64_t lower = eq & ((1ull << lane) - 1);
+            pv = lower ? (uint16_t)(base + 63 - __clzll(lower)) : head[h];
+        }
+        if (p < bn) pg[p] = pv;
+        if (valid) {
+            const uint64_t higher = eq & ~((2ull << lane) - 1);
+            if (!higher) head[h] = (uint16_t)p;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// K1b: longest match of every position + greedy path + compaction
+// ------------------------------------------------------------------------------------
+
+#define MT 1024
+#define MW (MT / 64)
+#define DATA_WORDS 8200
+
+struct __attribute__((aligned(16))) MatchLDS {
+    uint32_t data[DATA_WORDS];  // the block, zero padded
+    uint16_t prev[DMX_BLK];     // hash chains (K1a)
+    uint8_t len8[DMX_BLK];      // best length - 3 (matches)
+    uint32_t lit[DMX_BLK / 32]; // 1 = literal at that position
+    uint32_t tsm[DMX_BLK / 32]; // token starts, 32 positions per word
+    uint32_t exitp[DMX_BLK / 32];
+    uint32_t hist[DMX_HIST];
+    uint32_t wexit[MW];
+    uint32_t wsum[MW];
+    uint32_t ctr;
+    uint32_t ntok;
+    unsigned long long adl_s, adl_t;
+};
+
+__device__ __forceinline__ uint32_t ld4(const uint32_t* W, uint32_t p) {
+    const uint32_t w0 = W[p >> 2], w1 = W[(p >> 2) + 1];
+    return __builtin_amdgcn_alignbyte(w1, w0, p & 3);
+}
+
+__device__ __forceinline__ uint32_t adv_of(const MatchLDS& L, uint32_t p) {
+    return ((L.lit[p >> 5] >> (p & 31)) & 1u) ? 1u : (uint32_t)L.len8[p] + 3u;
+}
+
+// Resolve segment s (positions [32s, 32s+32)) for a path entering at e >= 32s.
+// The word tsm[s] holds a path through the segment; if the walk from e meets one of
+// its positions the rest coincides (the next-function is deterministic).
+__device__ uint32_t resolve_seg(MatchLDS& L, uint32_t s, uint32_t e, uint32_t bn, bool& merged) {
+    const uint32_t lo = s << 5;
+    merged = false;
+    if (e >= lo + 32 || e >= bn) { L.tsm[s] = 0; return e; }
+    const uint32_t m = L.tsm[s];
+    uint32_t nm = 0, p = e;
+    while (p < lo + 32 && p < bn) {
+        const uint32_t bit = 1u << (p - lo);
+        if (m & bit) {
+            L.tsm[s] = nm | (m & ~(bit - 1u));
+            merged = true;
+            return L.exitp[s];
+        }
+        nm |= bit;
+        p += adv_of(L, p);
+    }
+    L.tsm[s] = nm;
+    return p;
+}
+
+__global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
+                                                       int32_t max_chain, uint16_t* __restrict__ prev_g,
+                                                       uint32_t* __restrict__ tok_g, uint32_t* __restrict__ hist_g,
+                                                       dmx_blkinfo* __restrict__ info) {
+    __shared__ MatchLDS L;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t b = blockIdx.x;
+    const uint64_t off = (uint64_t)b * sw;
+    const uint32_t bn = (uint32_t)((n - off) < sw ? (n - off) : sw);
+    const uint8_t* d = in + off;
+    uint16_t* pg = prev_g + (uint64_t)b * DMX_BLK;  // chains in; distances out (same slots)
+    uint8_t* D8 = reinterpret_cast<uint8_t*>(L.data);
+
+    // ---- P0: stage the block and its chains in LDS ----
+    if (tid == 0) { L.ctr = 0; L.adl_s = 0; L.adl_t = 0; }
+    for (uint32_t k = tid; k < DMX_HIST; k += MT) L.hist[k] = 0;
+    const bool aligned16 = ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
+    for (uint32_t k = tid; k < DATA_WORDS / 4; k += MT) {   // 16-byte chunks
+        const uint32_t p = k << 4;
+        uint4 v;
+        if (aligned16 && p + 16 <= bn) {
+            v = *reinterpret_cast<const uint4*>(d + p);
+        } else {
+            uint32_t w[4] = {0, 0, 0, 0};
+            for (uint32_t j = 0; j < 16; j++)
+                if (p + j < bn) w[j >> 2] |= (uint32_t)d[p + j] << (8 * (j & 3));
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        *reinterpret_cast<uint4*>(&L.data[k << 2]) = v;
+    }
+    {
+        const uint32_t nch = (bn * 2 + 15) >> 4;  // prev entries needed: [0, bn)
+        const uint4* src = reinterpret_cast<const uint4*>(pg);
+        uint4* dst = reinterpret_cast<uint4*>(L.prev);
+        for (uint32_t k = tid; k < nch; k += MT) dst[k] = src[k];
+    }
+    __syncthreads();
+
+    {   // Adler-32 partial sums of this block
+        uint64_t s = 0, t = 0;
+        const uint32_t lo = tid << 5;
+        for (uint32_t j = 0; j < 32; j++) {
+            const uint32_t p = lo + j;
+            if (p < bn) { const uint32_t c = D8[p]; s += c; t += (uint64_t)p * c; }
+        }
+        s = wave_sum_u64(s);
+        t = wave_sum_u64(t);
+        if (lane == 0) { atomicAdd(&L.adl_s, (unsigned long long)s); atomicAdd(&L.adl_t, (unsigned long long)t); }
+    }
+
+    // ---- P1: longest match at every position (dynamic 64-position chunks per wave) ----
+    const uint32_t nchunks = (bn + 63) >> 6;
+    for (;;) {
+        uint32_t c = 0;
+        if (lane == 0) c = atomicAdd(&L.ctr, 1u);
+        c = __shfl(c, 0);
+        if (c >= nchunks) break;
+        const uint32_t i = (c << 6) + lane;
+        uint32_t best = 2, bq = DMX_NONE16;
+        if (i + 2 < bn) {
+            const uint32_t lim = (bn - i) < MAXLEN ? (bn - i) : MAXLEN;
+            uint32_t q = L.prev[i];
+            int steps = 0;
+            while (q != DMX_NONE16) {
+                if (max_chain > 0 && steps >= max_chain) break;
+                steps++;
+                if (D8[q + best] == D8[i + best]) {      // cannot beat `best` otherwise
+                    uint32_t k = 0;
+                    for (;;) {
+                        const uint32_t x = ld4(L.data, i + k) ^ ld4(L.data, q + k);
+                        if (x) { k += __builtin_ctz(x) >> 3; break; }
+                        k += 4;
+                        if (k >= lim) break;
+                    }
+                    if (k > lim) k = lim;
+                    if (k > best) {                      // strict >: ties keep the nearer
+                        best = k;
+                        bq = q;
+                        if (k == lim) break;
+                    }
+                }
+                q = L.prev[q];
+            }
+        }
+        const bool is_lit = (bq == DMX_NONE16);
+        const uint64_t lm = __ballot(is_lit);
+        if (lane == 0) { L.lit[c << 1] = (uint32_t)lm; L.lit[(c << 1) + 1] = (uint32_t)(lm >> 32); }
+        if (i < bn) {
+            L.len8[i] = is_lit ? 0 : (uint8_t)(best - 3);
+            if (!is_lit) pg[i] = (uint16_t)(i - bq);
+        }
+    }
+    __syncthreads();
+
+    // ---- P2: greedy path ----
+    {   // W1: speculative walk of every 32-position segment from its start
+        const uint32_t lo = tid << 5;
+        uint32_t m = 0, p = lo;
+        while (p < lo + 32 && p < bn) { m |= 1u << (p - lo); p += adv_of(L, p); }
+        L.tsm[tid] = m;
+        L.exitp[tid] = p;
+    }
+    __syncthreads();
+    if (lane == 0) {  // W2: resolve the wave's 64 segments assuming it is entered at 2048*wave
+        uint32_t e = wave << 11;
+        bool mg;
+        for (uint32_t s = wave << 6; s < (wave << 6) + 64; s++) e = resolve_seg(L, s, e, bn, mg);
+        L.wexit[wave] = e;
+    }
+    __syncthreads();
+    if (tid == 0) {   // W3: fix the waves whose true entry differs, until the paths merge
+        uint32_t E = L.wexit[0];
+        for (uint32_t w = 1; w < MW; w++) {
+            if (E == (w << 11)) { E = L.wexit[w]; continue; }
+            uint32_t e = E;
+            bool mg = false;
+            for (uint32_t s = w << 6; s < (w << 6) + 64; s++) {
+                e = resolve_seg(L, s, e, bn, mg);
+                if (mg) { e = L.wexit[w]; break; }
+            }
+            E = e;
+        }
+    }
+    __syncthreads();
+
+    // ---- P3: compaction + histograms ----
+    {
+        const uint32_t m = L.tsm[tid];
+        const uint32_t cnt = __popc(m);
+        uint32_t x = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        if (lane == 63) L.wsum[wave] = x;
+        __syncthreads();
+        if (wave == 0) {
+            uint32_t v = lane < MW ? L.wsum[lane] : 0, z = v;
+#pragma unroll
+            for (int o = 1; o < MW; o <<= 1) {
+                const uint32_t y = __shfl_up(z, o);
+                if (lane >= (uint32_t)o) z += y;
+            }
+            if (lane < MW) L.wsum[lane] = z - v;
+            if (lane == MW - 1) L.ntok = z;
+        }
+        __syncthreads();
+        uint32_t k = L.wsum[wave] + x - cnt;
+        uint32_t* tb = tok_g + (uint64_t)b * DMX_BLK;
+        uint32_t mm = m;
+        while (mm) {
+            const uint32_t bit = __builtin_ctz(mm);
+            mm &= mm - 1;
+            const uint32_t p = (tid << 5) + bit;
+            uint32_t t;
+            if ((L.lit[tid] >> bit) & 1u) {
+                t = D8[p];
+                atomicAdd(&L.hist[t], 1u);
+            } else {
+                const uint32_t len = (uint32_t)L.len8[p] + 3u, dist = pg[p];
+                t = (dist << 9) | len;
+                uint32_t s, eb, ev;
+                len_sym(len, s, eb, ev);
+                atomicAdd(&L.hist[s], 1u);
+                dist_sym(dist, s, eb, ev);
+                atomicAdd(&L.hist[DMX_DIST0 + s], 1u);
+            }
+            tb[k++] = t;
+        }
+    }
+    __syncthreads();
+    for (uint32_t k = tid; k < DMX_HIST; k += MT) hist_g[(uint64_t)b * DMX_HIST + k] = L.hist[k];
+    if (tid == 0) {
+        info[b].ntok = L.ntok;
+        info[b].n = bn;
+        info[b].adl_s = L.adl_s;
+        info[b].adl_w = (uint64_t)bn * L.adl_s - L.adl_t;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// K2: Huffman codes + block type (one wave per block)
+// ------------------------------------------------------------------------------------
+
+struct HuffLDS {
+    uint32_t f[320];
+    uint32_t fs[320];
+    uint32_t nodew[320];
+    uint16_t sym[320];
+    uint16_t lpar[320];
+    uint16_t npar[320];
+    uint8_t ndep[320];
+    int32_t blc[64];
+    int32_t m;
+};
+
+struct K2LDS {
+    HuffLDS H;
+    uint32_t fll[288];
+    uint32_t fd[32];
+    uint32_t fcl[20];
+    uint8_t lll[288];
+    uint8_t ld[32];
+    uint8_t lcl[20];
+    uint8_t rle_sym[320];
+    uint8_t rle_ext[320];
+    uint32_t code[320];  // canonical codes (bit-reversed) | len << 16
+    uint32_t hdr[DMX_HDR_WORDS];
+    int32_t rle_n, hlit, hdist, hclen;
+    uint32_t hdr_pos;
+};
+
+__constant__ uint8_t c_clorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+__constant__ uint8_t c_cl_eb[19] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 3, 7};
+
+// Code lengths for freq H.f[0..n) limited to maxbits: symbols sorted
+// by (freq, symbol); two-queue merge (ties take the leaf); depths; overflow
+// redistribution; longest lengths to the least frequent symbols.
+__device__ void huff_lengths(HuffLDS& H, int n, int maxbits, uint8_t* len, uint32_t lane) {
+    uint32_t m = 0;
+    for (int j = 0; j < n; j += 64) {
+        const int s = j + (int)lane;
+        const bool used = s < n && H.f[s] != 0;
+        if (s < n) len[s] = 0;
+        m += __popcll(__ballot(used));
+    }
+    __syncthreads();
+    if (m == 0) return;
+    if (m == 1) {
+        if (lane == 0) {
+            int s0 = 0;
+            while (H.f[s0] == 0) s0++;
+            len[s0] = 1;
+            len[s0 == 0 ? 1 : 0] = 1;
+        }
+        __syncthreads();
+        return;
+    }
+    // rank of each used symbol among used symbols by key (freq << 9 | sym)
+    {
+        uint32_t key[5];
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            const int s = j * 64 + (int)lane;
+            key[j] = (s < n && H.f[s]) ? ((H.f[s] << 9) | (uint32_t)s) : 0xFFFFFFFFu;
+        }
+        uint32_t r[5] = {0, 0, 0, 0, 0};
+        for (int s2 = 0; s2 < n; s2++) {
+            const uint32_t f2 = H.f[s2];
+            const uint32_t k2 = f2 ? ((f2 << 9) | (uint32_t)s2) : 0xFFFFFFFFu;
+#pragma unroll
+            for (int j = 0; j < 5; j++) r[j] += (k2 < key[j]) ? 1u : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            if (key[j] != 0xFFFFFFFFu) {
+                H.sym[r[j]] = (uint16_t)(key[j] & 511u);
+                H.fs[r[j]] = key[j] >> 9;
+            }
+        }
+    }
+    for (int k = (int)lane; k < 64; k += 64) H.blc[k] = 0;
+    __syncthreads();
+    if (lane == 0) {
+        int li = 0, ni = 0, nn = 0;
+        const int mm = (int)m;
+        for (int k = 0; k < mm - 1; k++) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int pick = 0; pick < 2; pick++) {
+                if (li < mm && (ni >= nn || H.fs[li] <= H.nodew[ni])) {
+                    w += H.fs[li];
+                    H.lpar[li++] = (uint16_t)nn;
+                } else {
+                    w += H.nodew[ni];
+                    H.npar[ni++] = (uint16_t)nn;
+                }
+            }
+            H.nodew[nn++] = w;
+        }
+        H.ndep[nn - 1] = 0;
+        for (int j = nn - 2; j >= 0; j--) H.ndep[j] = (uint8_t)(H.ndep[H.npar[j]] + 1);
+        int maxd = 0;
+        for (int k = 0; k < mm; k++) {
+            const int dpt = H.ndep[H.lpar[k]] + 1;
+            H.blc[dpt]++;
+            if (dpt > maxd) maxd = dpt;
+        }
+        if (maxd > maxbits) {
+            for (int dd = maxbits + 1; dd <= maxd; dd++) { H.blc[maxbits] += H.blc[dd]; H.blc[dd] = 0; }
+            uint32_t total = 0;
+            for (int dd = 1; dd <= maxbits; dd++) total += (uint32_t)H.blc[dd] << (maxbits - dd);
+            while (total != (1u << maxbits)) {
+                H.blc[maxbits]--;
+                for (int dd = maxbits - 1; dd >= 1; dd--) {
+                    if (H.blc[dd]) { H.blc[dd]--; H.blc[dd + 1] += 2; break; }
+                }
+                total--;
+            }
+        }
+        int k = 0;
+        for (int dd = maxbits; dd >= 1; dd--)
+            for (int c = 0; c < H.blc[dd]; c++) len[H.sym[k++]] = (uint8_t)dd;
+    }
+    __syncthreads();
+}
+
+// canonical codes (RFC 1951 §3.2.2), bit-reversed, packed code | len << 16
+__device__ void canon_codes(const uint8_t* len, int n, uint32_t* out, uint32_t lane) {
+    if (lane == 0) {
+        int bl[16] = {0};
+        for (int s = 0; s < n; s++) bl[len[s]]++;
+        bl[0] = 0;
+        uint32_t next[16], c = 0;
+        for (int b = 1; b < 16; b++) { c = (c + bl[b - 1]) << 1; next[b] = c; }
+        for (int s = 0; s < n; s++) {
+            const uint32_t l = len[s];
+            if (!l) { out[s] = 0; continue; }
+            const uint32_t v = next[l]++;
+            out[s] = (__brev(v) >> (32 - l)) | (l << 16);
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void hdr_put(K2LDS& S, uint32_t v, uint32_t nb) {  // lane 0 only
+    if (!nb) return;
+    const uint32_t p = S.hdr_pos;
+    const uint32_t w = p >> 5, sh = p & 31;
+    S.hdr[w] |= v << sh;
+    if (sh + nb > 32) S.hdr[w + 1] |= v >> (32 - sh);
+    S.hdr_pos = p + nb;
+}
+
+__global__ __launch_bounds__(64) void dmx_huff_kernel(const uint32_t* __restrict__ hist_g, dmx_blkinfo* __restrict__ info,
+                                                      uint32_t* __restrict__ codes_g, uint32_t* __restrict__ hdr_g,
+                                                      uint32_t nblk, uint32_t flags) {
+    __shared__ K2LDS S;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    const uint32_t* hg = hist_g + (uint64_t)b * DMX_HIST;
+    const uint32_t bn = info[b].n;
+    const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1) ? 1u : 0u;
+
+    for (int s = (int)lane; s < 288; s += 64) S.fll[s] = s < 286 ? hg[s] : 0;
+    for (int s = (int)lane; s < 32; s += 64) S.fd[s] = s < 30 ? hg[DMX_DIST0 + s] : 0;
+    for (int k = (int)lane; k < DMX_HDR_WORDS; k += 64) S.hdr[k] = 0;
+    __syncthreads();
+    if (lane == 0) S.fll[256] = 1;  // end of block
+    __syncthreads();
+
+    // lit/len and distance code lengths
+    for (int s = (int)lane; s < 286; s += 64) S.H.f[s] = S.fll[s];
+    __syncthreads();
+    huff_lengths(S.H, 286, 15, S.lll, lane);
+    for (int s = (int)lane; s < 30; s += 64) S.H.f[s] = S.fd[s];
+    __syncthreads();
+    huff_lengths(S.H, 30, 15, S.ld, lane);
+    if (lane == 0) {
+        int any = 0;
+        for (int s = 0; s < 30; s++) any |= S.ld[s];
+        if (!any) { S.ld[0] = 1; S.ld[1] = 1; }   // no matches: two 1-bit codes
+        int hl = 286;
+        while (hl > 257 && S.lll[hl - 1] == 0) hl--;
+        int hd = 30;
+        while (hd > 1 && S.ld[hd - 1] == 0) hd--;
+        S.hlit = hl;
+        S.hdist = hd;
+        // RLE of the concatenated length sequence
+        for (int k = 0; k < 20; k++) S.fcl[k] = 0;
+        const int ns = hl + hd;
+        int i = 0, rn = 0;
+#define SEQ(k) ((k) < hl ? S.lll[(k)] : S.ld[(k) - hl])
+#define EMIT(SY, EX) do { S.rle_sym[rn] = (uint8_t)(SY); S.rle_ext[rn] = (uint8_t)(EX); rn++; S.fcl[(SY)]++; } while (0)
+        while (i < ns) {
+            const int v = SEQ(i);
+            int run = 1;
+            while (i + run < ns && SEQ(i + run) == v) run++;
+            if (v == 0) {
+                int r = run;
+                while (r >= 11) { const int c = r < 138 ? r : 138; EMIT(18, c - 11); r -= c; }
+                if (r >= 3) { EMIT(17, r - 3); r = 0; }
+                while (r > 0) { EMIT(0, 0); r--; }
+            } else {
+                EMIT(v, 0);
+                int r = run - 1;
+                while (r >= 3) { const int c = r < 6 ? r : 6; EMIT(16, c - 3); r -= c; }
+                while (r > 0) { EMIT(v, 0); r--; }
+            }
+            i += run;
+        }
+#undef EMIT
+#undef SEQ
+        S.rle_n = rn;
+    }
+    __syncthreads();
+    for (int s = (int)lane; s < 19; s += 64) S.H.f[s] = S.fcl[s];
+    __syncthreads();
+    huff_lengths(S.H, 19, 7, S.lcl, lane);
+    if (lane == 0) {
+        int hc = 19;
+        while (hc > 4 && S.lcl[c_clorder[hc - 1]] == 0) hc--;
+        S.hclen = hc;
+    }
+    __syncthreads();
+
+    // exact costs
+    uint64_t dyn_body = 0, fix_body = 0, extra = 0;
+    for (int s = (int)lane; s < 286; s += 64) {
+        const uint64_t f = S.fll[s];
+        dyn_body += f * S.lll[s];
+        fix_body += f * fixed_len((uint32_t)s);
+        if (s >= 257) extra += f * len_eb_of_sym((uint32_t)s);
+    }
+    if (lane < 30) {
+        const uint64_t f = S.fd[lane];
+        dyn_body += f * S.ld[lane];
+        fix_body += f * 5;
+        extra += f * dist_eb_of_sym(lane);
+    }
+    uint64_t hdr_rle = 0;
+    for (int k = (int)lane; k < S.rle_n; k += 64) hdr_rle += S.lcl[S.rle_sym[k]] + c_cl_eb[S.rle_sym[k]];
+    dyn_body = wave_sum_u64(dyn_body);
+    fix_body = wave_sum_u64(fix_body);
+    extra = wave_sum_u64(extra);
+    hdr_rle = wave_sum_u64(hdr_rle);
+    const uint64_t dyn_hdr = 3 + 5 + 5 + 4 + 3 * (uint64_t)S.hclen + hdr_rle;
+    const uint64_t dyn_bits = dyn_hdr + dyn_body + extra;
+    const uint64_t fix_bits = 3 + fix_body + extra;
+    const uint64_t sto_bits = 3 + 7 + 32 + 8 * (uint64_t)bn;
+    uint32_t bt = 2;
+    uint64_t best = dyn_bits;
+    if (fix_bits <= best) { best = fix_bits; bt = 1; }
+    if (sto_bits < best) bt = 0;
+
+    // code table for the packer (fixed codes for BTYPE 1)
+    if (bt == 1) {
+        for (int s = (int)lane; s < 288; s += 64) S.lll[s] = (uint8_t)fixed_len((uint32_t)s);
+        for (int s = (int)lane; s < 30; s += 64) S.ld[s] = 5;
+        __syncthreads();
+    }
+    canon_codes(S.lll, 286, S.code, lane);
+    canon_codes(S.ld, 30, S.code + DMX_DIST0, lane);
+    uint32_t* cg = codes_g + (uint64_t)b * DMX_HIST;
+    for (int s = (int)lane; s < 316; s += 64) cg[s] = S.code[s];
+
+    // header bits
+    if (lane == 0) {
+        S.hdr_pos = 0;
+        hdr_put(S, final_bit | (bt << 1), 3);
+        if (bt == 2) {
+            hdr_put(S, (uint32_t)(S.hlit - 257), 5);
+            hdr_put(S, (uint32_t)(S.hdist - 1), 5);
+            hdr_put(S, (uint32_t)(S.hclen - 4), 4);
+            for (int k = 0; k < S.hclen; k++) hdr_put(S, S.lcl[c_clorder[k]], 3);
+        }
+    }
+    __syncthreads();
+    if (bt == 2) {
+        canon_codes(S.lcl, 19, S.code, lane);   // reuse: cl codes
+        if (lane == 0) {
+            for (int k = 0; k < S.rle_n; k++) {
+                const uint32_t sy = S.rle_sym[k], cw = S.code[sy];
+                hdr_put(S, cw & 0xFFFFu, cw >> 16);
+                hdr_put(S, S.rle_ext[k], c_cl_eb[sy]);
+            }
+        }
+        __syncthreads();
+    }
+    const uint32_t hbits = S.hdr_pos;
+    uint32_t* hgout = hdr_g + (uint64_t)b * DMX_HDR_WORDS;
+    for (uint32_t k = lane; k < (hbits + 31) / 32; k += 64) hgout[k] = S.hdr[k];
+    if (lane == 0) {
+        info[b].btype = bt;
+        info[b].hdr_bits = hbits;
+        info[b].body_bits = (bt == 2 ? dyn_body : fix_body) + extra;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// K3: block offsets (scan), Adler-32, framing
+// ------------------------------------------------------------------------------------
+
+// x -> s ? align8(x + a) + c : x + c   (stored blocks re-align; composable)
+struct Mono {
+    uint32_t s;
+    uint64_t a, c;
+};
+__device__ __forceinline__ uint64_t align8(uint64_t x) { return (x + 7) & ~7ull; }
+__device__ __forceinline__ Mono mcompose(const Mono& f, const Mono& g) {  // f first, then g
+    Mono r;
+    if (!g.s) { r.s = f.s; r.a = f.a; r.c = f.c + g.c; }
+    else if (!f.s) { r.s = 1; r.a = f.c + g.a; r.c = g.c; }
+    else { r.s = 1; r.a = f.a; r.c = align8(f.c + g.a) + g.c; }
+    return r;
+}
+__device__ __forceinline__ uint64_t mapply(const Mono& f, uint64_t x) { return f.s ? align8(x + f.a) + f.c : x + f.c; }
+__device__ __forceinline__ Mono mshfl_up(const Mono& v, int o) {
+    Mono r;
+    r.s = __shfl_up(v.s, o);
+    r.a = __shfl_up(v.a, o);
+    r.c = __shfl_up(v.c, o);
+    return r;
+}
+
+__device__ __forceinline__ void gor_bits(uint32_t* out32, uint64_t pos, uint32_t v, uint32_t nb) {
+    if (!nb) return;
+    const uint64_t w = pos >> 5;
+    const uint32_t sh = (uint32_t)(pos & 31);
+    atomicOr(&out32[w], v << sh);
+    if (sh + nb > 32) atomicOr(&out32[w + 1], v >> (32 - sh));
+}
+
+#define ST 1024
+#define ADL_MOD 65521u
+
+__global__ __launch_bounds__(ST) void dmx_scan_kernel(dmx_blkinfo* __restrict__ info, uint32_t nblk, uint64_t n,
+                                                      uint32_t sw, uint32_t flags, uint64_t out_cap,
+                                                      uint32_t* __restrict__ out32, dmx_result* __restrict__ res) {
+    __shared__ Mono wtot[ST / 64];
+    __shared__ Mono carry_s;
+    __shared__ uint64_t red[ST / 64][5];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t start = (flags & DMX_F_HEADER) ? 16 : 0;
+    if (tid == 0) { carry_s.s = 0; carry_s.a = 0; carry_s.c = 0; }
+    uint64_t adl_s1 = 0, adl_s2 = 0, ntok = 0, nsto = 0, nfix = 0;
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < nblk; c0 += ST) {
+        const uint32_t b = c0 + tid;
+        Mono e = {0, 0, 0};
+        dmx_blkinfo bi;
+        if (b < nblk) {
+            bi = info[b];
+            if (bi.btype == 0) { e.s = 1; e.a = 3; e.c = 32 + 8 * (uint64_t)bi.n; }
+            else { e.c = bi.hdr_bits + bi.body_bits; }
+            const uint64_t end_b = (uint64_t)b * sw + bi.n;
+            adl_s1 += bi.adl_s % ADL_MOD;
+            adl_s2 += (bi.adl_w % ADL_MOD + ((n - end_b) % ADL_MOD) * (bi.adl_s % ADL_MOD)) % ADL_MOD;
+            ntok += bi.ntok;
+            nsto += bi.btype == 0;
+            nfix += bi.btype == 1;
+        }
+        Mono x = e;  // inclusive scan in the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const Mono y = mshfl_up(x, o);
+            if (lane >= (uint32_t)o) x = mcompose(y, x);
+        }
+        if (lane == 63) wtot[wave] = x;
+        __syncthreads();
+        if (tid == 0) {   // exclusive prefix over waves, seeded with the carry
+            Mono acc = carry_s;
+            for (int w = 0; w < ST / 64; w++) {
+                const Mono t = wtot[w];
+                wtot[w] = acc;
+                acc = mcompose(acc, t);
+            }
+            carry_s = acc;
+        }
+        __syncthreads();
+        const Mono before = mshfl_up(x, 1);   // inclusive prefix of lane-1 (all lanes active)
+        if (b < nblk) {
+            const Mono excl_w = wtot[wave];
+            const Mono pre = (lane == 0) ? excl_w : mcompose(excl_w, before);
+            const uint64_t o = mapply(pre, start);
+            info[b].off_bits = o;
+            info[b].len_bits = mapply(e, o) - o;
+        }
+        __syncthreads();
+    }
+    // reductions
+    adl_s1 = wave_sum_u64(adl_s1 % ADL_MOD);
+    adl_s2 = wave_sum_u64(adl_s2 % ADL_MOD);
+    ntok = wave_sum_u64(ntok);
+    nsto = wave_sum_u64(nsto);
+    nfix = wave_sum_u64(nfix);
+    if (lane == 0) { red[wave][0] = adl_s1; red[wave][1] = adl_s2; red[wave][2] = ntok; red[wave][3] = nsto; red[wave][4] = nfix; }
+    __syncthreads();
+    __shared__ uint64_t s_end, s_T;
+    __shared__ uint32_t s_adler;
+    __shared__ int32_t s_status;
+    if (tid == 0) {
+        uint64_t s1 = 0, s2 = 0, nt = 0, ns = 0, nf = 0;
+        for (int w = 0; w < ST / 64; w++) { s1 += red[w][0]; s2 += red[w][1]; nt += red[w][2]; ns += red[w][3]; nf += red[w][4]; }
+        s1 = (1 + s1) % ADL_MOD;
+        s2 = (n % ADL_MOD + s2) % ADL_MOD;
+        const uint32_t adler = (uint32_t)((s2 << 16) | s1);
+        uint64_t T = mapply(carry_s, start);
+        if (nblk == 0 && (flags & DMX_F_FINAL)) T = start + 10;   // empty input: fixed block, EOB only
+        uint64_t end = (flags & DMX_F_FINAL) ? align8(T) : (nblk == 0 ? align8(T) : align8(T + 3) + 32);
+        uint64_t out_len = end / 8 + ((flags & DMX_F_TRAILER) ? 4 : 0);
+        int32_t status = 0;
+        if (((out_len + 3) & ~3ull) > out_cap) status = -(int32_t)E_SZ;
+        res->out_len = out_len;
+        res->end_bits = T;
+        res->n = n;
+        res->ntokens = nt;
+        res->adler = adler;
+        res->status = status;
+        res->nblocks = nblk;
+        res->nstored = (uint32_t)ns;
+        res->nfixed = (uint32_t)nf;
+        res->ndynamic = nblk - (uint32_t)ns - (uint32_t)nf;
+        s_end = end;
+        s_T = T;
+        s_adler = adler;
+        s_status = status;
+    }
+    __syncthreads();
+    if (s_status) return;
+    // zero every word a block shares with a neighbour or with the framing
+    for (uint32_t b = tid; b < nblk; b += ST) {
+        const uint64_t o = info[b].off_bits, l = info[b].len_bits;
+        out32[o >> 5] = 0;
+        out32[(o + l - 1) >> 5] = 0;
+    }
+    const uint64_t T = s_T, end = s_end;
+    const uint64_t tail_end = end + ((flags & DMX_F_TRAILER) ? 32 : 0);
+    for (uint64_t w = (T >> 5) + tid; w < ((tail_end + 31) >> 5); w += ST) out32[w] = 0;
+    if (tid == 0 && start) out32[0] = 0;
+    __syncthreads();
+    if (tid == 0) {
+        if (flags & DMX_F_HEADER) gor_bits(out32, 0, 0x9C78u, 16);
+        if (nblk == 0 && (flags & DMX_F_FINAL)) gor_bits(out32, start, 3u, 3);  // BFINAL=1, BTYPE=01, EOB=0000000
+        if (!(flags & DMX_F_FINAL) && nblk > 0) gor_bits(out32, align8(T + 3) + 16, 0xFFFFu, 16);  // sync flush
+        if (flags & DMX_F_TRAILER) {
+            const uint32_t a = s_adler;
+            const uint32_t be = (a >> 24) | ((a >> 8) & 0xFF00u) | ((a << 8) & 0xFF0000u) | (a << 24);
+            gor_bits(out32, end, be, 32);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// K4: bit packing
+// ------------------------------------------------------------------------------------
+
+#define PT 256
+
+__device__ __forceinline__ void st_or64(uint32_t* st, uint32_t pos, uint64_t v, uint32_t nb) {
+    if (!nb) return;
+    const uint32_t w = pos >> 5, sh = pos & 31;
+    const uint64_t a = v << sh;
+    atomicOr(&st[w], (uint32_t)a);
+    if (sh + nb > 32) atomicOr(&st[w + 1], (uint32_t)(a >> 32));
+    if (sh + nb > 64) atomicOr(&st[w + 2], (uint32_t)(v >> (64 - sh)));
+}
+
+__global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict__ in, uint32_t sw,
+                                                      const uint32_t* __restrict__ tok_g, const uint32_t* __restrict__ codes_g,
+                                                      const uint32_t* __restrict__ hdr_g, const dmx_blkinfo* __restrict__ info,
+                                                      uint32_t nblk, uint32_t flags, uint32_t* __restrict__ out32,
+                                                      dmx_result* __restrict__ res) {
+    __shared__ uint32_t stage[DMX_STAGE_WORDS];
+    __shared__ uint32_t code[DMX_HIST];
+    __shared__ uint32_t wsum[PT / 64];
+    if (res->status) return;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t b = blockIdx.x;
+    const dmx_blkinfo bi = info[b];
+    const uint64_t O = bi.off_bits, Lb = bi.len_bits;
+    const uint32_t s0 = (uint32_t)(O & 31);
+    const uint32_t nwords = (uint32_t)((s0 + Lb + 31) >> 5);
+    const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1) ? 1u : 0u;
+    for (uint32_t k = tid; k < nwords; k += PT) stage[k] = 0;
+    for (uint32_t k = tid; k < 316; k += PT) code[k] = codes_g[(uint64_t)b * DMX_HIST + k];
+    __syncthreads();
+    if (bi.btype == 0) {
+        const uint8_t* d = in + (uint64_t)b * sw;
+        const uint32_t P = (s0 + 3 + 7) & ~7u;
+        if (tid == 0) {
+            st_or64(stage, s0, final_bit, 3);
+            st_or64(stage, P, (bi.n & 0xFFFFu) | ((~bi.n & 0xFFFFu) << 16), 32);
+        }
+        __syncthreads();
+        uint8_t* st8 = reinterpret_cast<uint8_t*>(stage) + ((P + 32) >> 3);
+        for (uint32_t k = tid; k < bi.n; k += PT) st8[k] = d[k];
+    } else {
+        const uint32_t* hg = hdr_g + (uint64_t)b * DMX_HDR_WORDS;
+        const uint32_t hb = bi.hdr_bits;
+        for (uint32_t k = tid; k < (hb + 31) / 32; k += PT) {
+            const uint32_t nb = (hb - 32 * k) < 32 ? (hb - 32 * k) : 32;
+            st_or64(stage, s0 + 32 * k, hg[k], nb);
+        }
+        const uint32_t* tb = tok_g + (uint64_t)b * DMX_BLK;
+        uint32_t pos = s0 + hb;
+        for (uint32_t c = 0; c < bi.ntok; c += PT) {
+            const uint32_t j = c + tid;
+            uint64_t v = 0;
+            uint32_t nb = 0;
+            if (j < bi.ntok) {
+                const uint32_t t = tb[j];
+                if ((t >> 9) == 0) {
+                    const uint32_t cw = code[t];
+                    v = cw & 0xFFFFu;
+                    nb = cw >> 16;
+                } else {
+                    uint32_t s, eb, ev;
+                    len_sym(t & 0x1FFu, s, eb, ev);
+                    uint32_t cw = code[s];
+                    v = (cw & 0xFFFFu) | ((uint64_t)ev << (cw >> 16));
+                    nb = (cw >> 16) + eb;
+                    dist_sym(t >> 9, s, eb, ev);
+                    cw = code[DMX_DIST0 + s];
+                    v |= ((uint64_t)(cw & 0xFFFFu) | ((uint64_t)ev << (cw >> 16))) << nb;
+                    nb += (cw >> 16) + eb;
+                }
+            }
+            uint32_t x = nb;   // exclusive scan of bit counts over the workgroup
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o);
+                if (lane >= (uint32_t)o) x += y;
+            }
+            if (lane == 63) wsum[wave] = x;
+            __syncthreads();
+            uint32_t wbase = 0, tot = 0;
+#pragma unroll
+            for (int w = 0; w < PT / 64; w++) {
+                const uint32_t t = wsum[w];
+                if ((uint32_t)w < wave) wbase += t;
+                tot += t;
+            }
+            st_or64(stage, pos + wbase + x - nb, v, nb);
+            pos += tot;
+            __syncthreads();
+        }
+        if (tid == 0) {
+            const uint32_t cw = code[256];
+            st_or64(stage, pos, cw & 0xFFFFu, cw >> 16);
+        }
+    }
+    __syncthreads();
+    const uint64_t gw0 = O >> 5;
+    const bool first_partial = s0 != 0;
+    const bool last_partial = ((s0 + Lb) & 31) != 0;
+    for (uint32_t k = tid; k < nwords; k += PT) {
+        const uint32_t v = stage[k];
+        if ((k == 0 && first_partial) || (k == nwords - 1 && last_partial)) atomicOr(&out32[gw0 + k], v);
+        else out32[gw0 + k] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// host side of the HIP layer (C ABI)
+// ------------------------------------------------------------------------------------
+
+#define DMX_EV_RING 32
+
+struct dmx_ctx {
+    int device;
+    hipStream_t stream;
+    uint64_t cap_blocks;
+    uint16_t* prev;   // cap_blocks * DMX_BLK (chains, then distances)
+    uint32_t* tok;    // cap_blocks * DMX_BLK
+    uint32_t* hist;   // cap_blocks * DMX_HIST
+    uint32_t* codes;  // cap_blocks * DMX_HIST
+    uint32_t* hdr;    // cap_blocks * DMX_HDR_WORDS
+    dmx_blkinfo* info;
+    dmx_result* res;
+    // last encode (introspection)
+    uint32_t last_nblk;
+    // host staging for dmx_encode_host
+    void* d_in;
+    uint64_t d_in_cap;
+    void* d_out;
+    uint64_t d_out_cap;
+    // timing: a ring of event sets so timed encodes never block the host
+    int timing;
+    hipEvent_t ev[DMX_EV_RING][6];
+    int ev_used[DMX_EV_RING];
+    uint32_t ev_next;
+    double stage_ms[5];
+    uint32_t stage_n;
+};
+
+static int hip_fail(hipError_t e, const char* what) {
+    if (e != hipSuccess) {
+        fprintf(stderr, "dmx: %s failed: %s\n", what, hipGetErrorString(e));
+        return 1;
+    }
+    return 0;
+}
+#define HIPCHK(x) do { if (hip_fail((x), #x)) return -(int)E_DEVICE; } while (0)
+
+extern "C" uint64_t dmx_max_compressed(uint64_t n, int32_t sw) {
+    if (sw <= 0 || sw > DMX_BLK) sw = DMX_BLK;
+    const uint64_t nblk = (n + (uint64_t)sw - 1) / (uint64_t)sw;
+    return ((n + 5 * nblk + 2 + 4 + 5 + 16) + 3) & ~3ull;
+}
+
+static void ctx_free_ws(dmx_ctx* c) {
+    if (c->prev) (void)hipFree(c->prev);
+    if (c->tok) (void)hipFree(c->tok);
+    if (c->hist) (void)hipFree(c->hist);
+    if (c->codes) (void)hipFree(c->codes);
+    if (c->hdr) (void)hipFree(c->hdr);
+    if (c->info) (void)hipFree(c->info);
+    c->prev = NULL; c->tok = NULL; c->hist = NULL; c->codes = NULL; c->hdr = NULL; c->info = NULL;
+    c->cap_blocks = 0;
+}
+
+static int ctx_reserve(dmx_ctx* c, uint64_t nblk) {
+    if (nblk <= c->cap_blocks) return 0;
+    ctx_free_ws(c);
+    const uint64_t cb = nblk < 1 ? 1 : nblk;
+    HIPCHK(hipMalloc(&c->prev, cb * DMX_BLK * sizeof(uint16_t)));
+    HIPCHK(hipMalloc(&c->tok, cb * DMX_BLK * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&c->hist, cb * DMX_HIST * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&c->codes, cb * DMX_HIST * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&c->hdr, cb * DMX_HDR_WORDS * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&c->info, cb * sizeof(dmx_blkinfo)));
+    c->cap_blocks = cb;
+    return 0;
+}
+
+extern "C" int dmx_ctx_create(int device, uint64_t max_input, dmx_ctx** out) {
+    *out = NULL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        fprintf(stderr, "dmx: no HIP device available (the encoder has no CPU fallback)\n");
+        return -(int)E_NEXIST;
+    }
+    if (device < 0 || device >= ndev) return -(int)E_RANGE;
+    HIPCHK(hipSetDevice(device));
+    dmx_ctx* c = (dmx_ctx*)calloc(1, sizeof(dmx_ctx));
+    if (!c) return -(int)E_MALLOC;
+    c->device = device;
+    if (hip_fail(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate")) { free(c); return -(int)E_DEVICE; }
+    if (hip_fail(hipMalloc(&c->res, sizeof(dmx_result)), "hipMalloc(res)")) { free(c); return -(int)E_DEVICE; }
+    for (int j = 0; j < DMX_EV_RING; j++)
+        for (int k = 0; k < 6; k++) (void)hipEventCreate(&c->ev[j][k]);
+    const uint64_t nb = (max_input + DMX_BLK - 1) / DMX_BLK;
+    const int r = ctx_reserve(c, nb);
+    if (r) { dmx_ctx_destroy(c); return r; }
+    *out = c;
+    return 0;
+}
+
+extern "C" int dmx_ctx_reserve(dmx_ctx* c, uint64_t n, int32_t sw) {
+    if (!c) return -(int)E_INVAL;
+    if (sw == 0) sw = DMX_BLK;
+    if (sw < 1 || sw > DMX_BLK) return -(int)E_RANGE;
+    HIPCHK(hipSetDevice(c->device));
+    const uint64_t nblk = (n + (uint64_t)sw - 1) / (uint64_t)sw;
+    if (nblk <= c->cap_blocks) return 0;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipDeviceSynchronize());
+    return ctx_reserve(c, nblk);
+}
+
+extern "C" void dmx_ctx_destroy(dmx_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    ctx_free_ws(c);
+    if (c->res) (void)hipFree(c->res);
+    if (c->d_in) (void)hipFree(c->d_in);
+    if (c->d_out) (void)hipFree(c->d_out);
+    for (int j = 0; j < DMX_EV_RING; j++)
+        for (int k = 0; k < 6; k++) if (c->ev[j][k]) (void)hipEventDestroy(c->ev[j][k]);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    free(c);
+}
+
+static void ctx_collect_set(dmx_ctx* c, int j) {
+    if (!c->ev_used[j]) return;
+    c->ev_used[j] = 0;
+    if (hipEventSynchronize(c->ev[j][5]) != hipSuccess) return;
+    for (int k = 0; k < 5; k++) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, c->ev[j][k], c->ev[j][k + 1]) == hipSuccess) c->stage_ms[k] += ms;
+    }
+    c->stage_n++;
+}
+
+extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* d_out, uint64_t out_cap,
+                                const dmx_opts* opts, void* stream) {
+    if (!c || !d_out || (!d_in && n)) return -(int)E_INVAL;
+    dmx_opts o = {0, 0, DMX_ZLIB, 0};
+    if (opts) o = *opts;
+    if (o.sw == 0) o.sw = DMX_BLK;
+    if (o.sw < 1 || o.sw > DMX_BLK) return -(int)E_RANGE;
+    if (o.max_chain < 0) return -(int)E_RANGE;
+    if ((reinterpret_cast<uintptr_t>(d_out) & 3) != 0) return -(int)E_INVAL;
+    const uint64_t nblk64 = (n + (uint64_t)o.sw - 1) / (uint64_t)o.sw;
+    if (nblk64 > c->cap_blocks || nblk64 > 0x7FFFFFFFull) return -(int)E_SZ;
+    const uint32_t nblk = (uint32_t)nblk64;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipEvent_t* ev = NULL;
+    if (c->timing) {
+        const int j = (int)(c->ev_next++ % DMX_EV_RING);
+        ctx_collect_set(c, j);
+        ev = c->ev[j];
+        c->ev_used[j] = 1;
+        (void)hipEventRecord(ev[0], s);
+    }
+    if (nblk) {
+        hipLaunchKernelGGL(dmx_chain_kernel, dim3(nblk), dim3(64), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw, c->prev);
+        if (ev) (void)hipEventRecord(ev[1], s);
+        hipLaunchKernelGGL(dmx_match_kernel, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw,
+                           o.max_chain, c->prev, c->tok, c->hist, c->info);
+        if (ev) (void)hipEventRecord(ev[2], s);
+        hipLaunchKernelGGL(dmx_huff_kernel, dim3(nblk), dim3(64), 0, s, c->hist, c->info, c->codes, c->hdr, nblk, o.flags);
+        if (ev) (void)hipEventRecord(ev[3], s);
+    } else if (ev) {
+        (void)hipEventRecord(ev[1], s);
+        (void)hipEventRecord(ev[2], s);
+        (void)hipEventRecord(ev[3], s);
+    }
+    hipLaunchKernelGGL(dmx_scan_kernel, dim3(1), dim3(ST), 0, s, c->info, nblk, n, (uint32_t)o.sw, o.flags, out_cap,
+                       (uint32_t*)d_out, c->res);
+    if (ev) (void)hipEventRecord(ev[4], s);
+    if (nblk)
+        hipLaunchKernelGGL(dmx_pack_kernel, dim3(nblk), dim3(PT), 0, s, (const uint8_t*)d_in, (uint32_t)o.sw, c->tok,
+                           c->codes, c->hdr, c->info, nblk, o.flags, (uint32_t*)d_out, c->res);
+    if (ev) (void)hipEventRecord(ev[5], s);
+    HIPCHK(hipGetLastError());
+    c->last_nblk = nblk;
+    return 0;
+}
+
+extern "C" int dmx_encode_result(dmx_ctx* c, dmx_result* r, void* stream) {
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(hipMemcpyAsync(r, c->res, sizeof(dmx_result), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
+extern "C" int dmx_ctx_set_timing(dmx_ctx* c, int enable) {
+    (void)hipSetDevice(c->device);
+    for (int j = 0; j < DMX_EV_RING; j++) c->ev_used[j] = 0;
+    c->timing = enable;
+    for (int k = 0; k < 5; k++) c->stage_ms[k] = 0;
+    c->stage_n = 0;
+    return 0;
+}
+
+extern "C" int dmx_ctx_stage_times(dmx_ctx* c, double* ms5, uint32_t* count) {
+    (void)hipSetDevice(c->device);
+    for (int j = 0; j < DMX_EV_RING; j++) ctx_collect_set(c, j);
+    for (int k = 0; k < 5; k++) ms5[k] = c->stage_n ? c->stage_ms[k] / c->stage_n : 0.0;
+    *count = c->stage_n;
+    return 0;
+}
+
+extern "C" int dmx_last_blocks(dmx_ctx* c, uint32_t* ntok, uint8_t* btype, uint32_t* hdr_bits, uint32_t cap) {
+    const uint32_t nb = c->last_nblk < cap ? c->last_nblk : cap;
+    if (!nb) return 0;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipDeviceSynchronize());
+    dmx_blkinfo* h = (dmx_blkinfo*)malloc(sizeof(dmx_blkinfo) * nb);
+    if (!h) return -(int)E_MALLOC;
+    if (hip_fail(hipMemcpy(h, c->info, sizeof(dmx_blkinfo) * nb, hipMemcpyDeviceToHost), "hipMemcpy")) { free(h); return -(int)E_DEVICE; }
+    for (uint32_t b = 0; b < nb; b++) {
+        if (ntok) ntok[b] = h[b].ntok;
+        if (btype) btype[b] = (uint8_t)h[b].btype;
+        if (hdr_bits) hdr_bits[b] = h[b].hdr_bits;
+    }
+    free(h);
+    return (int)nb;
+}
+
+extern "C" int dmx_last_tokens(dmx_ctx* c, uint32_t blk, uint32_t* tok, uint32_t cap) {
+    if (blk >= c->last_nblk) return -(int)E_RANGE;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipDeviceSynchronize());
+    dmx_blkinfo bi;
+    HIPCHK(hipMemcpy(&bi, c->info + blk, sizeof(bi), hipMemcpyDeviceToHost));
+    const uint32_t nt = bi.ntok < cap ? bi.ntok : cap;
+    if (nt) HIPCHK(hipMemcpy(tok, c->tok + (uint64_t)blk * DMX_BLK, nt * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return (int)bi.ntok;
+}
+
+extern "C" int dmx_last_code_lengths(dmx_ctx* c, uint32_t blk, uint8_t* lens316) {
+    if (blk >= c->last_nblk) return -(int)E_RANGE;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipDeviceSynchronize());
+    uint32_t cw[316];
+    HIPCHK(hipMemcpy(cw, c->codes + (uint64_t)blk * DMX_HIST, sizeof(cw), hipMemcpyDeviceToHost));
+    for (int s = 0; s < 316; s++) lens316[s] = (uint8_t)(cw[s] >> 16);
+    return 0;
+}
+
+// --- host-buffer convenience on a cached context per device ---
+
+#include <pthread.h>
+static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
+static dmx_ctx* g_ctx[64];
+
+extern "C" dmx_ctx* dmx_cached_ctx(int device, uint64_t max_input, int* err) {
+    *err = 0;
+    if (device < 0 || device >= 64) { *err = -(int)E_RANGE; return NULL; }
+    if (!g_ctx[device]) {
+        int r = dmx_ctx_create(device, max_input, &g_ctx[device]);
+        if (r) { *err = r; return NULL; }
+    }
+    return g_ctx[device];
+}
+
+static int ensure_buf(void** p, uint64_t* cap, uint64_t need) {
+    if (*cap >= need && *p) return 0;
+    if (*p) (void)hipFree(*p);
+    *p = NULL;
+    *cap = 0;
+    HIPCHK(hipMalloc(p, need ? need : 16));
+    *cap = need;
+    return 0;
+}
+
+extern "C" int dmx_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t out_cap, uint64_t* out_len,
+                               const dmx_opts* opts) {
+    dmx_opts o = {0, 0, DMX_ZLIB, 0};
+    if (opts) o = *opts;
+    if (o.sw == 0) o.sw = DMX_BLK;
+    if (o.sw < 1 || o.sw > DMX_BLK) return -(int)E_RANGE;
+    const char* dev_s = getenv("DMX_DEVICE");
+    const int dev = dev_s ? atoi(dev_s) : 0;
+    pthread_mutex_lock(&g_mu);
+    int err = 0;
+    dmx_ctx* c = dmx_cached_ctx(dev, n, &err);
+    int r = err;
+    if (!r) {
+        const uint64_t nblk = (n + (uint64_t)o.sw - 1) / (uint64_t)o.sw;
+        r = ctx_reserve(c, nblk);
+    }
+    const uint64_t dcap = dmx_max_compressed(n, o.sw);
+    if (!r) r = ensure_buf(&c->d_in, &c->d_in_cap, n + 16);
+    if (!r) r = ensure_buf(&c->d_out, &c->d_out_cap, dcap);
+    if (!r && hip_fail(hipSetDevice(c->device), "hipSetDevice")) r = -(int)E_DEVICE;
+    if (!r && n && hip_fail(hipMemcpyAsync(c->d_in, in, n, hipMemcpyHostToDevice, c->stream), "H2D")) r = -(int)E_DEVICE;
+    if (!r) r = dmx_encode_async(c, c->d_in, n, c->d_out, c->d_out_cap, &o, NULL);
+    dmx_result res;
+    if (!r) r = dmx_encode_result(c, &res, NULL);
+    if (!r && res.status) r = res.status;
+    if (!r && res.out_len > out_cap) r = -(int)E_SZ;
+    if (!r && hip_fail(hipMemcpy(out, c->d_out, res.out_len, hipMemcpyDeviceToHost), "D2H")) r = -(int)E_DEVICE;
+    if (!r) *out_len = res.out_len;
+    pthread_mutex_unlock(&g_mu);
+    return r;
+}

@@ -1,0 +1,185 @@
+/*
+ * dmx.h -- C-ABI of libdmx, the MI355X-native DEFLATE encoder.
+ *
+ * Part 1 is the drop-in boundary: the exact entry points of the reference's public
+ * codec API, src/include/deflate_ext.h of mparker97/deflate_compression, so a C
+ * caller of the reference links against libdmx.so unchanged.
+ * Part 2 is the device layer those entry points call: device-resident buffers,
+ * explicit HIP streams, no allocation inside an encode (graph-capturable).
+ *
+ * All signatures are plain C types; no torch types cross this boundary.
+ */
+#ifndef DMX_H
+#define DMX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ======================= Part 1: reference API (deflate_ext.h) ======================= */
+
+/* deflate_ext.h:6 -- deflate_decompress option: append a '\0' after the output */
+#define DEFLATE_NULLTERM 1
+
+/* deflate_ext.h:8 -- sliding-window index / window size type */
+typedef unsigned short swi;
+
+/* globals.h:42-46 -- byte string with explicit length */
+struct string_len {
+    unsigned char* str;
+    size_t len;
+};
+
+/* deflate_ext.h:10-14 -- opaque compressor state + spawn/init/deinit.
+ * Replaces struct deflate_compr (deflate_compress.c:69-81) and SPAWNABLE
+ * (globals.h:20-29).  init never longjmps; errors surface from deflate_compress. */
+typedef struct deflate_compr deflate_compr_t;
+deflate_compr_t* spawn_deflate_compr_t(void);
+void deflate_compr_init(deflate_compr_t* com, int fd_in, int fd_out, int fd_stats, swi sw);
+void deflate_compr_deinit(deflate_compr_t* com);
+
+/* deflate_ext.h:17, impl deflate_compress.c:362-376.
+ * Reads fd_in to EOF, writes a zlib stream (RFC 1950/1951) to fd_out, and if
+ * fd_stats >= 0 one 24-byte struct compress_stats per token.  sw = block size /
+ * window (1..32768; 0 means 32768).  ops is unused (as in the reference).
+ * The parse is the reference's: exhaustive hash-chain search, greedy, longest
+ * match >= 3, ties to the nearest (DMX_MAX_CHAIN=K in the environment selects the
+ * bounded fast mode).  Returns 0, or -E_* on error (the reference returned
+ * nothing).  The encode runs on the MI355X (device DMX_DEVICE, default 0); there is
+ * no CPU fallback: without a usable GPU it fails with -E_NEXIST. */
+int deflate_compress(int fd_in, int fd_out, int fd_stats, swi sw, int ops);
+
+/* deflate_ext.h:16, impl deflate_decompress.c:371-409 (that implementation does not
+ * compile; this one is a fresh RFC 1950/1951 inflate).
+ * Inflates compr_dat (zlib stream) into a malloc'd decompr_dat->str that the
+ * caller frees.  ops & DEFLATE_NULLTERM appends a '\0' (not counted in len).
+ * Returns 0 or -E_*. */
+int deflate_decompress(struct string_len* decompr_dat, struct string_len* compr_dat, int ops);
+
+/* deflate_ext.h:19-31 -- per-token record written to fd_stats.
+ * bytes = 1 + input offset of the token; ll/d = literal byte (d == 0) or length/
+ * distance.  The reference's *_bits fields were adaptive-Huffman running
+ * estimates; here they are the exact costs of the block the token is in:
+ * tree_bits = header bits of the block, ll_bits / d_bits = running lit/len and
+ * distance bits (codes + extra bits) inside the block up to this token. */
+struct compress_stats {
+    int bytes;
+    int tree_bits;
+    int ll_bits;
+    int d_bits;
+    int ll;
+    int d;
+};
+
+/* Error codes: global_errors.h:64-75 and deflate_errors.h:132-147 (returned negated). */
+#define E_LEN 1
+#define E_MALLOC 2
+#define E_FORK 3
+#define E_PIPE 4
+#define E_CRC 5
+#define E_SZ 6
+#define E_EXIST 7
+#define E_NEXIST 8
+#define E_NONULL 9
+#define E_RANGE 10
+#define E_INVAL 11
+#define E_RESERV 12
+#define DEFLATE_ERROR_MASK (1U << 24)
+#define E_HUFAMB (DEFLATE_ERROR_MASK + 1)
+#define E_HUFINV (DEFLATE_ERROR_MASK + 2)
+#define E_HUFVAL (DEFLATE_ERROR_MASK + 3)
+#define E_HUFDIS (DEFLATE_ERROR_MASK + 4)
+#define E_ZADL32 (DEFLATE_ERROR_MASK + 5)
+#define E_ZHEAD (DEFLATE_ERROR_MASK + 6)
+#define E_ZFCHCK (DEFLATE_ERROR_MASK + 7)
+#define E_ZCMPMT (DEFLATE_ERROR_MASK + 8)
+#define E_ZSLWIN (DEFLATE_ERROR_MASK + 9)
+#define E_ZPDICT (DEFLATE_ERROR_MASK + 10)
+#define E_ZBSZ (DEFLATE_ERROR_MASK + 11)
+#define E_ZNLEN (DEFLATE_ERROR_MASK + 12)
+#define E_ZINV (DEFLATE_ERROR_MASK + 13)
+#define E_ZBTYPE (DEFLATE_ERROR_MASK + 14)
+/* dmx additions (outside both reference ranges) */
+#define E_DEVICE (DEFLATE_ERROR_MASK + 64) /* HIP runtime / launch failure */
+
+/* ============================ Part 2: device layer ============================ */
+
+/* Stream framing flags (dmx_opts.flags). DMX_ZLIB = a complete zlib stream. */
+#define DMX_F_HEADER 1u  /* write the 2-byte zlib header 78 9C */
+#define DMX_F_TRAILER 2u /* write the Adler-32 trailer (big-endian) */
+#define DMX_F_FINAL 4u   /* last block carries BFINAL; otherwise the stream ends with
+                            an empty stored block (sync flush) so it is byte-aligned
+                            and another shard can be appended */
+#define DMX_ZLIB (DMX_F_HEADER | DMX_F_TRAILER | DMX_F_FINAL)
+
+typedef struct {
+    int32_t sw;        /* block size 1..32768 (0 = 32768) */
+    int32_t max_chain; /* 0 = exhaustive (reference semantics); K > 0 = the K newest chain entries */
+    uint32_t flags;    /* DMX_F_* */
+    int32_t reserved;
+} dmx_opts;
+
+/* Result of one encode, filled on the device, fetched by dmx_encode_result(). */
+typedef struct {
+    uint64_t out_len;   /* bytes written to d_out */
+    uint64_t end_bits;  /* bit position after the last block (before flush/trailer) */
+    uint64_t n;         /* input bytes */
+    uint64_t ntokens;   /* tokens over all blocks */
+    uint32_t adler;     /* Adler-32 of this input (RFC 1950 §8.2) */
+    int32_t status;     /* 0 or -E_* */
+    uint32_t nblocks;
+    uint32_t nstored, nfixed, ndynamic;
+    uint32_t pad[2];
+} dmx_result;
+
+typedef struct dmx_ctx dmx_ctx;
+
+/* Allocate a device context (own HIP stream + workspace) for inputs up to max_input. */
+int dmx_ctx_create(int device, uint64_t max_input, dmx_ctx** out);
+void dmx_ctx_destroy(dmx_ctx* ctx);
+/* Grow the workspace (synchronising) so that n bytes with block size sw fit. */
+int dmx_ctx_reserve(dmx_ctx* ctx, uint64_t n, int32_t sw);
+/* Worst-case output bytes for n input bytes with block size sw. */
+uint64_t dmx_max_compressed(uint64_t n, int32_t sw);
+
+/* Enqueue the whole encode of device buffer d_in[0..n) into d_out (capacity
+ * out_cap) on `stream` (hipStream_t; NULL = the context's stream).  No host
+ * synchronisation, no allocation.  Returns 0 or -E_* for argument errors. */
+int dmx_encode_async(dmx_ctx* ctx, const void* d_in, uint64_t n, void* d_out, uint64_t out_cap,
+                     const dmx_opts* opts, void* stream);
+/* Wait for the last encode on `stream` and copy its dmx_result to the host. */
+int dmx_encode_result(dmx_ctx* ctx, dmx_result* r, void* stream);
+
+/* Host-buffer convenience (H2D, encode, D2H) on a cached per-device context.
+ * *out_len receives the stream length; out must hold dmx_max_compressed(n, sw). */
+int dmx_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t out_cap,
+                    uint64_t* out_len, const dmx_opts* opts);
+
+/* Introspection of the last encode of ctx (tests / fd_stats): per-block token
+ * counts and the token stream (t = byte | dist << 9 | len),
+ * per-block BTYPE, and the lit/len + distance code lengths (286 + 30 per block). */
+int dmx_last_blocks(dmx_ctx* ctx, uint32_t* ntok, uint8_t* btype, uint32_t* hdr_bits,
+                    uint32_t nblk_cap);
+int dmx_last_tokens(dmx_ctx* ctx, uint32_t blk, uint32_t* tok, uint32_t cap);
+int dmx_last_code_lengths(dmx_ctx* ctx, uint32_t blk, uint8_t* lens316);
+
+/* Per-kernel HIP-event timing of subsequent encodes on the context's launches
+ * (bench): enable, then read the mean milliseconds per launch of each stage
+ * {chain, match, huff, scan, pack} and the number of timed launches. */
+int dmx_ctx_set_timing(dmx_ctx* ctx, int enable);
+int dmx_ctx_stage_times(dmx_ctx* ctx, double* ms5, uint32_t* count);
+
+/* Adler-32 combine (RFC 1950 math): adler of A||B from adler(A), adler(B), len(B). */
+uint32_t dmx_adler32_combine(uint32_t a, uint32_t b, uint64_t len_b);
+
+/* Seeded synthetic inputs for the bench/tests (host, deterministic). */
+void dmx_gen_text(uint8_t* buf, uint64_t n, uint64_t seed);    /* enwik-style wiki text */
+void dmx_gen_random(uint8_t* buf, uint64_t n, uint64_t seed);  /* splitmix64 bytes */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DMX_H */

@@ -1,0 +1,207 @@
+"""HIP path vs the CPU oracle (and the reference's golden tokens) on the MI355X.
+
+Bar: bit-exact.  Token streams equal the reference's (tests/golden, exhaustive
+mode); compressed bytes equal the oracle's stream byte for byte; every stream
+inflates to the input with zlib and with our own deflate_decompress.
+"""
+import hashlib
+import json
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import deflate_compression_amd as D  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+MAN = json.load(open(os.path.join(GOLD, "manifest.json")))
+
+
+@pytest.fixture(scope="module")
+def enc():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    e = D.Encoder(0, 8 << 20)
+    yield e
+    e.close()
+
+
+def check_stream(z: bytes, data: bytes):
+    assert zlib.decompress(z) == data
+    assert D.deflate_decompress(z) == data
+
+
+def test_golden_tokens_exact(enc, golden_cases, golden_tokens):
+    """Per block: GPU tokens == the reference encoder's tokens; bytes == oracle bytes."""
+    for name, data in golden_cases.items():
+        z, r = enc.compress_bytes(data)
+        assert r.nblocks == 1
+        t = enc.tokens(0)
+        assert np.array_equal(t, golden_tokens[name]), name
+        assert hashlib.sha256(t.astype("<u4").tobytes()).hexdigest() == MAN["cases"][name]["tokens_sha256"]
+        assert z == O.compress(data), name
+        check_stream(z, data)
+
+
+def test_code_lengths_match_oracle(enc, golden_cases):
+    for name in ("bee0", "alldist", "px_sunrise_a", "abcd32k", "zeros32k"):
+        data = golden_cases[name]
+        enc.compress_bytes(data)
+        bt, costs, lll, ld = O.plan(O.parse_block(data), len(data))
+        _, gbt, _ = enc.blocks(1)
+        assert int(gbt[0]) == bt, name
+        if bt == 2:
+            ln = enc.code_lengths(0)
+            assert np.array_equal(ln[:286], lll) and np.array_equal(ln[286:], ld), name
+
+
+@pytest.mark.parametrize("kind,n", [("bee", 57641), ("text", 1 << 20), ("zeros", 1 << 20), ("random", 300000),
+                                    ("text", 3 * 32768 + 17), ("mixed", 400000)])
+def test_multiblock_stream_identical(enc, golden_cases, kind, n):
+    if kind == "bee":
+        data = golden_cases["bee0"] + golden_cases["bee1"]
+    elif kind == "text":
+        data = D.gen_text(n, 0xE5818).tobytes()
+    elif kind == "zeros":
+        data = bytes(n)
+    elif kind == "random":
+        data = D.gen_random(n, 0x5EED).tobytes()
+    else:
+        a = D.gen_text(n, 7)
+        a[100000:150000] = 0
+        a[200000:260000] = D.gen_random(60000, 9)
+        data = a.tobytes()
+    z, r = enc.compress_bytes(data)
+    zo = O.compress(data)
+    assert z == zo
+    assert r.adler == zlib.adler32(data)
+    check_stream(z, data)
+
+
+def test_config_c1_size(enc, golden_cases):
+    bee = golden_cases["bee0"] + golden_cases["bee1"]
+    z, _ = enc.compress_bytes(bee)
+    assert len(z) == 24895   # S_ref of C1: 0 % size penalty
+
+
+def test_config_c2_zeros(enc):
+    """C2: 1 MiB of zeros = 32 blocks: literal, 127 x (258, 1), literal/short per block."""
+    data = bytes(1 << 20)
+    z, r = enc.compress_bytes(data)
+    assert r.nblocks == 32
+    for b in (0, 31):
+        t = enc.tokens(b)
+        assert np.array_equal(t, O.parse_block(data[:32768]))
+    check_stream(z, data)
+    assert len(z) <= 1.02 * 1466
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 16, 64])
+def test_bounded_chain_parity(enc, k):
+    data = D.gen_text(300000, 11).tobytes()
+    z, _ = enc.compress_bytes(data, max_chain=k)
+    assert z == O.compress(data, max_chain=k)
+    check_stream(z, data)
+
+
+@pytest.mark.parametrize("sw", [1, 2, 3, 64, 1000, 4095, 4096, 32767, 32768])
+def test_window_sizes(enc, sw):
+    data = D.gen_text(70000 if sw >= 64 else 3000, 5).tobytes()
+    z, _ = enc.compress_bytes(data, sw=sw)
+    assert z == O.compress(data, sw=sw)
+    check_stream(z, data)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 4, 5, 63, 64, 65, 257, 258, 259, 32766, 32767, 32768, 32769, 65541])
+def test_edge_sizes(enc, golden_cases, n):
+    base = (golden_cases["bee0"] + golden_cases["bee1"]) * 2
+    data = base[:n]
+    z, _ = enc.compress_bytes(data)
+    assert z == O.compress(data)
+    check_stream(z, data)
+
+
+def test_runs_and_periodic(enc):
+    rng = np.random.default_rng(3)
+    parts = []
+    for _ in range(200):
+        parts.append(bytes([int(rng.integers(0, 256))]) * int(rng.integers(1, 700)))
+        parts.append((b"xyz" * 200)[: int(rng.integers(1, 500))])
+    data = b"".join(parts)
+    z, _ = enc.compress_bytes(data)
+    assert z == O.compress(data)
+    check_stream(z, data)
+
+
+def test_shards_stitch(enc):
+    """Multi-GPU shard framing: raw shards ending in a sync flush, concatenated,
+    header on the first, BFINAL on the last, Adler combined on the host."""
+    data = D.gen_text(5 * 32768 + 999, 21).tobytes()
+    cut = [0, 2 * 32768, 4 * 32768, len(data)]
+    pieces, adl = [], None
+    for i in range(3):
+        part = data[cut[i]:cut[i + 1]]
+        fl = (D.DMX_F_HEADER if i == 0 else 0) | (D.DMX_F_FINAL if i == 2 else 0)
+        z, r = enc.compress_bytes(part, flags=fl)
+        pieces.append(z)
+        adl = r.adler if adl is None else D.adler32_combine(adl, r.adler, len(part))
+    stream = b"".join(pieces) + adl.to_bytes(4, "big")
+    check_stream(stream, data)
+    assert adl == zlib.adler32(data)
+
+
+def test_raw_deflate_flags(enc):
+    data = D.gen_text(100000, 4).tobytes()
+    z, _ = enc.compress_bytes(data, flags=D.DMX_F_FINAL)
+    assert zlib.decompressobj(-15).decompress(z) == data
+    assert zlib.decompress(b"\x78\x9c" + z + zlib.adler32(data).to_bytes(4, "big")) == data
+
+
+def test_fd_api_and_stats(tmp_path, golden_cases):
+    """deflate_compress(fd_in, fd_out, fd_stats, sw, ops) drop-in: file in, zlib out,
+    one compress_stats record per token; the check_lld replay contract on the records."""
+    data = golden_cases["bee0"] + golden_cases["bee1"]
+    fi, fo, fs = tmp_path / "in", tmp_path / "out", tmp_path / "st"
+    fi.write_bytes(data)
+    with open(fi, "rb") as a, open(fo, "wb") as b, open(fs, "wb") as c:
+        assert D.deflate_compress(a.fileno(), b.fileno(), c.fileno(), 32768, 0) == 0
+    z = fo.read_bytes()
+    assert z == O.compress(data)
+    st = np.frombuffer(fs.read_bytes(), dtype="<i4").reshape(-1, 6)
+    toks = np.concatenate(O.parse(data))
+    assert st.shape[0] == toks.size
+    ll, d = st[:, 4].astype(np.uint32), st[:, 5].astype(np.uint32)
+    rt = np.where(d == 0, ll, (d << 9) | ll).astype(np.uint32)
+    assert np.array_equal(rt, toks)
+    # bytes = 1 + token start offset (deflate_compress.c:235, :313)
+    assert st[0, 0] == 1 and st[1, 0] == 2
+    # replay block by block (tests/check_lld.c:20-39)
+    assert O.replay(rt[: O.parse_block(data[:32768]).size]) == data[:32768]
+
+
+def test_fd_api_errors(tmp_path):
+    fi = tmp_path / "in"
+    fi.write_bytes(b"abc")
+    with open(fi, "rb") as a:
+        assert D.deflate_compress(a.fileno(), -1, -1, 40000 & 0xFFFF, 0) == -D.E["E_RANGE"]
+
+
+def test_c3_scale_roundtrip(enc):
+    """C3 size (100 000 000 B of enwik-style text): size-independent properties."""
+    n = 100_000_000
+    a = D.gen_text(n, 0xE5818)
+    t = torch.from_numpy(a).cuda()
+    enc.reserve(n)
+    out, r = enc.compress_tensor(t)
+    z = out.cpu().numpy().tobytes()
+    assert r.nblocks == 3052 and r.adler == zlib.adler32(a)
+    assert zlib.decompress(z) == a.tobytes()
+    # bytes of a few blocks equal the oracle's block encoding (first, middle, last)
+    assert 0.3 < len(z) / n < 0.5
+    for b in (0, 1526, 3051):
+        blk = a[b * 32768:(b + 1) * 32768].tobytes()
+        assert np.array_equal(enc.tokens(b), O.parse_block(blk))
