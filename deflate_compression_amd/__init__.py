@@ -108,6 +108,7 @@ def lib() -> ctypes.CDLL:
         "dmx_ctx_set_timing": ([vp, ctypes.c_int], ctypes.c_int),
         "dmx_ctx_stage_times": ([vp, ctypes.POINTER(ctypes.c_double), u32p], ctypes.c_int),
         "dmx_adler32_combine": ([u32, u32, u64], u32),
+        "dmx_debug_stamps": ([vp, ctypes.POINTER(u64), u32], ctypes.c_int),
         "dmx_gen_text": ([vp, u64, u64], None),
         "dmx_gen_random": ([vp, u64, u64], None),
     }
@@ -265,14 +266,23 @@ class Encoder:
                "dmx_last_code_lengths")
         return ln
 
+    def stamps(self, nblk: int):
+        """[nblk, 8] {build, search, walk+compaction cycles, tokens, search iterations, W1, W1-W3 cycles, 0}
+        (needs DMX_STAMPS=1)."""
+        import numpy as np
+        a = np.zeros((nblk, 8), np.uint64)
+        _check(self._L.dmx_debug_stamps(self._ctx, a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), nblk),
+               "dmx_debug_stamps")
+        return a
+
     def set_timing(self, on: bool) -> None:
         self._L.dmx_ctx_set_timing(self._ctx, 1 if on else 0)
 
     def stage_times(self):
-        ms = (ctypes.c_double * 5)()
+        ms = (ctypes.c_double * 6)()
         cnt = ctypes.c_uint32(0)
         self._L.dmx_ctx_stage_times(self._ctx, ms, ctypes.byref(cnt))
-        return dict(zip(["chain", "match", "huff", "scan", "pack"], list(ms))), cnt.value
+        return dict(zip(["chain", "match", "huff", "scan", "pack", "total"], list(ms))), cnt.value
 
     # -- host convenience on this context via torch tensors --
     def compress_tensor(self, t_in, stream=None, opts: Opts | None = None):

@@ -6,8 +6,8 @@
 #include <stdint.h>
 
 #define DMX_BLK 32768          /* max block size = LZ77 window (RFC 1951 §2) */
-#define DMX_HASH_SHIFT 18      /* 14-bit bucket: (trigram * 0x9E3779B1) >> 18 */
-#define DMX_NBUCKET 16384
+#define DMX_HASH_SHIFT 19      /* 13-bit bucket: (trigram * 0x9E3779B1) >> 19 */
+#define DMX_NBUCKET 8192
 #define DMX_NONE16 0xFFFFu     /* end of a hash chain */
 #define DMX_HIST 320           /* per-block histogram stride: 286 lit/len + 30 dist (+pad) */
 #define DMX_DIST0 286          /* first distance slot in hist / code tables */

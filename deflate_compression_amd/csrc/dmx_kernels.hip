@@ -2,13 +2,13 @@
 //
 // The input is cut into independent sw-byte blocks (sw <= 32768 = the window).
 // Per encode, five launches on one HIP stream:
-//   K1a dmx_chain_kernel  one wave per block: builds the hash chains prev[] of
-//                         deflate_compress.c:312-319 (every position at the head of
-//                         its bucket) in position order, 64 positions per step,
-//                         in-wave conflicts resolved with ballots; prev[] -> HBM.
-//   K1b dmx_match_kernel  one 1024-thread workgroup per block, block + chains in
-//                         LDS: the longest match of EVERY position (chain walk of
-//                         deflate_compress.c:243-264, newest first, strict >),
+//   K1  dmx_match_kernel  one 1024-thread workgroup per block, block staged in LDS.
+//                         Wave 0 builds the hash chains of deflate_compress.c:312-319
+//                         (every position at the head of its bucket) in LDS, 64
+//                         positions per step with ballots;
+//                         all 16 waves search the longest match of EVERY position
+//                         (chain walk of :243-264, newest first, strict >) with
+//                         lane-persistent work distribution,
 //                         then the greedy path 0 -> i + max(len,1) (:265-288) by
 //                         speculative 32-position segments + two fix-up levels,
 //                         token compaction (block scan) and lit/len + dist
@@ -84,59 +84,102 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 }
 
 // ------------------------------------------------------------------------------------
-// K1a: hash chains
+// K1a: bucket-sorted positions (one wave per block, several blocks per CU)
 // ------------------------------------------------------------------------------------
 
-__global__ __launch_bounds__(64) void dmx_chain_kernel(const uint8_t* __restrict__ in, uint64_t n,
-                                                       uint32_t sw, uint16_t* __restrict__ prev_g) {
-    __shared__ uint64_t head64[DMX_NBUCKET / 4];
-    uint16_t* head = reinterpret_cast<uint16_t*>(head64);
+// Trigram at p (bytes p, p+1, p+2 little-endian; zero past the block end).
+__device__ __forceinline__ uint32_t g_tri(const uint8_t* __restrict__ d, uint32_t p, uint32_t bn) {
+    if (p + 4 <= bn) {
+        uint32_t v;
+        __builtin_memcpy(&v, d + p, 4);   // unaligned global dword (fine for global memory)
+        return v & 0xFFFFFFu;
+    }
+    uint32_t v = 0;
+    for (uint32_t j = 0; j < 3; j++)
+        if (p + j < bn) v |= (uint32_t)d[p + j] << (8 * j);
+    return v;
+}
+
+// The reference's hash chains (deflate_compress.c:312-319: every position goes to the head
+// of its bucket's chain, so the chain of position i lists the earlier positions of its
+// bucket newest first) in array form: S = the block's positions sorted by (bucket,
+// position), built from rank(p) = number of earlier positions in p's bucket and the start
+// of every bucket: S[start(bucket(p)) + rank(p)] = p.  For the entry k of position p = S[k],
+// the chain of p is S[k-1], S[k-2], ..., S[start(bucket)] -- directly indexable, so the
+// match kernel can examine many candidates of one position in parallel.
+// Pass 1 (position order, 64 per step): rank = running count of the bucket + earlier lanes
+// of the step in the same bucket.  Lanes sharing a bucket are grouped by writing the lane
+// id into a byte scratch indexed by the bucket and reading it back (every member reads the
+// same representative): 6 ballots on that id, skipped when every lane reads itself back.
+// Output: rank(p) (u16, NONE for the last two positions, which have no trigram) and the
+// bucket starts (exclusive scan of the counts); the match kernel scatters S in LDS.
+#define CK_PF 4
+__global__ __launch_bounds__(64) void dmx_chain_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
+                                                       uint16_t* __restrict__ rank_g, uint16_t* __restrict__ start_g) {
+    __shared__ uint32_t cnt32[DMX_NBUCKET / 2];
+    __shared__ uint8_t scr_raw[DMX_NBUCKET];
+    uint16_t* cnt = reinterpret_cast<uint16_t*>(cnt32);
+    volatile uint8_t* scr = scr_raw;   // the read-back must see the other lanes' writes
     const uint32_t lane = threadIdx.x;
     const uint64_t off = (uint64_t)blockIdx.x * sw;
     const uint32_t bn = (uint32_t)((n - off) < sw ? (n - off) : sw);
     const uint8_t* d = in + off;
-    uint16_t* pg = prev_g + (uint64_t)blockIdx.x * DMX_BLK;
-
-    for (uint32_t k = lane; k < DMX_NBUCKET / 4; k += 64) head64[k] = ~0ull;
+    uint16_t* rg = rank_g + (uint64_t)blockIdx.x * DMX_BLK;
+    for (uint32_t k = lane; k < DMX_NBUCKET / 2; k += 64) cnt32[k] = 0;
     __syncthreads();
-
     const uint32_t nsteps = (bn + 63) >> 6;
-    uint32_t c0 = lane < bn ? d[lane] : 0;
-    uint32_t cx = (lane < 2 && 64 + lane < bn) ? d[64 + lane] : 0;
-    for (uint32_t s = 0; s < nsteps; s++) {
-        const uint32_t base = s << 6;
-        const uint32_t b0 = c0, bx = cx;
-        {   // prefetch the next step's bytes while this one is hashed
-            const uint32_t np = base + 64 + lane;
-            c0 = np < bn ? d[np] : 0;
-            cx = (lane < 2 && np + 64 < bn) ? d[np + 64] : 0;
-        }
-        uint32_t b1 = __shfl_down(b0, 1);
-        uint32_t b2 = __shfl_down(b0, 2);
-        const uint32_t x0 = __shfl(bx, 0), x1 = __shfl(bx, 1);
-        if (lane == 63) { b1 = x0; b2 = x1; }
-        else if (lane == 62) { b2 = x0; }
-        const uint32_t p = base + lane;
-        const bool valid = p + 2 < bn;
-        const uint32_t h = dmx_hash(b0 | (b1 << 8) | (b2 << 16));
-        uint64_t eq = __ballot(valid);
+    uint32_t ring[CK_PF];
 #pragma unroll
-        for (int bit = 0; bit < 14; bit++) {
-            const bool hb = (h >> bit) & 1;
-            const uint64_t m = __ballot(hb);
-            eq &= hb ? m : ~m;
-        }
-        uint16_t pv = DMX_NONE16;
-        if (valid) {
-            const uint64_t lower = eq & ((1ull << lane) - 1);
-            pv = lower ? (uint16_t)(base + 63 - __clzll(lower)) : head[h];
-        }
-        if (p < bn) pg[p] = pv;
-        if (valid) {
-            const uint64_t higher = eq & ~((2ull << lane) - 1);
-            if (!higher) head[h] = (uint16_t)p;
+    for (int j = 0; j < CK_PF; j++) ring[j] = g_tri(d, 64 * j + lane, bn);
+    for (uint32_t s0 = 0; s0 < nsteps; s0 += CK_PF) {
+#pragma unroll
+        for (int j = 0; j < CK_PF; j++) {
+            const uint32_t s = s0 + j;
+            if (s >= nsteps) break;
+            const uint32_t p = (s << 6) + lane;
+            const uint32_t tri = ring[j];
+            ring[j] = g_tri(d, p + 64 * CK_PF, bn);   // CK_PF steps ahead
+            const bool valid = p + 2 < bn;
+            const uint32_t h = dmx_hash(tri);
+            if (valid) scr[h] = (uint8_t)lane;
+            const uint32_t rep = valid ? (uint32_t)scr[h] : lane;
+            uint64_t eq = 1ull << lane;
+            if (__ballot(rep != lane)) {
+                eq = __ballot(valid);
+#pragma unroll
+                for (int bit = 0; bit < 6; bit++) {
+                    const bool hb = (rep >> bit) & 1;
+                    const uint64_t m = __ballot(hb);
+                    eq &= hb ? m : ~m;
+                }
+            }
+            uint32_t rank = 0;
+            if (valid) rank = (uint32_t)cnt[h] + (uint32_t)__popcll(eq & ((1ull << lane) - 1));
+            if (valid && !(eq & ~((2ull << lane) - 1))) cnt[h] = (uint16_t)(rank + 1);
+            if (p < bn) rg[p] = valid ? (uint16_t)rank : DMX_NONE16;
         }
     }
+    __syncthreads();
+    {   // exclusive scan of the bucket counts (128 per lane), in place -> bucket starts
+        uint32_t run = 0;
+        for (uint32_t k = 0; k < DMX_NBUCKET / 64; k++) run += cnt[lane * (DMX_NBUCKET / 64) + k];
+        uint32_t x = run;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        uint32_t acc = x - run;
+        for (uint32_t k = 0; k < DMX_NBUCKET / 64; k++) {
+            const uint32_t j = lane * (DMX_NBUCKET / 64) + k;
+            const uint32_t c = cnt[j];
+            cnt[j] = (uint16_t)acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    uint16_t* stg = start_g + (uint64_t)blockIdx.x * DMX_NBUCKET;   // bucket starts for the match kernel
+    for (uint32_t k = lane; k < DMX_NBUCKET / 2; k += 64) reinterpret_cast<uint32_t*>(stg)[k] = cnt32[k];
 }
 
 // ------------------------------------------------------------------------------------
@@ -148,68 +191,160 @@ __global__ __launch_bounds__(64) void dmx_chain_kernel(const uint8_t* __restrict
 #define DATA_WORDS 8200
 
 struct __attribute__((aligned(16))) MatchLDS {
-    uint32_t data[DATA_WORDS];  // the block, zero padded
-    uint16_t prev[DMX_BLK];     // hash chains (K1a)
-    uint8_t len8[DMX_BLK];      // best length - 3 (matches)
-    uint32_t lit[DMX_BLK / 32]; // 1 = literal at that position
-    uint32_t tsm[DMX_BLK / 32]; // token starts, 32 positions per word
+    uint32_t data[DATA_WORDS];    // the block, zero padded
+    uint16_t sorted[DMX_BLK];     // positions sorted by (bucket, position) (K1a); after the search: best distances
+    uint16_t bstart[DMX_NBUCKET]; // start of every bucket in `sorted`
+    uint8_t len8[DMX_BLK];        // best length - 3 (matches)
+    uint32_t lit[DMX_BLK / 32];   // 1 = literal at that position
+    uint32_t tsm[DMX_BLK / 32];   // token starts, 32 positions per word
     uint32_t exitp[DMX_BLK / 32];
     uint32_t hist[DMX_HIST];
     uint32_t wexit[MW];
     uint32_t wsum[MW];
-    uint32_t ctr;
     uint32_t ntok;
     unsigned long long adl_s, adl_t;
 };
 
-__device__ __forceinline__ uint32_t ld4(const uint32_t* W, uint32_t p) {
-    const uint32_t w0 = W[p >> 2], w1 = W[(p >> 2) + 1];
-    return __builtin_amdgcn_alignbyte(w1, w0, p & 3);
+// Byte-granular reads of the LDS block built from ALIGNED reads + funnel shifts:
+// an unaligned ds_read costs ~8x an aligned one on gfx950 (tools/ldsbench.hip:
+// ~1000 vs ~130-220 cycles per wave-instruction with 16 waves resident).
+__device__ __forceinline__ uint64_t fsh64(uint64_t lo, uint64_t hi, uint32_t sh) {   // sh in [0, 64)
+    return sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
+}
+__device__ __forceinline__ uint64_t ld8(const uint32_t* W, uint32_t p) {   // bytes p..p+7
+    const uint64_t* Q = reinterpret_cast<const uint64_t*>(W);
+    const uint32_t a = p >> 3;
+    return fsh64(Q[a], Q[a + 1], (p & 7) << 3);
+}
+__device__ __forceinline__ uint32_t ld4(const uint32_t* W, uint32_t p) {   // bytes p..p+3
+    return __builtin_amdgcn_alignbyte(W[(p >> 2) + 1], W[p >> 2], p & 3);
 }
 
 __device__ __forceinline__ uint32_t adv_of(const MatchLDS& L, uint32_t p) {
     return ((L.lit[p >> 5] >> (p & 31)) & 1u) ? 1u : (uint32_t)L.len8[p] + 3u;
 }
 
-// Resolve segment s (positions [32s, 32s+32)) for a path entering at e >= 32s.
-// The word tsm[s] holds a path through the segment; if the walk from e meets one of
-// its positions the rest coincides (the next-function is deterministic).
-__device__ uint32_t resolve_seg(MatchLDS& L, uint32_t s, uint32_t e, uint32_t bn, bool& merged) {
-    const uint32_t lo = s << 5;
+// Longest match (>= 3, ties to the nearest) of every position, deflate_compress.c:243-264.
+// Work unit = one entry k of the bucket-sorted array S (position i = S[k]); thread tid
+// takes entries tid, tid+1024, ...  Its chain is S[k-1], S[k-2], ..., S[start(bucket)]
+// (newest first, K1a), capped at K entries.  The chain is examined CW entries per
+// iteration: the CW slots and then the CW 8-byte data words are independent loads, so one
+// iteration costs two LDS round trips for CW candidates (the search is LDS-latency bound:
+// a dependent ds_read costs ~200-300 cycles with 16 waves resident).  8 aligned-read
+// bytes give the exact length of a candidate whose match is < 8 bytes; longer ones extend
+// 8 bytes per step.  The kept key is len << 15 | q: longest, then nearest (largest q) --
+// the reference's newest-first walk with strict > (:249-263).  A position stops early
+// once its best reaches the longest possible length min(258, bytes left).
+#define CW 4
+__device__ __forceinline__ uint32_t match_bytes(uint64_t x) {   // equal leading bytes of an 8-byte xor
+    return x ? ((uint32_t)__builtin_ctzll(x) >> 3) : 8u;
+}
+
+__device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint16_t* __restrict__ pg,
+                                     uint32_t tid) {
+    const uint32_t K = max_chain > 0 ? (uint32_t)max_chain : 0xFFFFFFFFu;
+    const uint32_t nvalid = bn > 2 ? bn - 2 : 0;   // positions with a full trigram = entries of S
+    uint32_t iters = 0;
+    for (uint32_t k0 = 0; k0 < nvalid; k0 += MT) {
+        const uint32_t k = k0 + tid;
+        const bool act = k < nvalid;
+        uint32_t i = 0, nc = 0, lim = 0, bestkey = 0;
+        uint64_t iv = 0;
+        if (act) {
+            i = L.sorted[k];
+            const uint32_t h = dmx_hash(ld4(L.data, i) & 0xFFFFFFu);
+            iv = ld8(L.data, i);
+            const uint32_t rank = k - (uint32_t)L.bstart[h];
+            nc = min(rank, K);
+            lim = (bn - i) < MAXLEN ? (bn - i) : MAXLEN;
+        }
+        for (uint32_t c = 0;; c += CW) {
+            const bool more = act && c < nc && (bestkey >> 15) < lim;
+            if (__ballot(more) == 0) break;
+            iters++;
+            if (more) {
+                uint32_t q[CW];
+                uint64_t w[CW];
+#pragma unroll
+                for (int j = 0; j < CW; j++) q[j] = (c + j < nc) ? (uint32_t)L.sorted[k - 1 - c - j] : DMX_NONE16;
+#pragma unroll
+                for (int j = 0; j < CW; j++) w[j] = q[j] != DMX_NONE16 ? ld8(L.data, q[j]) : ~iv;
+#pragma unroll
+                for (int j = 0; j < CW; j++) {
+                    uint32_t len = match_bytes(iv ^ w[j]);
+                    if (len == 8 && lim > 8 && (bestkey >> 15) < lim) {   // long candidate: extend 8 bytes per step
+                        uint32_t kk = 8;
+                        for (;;) {
+                            const uint32_t mb = match_bytes(ld8(L.data, i + kk) ^ ld8(L.data, q[j] + kk));
+                            kk += mb;
+                            if (mb < 8 || kk >= lim) break;
+                        }
+                        len = kk;
+                    }
+                    if (len > lim) len = lim;
+                    const uint32_t key = len >= 3 ? ((len << 15) | q[j]) : 0;
+                    bestkey = max(bestkey, key);
+                }
+            }
+        }
+        if (act) {
+            if (bestkey == 0) {
+                atomicOr(&L.lit[i >> 5], 1u << (i & 31));
+                L.len8[i] = 0;
+            } else {
+                L.len8[i] = (uint8_t)((bestkey >> 15) - 3);
+                pg[i] = (uint16_t)(i - (bestkey & 0x7FFFu));
+            }
+        }
+    }
+    // the last two positions have no trigram: literals
+    if (tid < 2 && bn >= 1 + tid) {
+        const uint32_t p = bn - 1 - tid;
+        atomicOr(&L.lit[p >> 5], 1u << (p & 31));
+        L.len8[p] = 0;
+    }
+    return iters;
+}
+
+// Resolve segment s (positions [32s, 32s+32)) for a path entering at e >= 32s, against the
+// path word m of that segment: if the walk from e meets one of m's positions the rest
+// coincides (the next-function is deterministic).  Scalar code: every input is uniform.
+__device__ __forceinline__ uint32_t resolve_word(const MatchLDS& L, uint32_t lo, uint32_t e, uint32_t bn, uint32_t m,
+                                                 uint32_t lw, uint32_t x, uint32_t& nm_out, bool& merged) {
     merged = false;
-    if (e >= lo + 32 || e >= bn) { L.tsm[s] = 0; return e; }
-    const uint32_t m = L.tsm[s];
+    if (e >= lo + 32 || e >= bn) { nm_out = 0; return e; }
     uint32_t nm = 0, p = e;
     while (p < lo + 32 && p < bn) {
         const uint32_t bit = 1u << (p - lo);
-        if (m & bit) {
-            L.tsm[s] = nm | (m & ~(bit - 1u));
-            merged = true;
-            return L.exitp[s];
-        }
+        if (m & bit) { nm_out = nm | (m & ~(bit - 1u)); merged = true; return x; }
         nm |= bit;
-        p += adv_of(L, p);
+        p += ((lw >> (p - lo)) & 1u) ? 1u : (uint32_t)L.len8[p] + 3u;
     }
-    L.tsm[s] = nm;
+    nm_out = nm;
     return p;
 }
 
 __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
-                                                       int32_t max_chain, uint16_t* __restrict__ prev_g,
+                                                       int32_t max_chain, uint16_t* __restrict__ rank_dist_g,
+                                                       const uint16_t* __restrict__ start_g,
                                                        uint32_t* __restrict__ tok_g, uint32_t* __restrict__ hist_g,
-                                                       dmx_blkinfo* __restrict__ info) {
+                                                       dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg) {
     __shared__ MatchLDS L;
+    __shared__ uint64_t st_search, st_iters, st_w1, st_w23;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t b = blockIdx.x;
     const uint64_t off = (uint64_t)b * sw;
     const uint32_t bn = (uint32_t)((n - off) < sw ? (n - off) : sw);
     const uint8_t* d = in + off;
-    uint16_t* pg = prev_g + (uint64_t)b * DMX_BLK;  // chains in; distances out (same slots)
+    uint16_t* pg = rank_dist_g + (uint64_t)b * DMX_BLK;   // ranks in; best distances out (same slots)
+    const uint16_t* stg = start_g + (uint64_t)b * DMX_NBUCKET;
     uint8_t* D8 = reinterpret_cast<uint8_t*>(L.data);
 
-    // ---- P0: stage the block and its chains in LDS ----
-    if (tid == 0) { L.ctr = 0; L.adl_s = 0; L.adl_t = 0; }
+    // ---- P0: stage the block, the bucket starts and the bucket-sorted positions in LDS ----
+    if (tid == 0) { L.adl_s = 0; L.adl_t = 0; }
+    if (dbg && tid == 0) { st_search = 0; st_iters = 0; }
     for (uint32_t k = tid; k < DMX_HIST; k += MT) L.hist[k] = 0;
+    for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) L.lit[k] = 0;
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
     for (uint32_t k = tid; k < DATA_WORDS / 4; k += MT) {   // 16-byte chunks
         const uint32_t p = k << 4;
@@ -225,68 +360,59 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         *reinterpret_cast<uint4*>(&L.data[k << 2]) = v;
     }
     {
-        const uint32_t nch = (bn * 2 + 15) >> 4;  // prev entries needed: [0, bn)
-        const uint4* src = reinterpret_cast<const uint4*>(pg);
-        uint4* dst = reinterpret_cast<uint4*>(L.prev);
-        for (uint32_t k = tid; k < nch; k += MT) dst[k] = src[k];
+        const uint4* bs = reinterpret_cast<const uint4*>(stg);
+        uint4* bd = reinterpret_cast<uint4*>(L.bstart);
+        for (uint32_t k = tid; k < DMX_NBUCKET * 2 / 16; k += MT) bd[k] = bs[k];
+    }
+    __syncthreads();
+    {   // S[start(bucket(p)) + rank(p)] = p (scatter in LDS); ranks read as 16-byte vectors,
+        // all four loads in flight before the first use
+        uint4 rv[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t c4 = tid + (uint32_t)j * MT;
+            rv[j] = (c4 * 8 < bn) ? reinterpret_cast<const uint4*>(pg)[c4] : make_uint4(~0u, ~0u, ~0u, ~0u);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t w[4] = {rv[j].x, rv[j].y, rv[j].z, rv[j].w};
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const uint32_t p = (tid + (uint32_t)j * MT) * 8 + (uint32_t)e;
+                const uint32_t r = (w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+                if (p < bn && r != DMX_NONE16)
+                    L.sorted[(uint32_t)L.bstart[dmx_hash(ld4(L.data, p) & 0xFFFFFFu)] + r] = (uint16_t)p;
+            }
+        }
     }
     __syncthreads();
 
     {   // Adler-32 partial sums of this block
         uint64_t s = 0, t = 0;
-        const uint32_t lo = tid << 5;
-        for (uint32_t j = 0; j < 32; j++) {
-            const uint32_t p = lo + j;
-            if (p < bn) { const uint32_t c = D8[p]; s += c; t += (uint64_t)p * c; }
+        const uint32_t lo = tid << 5;   // 32 bytes per thread, read as two 16-byte vectors
+        const uint4 v0 = *reinterpret_cast<const uint4*>(&L.data[lo >> 2]);
+        const uint4 v1 = *reinterpret_cast<const uint4*>(&L.data[(lo >> 2) + 4]);
+        const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+        for (uint32_t j = 0; j < 32; j++) {   // bytes past bn are zero in LDS
+            const uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            s += c;
+            t += (uint64_t)(lo + j) * c;
         }
         s = wave_sum_u64(s);
         t = wave_sum_u64(t);
         if (lane == 0) { atomicAdd(&L.adl_s, (unsigned long long)s); atomicAdd(&L.adl_t, (unsigned long long)t); }
     }
 
-    // ---- P1: longest match at every position (dynamic 64-position chunks per wave) ----
-    const uint32_t nchunks = (bn + 63) >> 6;
-    for (;;) {
-        uint32_t c = 0;
-        if (lane == 0) c = atomicAdd(&L.ctr, 1u);
-        c = __shfl(c, 0);
-        if (c >= nchunks) break;
-        const uint32_t i = (c << 6) + lane;
-        uint32_t best = 2, bq = DMX_NONE16;
-        if (i + 2 < bn) {
-            const uint32_t lim = (bn - i) < MAXLEN ? (bn - i) : MAXLEN;
-            uint32_t q = L.prev[i];
-            int steps = 0;
-            while (q != DMX_NONE16) {
-                if (max_chain > 0 && steps >= max_chain) break;
-                steps++;
-                if (D8[q + best] == D8[i + best]) {      // cannot beat `best` otherwise
-                    uint32_t k = 0;
-                    for (;;) {
-                        const uint32_t x = ld4(L.data, i + k) ^ ld4(L.data, q + k);
-                        if (x) { k += __builtin_ctz(x) >> 3; break; }
-                        k += 4;
-                        if (k >= lim) break;
-                    }
-                    if (k > lim) k = lim;
-                    if (k > best) {                      // strict >: ties keep the nearer
-                        best = k;
-                        bq = q;
-                        if (k == lim) break;
-                    }
-                }
-                q = L.prev[q];
-            }
-        }
-        const bool is_lit = (bq == DMX_NONE16);
-        const uint64_t lm = __ballot(is_lit);
-        if (lane == 0) { L.lit[c << 1] = (uint32_t)lm; L.lit[(c << 1) + 1] = (uint32_t)(lm >> 32); }
-        if (i < bn) {
-            L.len8[i] = is_lit ? 0 : (uint8_t)(best - 3);
-            if (!is_lit) pg[i] = (uint16_t)(i - bq);
-        }
+    // ---- P1: longest match of every position ----
+    const uint64_t t0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
+    const uint32_t its = search_positions(L, bn, max_chain, pg, tid);
+    if (dbg && lane == 0) {
+        atomicAdd((unsigned long long*)&st_iters, (unsigned long long)its);
+        atomicMax((unsigned long long*)&st_search, (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
     }
     __syncthreads();
+    const uint64_t t1 = dbg ? __builtin_amdgcn_s_memtime() : 0;
 
     // ---- P2: greedy path ----
     {   // W1: speculative walk of every 32-position segment from its start
@@ -296,12 +422,29 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         L.tsm[tid] = m;
         L.exitp[tid] = p;
     }
-    __syncthreads();
-    if (lane == 0) {  // W2: resolve the wave's 64 segments assuming it is entered at 2048*wave
+    {   // the sorted positions are dead: stage the best distances in their LDS slots
+        __syncthreads();
+        const uint32_t nch = (bn * 2 + 15) >> 4;
+        const uint4* src = reinterpret_cast<const uint4*>(pg);
+        uint4* dst = reinterpret_cast<uint4*>(L.sorted);
+        for (uint32_t k = tid; k < nch; k += MT) dst[k] = src[k];
+    }
+    if (dbg && tid == 0) st_w1 = __builtin_amdgcn_s_memtime() - t1;
+    {   // W2: each wave resolves its 64 segments assuming it is entered at 2048*wave.
+        // Segment words live one per lane; the serial loop runs on uniform values.
+        uint32_t myw = L.tsm[tid];
+        const uint32_t myx = L.exitp[tid], myl = L.lit[tid];
         uint32_t e = wave << 11;
-        bool mg;
-        for (uint32_t s = wave << 6; s < (wave << 6) + 64; s++) e = resolve_seg(L, s, e, bn, mg);
-        L.wexit[wave] = e;
+        for (uint32_t j = 0; j < 64; j++) {
+            const uint32_t m = __builtin_amdgcn_readlane(myw, (int)j), x = __builtin_amdgcn_readlane(myx, (int)j),
+                           lw = __builtin_amdgcn_readlane(myl, (int)j);
+            uint32_t nm;
+            bool mg;
+            e = resolve_word(L, ((wave << 6) + j) << 5, e, bn, m, lw, x, nm, mg);
+            if (lane == j) myw = nm;
+        }
+        L.tsm[tid] = myw;
+        if (lane == 0) L.wexit[wave] = e;
     }
     __syncthreads();
     if (tid == 0) {   // W3: fix the waves whose true entry differs, until the paths merge
@@ -309,15 +452,18 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         for (uint32_t w = 1; w < MW; w++) {
             if (E == (w << 11)) { E = L.wexit[w]; continue; }
             uint32_t e = E;
-            bool mg = false;
             for (uint32_t s = w << 6; s < (w << 6) + 64; s++) {
-                e = resolve_seg(L, s, e, bn, mg);
+                uint32_t nm;
+                bool mg;
+                e = resolve_word(L, s << 5, e, bn, L.tsm[s], L.lit[s], 0, nm, mg);
+                L.tsm[s] = nm;
                 if (mg) { e = L.wexit[w]; break; }
             }
             E = e;
         }
     }
     __syncthreads();
+    if (dbg && tid == 0) st_w23 = __builtin_amdgcn_s_memtime() - t1;
 
     // ---- P3: compaction + histograms ----
     {
@@ -344,17 +490,18 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         __syncthreads();
         uint32_t k = L.wsum[wave] + x - cnt;
         uint32_t* tb = tok_g + (uint64_t)b * DMX_BLK;
+        const uint32_t lw = L.lit[tid];
         uint32_t mm = m;
         while (mm) {
             const uint32_t bit = __builtin_ctz(mm);
             mm &= mm - 1;
             const uint32_t p = (tid << 5) + bit;
             uint32_t t;
-            if ((L.lit[tid] >> bit) & 1u) {
+            if ((lw >> bit) & 1u) {
                 t = D8[p];
                 atomicAdd(&L.hist[t], 1u);
             } else {
-                const uint32_t len = (uint32_t)L.len8[p] + 3u, dist = pg[p];
+                const uint32_t len = (uint32_t)L.len8[p] + 3u, dist = L.sorted[p];
                 t = (dist << 9) | len;
                 uint32_t s, eb, ev;
                 len_sym(len, s, eb, ev);
@@ -367,6 +514,15 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
     }
     __syncthreads();
     for (uint32_t k = tid; k < DMX_HIST; k += MT) hist_g[(uint64_t)b * DMX_HIST + k] = L.hist[k];
+    if (dbg && tid == 0) {
+        dbg[(uint64_t)b * 8 + 0] = 0;
+        dbg[(uint64_t)b * 8 + 1] = st_search;
+        dbg[(uint64_t)b * 8 + 2] = __builtin_amdgcn_s_memtime() - t1;
+        dbg[(uint64_t)b * 8 + 3] = L.ntok;
+        dbg[(uint64_t)b * 8 + 4] = st_iters;
+        dbg[(uint64_t)b * 8 + 5] = st_w1;
+        dbg[(uint64_t)b * 8 + 6] = st_w23;
+    }
     if (tid == 0) {
         info[b].ntok = L.ntok;
         info[b].n = bn;
@@ -948,13 +1104,16 @@ struct dmx_ctx {
     int device;
     hipStream_t stream;
     uint64_t cap_blocks;
-    uint16_t* prev;   // cap_blocks * DMX_BLK (chains, then distances)
+    uint16_t* prev;   // cap_blocks * DMX_BLK: bucket ranks (chain kernel), then best distances
+    uint16_t* bstart; // cap_blocks * DMX_NBUCKET: bucket starts in the sorted array
     uint32_t* tok;    // cap_blocks * DMX_BLK
     uint32_t* hist;   // cap_blocks * DMX_HIST
     uint32_t* codes;  // cap_blocks * DMX_HIST
     uint32_t* hdr;    // cap_blocks * DMX_HDR_WORDS
     dmx_blkinfo* info;
     dmx_result* res;
+    uint64_t* dbg;        // optional per-block phase stamps (DMX_STAMPS=1)
+    uint64_t dbg_cap;
     // last encode (introspection)
     uint32_t last_nblk;
     // host staging for dmx_encode_host
@@ -967,7 +1126,7 @@ struct dmx_ctx {
     hipEvent_t ev[DMX_EV_RING][6];
     int ev_used[DMX_EV_RING];
     uint32_t ev_next;
-    double stage_ms[5];
+    double stage_ms[6];
     uint32_t stage_n;
 };
 
@@ -988,12 +1147,13 @@ extern "C" uint64_t dmx_max_compressed(uint64_t n, int32_t sw) {
 
 static void ctx_free_ws(dmx_ctx* c) {
     if (c->prev) (void)hipFree(c->prev);
+    if (c->bstart) (void)hipFree(c->bstart);
     if (c->tok) (void)hipFree(c->tok);
     if (c->hist) (void)hipFree(c->hist);
     if (c->codes) (void)hipFree(c->codes);
     if (c->hdr) (void)hipFree(c->hdr);
     if (c->info) (void)hipFree(c->info);
-    c->prev = NULL; c->tok = NULL; c->hist = NULL; c->codes = NULL; c->hdr = NULL; c->info = NULL;
+    c->prev = NULL; c->bstart = NULL; c->tok = NULL; c->hist = NULL; c->codes = NULL; c->hdr = NULL; c->info = NULL;
     c->cap_blocks = 0;
 }
 
@@ -1002,6 +1162,7 @@ static int ctx_reserve(dmx_ctx* c, uint64_t nblk) {
     ctx_free_ws(c);
     const uint64_t cb = nblk < 1 ? 1 : nblk;
     HIPCHK(hipMalloc(&c->prev, cb * DMX_BLK * sizeof(uint16_t)));
+    HIPCHK(hipMalloc(&c->bstart, cb * DMX_NBUCKET * sizeof(uint16_t)));
     HIPCHK(hipMalloc(&c->tok, cb * DMX_BLK * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&c->hist, cb * DMX_HIST * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&c->codes, cb * DMX_HIST * sizeof(uint32_t)));
@@ -1052,6 +1213,7 @@ extern "C" void dmx_ctx_destroy(dmx_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     ctx_free_ws(c);
     if (c->res) (void)hipFree(c->res);
+    if (c->dbg) (void)hipFree(c->dbg);
     if (c->d_in) (void)hipFree(c->d_in);
     if (c->d_out) (void)hipFree(c->d_out);
     for (int j = 0; j < DMX_EV_RING; j++)
@@ -1060,6 +1222,7 @@ extern "C" void dmx_ctx_destroy(dmx_ctx* c) {
     free(c);
 }
 
+// stage times per encode: [chain, match, huff, scan, pack] + the whole encode
 static void ctx_collect_set(dmx_ctx* c, int j) {
     if (!c->ev_used[j]) return;
     c->ev_used[j] = 0;
@@ -1068,6 +1231,8 @@ static void ctx_collect_set(dmx_ctx* c, int j) {
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, c->ev[j][k], c->ev[j][k + 1]) == hipSuccess) c->stage_ms[k] += ms;
     }
+    float tot = 0.f;
+    if (hipEventElapsedTime(&tot, c->ev[j][0], c->ev[j][5]) == hipSuccess) c->stage_ms[5] += tot;
     c->stage_n++;
 }
 
@@ -1094,10 +1259,21 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         (void)hipEventRecord(ev[0], s);
     }
     if (nblk) {
-        hipLaunchKernelGGL(dmx_chain_kernel, dim3(nblk), dim3(64), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw, c->prev);
+        uint64_t* dbg = NULL;
+        if (getenv("DMX_STAMPS")) {
+            if (c->dbg_cap < nblk) {
+                if (c->dbg) (void)hipFree(c->dbg);
+                c->dbg = NULL;
+                c->dbg_cap = 0;
+                if (hipMalloc(&c->dbg, (uint64_t)nblk * 8 * sizeof(uint64_t)) == hipSuccess) c->dbg_cap = nblk;
+            }
+            dbg = c->dbg;
+        }
+        hipLaunchKernelGGL(dmx_chain_kernel, dim3(nblk), dim3(64), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw, c->prev,
+                           c->bstart);
         if (ev) (void)hipEventRecord(ev[1], s);
         hipLaunchKernelGGL(dmx_match_kernel, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw,
-                           o.max_chain, c->prev, c->tok, c->hist, c->info);
+                           o.max_chain, c->prev, c->bstart, c->tok, c->hist, c->info, dbg);
         if (ev) (void)hipEventRecord(ev[2], s);
         hipLaunchKernelGGL(dmx_huff_kernel, dim3(nblk), dim3(64), 0, s, c->hist, c->info, c->codes, c->hdr, nblk, o.flags);
         if (ev) (void)hipEventRecord(ev[3], s);
@@ -1130,15 +1306,15 @@ extern "C" int dmx_ctx_set_timing(dmx_ctx* c, int enable) {
     (void)hipSetDevice(c->device);
     for (int j = 0; j < DMX_EV_RING; j++) c->ev_used[j] = 0;
     c->timing = enable;
-    for (int k = 0; k < 5; k++) c->stage_ms[k] = 0;
+    for (int k = 0; k < 6; k++) c->stage_ms[k] = 0;
     c->stage_n = 0;
     return 0;
 }
 
-extern "C" int dmx_ctx_stage_times(dmx_ctx* c, double* ms5, uint32_t* count) {
+extern "C" int dmx_ctx_stage_times(dmx_ctx* c, double* ms6, uint32_t* count) {
     (void)hipSetDevice(c->device);
     for (int j = 0; j < DMX_EV_RING; j++) ctx_collect_set(c, j);
-    for (int k = 0; k < 5; k++) ms5[k] = c->stage_n ? c->stage_ms[k] / c->stage_n : 0.0;
+    for (int k = 0; k < 6; k++) ms6[k] = c->stage_n ? c->stage_ms[k] / c->stage_n : 0.0;
     *count = c->stage_n;
     return 0;
 }
@@ -1238,4 +1414,15 @@ extern "C" int dmx_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint
     if (!r) *out_len = res.out_len;
     pthread_mutex_unlock(&g_mu);
     return r;
+}
+
+// Per-block match-kernel phase stamps of the last encode (DMX_STAMPS=1): for each block
+// {cycles to build the chains (wave 0), cycles until the last wave finished searching,
+//  cycles of walk + compaction, tokens}.  Diagnostic only.
+extern "C" int dmx_debug_stamps(dmx_ctx* c, uint64_t* out, uint32_t nblk) {
+    if (!c->dbg || nblk > c->dbg_cap || nblk > c->last_nblk) return -(int)E_RANGE;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(out, c->dbg, (uint64_t)nblk * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return 0;
 }

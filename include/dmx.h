@@ -168,9 +168,13 @@ int dmx_last_code_lengths(dmx_ctx* ctx, uint32_t blk, uint8_t* lens316);
 
 /* Per-kernel HIP-event timing of subsequent encodes on the context's launches
  * (bench): enable, then read the mean milliseconds per launch of each stage
- * {chain, match, huff, scan, pack} and the number of timed launches. */
+ * {chain, match, huff, scan, pack} and of the whole encode, and the number of timed encodes. */
 int dmx_ctx_set_timing(dmx_ctx* ctx, int enable);
-int dmx_ctx_stage_times(dmx_ctx* ctx, double* ms5, uint32_t* count);
+int dmx_ctx_stage_times(dmx_ctx* ctx, double* ms6, uint32_t* count);
+
+/* Diagnostic: per-block match-kernel phase stamps (cycles) of the last encode, when the
+ * process runs with DMX_STAMPS=1: 8 x u64 per block (see dmx_kernels.hip). */
+int dmx_debug_stamps(dmx_ctx* ctx, uint64_t* out8, uint32_t nblk);
 
 /* Adler-32 combine (RFC 1950 math): adler of A||B from adler(A), adler(B), len(B). */
 uint32_t dmx_adler32_combine(uint32_t a, uint32_t b, uint64_t len_b);

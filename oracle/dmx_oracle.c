@@ -27,7 +27,7 @@
  *    The bucket function does not change the exhaustive result (every candidate
  *    with an equal 3-byte prefix shares the bucket whatever the hash is);
  *    DMX_HASH_MORTON selects the reference's dup_hash (:115-135, 1024 buckets),
- *    DMX_HASH_MUL the 14-bit multiplicative hash the GPU uses.  With
+ *    DMX_HASH_MUL the 13-bit multiplicative hash the GPU uses.  With
  *    max_chain = K > 0 only the K newest entries of the hash chain are examined
  *    (the bounded "fast" mode); that mode is defined on DMX_HASH_MUL.
  *
@@ -67,10 +67,10 @@ static unsigned orc_hash_morton(const uint8_t* p) {
     return (x | (y << 1) | (z << 2)) % 1024u;
 }
 
-/* 14-bit multiplicative hash of the 24-bit little-endian trigram. */
+/* 13-bit multiplicative hash of the 24-bit little-endian trigram. */
 static unsigned orc_hash_mul(const uint8_t* p) {
     uint32_t t = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
-    return (uint32_t)(t * 0x9E3779B1u) >> 18;
+    return (uint32_t)(t * 0x9E3779B1u) >> 19;
 }
 
 /* ---- 1. parse ----------------------------------------------------------------- */
@@ -80,7 +80,7 @@ int dmx_oracle_parse_block(const uint8_t* d, int n, int max_chain, int hash_kind
                            uint32_t* tok) {
     int ntok = 0;
     if (n <= 0) return 0;
-    const int nb = hash_kind == DMX_HASH_MORTON ? 1024 : 16384;
+    const int nb = hash_kind == DMX_HASH_MORTON ? 1024 : 8192;
     uint32_t* head = (uint32_t*)malloc(sizeof(uint32_t) * nb);
     uint32_t* prev = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n);
     for (int b = 0; b < nb; b++) head[b] = ORC_NONE;

@@ -41,7 +41,7 @@ def test_all_declared_symbols_exported():
 def test_library_is_gfx950_code_object():
     blob = open(D.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
-    for k in (b"dmx_chain_kernel", b"dmx_match_kernel", b"dmx_huff_kernel", b"dmx_scan_kernel",
+    for k in (b"dmx_match_kernel", b"dmx_huff_kernel", b"dmx_scan_kernel",
               b"dmx_pack_kernel"):
         assert k in blob
 

@@ -1,0 +1,22 @@
+"""Diagnostic: per-phase cycle stamps of the match kernel (run with DMX_STAMPS=1)."""
+import os, sys, json
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ["DMX_STAMPS"] = "1"
+import numpy as np, torch
+import deflate_compression_amd as D
+
+def run(kind, n, mc):
+    a = D.gen_text(n, 0xE5818) if kind == "text" else (D.gen_random(n, 1) if kind == "random" else np.zeros(n, np.uint8))
+    t = torch.from_numpy(a).cuda()
+    e = D.Encoder(0, n, max_chain=mc)
+    for _ in range(2):
+        out, r = e.compress_tensor(t)
+    st = e.stamps(r.nblocks).astype(np.float64)
+    e.close()
+    print(json.dumps({"kind": kind, "mc": mc, "build_kcyc": round(st[:, 0].mean() / 1e3, 1),
+                      "search_kcyc": round(st[:, 1].mean() / 1e3, 1), "walk_kcyc": round(st[:, 2].mean() / 1e3, 1),
+                      "tokens": round(st[:, 3].mean(), 1), "iters_per_wave": round(st[:, 4].mean() / 16, 1),
+                      "w1_kcyc": round(st[:, 5].mean() / 1e3, 1), "w1w3_kcyc": round(st[:, 6].mean() / 1e3, 1)}))
+
+for kind, mc in [("text", 1), ("text", 16), ("text", 0), ("random", 0), ("zeros", 0)]:
+    run(kind, 20_000_000 if kind == "text" else 64 << 20, mc)
