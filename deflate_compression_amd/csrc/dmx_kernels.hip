@@ -188,7 +188,7 @@ __global__ __launch_bounds__(64) void dmx_chain_kernel(const uint8_t* __restrict
 
 #define MT 1024
 #define MW (MT / 64)
-#define DATA_WORDS 8200
+#define DATA_WORDS 8208   // 32 KiB + slack for 32-byte extension reads past the end (zeroed)
 
 struct __attribute__((aligned(16))) MatchLDS {
     uint32_t data[DATA_WORDS];    // the block, zero padded
@@ -225,40 +225,121 @@ __device__ __forceinline__ uint32_t adv_of(const MatchLDS& L, uint32_t p) {
 }
 
 // Longest match (>= 3, ties to the nearest) of every position, deflate_compress.c:243-264.
-// Work unit = one entry k of the bucket-sorted array S (position i = S[k]); thread tid
-// takes entries tid, tid+1024, ...  Its chain is S[k-1], S[k-2], ..., S[start(bucket)]
-// (newest first, K1a), capped at K entries.  The chain is examined CW entries per
-// iteration: the CW slots and then the CW 8-byte data words are independent loads, so one
-// iteration costs two LDS round trips for CW candidates (the search is LDS-latency bound:
-// a dependent ds_read costs ~200-300 cycles with 16 waves resident).  8 aligned-read
-// bytes give the exact length of a candidate whose match is < 8 bytes; longer ones extend
-// 8 bytes per step.  The kept key is len << 15 | q: longest, then nearest (largest q) --
-// the reference's newest-first walk with strict > (:249-263).  A position stops early
-// once its best reaches the longest possible length min(258, bytes left).
+// Work unit = one entry k of the bucket-sorted array S (position i = S[k]); a wave takes
+// 64 consecutive entries (lane = entry), waves take chunks round-robin.  The chain of
+// entry k is S[k-1], S[k-2], ..., S[start(bucket)] (newest first, K1a), capped at K.
+// Candidate j of lane l is entry k-j -- the entry j lanes below -- so every lane loads
+// only its OWN position and first 16 bytes once, and the wave shifts (position, 16 bytes)
+// down one lane per step with DPP wave_shr:1; lane 0 is fed from a halo of the KD
+// entries below the chunk.  Each step compares 64 candidates with ~20 VALU instructions
+// and no LDS traffic: 16 bytes give the exact length of any match < 16 (the usual case);
+// longer candidates extend from LDS 8 bytes per step.  Chains longer than KD (exhaustive
+// mode) continue from LDS, CW candidates per iteration.  The kept key is len << 15 | q:
+// longest, then nearest (largest q) -- the reference's newest-first walk with strict >
+// (:249-263).  A lane stops comparing once its best is the longest possible length.
+#define KD 32
 #define CW 4
 __device__ __forceinline__ uint32_t match_bytes(uint64_t x) {   // equal leading bytes of an 8-byte xor
     return x ? ((uint32_t)__builtin_ctzll(x) >> 3) : 8u;
 }
+__device__ __forceinline__ uint32_t wshr(uint32_t v, uint32_t lane0) {   // lane l <- lane l-1; lane 0 <- lane0
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)lane0, (int)v, 0x138, 0xF, 0xF, false);
+}
+// Length of a candidate known to match bytes [0, kk): 32 more bytes per LDS round trip
+// (four independent 8-byte reads per side).
+__device__ __forceinline__ uint32_t ext_len(const MatchLDS& L, uint32_t i, uint32_t q, uint32_t kk, uint32_t lim) {
+    for (;;) {
+        uint64_t a[4], b[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) { a[j] = ld8(L.data, i + kk + 8 * j); b[j] = ld8(L.data, q + kk + 8 * j); }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t mb = match_bytes(a[j] ^ b[j]);
+            kk += mb;
+            if (mb < 8 || kk >= lim) return kk;
+        }
+    }
+}
+// Could candidate q (known to match [0, 16)) be strictly longer than best (>= 16)? Only if
+// it also matches the byte at offset best.
+__device__ __forceinline__ bool may_beat(const MatchLDS& L, uint32_t i, uint32_t q, uint32_t best) {
+    const uint8_t* D8 = reinterpret_cast<const uint8_t*>(L.data);
+    return D8[q + best] == D8[i + best];
+}
+
+// DPP row_shr:n (n = 1, 2, 4, 8) in VALU; lanes without a source read 0.  (__shfl_* lowers
+// to ds_bpermute_b32, an LDS round trip.)
+__device__ __forceinline__ uint32_t dpp_shr(uint32_t v, int n) {
+    switch (n) {
+        case 1: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);
+        case 2: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);
+        case 4: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);
+        default: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);
+    }
+}
 
 __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint16_t* __restrict__ pg,
                                      uint32_t tid) {
+    const uint32_t lane = tid & 63, wave = tid >> 6;
     const uint32_t K = max_chain > 0 ? (uint32_t)max_chain : 0xFFFFFFFFu;
     const uint32_t nvalid = bn > 2 ? bn - 2 : 0;   // positions with a full trigram = entries of S
     uint32_t iters = 0;
-    for (uint32_t k0 = 0; k0 < nvalid; k0 += MT) {
-        const uint32_t k = k0 + tid;
+    for (uint32_t k0 = wave << 6; k0 < nvalid; k0 += MT) {
+        const uint32_t k = k0 + lane;
         const bool act = k < nvalid;
         uint32_t i = 0, nc = 0, lim = 0, bestkey = 0;
-        uint64_t iv = 0;
+        uint64_t iv0 = 0, iv1 = 0;
         if (act) {
             i = L.sorted[k];
-            const uint32_t h = dmx_hash(ld4(L.data, i) & 0xFFFFFFu);
-            iv = ld8(L.data, i);
-            const uint32_t rank = k - (uint32_t)L.bstart[h];
+            iv0 = ld8(L.data, i);
+            iv1 = ld8(L.data, i + 8);
+            const uint32_t rank = k - (uint32_t)L.bstart[dmx_hash((uint32_t)iv0 & 0xFFFFFFu)];
             nc = min(rank, K);
             lim = (bn - i) < MAXLEN ? (bn - i) : MAXLEN;
         }
-        for (uint32_t c = 0;; c += CW) {
+        // halo: lane l < KD holds entry k0-1-l
+        uint32_t hq = 0;
+        uint64_t hv0 = 0, hv1 = 0;
+        if (lane < KD && k0 >= lane + 1) {
+            hq = L.sorted[k0 - 1 - lane];
+            hv0 = ld8(L.data, hq);
+            hv1 = ld8(L.data, hq + 8);
+        }
+        uint32_t xq = i, x0l = (uint32_t)iv0, x0h = (uint32_t)(iv0 >> 32), x1l = (uint32_t)iv1, x1h = (uint32_t)(iv1 >> 32);
+        const uint32_t h0l = (uint32_t)hv0, h0h = (uint32_t)(hv0 >> 32), h1l = (uint32_t)hv1, h1h = (uint32_t)(hv1 >> 32);
+        // wave-uniform bound: the largest chain length of the chunk, capped at KD
+        uint32_t jmax = act ? min(nc, (uint32_t)KD) : 0;
+        jmax = max(jmax, dpp_shr(jmax, 1));
+        jmax = max(jmax, dpp_shr(jmax, 2));
+        jmax = max(jmax, dpp_shr(jmax, 4));
+        jmax = max(jmax, dpp_shr(jmax, 8));
+        jmax = max(max(__builtin_amdgcn_readlane(jmax, 15), __builtin_amdgcn_readlane(jmax, 31)),
+                   max(__builtin_amdgcn_readlane(jmax, 47), __builtin_amdgcn_readlane(jmax, 63)));
+        const uint32_t lim_eff = act ? lim : 0;
+        for (uint32_t j = 1; j <= jmax; j++) {
+            iters++;
+            const int src = (int)j - 1;
+            xq = wshr(xq, __builtin_amdgcn_readlane(hq, src));
+            x0l = wshr(x0l, __builtin_amdgcn_readlane(h0l, src));
+            x0h = wshr(x0h, __builtin_amdgcn_readlane(h0h, src));
+            x1l = wshr(x1l, __builtin_amdgcn_readlane(h1l, src));
+            x1h = wshr(x1h, __builtin_amdgcn_readlane(h1h, src));
+            // straight-line compare of the 16 shifted bytes (no branches on the common path)
+            const uint32_t m0 = match_bytes(iv0 ^ (((uint64_t)x0h << 32) | x0l));
+            const uint32_t m1 = match_bytes(iv1 ^ (((uint64_t)x1h << 32) | x1l));
+            uint32_t m = m0 < 8 ? m0 : 8 + m1;
+            const bool valid = j <= nc;                    // candidate j exists (act folded into lim_eff)
+            m = min(m, lim_eff);
+            const uint32_t bl = bestkey >> 15;
+            const bool ext = valid && m == 16 && lim_eff > 16 && bl < lim_eff;
+            if (__ballot(ext)) {                           // rare: a candidate matching >= 16 bytes
+                if (ext && (bl < 16 || may_beat(L, i, xq, bl))) m = min(ext_len(L, i, xq, 16, lim_eff), lim_eff);
+            }
+            const uint32_t key = (valid && m >= 3) ? ((m << 15) | xq) : 0u;
+            bestkey = max(bestkey, key);
+        }
+        // chains longer than KD (exhaustive mode): continue from LDS, CW candidates per iteration
+        for (uint32_t c = KD;; c += CW) {
             const bool more = act && c < nc && (bestkey >> 15) < lim;
             if (__ballot(more) == 0) break;
             iters++;
@@ -268,22 +349,15 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
 #pragma unroll
                 for (int j = 0; j < CW; j++) q[j] = (c + j < nc) ? (uint32_t)L.sorted[k - 1 - c - j] : DMX_NONE16;
 #pragma unroll
-                for (int j = 0; j < CW; j++) w[j] = q[j] != DMX_NONE16 ? ld8(L.data, q[j]) : ~iv;
+                for (int j = 0; j < CW; j++) w[j] = q[j] != DMX_NONE16 ? ld8(L.data, q[j]) : ~iv0;
 #pragma unroll
                 for (int j = 0; j < CW; j++) {
-                    uint32_t len = match_bytes(iv ^ w[j]);
-                    if (len == 8 && lim > 8 && (bestkey >> 15) < lim) {   // long candidate: extend 8 bytes per step
-                        uint32_t kk = 8;
-                        for (;;) {
-                            const uint32_t mb = match_bytes(ld8(L.data, i + kk) ^ ld8(L.data, q[j] + kk));
-                            kk += mb;
-                            if (mb < 8 || kk >= lim) break;
-                        }
-                        len = kk;
-                    }
+                    uint32_t len = match_bytes(iv0 ^ w[j]);
+                    const uint32_t bl = bestkey >> 15;
+                    if (len == 8 && lim > 8 && bl < lim && (bl < 8 || may_beat(L, i, q[j], bl)))
+                        len = ext_len(L, i, q[j], 8, lim);
                     if (len > lim) len = lim;
-                    const uint32_t key = len >= 3 ? ((len << 15) | q[j]) : 0;
-                    bestkey = max(bestkey, key);
+                    if (len >= 3) bestkey = max(bestkey, (len << 15) | q[j]);
                 }
             }
         }
