@@ -48,25 +48,28 @@ def make_input(kind: str, n: int, seed: int):
     return np.zeros(n, dtype=np.uint8)
 
 
-def cpu_baseline(data, max_chain: int, budget_s: float):
+def cpu_baseline(data, budget_s: float):
     """Time the CPU side on rank 0: the reference encoder itself (oracle/_ref, built
     from /root/reference's own sources; one process per 32 KiB block, as it is only
     correct for one window) if that binary is present, plus our C port of the
-    reference parse + emitter (oracle/dmx_oracle.c).  Bounded samples, 1 core each."""
-    import numpy as np
+    reference parse + emitter (oracle/dmx_oracle.c).  Bounded samples, 1 core each.
+    The port runs the reference's exhaustive parse, so its output size over the
+    sample is the reference-semantics size S_ref the GPU's size is compared with."""
     from oracle import oracle as O
     out = {}
-    # port: whole blocks until the budget is used
+    # port: whole 1 MiB pieces (32 blocks each) until the budget is used
     t0 = time.perf_counter()
     done = 0
+    zbytes = 0
     blk = 1 << 20
     while done < data.size and time.perf_counter() - t0 < budget_s:
-        O.compress(data[done:done + blk], max_chain=max_chain)
+        zbytes += len(O.compress(data[done:done + blk], max_chain=0)) - 6   # minus zlib framing
         done += min(blk, data.size - done)
     dt = time.perf_counter() - t0
     out["port"] = {"value": done / dt / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
                    "sample": f"first {done} B of the workload, oracle/dmx_oracle.c compress "
-                             f"(reference parse, max_chain={max_chain}, + Huffman/emitter), 1 thread"}
+                             f"(reference exhaustive parse + Huffman/emitter), 1 thread"}
+    out["s_ref"] = (done, zbytes + 6)
     if O.ref_available():
         t0 = time.perf_counter()
         done = 0
@@ -88,10 +91,16 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="text", choices=sorted(WORKLOADS))
     ap.add_argument("--bytes", type=int, default=0, help="override bytes per rank")
-    ap.add_argument("--max-chain", type=int, default=int(os.environ.get("DMX_MAX_CHAIN", "0")))
+    ap.add_argument("--max-chain", type=int, default=int(os.environ.get("DMX_MAX_CHAIN", "8")),
+                    help="0 = exhaustive (reference parse); K = K newest chain entries (default 8)")
+    ap.add_argument("--lazy", type=int, default=int(os.environ.get("DMX_LAZY", "1")),
+                    help="1 = lazy evaluation parse (DMX_F_LAZY, SURVEY §8 f2)")
+    ap.add_argument("--exhaustive-steps", type=int, default=3,
+                    help="also time this many exhaustive-parse steps (reported under 'exhaustive')")
     ap.add_argument("--gather", default="root", choices=["root", "all", "none"])
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds per CPU baseline leg (0 = skip)")
-    ap.add_argument("--traffic-csv", default="", help="rocprofv3 counter CSV (FETCH_SIZE/WRITE_SIZE) for roofline.traffic")
+    ap.add_argument("--traffic-csv", default="",
+                    help="comma-separated rocprofv3 counter CSVs / dirs (FETCH_SIZE and WRITE_SIZE passes)")
     args = ap.parse_args()
 
     import numpy as np
@@ -124,6 +133,8 @@ def main() -> int:
         host = make_input(gen, per_rank, seed + rank)
     n = int(host.size)
     flags = D.DMX_ZLIB if world == 1 else S.shard_flags(rank, world)
+    if args.lazy:
+        flags |= D.DMX_F_LAZY
     enc = D.Encoder(local, n, 32768, args.max_chain, flags)
     d_in = torch.from_numpy(host).to(dev)
     cap = D.max_compressed(n)
@@ -164,6 +175,21 @@ def main() -> int:
     stage_ms, nstage = enc.stage_times()
     enc.set_timing(False)
     dt = t1 - t0
+    exh = None
+    if world == 1 and args.max_chain != 0 and args.exhaustive_steps > 0:
+        # the reference's own parse (every earlier position of the bucket), same input
+        ex = D.Encoder(local, n, 32768, 0, flags & ~D.DMX_F_LAZY)
+        ex.encode_async(d_in.data_ptr(), n, d_out.data_ptr(), cap, stream)
+        ex_len = int(ex.result(stream).out_len)
+        torch.cuda.synchronize(dev)
+        e0 = time.perf_counter()
+        for _ in range(args.exhaustive_steps):
+            ex.encode_async(d_in.data_ptr(), n, d_out.data_ptr(), cap, stream)
+        torch.cuda.synchronize(dev)
+        e1 = time.perf_counter()
+        ex.close()
+        exh = {"value": round(n * args.exhaustive_steps / (e1 - e0) / 1e9, 3), "unit": "GB/s",
+               "ratio": round(ex_len / n, 5), "compressed_bytes": ex_len, "steps": args.exhaustive_steps}
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -182,16 +208,23 @@ def main() -> int:
         algo_bytes = n + out_len   # per launch on this rank: input read + stream written
         achieved = algo_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
         traffic = None
-        if args.traffic_csv and os.path.exists(args.traffic_csv):
+        if args.traffic_csv:
             try:
-                from tools.pmc import traffic_per_launch
-                traffic = traffic_per_launch(args.traffic_csv, f"dmx_{dom}_kernel")
+                import importlib.util
+                spec = importlib.util.spec_from_file_location("pmc", os.path.join(REPO, "tools", "pmc.py"))
+                pmc = importlib.util.module_from_spec(spec)
+                spec.loader.exec_module(pmc)
+                traffic = pmc.traffic_per_launch(args.traffic_csv, f"dmx_{dom}_kernel")
             except Exception as e:  # pragma: no cover
                 log("traffic csv unreadable:", e)
         cpu = {}
         if world == 1 and args.cpu_budget > 0:
-            cpu = cpu_baseline(host, args.max_chain, args.cpu_budget)
+            cpu = cpu_baseline(host, args.cpu_budget)
         base = cpu.get("reference") or cpu.get("port")
+        size_pct = s_ref_bytes = None
+        if "s_ref" in cpu and cpu["s_ref"][0] == n:
+            s_ref_bytes = cpu["s_ref"][1]
+            size_pct = round((out_len / s_ref_bytes - 1) * 100, 3)
         line = {
             "metric": "encode GB/s (uncompressed in) + compression ratio vs CPU ref, 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -209,10 +242,14 @@ def main() -> int:
                 "workload": desc,
                 "bytes_per_rank": n,
                 "block": 32768,
-                "parse": "exhaustive (reference semantics)" if args.max_chain == 0 else f"max_chain={args.max_chain}",
+                "parse": ("exhaustive (reference semantics)" if args.max_chain == 0 else f"max_chain={args.max_chain}")
+                         + (", lazy" if args.lazy else ", greedy"),
                 "parallelism": f"blocks sharded over {world} GPU(s)" + (f", gather={args.gather}" if world > 1 else ""),
             },
             "ratio": round(out_len / n, 5),
+            "size_vs_ref_pct": size_pct,
+            "s_ref_bytes": s_ref_bytes,
+            "exhaustive": exh,
             "compressed_bytes_rank0": out_len,
             "inflate_ok": ok,
             "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
@@ -223,7 +260,8 @@ def main() -> int:
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": traffic,
+                "traffic": traffic["bytes"] if traffic else None,
+                "traffic_detail": traffic,
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "launch_ms": round(dom_ms, 4),
                 "launches_timed": nstage,

@@ -23,7 +23,7 @@ import struct
 __all__ = [
     "DeflateError", "Opts", "Result", "Encoder", "lib", "compress", "deflate_compress",
     "deflate_decompress", "max_compressed", "adler32_combine", "gen_text", "gen_random",
-    "COMPRESS_STATS", "E", "DMX_F_HEADER", "DMX_F_TRAILER", "DMX_F_FINAL", "DMX_ZLIB",
+    "COMPRESS_STATS", "E", "DMX_F_HEADER", "DMX_F_TRAILER", "DMX_F_FINAL", "DMX_ZLIB", "DMX_F_LAZY",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -33,6 +33,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "dmx.h")
 DEFLATE_NULLTERM = 1
 DMX_F_HEADER, DMX_F_TRAILER, DMX_F_FINAL = 1, 2, 4
 DMX_ZLIB = 7
+DMX_F_LAZY = 8
 _M = 1 << 24
 # global_errors.h:64-75 and deflate_errors.h:134-147
 E = {
@@ -143,14 +144,14 @@ def max_compressed(n: int, sw: int = 32768) -> int:
     return int(lib().dmx_max_compressed(n, sw))
 
 
-def compress(data, sw: int = 32768, max_chain: int = 0, flags: int = DMX_ZLIB) -> bytes:
+def compress(data, sw: int = 32768, max_chain: int = 0, flags: int = DMX_ZLIB, lazy: bool = False) -> bytes:
     """Encode a host buffer on the GPU; returns the zlib stream (or raw DEFLATE with flags)."""
     L = lib()
     p, n, keep = _buf(data)
     cap = max_compressed(n, sw)
     out = ctypes.create_string_buffer(cap)
     olen = ctypes.c_uint64(0)
-    o = Opts(sw, max_chain, flags, 0)
+    o = Opts(sw, max_chain, flags | (DMX_F_LAZY if lazy else 0), 0)
     _check(L.dmx_encode_host(p, n, out, cap, ctypes.byref(olen), ctypes.byref(o)), "dmx_encode_host")
     del keep
     return out.raw[:olen.value]

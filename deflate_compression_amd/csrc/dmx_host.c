@@ -161,6 +161,8 @@ int deflate_compress(int fd_in, int fd_out, int fd_stats, swi sw, int ops) {
     o.sw = swv;
     o.max_chain = mc ? atoi(mc) : 0;
     o.flags = DMX_ZLIB;
+    const char* lz = getenv("DMX_LAZY");   /* 1 = lazy evaluation (DMX_F_LAZY); default greedy */
+    if (lz && atoi(lz) > 0) o.flags |= DMX_F_LAZY;
     o.reserved = 0;
     uint8_t* in = NULL;
     uint64_t n = 0;

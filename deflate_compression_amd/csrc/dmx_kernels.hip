@@ -239,6 +239,9 @@ __device__ __forceinline__ uint32_t adv_of(const MatchLDS& L, uint32_t p) {
 // (:249-263).  A lane stops comparing once its best is the longest possible length.
 #define KD 32
 #define CW 4
+__device__ __forceinline__ uint32_t ffbl(uint32_t x) {   // lowest set bit, ~0 for 0 (v_ffbl_b32)
+    return x ? (uint32_t)__builtin_ctz(x) : 0xFFFFFFFFu;
+}
 __device__ __forceinline__ uint32_t match_bytes(uint64_t x) {   // equal leading bytes of an 8-byte xor
     return x ? ((uint32_t)__builtin_ctzll(x) >> 3) : 8u;
 }
@@ -278,8 +281,21 @@ __device__ __forceinline__ uint32_t dpp_shr(uint32_t v, int n) {
     }
 }
 
+// Inclusive prefix sum over the wave: DPP row shifts inside each row of 16, row totals by readlane.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    const uint32_t r = threadIdx.x & 15, row = (threadIdx.x & 63) >> 4;
+    uint32_t y;
+    y = dpp_shr(x, 1); if (r >= 1) x += y;
+    y = dpp_shr(x, 2); if (r >= 2) x += y;
+    y = dpp_shr(x, 4); if (r >= 4) x += y;
+    y = dpp_shr(x, 8); if (r >= 8) x += y;
+    const uint32_t t0 = __builtin_amdgcn_readlane(x, 15), t1 = __builtin_amdgcn_readlane(x, 31),
+                   t2 = __builtin_amdgcn_readlane(x, 47);
+    return x + (row >= 1 ? t0 : 0u) + (row >= 2 ? t1 : 0u) + (row >= 3 ? t2 : 0u);
+}
+
 __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint16_t* __restrict__ pg,
-                                     uint32_t tid) {
+                                     uint32_t tid, bool stamp, uint64_t& tdef) {
     const uint32_t lane = tid & 63, wave = tid >> 6;
     const uint32_t K = max_chain > 0 ? (uint32_t)max_chain : 0xFFFFFFFFu;
     const uint32_t nvalid = bn > 2 ? bn - 2 : 0;   // positions with a full trigram = entries of S
@@ -288,25 +304,24 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
         const uint32_t k = k0 + lane;
         const bool act = k < nvalid;
         uint32_t i = 0, nc = 0, lim = 0, bestkey = 0;
-        uint64_t iv0 = 0, iv1 = 0;
+        uint64_t iv0 = 0;
         if (act) {
             i = L.sorted[k];
             iv0 = ld8(L.data, i);
-            iv1 = ld8(L.data, i + 8);
             const uint32_t rank = k - (uint32_t)L.bstart[dmx_hash((uint32_t)iv0 & 0xFFFFFFu)];
             nc = min(rank, K);
             lim = (bn - i) < MAXLEN ? (bn - i) : MAXLEN;
         }
         // halo: lane l < KD holds entry k0-1-l
         uint32_t hq = 0;
-        uint64_t hv0 = 0, hv1 = 0;
+        uint64_t hv0 = 0;
         if (lane < KD && k0 >= lane + 1) {
             hq = L.sorted[k0 - 1 - lane];
             hv0 = ld8(L.data, hq);
-            hv1 = ld8(L.data, hq + 8);
         }
-        uint32_t xq = i, x0l = (uint32_t)iv0, x0h = (uint32_t)(iv0 >> 32), x1l = (uint32_t)iv1, x1h = (uint32_t)(iv1 >> 32);
-        const uint32_t h0l = (uint32_t)hv0, h0h = (uint32_t)(hv0 >> 32), h1l = (uint32_t)hv1, h1h = (uint32_t)(hv1 >> 32);
+        uint32_t xq = i, x0 = (uint32_t)iv0, x1 = (uint32_t)(iv0 >> 32);
+        const uint32_t i0 = (uint32_t)iv0, i1 = (uint32_t)(iv0 >> 32);
+        const uint32_t h0 = (uint32_t)hv0, h1 = (uint32_t)(hv0 >> 32);
         // wave-uniform bound: the largest chain length of the chunk, capped at KD
         uint32_t jmax = act ? min(nc, (uint32_t)KD) : 0;
         jmax = max(jmax, dpp_shr(jmax, 1));
@@ -316,28 +331,63 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
         jmax = max(max(__builtin_amdgcn_readlane(jmax, 15), __builtin_amdgcn_readlane(jmax, 31)),
                    max(__builtin_amdgcn_readlane(jmax, 47), __builtin_amdgcn_readlane(jmax, 63)));
         const uint32_t lim_eff = act ? lim : 0;
+        uint32_t full = 0;   // bit j-1: candidate j matches all 8 bytes (length still open)
         for (uint32_t j = 1; j <= jmax; j++) {
             iters++;
             const int src = (int)j - 1;
             xq = wshr(xq, __builtin_amdgcn_readlane(hq, src));
-            x0l = wshr(x0l, __builtin_amdgcn_readlane(h0l, src));
-            x0h = wshr(x0h, __builtin_amdgcn_readlane(h0h, src));
-            x1l = wshr(x1l, __builtin_amdgcn_readlane(h1l, src));
-            x1h = wshr(x1h, __builtin_amdgcn_readlane(h1h, src));
-            // straight-line compare of the 16 shifted bytes (no branches on the common path)
-            const uint32_t m0 = match_bytes(iv0 ^ (((uint64_t)x0h << 32) | x0l));
-            const uint32_t m1 = match_bytes(iv1 ^ (((uint64_t)x1h << 32) | x1l));
-            uint32_t m = m0 < 8 ? m0 : 8 + m1;
-            const bool valid = j <= nc;                    // candidate j exists (act folded into lim_eff)
-            m = min(m, lim_eff);
-            const uint32_t bl = bestkey >> 15;
-            const bool ext = valid && m == 16 && lim_eff > 16 && bl < lim_eff;
-            if (__ballot(ext)) {                           // rare: a candidate matching >= 16 bytes
-                if (ext && (bl < 16 || may_beat(L, i, xq, bl))) m = min(ext_len(L, i, xq, 16, lim_eff), lim_eff);
-            }
-            const uint32_t key = (valid && m >= 3) ? ((m << 15) | xq) : 0u;
-            bestkey = max(bestkey, key);
+            x0 = wshr(x0, __builtin_amdgcn_readlane(h0, src));
+            x1 = wshr(x1, __builtin_amdgcn_readlane(h1, src));
+            // equal leading bytes of the 8-byte window, branch-free: ffbl(0) = ~0
+            const uint32_t m8 = min(ffbl(i0 ^ x0), min(ffbl(i1 ^ x1), 32u) + 32u) >> 3;
+            const bool valid = j <= nc;
+            const uint32_t m = min(m8, lim_eff);
+            bestkey = max(bestkey, (valid && m >= 3) ? ((m << 15) | xq) : 0u);
+            full |= (valid && m8 == 8 && lim_eff > 8) ? (1u << src) : 0u;
         }
+        const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
+        // Candidates matching all 8 bytes (any of them beats every key above): exact length
+        // from LDS.  Round 1: each lane's nearest one; a lane whose best is then the longest
+        // possible is done (runs end here).  The rest are spread over the wave's lanes through
+        // an LDS queue (one round for typical text instead of max-popcount rounds) and merged
+        // with atomicMax on the key, which orders longest, then nearest.
+        if (__ballot(full != 0)) {
+            if (full) {
+                const uint32_t j = (uint32_t)__builtin_ctz(full) + 1u;
+                full &= full - 1u;
+                const uint32_t q = L.sorted[k - j];
+                const uint32_t len = min(ext_len(L, i, q, 8, lim_eff), lim_eff);
+                bestkey = max(bestkey, (len << 15) | q);
+            }
+            if ((bestkey >> 15) >= lim_eff) full = 0;
+            const uint32_t cnt = __popc(full);
+            const uint32_t incl = wave_incl_scan(cnt);
+            const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
+            volatile uint32_t* Q = L.tsm + (wave << 6);     // P2 arrays, free during the search
+            volatile uint32_t* B = L.exitp + (wave << 6);
+            for (uint32_t base = 0; base < T; base += 64) {
+                B[lane] = 0;
+                uint32_t f = full, idx = incl - cnt;
+                while (f) {
+                    const uint32_t j = (uint32_t)__builtin_ctz(f) + 1u;
+                    f &= f - 1u;
+                    if (idx >= base && idx < base + 64) Q[idx - base] = (k - j) | (lane << 16);
+                    idx++;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (base + lane < T) {
+                    const uint32_t it = Q[lane], o = it >> 16;
+                    const uint32_t q = L.sorted[it & 0xFFFFu], ii = L.sorted[k0 + o];
+                    const uint32_t lo = min(bn - ii, (uint32_t)MAXLEN);
+                    const uint32_t len = min(ext_len(L, ii, q, 8, lo), lo);
+                    atomicMax((uint32_t*)&B[o], (len << 15) | q);
+                }
+                __builtin_amdgcn_wave_barrier();
+                bestkey = max(bestkey, (uint32_t)B[lane]);
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
         // chains longer than KD (exhaustive mode): continue from LDS, CW candidates per iteration
         for (uint32_t c = KD;; c += CW) {
             const bool more = act && c < nc && (bestkey >> 15) < lim;
@@ -367,8 +417,10 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
                 L.len8[i] = 0;
             } else {
                 L.len8[i] = (uint8_t)((bestkey >> 15) - 3);
-                pg[i] = (uint16_t)(i - (bestkey & 0x7FFFu));
             }
+            // distance in bucket order: one coalesced 128-byte store per wave (a store to
+            // pg[i] would scatter 2-byte partial-line writes over the block)
+            pg[k] = (uint16_t)(bestkey ? i - (bestkey & 0x7FFFu) : 0u);
         }
     }
     // the last two positions have no trigram: literals
@@ -399,12 +451,12 @@ __device__ __forceinline__ uint32_t resolve_word(const MatchLDS& L, uint32_t lo,
 }
 
 __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
-                                                       int32_t max_chain, uint16_t* __restrict__ rank_dist_g,
+                                                       int32_t max_chain, uint32_t lazy, uint16_t* __restrict__ rank_dist_g,
                                                        const uint16_t* __restrict__ start_g,
                                                        uint32_t* __restrict__ tok_g, uint32_t* __restrict__ hist_g,
                                                        dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg) {
     __shared__ MatchLDS L;
-    __shared__ uint64_t st_search, st_iters, st_w1, st_w23;
+    __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t b = blockIdx.x;
     const uint64_t off = (uint64_t)b * sw;
@@ -415,8 +467,9 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
     uint8_t* D8 = reinterpret_cast<uint8_t*>(L.data);
 
     // ---- P0: stage the block, the bucket starts and the bucket-sorted positions in LDS ----
+    const uint64_t tbeg = dbg ? __builtin_amdgcn_s_memtime() : 0;
     if (tid == 0) { L.adl_s = 0; L.adl_t = 0; }
-    if (dbg && tid == 0) { st_search = 0; st_iters = 0; }
+    if (dbg && tid == 0) { st_search = 0; st_iters = 0; st_def = 0; }
     for (uint32_t k = tid; k < DMX_HIST; k += MT) L.hist[k] = 0;
     for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) L.lit[k] = 0;
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
@@ -480,13 +533,40 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
 
     // ---- P1: longest match of every position ----
     const uint64_t t0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
-    const uint32_t its = search_positions(L, bn, max_chain, pg, tid);
+    uint64_t tdef = 0;
+    const uint32_t its = search_positions(L, bn, max_chain, pg, tid, dbg != nullptr, tdef);
     if (dbg && lane == 0) {
         atomicAdd((unsigned long long*)&st_iters, (unsigned long long)its);
         atomicMax((unsigned long long*)&st_search, (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
+        atomicMax((unsigned long long*)&st_def, (unsigned long long)tdef);
     }
     __syncthreads();
     const uint64_t t1 = dbg ? __builtin_amdgcn_s_memtime() : 0;
+
+    // ---- P1b (DMX_F_LAZY): lazy evaluation as a per-position rule on the search results.
+    // Position p (a match) becomes a literal when p+1 holds a strictly longer match; the
+    // walk below then emits the literal and re-decides at p+1 -- exactly the sequential
+    // rule of dmx_oracle_parse_block_ex.  Each thread owns one 32-position literal word.
+    if (lazy) {
+        const uint32_t lw = L.lit[tid];
+        const uint32_t nb0 = (tid + 1 < DMX_BLK / 32) ? (L.lit[tid + 1] & 1u) : 1u;
+        const uint32_t* l32 = reinterpret_cast<const uint32_t*>(L.len8);
+        uint32_t lv[9];
+#pragma unroll
+        for (int j = 0; j < 8; j++) lv[j] = l32[tid * 8 + j];
+        lv[8] = (tid + 1 < DMX_BLK / 32) ? l32[tid * 8 + 8] : 0u;
+        const uint32_t litn = (lw >> 1) | (nb0 << 31);   // literal bit of p+1
+        uint32_t longer = 0;                              // len(p+1) > len(p)
+#pragma unroll
+        for (int bb = 0; bb < 32; bb++) {
+            const uint32_t cur = (lv[bb >> 2] >> (8 * (bb & 3))) & 0xFFu;
+            const uint32_t nxt = (lv[(bb + 1) >> 2] >> (8 * ((bb + 1) & 3))) & 0xFFu;
+            longer |= (nxt > cur ? 1u : 0u) << bb;
+        }
+        __syncthreads();
+        L.lit[tid] = lw | (~lw & ~litn & longer);
+        __syncthreads();
+    }
 
     // ---- P2: greedy path ----
     {   // W1: speculative walk of every 32-position segment from its start
@@ -496,12 +576,29 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         L.tsm[tid] = m;
         L.exitp[tid] = p;
     }
-    {   // the sorted positions are dead: stage the best distances in their LDS slots
+    {   // the sorted positions are dead: permute the best distances (bucket order in pg)
+        // into position order in the same LDS slots, through registers (32 per thread)
         __syncthreads();
-        const uint32_t nch = (bn * 2 + 15) >> 4;
-        const uint4* src = reinterpret_cast<const uint4*>(pg);
-        uint4* dst = reinterpret_cast<uint4*>(L.sorted);
-        for (uint32_t k = tid; k < nch; k += MT) dst[k] = src[k];
+        const uint32_t nvalid = bn > 2 ? bn - 2 : 0;
+        uint4 dv[4], pv[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t c = tid + (uint32_t)j * MT;   // 8 entries per 16-byte chunk
+            const bool in = c * 8 < nvalid;
+            dv[j] = in ? reinterpret_cast<const uint4*>(pg)[c] : make_uint4(0, 0, 0, 0);
+            pv[j] = in ? reinterpret_cast<const uint4*>(L.sorted)[c] : make_uint4(0, 0, 0, 0);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t dw[4] = {dv[j].x, dv[j].y, dv[j].z, dv[j].w}, pw[4] = {pv[j].x, pv[j].y, pv[j].z, pv[j].w};
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const uint32_t kk = (tid + (uint32_t)j * MT) * 8 + (uint32_t)e;
+                if (kk < nvalid)
+                    L.sorted[(pw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu] = (uint16_t)(dw[e >> 1] >> (16 * (e & 1)));
+            }
+        }
     }
     if (dbg && tid == 0) st_w1 = __builtin_amdgcn_s_memtime() - t1;
     {   // W2: each wave resolves its 64 segments assuming it is entered at 2048*wave.
@@ -589,13 +686,14 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
     __syncthreads();
     for (uint32_t k = tid; k < DMX_HIST; k += MT) hist_g[(uint64_t)b * DMX_HIST + k] = L.hist[k];
     if (dbg && tid == 0) {
-        dbg[(uint64_t)b * 8 + 0] = 0;
+        dbg[(uint64_t)b * 8 + 0] = t0 - tbeg;
         dbg[(uint64_t)b * 8 + 1] = st_search;
         dbg[(uint64_t)b * 8 + 2] = __builtin_amdgcn_s_memtime() - t1;
-        dbg[(uint64_t)b * 8 + 3] = L.ntok;
+        dbg[(uint64_t)b * 8 + 3] = st_def;
         dbg[(uint64_t)b * 8 + 4] = st_iters;
         dbg[(uint64_t)b * 8 + 5] = st_w1;
         dbg[(uint64_t)b * 8 + 6] = st_w23;
+        dbg[(uint64_t)b * 8 + 7] = __builtin_amdgcn_s_memtime() - tbeg;
     }
     if (tid == 0) {
         info[b].ntok = L.ntok;
@@ -1347,7 +1445,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                            c->bstart);
         if (ev) (void)hipEventRecord(ev[1], s);
         hipLaunchKernelGGL(dmx_match_kernel, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw,
-                           o.max_chain, c->prev, c->bstart, c->tok, c->hist, c->info, dbg);
+                           o.max_chain, (o.flags & DMX_F_LAZY) ? 1u : 0u, c->prev, c->bstart, c->tok, c->hist, c->info, dbg);
         if (ev) (void)hipEventRecord(ev[2], s);
         hipLaunchKernelGGL(dmx_huff_kernel, dim3(nblk), dim3(64), 0, s, c->hist, c->info, c->codes, c->hdr, nblk, o.flags);
         if (ev) (void)hipEventRecord(ev[3], s);

@@ -114,6 +114,9 @@ struct compress_stats {
                             an empty stored block (sync flush) so it is byte-aligned
                             and another shard can be appended */
 #define DMX_ZLIB (DMX_F_HEADER | DMX_F_TRAILER | DMX_F_FINAL)
+#define DMX_F_LAZY 8u    /* parse option: lazy evaluation, one position of
+                            lookahead -- a match at i becomes a literal when the match at
+                            i+1 is strictly longer.  Off = the reference's greedy parse. */
 
 typedef struct {
     int32_t sw;        /* block size 1..32768 (0 = 32768) */

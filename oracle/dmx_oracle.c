@@ -75,57 +75,96 @@ static unsigned orc_hash_mul(const uint8_t* p) {
 
 /* ---- 1. parse ----------------------------------------------------------------- */
 
-/* Parse one block; returns the number of tokens written to tok (<= n). */
-int dmx_oracle_parse_block(const uint8_t* d, int n, int max_chain, int hash_kind,
-                           uint32_t* tok) {
+/* Chain state of one block: every position < `ins` is at the head of its bucket chain. */
+typedef struct {
+    const uint8_t* d;
+    int n, max_chain, hash_kind, ins;
+    uint32_t* head;
+    uint32_t* prev;
+} orc_chains;
+
+static unsigned orc_bucket(const orc_chains* C, int i) {
+    return C->hash_kind == DMX_HASH_MORTON ? orc_hash_morton(C->d + i) : orc_hash_mul(C->d + i);
+}
+
+static void orc_insert_upto(orc_chains* C, int x) {   /* insert every position < x, :312-319 */
+    for (; C->ins < x; C->ins++) {
+        if (C->ins + 2 < C->n) {
+            unsigned h = orc_bucket(C, C->ins);
+            C->prev[C->ins] = C->head[h];
+            C->head[h] = (uint32_t)C->ins;
+        }
+    }
+}
+
+/* Longest match >= 3 at i among the chain (all earlier positions of the bucket, or the
+ * K newest), ties to the nearest; returns its length (< 3: none) and source in *pos. */
+static int orc_search(orc_chains* C, int i, int* pos) {
+    orc_insert_upto(C, i);
+    int best_len = 2, best_pos = -1;
+    const int n = C->n;
+    int lim = n - i < ORC_MAXLEN ? n - i : ORC_MAXLEN;
+    if (lim >= 3) {
+        uint32_t c = C->head[orc_bucket(C, i)];
+        int steps = 0;
+        while (c != ORC_NONE) {                     /* deflate_compress.c:249 */
+            if (C->max_chain > 0 && steps >= C->max_chain) break;
+            steps++;
+            const uint8_t* s = C->d + i;
+            const uint8_t* q = C->d + c;
+            int t = 0;                               /* check_dup_str, :164-180 */
+            while (t < lim && s[t] == q[t]) t++;
+            if (t > best_len) {                      /* strict >, :258 */
+                best_len = t;
+                best_pos = (int)c;
+                if (t == lim) break;                 /* nothing farther can be longer */
+            }
+            c = C->prev[c];
+        }
+    }
+    *pos = best_pos;
+    return best_pos < 0 ? 0 : best_len;
+}
+
+/* Parse one block; returns the number of tokens written to tok (<= n).
+ * lazy = 0: the reference's greedy parse.  lazy = 1 (RFC 1951 §4
+ * "lazy evaluation", one position of lookahead): a match at i is deferred -- i becomes
+ * a literal -- when the match at i+1 is strictly longer; the same rule then applies at
+ * i+1.  Both matches are searched with the same chains (all positions before them). */
+int dmx_oracle_parse_block_ex(const uint8_t* d, int n, int max_chain, int hash_kind, int lazy,
+                              uint32_t* tok) {
     int ntok = 0;
     if (n <= 0) return 0;
     const int nb = hash_kind == DMX_HASH_MORTON ? 1024 : 8192;
-    uint32_t* head = (uint32_t*)malloc(sizeof(uint32_t) * nb);
-    uint32_t* prev = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n);
-    for (int b = 0; b < nb; b++) head[b] = ORC_NONE;
+    orc_chains C = {d, n, max_chain, hash_kind, 0, (uint32_t*)malloc(sizeof(uint32_t) * nb),
+                    (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n)};
+    for (int b = 0; b < nb; b++) C.head[b] = ORC_NONE;
     int i = 0;
+    int cached = -1, cached_len = 0, cached_pos = -1;   /* the lookahead result at i+1 */
     while (i < n) {
-        int best_len = 2, best_pos = -1;
-        int lim = n - i < ORC_MAXLEN ? n - i : ORC_MAXLEN;
-        if (lim >= 3) {
-            unsigned h = hash_kind == DMX_HASH_MORTON ? orc_hash_morton(d + i) : orc_hash_mul(d + i);
-            uint32_t c = head[h];
-            int steps = 0;
-            while (c != ORC_NONE) {                     /* deflate_compress.c:249 */
-                if (max_chain > 0 && steps >= max_chain) break;
-                steps++;
-                const uint8_t* s = d + i;
-                const uint8_t* q = d + c;
-                int t = 0;                               /* check_dup_str, :164-180 */
-                while (t < lim && s[t] == q[t]) t++;
-                if (t > best_len) {                      /* strict >, :258 */
-                    best_len = t;
-                    best_pos = (int)c;
-                    if (t == lim) break;                 /* nothing farther can be longer */
-                }
-                c = prev[c];
-            }
+        int pos, len;
+        if (cached == i) { len = cached_len; pos = cached_pos; }
+        else len = orc_search(&C, i, &pos);
+        if (len >= 3 && lazy && i + 1 < n) {
+            int pos1, len1 = orc_search(&C, i + 1, &pos1);
+            cached = i + 1; cached_len = len1; cached_pos = pos1;
+            if (len1 > len) len = 0;                  /* defer: literal at i */
         }
-        int adv;
-        if (best_pos < 0) {                              /* literal, :266-272 */
+        if (len < 3) {                                /* literal, :266-272 */
             tok[ntok++] = d[i];
-            adv = 1;
-        } else {                                         /* len/dist, :273-279 */
-            tok[ntok++] = ((uint32_t)(i - best_pos) << 9) | (uint32_t)best_len;
-            adv = best_len;
-        }
-        for (int k = 0; k < adv; k++, i++) {             /* insert every position, :312-319 */
-            if (i + 2 < n) {
-                unsigned h = hash_kind == DMX_HASH_MORTON ? orc_hash_morton(d + i) : orc_hash_mul(d + i);
-                prev[i] = head[h];
-                head[h] = (uint32_t)i;
-            }
+            i += 1;
+        } else {                                      /* len/dist, :273-279 */
+            tok[ntok++] = ((uint32_t)(i - pos) << 9) | (uint32_t)len;
+            i += len;
         }
     }
-    free(head);
-    free(prev);
+    free(C.head);
+    free(C.prev);
     return ntok;
+}
+
+int dmx_oracle_parse_block(const uint8_t* d, int n, int max_chain, int hash_kind, uint32_t* tok) {
+    return dmx_oracle_parse_block_ex(d, n, max_chain, hash_kind, 0, tok);
 }
 
 /* ---- 2. symbols --------------------------------------------------------------- */
@@ -456,8 +495,8 @@ uint32_t dmx_oracle_adler32(const uint8_t* d, size_t n) {
  * -1 if `cap` is too small.  sw = block size (1..32768), max_chain as above.
  * If btypes != NULL it receives the chosen BTYPE of every block.
  */
-long long dmx_oracle_compress(const uint8_t* in, size_t n, int sw, int max_chain, int hash_kind,
-                              uint8_t* out, size_t cap, uint8_t* btypes) {
+long long dmx_oracle_compress_ex(const uint8_t* in, size_t n, int sw, int max_chain, int hash_kind,
+                                 int lazy, uint8_t* out, size_t cap, uint8_t* btypes) {
     if (sw <= 0 || sw > 32768) return -2;
     if (cap < 8) return -1;
     memset(out, 0, cap);
@@ -475,7 +514,7 @@ long long dmx_oracle_compress(const uint8_t* in, size_t n, int sw, int max_chain
     for (size_t b = 0; b < nblk; b++) {
         size_t off = b * (size_t)sw;
         int bn = (int)((n - off) < (size_t)sw ? (n - off) : (size_t)sw);
-        int ntok = dmx_oracle_parse_block(in + off, bn, max_chain, hash_kind, tok);
+        int ntok = dmx_oracle_parse_block_ex(in + off, bn, max_chain, hash_kind, lazy, tok);
         orc_plan_block(tok, ntok, bn, P);
         if (btypes) btypes[b] = (uint8_t)P->btype;
         orc_write_block(&w, in + off, bn, tok, ntok, P, b + 1 == nblk);
@@ -493,6 +532,11 @@ long long dmx_oracle_compress(const uint8_t* in, size_t n, int sw, int max_chain
     tail[2] = (uint8_t)(ad >> 8);
     tail[3] = (uint8_t)ad;
     return (long long)(2 + nbytes + 4);
+}
+
+long long dmx_oracle_compress(const uint8_t* in, size_t n, int sw, int max_chain, int hash_kind,
+                              uint8_t* out, size_t cap, uint8_t* btypes) {
+    return dmx_oracle_compress_ex(in, n, sw, max_chain, hash_kind, 0, out, cap, btypes);
 }
 
 /* Per-block plan, exported for tests: costs and lengths of a token stream. */

@@ -41,15 +41,15 @@ def lib():
         u8p = ctypes.POINTER(ctypes.c_uint8)
         u32p = ctypes.POINTER(ctypes.c_uint32)
         u64p = ctypes.POINTER(ctypes.c_uint64)
-        L.dmx_oracle_parse_block.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, u32p]
-        L.dmx_oracle_parse_block.restype = ctypes.c_int
+        L.dmx_oracle_parse_block_ex.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, u32p]
+        L.dmx_oracle_parse_block_ex.restype = ctypes.c_int
         L.dmx_oracle_huff_lengths.argtypes = [u32p, ctypes.c_int, ctypes.c_int, u8p]
         L.dmx_oracle_huff_lengths.restype = ctypes.c_int
         L.dmx_oracle_adler32.argtypes = [u8p, ctypes.c_size_t]
         L.dmx_oracle_adler32.restype = ctypes.c_uint32
-        L.dmx_oracle_compress.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
-                                          ctypes.c_int, u8p, ctypes.c_size_t, u8p]
-        L.dmx_oracle_compress.restype = ctypes.c_longlong
+        L.dmx_oracle_compress_ex.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int, u8p, ctypes.c_size_t, u8p]
+        L.dmx_oracle_compress_ex.restype = ctypes.c_longlong
         L.dmx_oracle_plan.argtypes = [u32p, ctypes.c_int, ctypes.c_int, u64p, u8p, u8p]
         L.dmx_oracle_plan.restype = ctypes.c_int
         _lib = L
@@ -65,19 +65,19 @@ def _as_u8(data) -> np.ndarray:
         data, np.ndarray) else np.ascontiguousarray(data, dtype=np.uint8)
 
 
-def parse_block(data, max_chain: int = 0, hash_kind: int = HASH_MUL) -> np.ndarray:
+def parse_block(data, max_chain: int = 0, hash_kind: int = HASH_MUL, lazy: bool = False) -> np.ndarray:
     """Token stream (uint32, see dmx_oracle.c header) of one block (<= 32768 bytes)."""
     a = _as_u8(data)
     assert a.size <= 32768
     tok = np.zeros(max(a.size, 1), dtype=np.uint32)
-    n = lib().dmx_oracle_parse_block(_u8(a), a.size, max_chain, hash_kind,
-                                     tok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+    n = lib().dmx_oracle_parse_block_ex(_u8(a), a.size, max_chain, hash_kind, int(lazy),
+                                        tok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
     return tok[:n].copy()
 
 
-def parse(data, sw: int = 32768, max_chain: int = 0, hash_kind: int = HASH_MUL) -> list:
+def parse(data, sw: int = 32768, max_chain: int = 0, hash_kind: int = HASH_MUL, lazy: bool = False) -> list:
     a = _as_u8(data)
-    return [parse_block(a[o:o + sw], max_chain, hash_kind) for o in range(0, a.size, sw)]
+    return [parse_block(a[o:o + sw], max_chain, hash_kind, lazy) for o in range(0, a.size, sw)]
 
 
 def huff_lengths(freq, maxbits: int) -> np.ndarray:
@@ -94,13 +94,13 @@ def adler32(data) -> int:
 
 
 def compress(data, sw: int = 32768, max_chain: int = 0, hash_kind: int = HASH_MUL,
-             want_btypes: bool = False):
+             want_btypes: bool = False, lazy: bool = False):
     a = _as_u8(data)
     nblk = (a.size + sw - 1) // sw
     cap = a.size + 5 * (nblk + 1) + 64
     out = np.zeros(cap, dtype=np.uint8)
     bt = np.zeros(max(nblk, 1), dtype=np.uint8)
-    r = lib().dmx_oracle_compress(_u8(a), a.size, sw, max_chain, hash_kind, _u8(out), cap, _u8(bt))
+    r = lib().dmx_oracle_compress_ex(_u8(a), a.size, sw, max_chain, hash_kind, int(lazy), _u8(out), cap, _u8(bt))
     if r < 0:
         raise RuntimeError(f"oracle compress failed: {r}")
     z = out[:r].tobytes()

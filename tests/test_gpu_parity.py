@@ -108,6 +108,27 @@ def test_bounded_chain_parity(enc, k):
     check_stream(z, data)
 
 
+@pytest.mark.parametrize("k", [0, 1, 4, 8, 16])
+def test_lazy_parity(enc, golden_cases, k):
+    """DMX_F_LAZY: byte-identical to the oracle's sequential lazy parse."""
+    data = (golden_cases["bee0"] + D.gen_text(200000, 12).tobytes() + bytes(5000)
+            + golden_cases["period7"] + D.gen_random(3000, 4).tobytes())
+    z, _ = enc.compress_bytes(data, max_chain=k, flags=D.DMX_ZLIB | D.DMX_F_LAZY)
+    assert z == O.compress(data, max_chain=k, lazy=True)
+    check_stream(z, data)
+
+
+def test_lazy_tokens_and_edges(enc, golden_cases):
+    for n in (0, 1, 2, 3, 4, 9, 258, 259, 32767, 32768, 32771):
+        data = ((golden_cases["bee0"] + golden_cases["bee1"]) * 2)[:n]
+        z, r = enc.compress_bytes(data, flags=D.DMX_ZLIB | D.DMX_F_LAZY)
+        assert z == O.compress(data, lazy=True), n
+        check_stream(z, data)
+    blk = golden_cases["bee0"]
+    enc.compress_bytes(blk, max_chain=8, flags=D.DMX_ZLIB | D.DMX_F_LAZY)
+    assert np.array_equal(enc.tokens(0), O.parse_block(blk, max_chain=8, lazy=True))
+
+
 @pytest.mark.parametrize("sw", [1, 2, 3, 64, 1000, 4095, 4096, 32767, 32768])
 def test_window_sizes(enc, sw):
     data = D.gen_text(70000 if sw >= 64 else 3000, 5).tobytes()

@@ -1,0 +1,104 @@
+"""Multi-rank shard framing + chunk gather, world_size 2 over gloo on CPU.
+
+The encoder itself needs a GPU, so on CPU each rank frames its shard with zlib's raw
+deflate in exactly the shape the HIP path emits (rank 0: zlib header; non-final:
+sync flush = empty stored block; last: BFINAL).  What is under test is the host
+logic that runs unchanged at N>1 on GPUs: shard_range, shard_flags, gather_chunks
+(root point-to-point and all-gather), and the Adler-32 combine + trailer.
+"""
+import os
+import socket
+import zlib
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from deflate_compression_amd import DMX_F_FINAL, DMX_F_HEADER, gen_text
+from deflate_compression_amd import shard as S
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _frame(data: bytes, flags: int) -> bytes:
+    c = zlib.compressobj(6, zlib.DEFLATED, -15)
+    body = c.compress(data) + c.flush(zlib.Z_FINISH if flags & DMX_F_FINAL else zlib.Z_SYNC_FLUSH)
+    return (b"\x78\x9c" if flags & DMX_F_HEADER else b"") + body
+
+
+def _worker(rank, world, port, n, root, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        full = gen_text(n, 7).tobytes()
+        lo, hi = S.shard_range(n, rank, world)
+        mine = full[lo:hi]
+        chunk = _frame(mine, S.shard_flags(rank, world))
+        t = torch.frombuffer(bytearray(chunk + b"\0" * 16), dtype=torch.uint8)  # padded buffer, like d_out
+        outs, lens = S.gather_chunks(t, len(chunk), root=root)
+        # per-shard Adler values are exchanged the same way as the lengths
+        ad = torch.tensor([zlib.adler32(mine), hi - lo], dtype=torch.int64)
+        ads = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(ads, ad)
+        if outs is not None:
+            adler = S.combine_adler([int(a[0]) for a in ads], [int(a[1]) for a in ads])
+            stream = b"".join(bytes(o.numpy()) for o in outs) + S.trailer(adler)
+            q.put((rank, lens, zlib.decompress(stream) == full, adler == zlib.adler32(full)))
+        else:
+            q.put((rank, lens, None, None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("root", [0, None], ids=["p2p_root", "all_gather"])
+@pytest.mark.parametrize("n", [5 * 32768 + 123, 32768, 1000])
+def test_gather_and_stitch_world2(root, n):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, n, root, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    res.sort()
+    lens = res[0][1]
+    assert res[1][1] == lens and len(lens) == world
+    checked = [r for r in res if r[2] is not None]
+    assert len(checked) == (1 if root == 0 else world)
+    for _, _, inflates, adler_ok in checked:
+        assert inflates and adler_ok
+
+
+def test_shard_range_partitions_blocks():
+    for n in [0, 1, 32767, 32768, 32769, 10 * 32768 + 5, 100_000_000]:
+        for world in [1, 2, 3, 8]:
+            rs = [S.shard_range(n, r, world) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            for (a, b), (c, d) in zip(rs, rs[1:]):
+                assert b == c
+            for a, b in rs:
+                assert a % 32768 == 0 and a <= b
+
+
+def test_shard_flags():
+    assert S.shard_flags(0, 1) == DMX_F_HEADER | DMX_F_FINAL
+    assert S.shard_flags(0, 4) == DMX_F_HEADER
+    assert S.shard_flags(2, 4) == 0
+    assert S.shard_flags(3, 4) == DMX_F_FINAL
+
+
+def test_combine_adler_matches_whole():
+    data = np.random.default_rng(3).integers(0, 256, 300_000, dtype=np.uint8).tobytes()
+    cuts = [0, 1, 65536, 65537, 200_000, len(data)]
+    parts = [data[a:b] for a, b in zip(cuts, cuts[1:])]
+    assert S.combine_adler([zlib.adler32(p) for p in parts], [len(p) for p in parts]) == zlib.adler32(data)

@@ -13,10 +13,14 @@ def run(kind, n, mc):
         out, r = e.compress_tensor(t)
     st = e.stamps(r.nblocks).astype(np.float64)
     e.close()
-    print(json.dumps({"kind": kind, "mc": mc, "build_kcyc": round(st[:, 0].mean() / 1e3, 1),
+    print(json.dumps({"kind": kind, "mc": mc, "p0_kcyc": round(st[:, 0].mean() / 1e3, 1),
                       "search_kcyc": round(st[:, 1].mean() / 1e3, 1), "walk_kcyc": round(st[:, 2].mean() / 1e3, 1),
-                      "tokens": round(st[:, 3].mean(), 1), "iters_per_wave": round(st[:, 4].mean() / 16, 1),
-                      "w1_kcyc": round(st[:, 5].mean() / 1e3, 1), "w1w3_kcyc": round(st[:, 6].mean() / 1e3, 1)}))
+                      "deferred_kcyc": round(st[:, 3].mean() / 1e3, 1), "iters_per_wave": round(st[:, 4].mean() / 16, 1),
+                      "w1_kcyc": round(st[:, 5].mean() / 1e3, 1), "w1w3_kcyc": round(st[:, 6].mean() / 1e3, 1),
+                      "total_kcyc": round(st[:, 7].mean() / 1e3, 1)}))
 
-for kind, mc in [("text", 1), ("text", 16), ("text", 0), ("random", 0), ("zeros", 0)]:
+cfgs = [("text", 1), ("text", 16), ("text", 0), ("random", 0), ("zeros", 0)]
+if len(sys.argv) > 1:
+    cfgs = [(a.split(":")[0], int(a.split(":")[1])) for a in sys.argv[1:]]
+for kind, mc in cfgs:
     run(kind, 20_000_000 if kind == "text" else 64 << 20, mc)
