@@ -268,10 +268,11 @@ class Encoder:
         return ln
 
     def stamps(self, nblk: int):
-        """[nblk, 8] {build, search, walk+compaction cycles, tokens, search iterations, W1, W1-W3 cycles, 0}
-        (needs DMX_STAMPS=1)."""
+        """[nblk, 16] match-kernel phase cycles (needs DMX_STAMPS=1): P0, search, walk+compaction,
+        deferred extension, search steps, W1, W1-W3, total, then P0 sub-phase ends (staged,
+        pass 1, pass 2) relative to the kernel start."""
         import numpy as np
-        a = np.zeros((nblk, 8), np.uint64)
+        a = np.zeros((nblk, 16), np.uint64)
         _check(self._L.dmx_debug_stamps(self._ctx, a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), nblk),
                "dmx_debug_stamps")
         return a

@@ -1,17 +1,18 @@
 // dmx_kernels.hip -- the MI355X (gfx950 / CDNA4) hot path of the DEFLATE encoder.
 //
 // The input is cut into independent sw-byte blocks (sw <= 32768 = the window).
-// Per encode, five launches on one HIP stream:
+// Per encode, four launches on one HIP stream:
 //   K1  dmx_match_kernel  one 1024-thread workgroup per block, block staged in LDS.
-//                         Wave 0 builds the hash chains of deflate_compress.c:312-319
-//                         (every position at the head of its bucket) in LDS, 64
-//                         positions per step with ballots;
-//                         all 16 waves search the longest match of EVERY position
-//                         (chain walk of :243-264, newest first, strict >) with
-//                         lane-persistent work distribution,
-//                         then the greedy path 0 -> i + max(len,1) (:265-288) by
-//                         speculative 32-position segments + two fix-up levels,
-//                         token compaction (block scan) and lit/len + dist
+//                         P0: the reference's hash chains (deflate_compress.c:312-319,
+//                         every position at the head of its bucket) as bucket-sorted
+//                         position arrays, by a two-pass LDS radix sort;
+//                         P1: the longest match of EVERY position (chain walk of
+//                         :243-264, newest first, strict >) -- one lane per entry,
+//                         candidates shifted through registers with DPP;
+//                         P2: the greedy path 0 -> i + max(len,1) (:265-288) by
+//                         speculative 32-position segments + two fix-up levels
+//                         (optionally lazy evaluation first, DMX_F_LAZY);
+//                         P3: token compaction (block scan) and lit/len + dist
 //                         histograms.  Tokens -> HBM.
 //   K2  dmx_huff_kernel   one wave per block: length-limited canonical Huffman
 //                         codes, RFC 1951 §3.2.7 header, exact stored/fixed/
@@ -84,115 +85,17 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 }
 
 // ------------------------------------------------------------------------------------
-// K1a: bucket-sorted positions (one wave per block, several blocks per CU)
-// ------------------------------------------------------------------------------------
-
-// Trigram at p (bytes p, p+1, p+2 little-endian; zero past the block end).
-__device__ __forceinline__ uint32_t g_tri(const uint8_t* __restrict__ d, uint32_t p, uint32_t bn) {
-    if (p + 4 <= bn) {
-        uint32_t v;
-        __builtin_memcpy(&v, d + p, 4);   // unaligned global dword (fine for global memory)
-        return v & 0xFFFFFFu;
-    }
-    uint32_t v = 0;
-    for (uint32_t j = 0; j < 3; j++)
-        if (p + j < bn) v |= (uint32_t)d[p + j] << (8 * j);
-    return v;
-}
-
-// The reference's hash chains (deflate_compress.c:312-319: every position goes to the head
-// of its bucket's chain, so the chain of position i lists the earlier positions of its
-// bucket newest first) in array form: S = the block's positions sorted by (bucket,
-// position), built from rank(p) = number of earlier positions in p's bucket and the start
-// of every bucket: S[start(bucket(p)) + rank(p)] = p.  For the entry k of position p = S[k],
-// the chain of p is S[k-1], S[k-2], ..., S[start(bucket)] -- directly indexable, so the
-// match kernel can examine many candidates of one position in parallel.
-// Pass 1 (position order, 64 per step): rank = running count of the bucket + earlier lanes
-// of the step in the same bucket.  Lanes sharing a bucket are grouped by writing the lane
-// id into a byte scratch indexed by the bucket and reading it back (every member reads the
-// same representative): 6 ballots on that id, skipped when every lane reads itself back.
-// Output: rank(p) (u16, NONE for the last two positions, which have no trigram) and the
-// bucket starts (exclusive scan of the counts); the match kernel scatters S in LDS.
-#define CK_PF 4
-__global__ __launch_bounds__(64) void dmx_chain_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
-                                                       uint16_t* __restrict__ rank_g, uint16_t* __restrict__ start_g) {
-    __shared__ uint32_t cnt32[DMX_NBUCKET / 2];
-    __shared__ uint8_t scr_raw[DMX_NBUCKET];
-    uint16_t* cnt = reinterpret_cast<uint16_t*>(cnt32);
-    volatile uint8_t* scr = scr_raw;   // the read-back must see the other lanes' writes
-    const uint32_t lane = threadIdx.x;
-    const uint64_t off = (uint64_t)blockIdx.x * sw;
-    const uint32_t bn = (uint32_t)((n - off) < sw ? (n - off) : sw);
-    const uint8_t* d = in + off;
-    uint16_t* rg = rank_g + (uint64_t)blockIdx.x * DMX_BLK;
-    for (uint32_t k = lane; k < DMX_NBUCKET / 2; k += 64) cnt32[k] = 0;
-    __syncthreads();
-    const uint32_t nsteps = (bn + 63) >> 6;
-    uint32_t ring[CK_PF];
-#pragma unroll
-    for (int j = 0; j < CK_PF; j++) ring[j] = g_tri(d, 64 * j + lane, bn);
-    for (uint32_t s0 = 0; s0 < nsteps; s0 += CK_PF) {
-#pragma unroll
-        for (int j = 0; j < CK_PF; j++) {
-            const uint32_t s = s0 + j;
-            if (s >= nsteps) break;
-            const uint32_t p = (s << 6) + lane;
-            const uint32_t tri = ring[j];
-            ring[j] = g_tri(d, p + 64 * CK_PF, bn);   // CK_PF steps ahead
-            const bool valid = p + 2 < bn;
-            const uint32_t h = dmx_hash(tri);
-            if (valid) scr[h] = (uint8_t)lane;
-            const uint32_t rep = valid ? (uint32_t)scr[h] : lane;
-            uint64_t eq = 1ull << lane;
-            if (__ballot(rep != lane)) {
-                eq = __ballot(valid);
-#pragma unroll
-                for (int bit = 0; bit < 6; bit++) {
-                    const bool hb = (rep >> bit) & 1;
-                    const uint64_t m = __ballot(hb);
-                    eq &= hb ? m : ~m;
-                }
-            }
-            uint32_t rank = 0;
-            if (valid) rank = (uint32_t)cnt[h] + (uint32_t)__popcll(eq & ((1ull << lane) - 1));
-            if (valid && !(eq & ~((2ull << lane) - 1))) cnt[h] = (uint16_t)(rank + 1);
-            if (p < bn) rg[p] = valid ? (uint16_t)rank : DMX_NONE16;
-        }
-    }
-    __syncthreads();
-    {   // exclusive scan of the bucket counts (128 per lane), in place -> bucket starts
-        uint32_t run = 0;
-        for (uint32_t k = 0; k < DMX_NBUCKET / 64; k++) run += cnt[lane * (DMX_NBUCKET / 64) + k];
-        uint32_t x = run;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o);
-            if (lane >= (uint32_t)o) x += y;
-        }
-        uint32_t acc = x - run;
-        for (uint32_t k = 0; k < DMX_NBUCKET / 64; k++) {
-            const uint32_t j = lane * (DMX_NBUCKET / 64) + k;
-            const uint32_t c = cnt[j];
-            cnt[j] = (uint16_t)acc;
-            acc += c;
-        }
-    }
-    __syncthreads();
-    uint16_t* stg = start_g + (uint64_t)blockIdx.x * DMX_NBUCKET;   // bucket starts for the match kernel
-    for (uint32_t k = lane; k < DMX_NBUCKET / 2; k += 64) reinterpret_cast<uint32_t*>(stg)[k] = cnt32[k];
-}
-
-// ------------------------------------------------------------------------------------
-// K1b: longest match of every position + greedy path + compaction
+// K1: bucket-sorted chains + longest match of every position + greedy path + compaction
 // ------------------------------------------------------------------------------------
 
 #define MT 1024
 #define MW (MT / 64)
+#define DMX_STAMPS 16   // diagnostic u64 stamps per block (DMX_STAMPS=1 in the environment)
 #define DATA_WORDS 8208   // 32 KiB + slack for 32-byte extension reads past the end (zeroed)
 
 struct __attribute__((aligned(16))) MatchLDS {
     uint32_t data[DATA_WORDS];    // the block, zero padded
-    uint16_t sorted[DMX_BLK];     // positions sorted by (bucket, position) (K1a); after the search: best distances
+    uint16_t sorted[DMX_BLK];     // positions sorted by (bucket, position) (P0); after the search: best distances
     uint16_t bstart[DMX_NBUCKET]; // start of every bucket in `sorted`
     uint8_t len8[DMX_BLK];        // best length - 3 (matches)
     uint32_t lit[DMX_BLK / 32];   // 1 = literal at that position
@@ -227,7 +130,7 @@ __device__ __forceinline__ uint32_t adv_of(const MatchLDS& L, uint32_t p) {
 // Longest match (>= 3, ties to the nearest) of every position, deflate_compress.c:243-264.
 // Work unit = one entry k of the bucket-sorted array S (position i = S[k]); a wave takes
 // 64 consecutive entries (lane = entry), waves take chunks round-robin.  The chain of
-// entry k is S[k-1], S[k-2], ..., S[start(bucket)] (newest first, K1a), capped at K.
+// entry k is S[k-1], S[k-2], ..., S[start(bucket)] (newest first, P0), capped at K.
 // Candidate j of lane l is entry k-j -- the entry j lanes below -- so every lane loads
 // only its OWN position and first 16 bytes once, and the wave shifts (position, 16 bytes)
 // down one lane per step with DPP wave_shr:1; lane 0 is fed from a halo of the KD
@@ -279,6 +182,16 @@ __device__ __forceinline__ uint32_t dpp_shr(uint32_t v, int n) {
         case 4: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);
         default: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);
     }
+}
+
+// LDS word accesses shared between lanes of one wave: relaxed workgroup-scope atomics keep
+// them as plain ds_read/ds_write and stop the compiler from caching or reordering them
+// (a volatile cast would drop the LDS address space and go through flat memory).
+__device__ __forceinline__ uint32_t lds_ld(uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // Inclusive prefix sum over the wave: DPP row shifts inside each row of 16, row totals by readlane.
@@ -363,27 +276,27 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
             const uint32_t cnt = __popc(full);
             const uint32_t incl = wave_incl_scan(cnt);
             const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
-            volatile uint32_t* Q = L.tsm + (wave << 6);     // P2 arrays, free during the search
-            volatile uint32_t* B = L.exitp + (wave << 6);
+            uint32_t* Q = L.tsm + (wave << 6);     // P2 arrays, free during the search
+            uint32_t* B = L.exitp + (wave << 6);
             for (uint32_t base = 0; base < T; base += 64) {
-                B[lane] = 0;
+                lds_st(&B[lane], 0u);
                 uint32_t f = full, idx = incl - cnt;
                 while (f) {
                     const uint32_t j = (uint32_t)__builtin_ctz(f) + 1u;
                     f &= f - 1u;
-                    if (idx >= base && idx < base + 64) Q[idx - base] = (k - j) | (lane << 16);
+                    if (idx >= base && idx < base + 64) lds_st(&Q[idx - base], (k - j) | (lane << 16));
                     idx++;
                 }
                 __builtin_amdgcn_wave_barrier();
                 if (base + lane < T) {
-                    const uint32_t it = Q[lane], o = it >> 16;
+                    const uint32_t it = lds_ld(&Q[lane]), o = it >> 16;
                     const uint32_t q = L.sorted[it & 0xFFFFu], ii = L.sorted[k0 + o];
                     const uint32_t lo = min(bn - ii, (uint32_t)MAXLEN);
                     const uint32_t len = min(ext_len(L, ii, q, 8, lo), lo);
-                    atomicMax((uint32_t*)&B[o], (len << 15) | q);
+                    __hip_atomic_fetch_max(&B[o], (len << 15) | q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
                 __builtin_amdgcn_wave_barrier();
-                bestkey = max(bestkey, (uint32_t)B[lane]);
+                bestkey = max(bestkey, lds_ld(&B[lane]));
                 __builtin_amdgcn_wave_barrier();
             }
         }
@@ -450,20 +363,62 @@ __device__ __forceinline__ uint32_t resolve_word(const MatchLDS& L, uint32_t lo,
     return p;
 }
 
+// Lanes of the wave holding the same value v as this lane (among the valid lanes): every
+// lane ORs its bit into the wave's slot G[v] and reads the slot back (LDS executes a wave's
+// instructions in order, so the read sees all ORs), then the slot is cleared for reuse.
+// 3 LDS instructions instead of one ballot per bit of v.
+__device__ __forceinline__ uint64_t group_of(unsigned long long* G, uint32_t v, bool valid) {
+    uint64_t eq = 0;
+    if (valid) {
+        __hip_atomic_fetch_or(&G[v], 1ull << (threadIdx.x & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        eq = __hip_atomic_load(&G[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&G[v], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return eq;
+}
+
+// T[v] += 1 for every valid lane (pair16: T holds two u16 counters per word); a single
+// add when the valid lanes share v (runs), instead of a 64-way conflicting LDS atomic.
+__device__ __forceinline__ void count_add(uint32_t* T, uint32_t v, bool valid, bool pair16) {
+    const uint64_t vm = __ballot(valid);
+    if (vm == 0) return;
+    const uint32_t first = (uint32_t)__builtin_ctzll(vm);
+    const uint32_t v0 = __builtin_amdgcn_readlane(v, (int)first);
+    if (__ballot(valid && v != v0) == 0) {
+        if ((threadIdx.x & 63) == first) {
+            const uint32_t c = (uint32_t)__popcll(vm);
+            if (pair16) atomicAdd(&T[v0 >> 1], c << (16 * (v0 & 1)));
+            else atomicAdd(&T[v0], c);
+        }
+    } else if (valid) {
+        if (pair16) atomicAdd(&T[v >> 1], 1u << (16 * (v & 1)));
+        else atomicAdd(&T[v], 1u);
+    }
+}
+
+// Exclusive prefix sum over the 1024 threads of the workgroup (all threads call it).
+__device__ __forceinline__ uint32_t block_excl_scan(MatchLDS& L, uint32_t v, uint32_t tid) {
+    const uint32_t incl = wave_incl_scan(v);
+    if ((tid & 63) == 63) L.wsum[tid >> 6] = incl;
+    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t w = 0; w < (tid >> 6); w++) base += L.wsum[w];
+    __syncthreads();
+    return base + incl - v;
+}
+
 __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
-                                                       int32_t max_chain, uint32_t lazy, uint16_t* __restrict__ rank_dist_g,
-                                                       const uint16_t* __restrict__ start_g,
+                                                       int32_t max_chain, uint32_t lazy, uint16_t* __restrict__ dist_g,
                                                        uint32_t* __restrict__ tok_g, uint32_t* __restrict__ hist_g,
                                                        dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg) {
     __shared__ MatchLDS L;
-    __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def;
+    __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def, tp0[3];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t b = blockIdx.x;
     const uint64_t off = (uint64_t)b * sw;
     const uint32_t bn = (uint32_t)((n - off) < sw ? (n - off) : sw);
     const uint8_t* d = in + off;
-    uint16_t* pg = rank_dist_g + (uint64_t)b * DMX_BLK;   // ranks in; best distances out (same slots)
-    const uint16_t* stg = start_g + (uint64_t)b * DMX_NBUCKET;
+    uint16_t* pg = dist_g + (uint64_t)b * DMX_BLK;   // best distances, bucket order (staging)
     uint8_t* D8 = reinterpret_cast<uint8_t*>(L.data);
 
     // ---- P0: stage the block, the bucket starts and the bucket-sorted positions in LDS ----
@@ -486,33 +441,127 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         }
         *reinterpret_cast<uint4*>(&L.data[k << 2]) = v;
     }
+    // Bucket-sorted positions S (stable by position inside a bucket) and bucket starts,
+    // built here instead of by a separate chain pass: a two-pass LSD radix sort of the
+    // positions by bucket, digit 1 = bucket & 127, digit 2 = bucket >> 7.  Wave w owns the
+    // 2048 entries [2048w, 2048w+2048) of a pass.  Sweep A counts (digit, wave) with LDS
+    // atomics (order-free); an exclusive scan, digit-major, turns the counts into
+    // destinations; sweep B walks the entries again, 64 per step, groups the lanes with
+    // equal digits by ballots (stable in lane order) and writes entry -> destination +
+    // earlier lanes of its group, advancing the (digit, wave) destination.  Pass 2 reads
+    // its source (the pass-1 order) into registers first, so it can write S in place.
+    // Bucket starts = exclusive scan of a bucket histogram taken in pass 1.
     {
-        const uint4* bs = reinterpret_cast<const uint4*>(stg);
-        uint4* bd = reinterpret_cast<uint4*>(L.bstart);
-        for (uint32_t k = tid; k < DMX_NBUCKET * 2 / 16; k += MT) bd[k] = bs[k];
-    }
-    __syncthreads();
-    {   // S[start(bucket(p)) + rank(p)] = p (scatter in LDS); ranks read as 16-byte vectors,
-        // all four loads in flight before the first use
-        uint4 rv[4];
+        const uint32_t nvalid = bn > 2 ? bn - 2 : 0;   // positions with a full trigram
+        uint32_t* C = L.tsm;                              // 16 x 128 digit counters (tsm + exitp)
+        uint32_t* H = reinterpret_cast<uint32_t*>(L.len8);   // 8192 bucket counts, u16 pairs
+        unsigned long long* G = reinterpret_cast<unsigned long long*>(L.len8 + DMX_BLK / 2);   // 16 x 128 lane masks
+        unsigned long long* Gw = G + (wave << 7);
+        for (uint32_t k = tid; k < 2 * (DMX_BLK / 32); k += MT) C[k] = 0;
+        for (uint32_t k = tid; k < DMX_NBUCKET / 2; k += MT) H[k] = 0;
+        for (uint32_t k = tid; k < 16 * 128; k += MT) G[k] = 0;
+        __syncthreads();
+        if (dbg && tid == 0) tp0[0] = __builtin_amdgcn_s_memtime();
+        const uint64_t lt = (1ull << lane) - 1ull;
+        const uint32_t x0 = (wave << 11) + lane;
+        // bucket of each of this lane's 32 entries, two 13-bit values per register; all
+        // 32 loads in flight at once
+        uint32_t hh[16];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t c4 = tid + (uint32_t)j * MT;
-            rv[j] = (c4 * 8 < bn) ? reinterpret_cast<const uint4*>(pg)[c4] : make_uint4(~0u, ~0u, ~0u, ~0u);
+        for (int st = 0; st < 32; st += 2) {
+            const uint32_t xa = x0 + ((uint32_t)st << 6), xb = xa + 64;
+            const uint32_t ha = xa < nvalid ? dmx_hash(ld4(L.data, xa) & 0xFFFFFFu) : 0u;
+            const uint32_t hb = xb < nvalid ? dmx_hash(ld4(L.data, xb) & 0xFFFFFFu) : 0u;
+            hh[st >> 1] = ha | (hb << 16);
+            if ((st & 7) == 6) __builtin_amdgcn_sched_barrier(0);   // 8 loads in flight per group
         }
+        // ---- pass 1: position order, digit = bucket & 127
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t w[4] = {rv[j].x, rv[j].y, rv[j].z, rv[j].w};
+        for (int st = 0; st < 32; st++) {
+            const uint32_t x = x0 + ((uint32_t)st << 6);
+            const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
+            count_add(H, h, x < nvalid, true);
+            count_add(C + (wave << 7), h & 127u, x < nvalid, false);
+        }
+        __syncthreads();
+        {   // destinations, digit-major: entry (dg, w) at order 16*dg + w; two per thread
+            const uint32_t o0 = tid * 2, o1 = o0 + 1;
+            const uint32_t i0 = ((o0 & 15) << 7) + (o0 >> 4), i1 = ((o1 & 15) << 7) + (o1 >> 4);
+            const uint32_t v0 = C[i0], v1 = C[i1];
+            const uint32_t ex = block_excl_scan(L, v0 + v1, tid);
+            C[i0] = ex;
+            C[i1] = ex + v0;
+        }
+        __syncthreads();
 #pragma unroll
-            for (int e = 0; e < 8; e++) {
-                const uint32_t p = (tid + (uint32_t)j * MT) * 8 + (uint32_t)e;
-                const uint32_t r = (w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
-                if (p < bn && r != DMX_NONE16)
-                    L.sorted[(uint32_t)L.bstart[dmx_hash(ld4(L.data, p) & 0xFFFFFFu)] + r] = (uint16_t)p;
+        for (int st = 0; st < 32; st++) {
+            const uint32_t x = x0 + ((uint32_t)st << 6);
+            const bool valid = x < nvalid;
+            const uint32_t dg = (hh[st >> 1] >> (16 * (st & 1))) & 127u;
+            const uint64_t eq = group_of(Gw, dg, valid);
+            const uint32_t c = valid ? C[(wave << 7) + dg] : 0u;
+            if (valid) {
+                L.sorted[c + (uint32_t)__popcll(eq & lt)] = (uint16_t)x;
+                if ((eq >> lane) == 1ull) C[(wave << 7) + dg] = c + (uint32_t)__popcll(eq);
             }
         }
+        __syncthreads();
+        if (dbg && tid == 0) tp0[1] = __builtin_amdgcn_s_memtime();
+        // ---- pass 2: pass-1 order, digit = bucket >> 7
+        for (uint32_t k = tid; k < 16 * 64; k += MT) C[k] = 0;
+        uint32_t pk[16];   // this lane's 32 source entries, two u16 per register
+#pragma unroll
+        for (int st = 0; st < 32; st += 2) {
+            const uint32_t xa = x0 + ((uint32_t)st << 6), xb = xa + 64;
+            const uint32_t pa = xa < nvalid ? (uint32_t)L.sorted[xa] : 0u;
+            const uint32_t pb = xb < nvalid ? (uint32_t)L.sorted[xb] : 0u;
+            pk[st >> 1] = pa | (pb << 16);
+        }
+#pragma unroll
+        for (int st = 0; st < 32; st += 2) {
+            const uint32_t xa = x0 + ((uint32_t)st << 6), xb = xa + 64;
+            const uint32_t pa = pk[st >> 1] & 0xFFFFu, pb = pk[st >> 1] >> 16;
+            const uint32_t ha = xa < nvalid ? dmx_hash(ld4(L.data, pa) & 0xFFFFFFu) : 0u;
+            const uint32_t hb = xb < nvalid ? dmx_hash(ld4(L.data, pb) & 0xFFFFFFu) : 0u;
+            hh[st >> 1] = ha | (hb << 16);
+            if ((st & 7) == 6) __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int st = 0; st < 32; st++) {
+            const uint32_t x = x0 + ((uint32_t)st << 6);
+            count_add(C + (wave << 6), ((hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu) >> 7, x < nvalid, false);
+        }
+        __syncthreads();
+        {   // destinations (dg, w) at order 16*dg + w, one per thread; bucket starts
+            const uint32_t i0 = ((tid & 15) << 6) + (tid >> 4);
+            const uint32_t v0 = C[i0];
+            const uint32_t ex = block_excl_scan(L, v0, tid);
+            uint32_t hv[8], hs = 0;
+#pragma unroll
+            for (int j = 0; j < 8; j++) { hv[j] = (H[tid * 4 + (j >> 1)] >> (16 * (j & 1))) & 0xFFFFu; hs += hv[j]; }
+            uint32_t hx = block_excl_scan(L, hs, tid);
+#pragma unroll
+            for (int j = 0; j < 8; j++) { L.bstart[tid * 8 + j] = (uint16_t)hx; hx += hv[j]; }
+            C[i0] = ex;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int st = 0; st < 32; st++) {
+            const uint32_t x = x0 + ((uint32_t)st << 6);
+            const bool valid = x < nvalid;
+            const uint32_t p = (pk[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
+            const uint32_t dg = ((hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu) >> 7;
+            const uint64_t eq = group_of(Gw, dg, valid);
+            const uint32_t c = valid ? C[(wave << 6) + dg] : 0u;
+            if (valid) {
+                L.sorted[c + (uint32_t)__popcll(eq & lt)] = (uint16_t)p;
+                if ((eq >> lane) == 1ull) C[(wave << 6) + dg] = c + (uint32_t)__popcll(eq);
+            }
+        }
+        __syncthreads();
+        if (dbg && tid == 0) tp0[2] = __builtin_amdgcn_s_memtime();
     }
-    __syncthreads();
 
     {   // Adler-32 partial sums of this block
         uint64_t s = 0, t = 0;
@@ -686,14 +735,17 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
     __syncthreads();
     for (uint32_t k = tid; k < DMX_HIST; k += MT) hist_g[(uint64_t)b * DMX_HIST + k] = L.hist[k];
     if (dbg && tid == 0) {
-        dbg[(uint64_t)b * 8 + 0] = t0 - tbeg;
-        dbg[(uint64_t)b * 8 + 1] = st_search;
-        dbg[(uint64_t)b * 8 + 2] = __builtin_amdgcn_s_memtime() - t1;
-        dbg[(uint64_t)b * 8 + 3] = st_def;
-        dbg[(uint64_t)b * 8 + 4] = st_iters;
-        dbg[(uint64_t)b * 8 + 5] = st_w1;
-        dbg[(uint64_t)b * 8 + 6] = st_w23;
-        dbg[(uint64_t)b * 8 + 7] = __builtin_amdgcn_s_memtime() - tbeg;
+        dbg[(uint64_t)b * DMX_STAMPS + 0] = t0 - tbeg;
+        dbg[(uint64_t)b * DMX_STAMPS + 1] = st_search;
+        dbg[(uint64_t)b * DMX_STAMPS + 2] = __builtin_amdgcn_s_memtime() - t1;
+        dbg[(uint64_t)b * DMX_STAMPS + 3] = st_def;
+        dbg[(uint64_t)b * DMX_STAMPS + 4] = st_iters;
+        dbg[(uint64_t)b * DMX_STAMPS + 5] = st_w1;
+        dbg[(uint64_t)b * DMX_STAMPS + 6] = st_w23;
+        dbg[(uint64_t)b * DMX_STAMPS + 7] = __builtin_amdgcn_s_memtime() - tbeg;
+        dbg[(uint64_t)b * DMX_STAMPS + 8] = tp0[0] - tbeg;   // P0 sub-phases: block staged
+        dbg[(uint64_t)b * DMX_STAMPS + 9] = tp0[1] - tbeg;   //   pass 1 done
+        dbg[(uint64_t)b * DMX_STAMPS + 10] = tp0[2] - tbeg;  //   pass 2 done
     }
     if (tid == 0) {
         info[b].ntok = L.ntok;
@@ -1276,8 +1328,7 @@ struct dmx_ctx {
     int device;
     hipStream_t stream;
     uint64_t cap_blocks;
-    uint16_t* prev;   // cap_blocks * DMX_BLK: bucket ranks (chain kernel), then best distances
-    uint16_t* bstart; // cap_blocks * DMX_NBUCKET: bucket starts in the sorted array
+    uint16_t* dist;   // cap_blocks * DMX_BLK: best distances in bucket order (match kernel staging)
     uint32_t* tok;    // cap_blocks * DMX_BLK
     uint32_t* hist;   // cap_blocks * DMX_HIST
     uint32_t* codes;  // cap_blocks * DMX_HIST
@@ -1318,14 +1369,13 @@ extern "C" uint64_t dmx_max_compressed(uint64_t n, int32_t sw) {
 }
 
 static void ctx_free_ws(dmx_ctx* c) {
-    if (c->prev) (void)hipFree(c->prev);
-    if (c->bstart) (void)hipFree(c->bstart);
+    if (c->dist) (void)hipFree(c->dist);
     if (c->tok) (void)hipFree(c->tok);
     if (c->hist) (void)hipFree(c->hist);
     if (c->codes) (void)hipFree(c->codes);
     if (c->hdr) (void)hipFree(c->hdr);
     if (c->info) (void)hipFree(c->info);
-    c->prev = NULL; c->bstart = NULL; c->tok = NULL; c->hist = NULL; c->codes = NULL; c->hdr = NULL; c->info = NULL;
+    c->dist = NULL; c->tok = NULL; c->hist = NULL; c->codes = NULL; c->hdr = NULL; c->info = NULL;
     c->cap_blocks = 0;
 }
 
@@ -1333,8 +1383,7 @@ static int ctx_reserve(dmx_ctx* c, uint64_t nblk) {
     if (nblk <= c->cap_blocks) return 0;
     ctx_free_ws(c);
     const uint64_t cb = nblk < 1 ? 1 : nblk;
-    HIPCHK(hipMalloc(&c->prev, cb * DMX_BLK * sizeof(uint16_t)));
-    HIPCHK(hipMalloc(&c->bstart, cb * DMX_NBUCKET * sizeof(uint16_t)));
+    HIPCHK(hipMalloc(&c->dist, cb * DMX_BLK * sizeof(uint16_t)));
     HIPCHK(hipMalloc(&c->tok, cb * DMX_BLK * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&c->hist, cb * DMX_HIST * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&c->codes, cb * DMX_HIST * sizeof(uint32_t)));
@@ -1437,15 +1486,13 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                 if (c->dbg) (void)hipFree(c->dbg);
                 c->dbg = NULL;
                 c->dbg_cap = 0;
-                if (hipMalloc(&c->dbg, (uint64_t)nblk * 8 * sizeof(uint64_t)) == hipSuccess) c->dbg_cap = nblk;
+                if (hipMalloc(&c->dbg, (uint64_t)nblk * DMX_STAMPS * sizeof(uint64_t)) == hipSuccess) c->dbg_cap = nblk;
             }
             dbg = c->dbg;
         }
-        hipLaunchKernelGGL(dmx_chain_kernel, dim3(nblk), dim3(64), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw, c->prev,
-                           c->bstart);
-        if (ev) (void)hipEventRecord(ev[1], s);
+        if (ev) (void)hipEventRecord(ev[1], s);   // stage "chain": folded into the match kernel (P0)
         hipLaunchKernelGGL(dmx_match_kernel, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw,
-                           o.max_chain, (o.flags & DMX_F_LAZY) ? 1u : 0u, c->prev, c->bstart, c->tok, c->hist, c->info, dbg);
+                           o.max_chain, (o.flags & DMX_F_LAZY) ? 1u : 0u, c->dist, c->tok, c->hist, c->info, dbg);
         if (ev) (void)hipEventRecord(ev[2], s);
         hipLaunchKernelGGL(dmx_huff_kernel, dim3(nblk), dim3(64), 0, s, c->hist, c->info, c->codes, c->hdr, nblk, o.flags);
         if (ev) (void)hipEventRecord(ev[3], s);
@@ -1595,6 +1642,6 @@ extern "C" int dmx_debug_stamps(dmx_ctx* c, uint64_t* out, uint32_t nblk) {
     if (!c->dbg || nblk > c->dbg_cap || nblk > c->last_nblk) return -(int)E_RANGE;
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpy(out, c->dbg, (uint64_t)nblk * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out, c->dbg, (uint64_t)nblk * DMX_STAMPS * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return 0;
 }

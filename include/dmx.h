@@ -176,8 +176,8 @@ int dmx_ctx_set_timing(dmx_ctx* ctx, int enable);
 int dmx_ctx_stage_times(dmx_ctx* ctx, double* ms6, uint32_t* count);
 
 /* Diagnostic: per-block match-kernel phase stamps (cycles) of the last encode, when the
- * process runs with DMX_STAMPS=1: 8 x u64 per block (see dmx_kernels.hip). */
-int dmx_debug_stamps(dmx_ctx* ctx, uint64_t* out8, uint32_t nblk);
+ * process runs with DMX_STAMPS=1: 16 x u64 per block (see dmx_kernels.hip). */
+int dmx_debug_stamps(dmx_ctx* ctx, uint64_t* out16, uint32_t nblk);
 
 /* Adler-32 combine (RFC 1950 math): adler of A||B from adler(A), adler(B), len(B). */
 uint32_t dmx_adler32_combine(uint32_t a, uint32_t b, uint64_t len_b);

@@ -17,7 +17,9 @@ def run(kind, n, mc):
                       "search_kcyc": round(st[:, 1].mean() / 1e3, 1), "walk_kcyc": round(st[:, 2].mean() / 1e3, 1),
                       "deferred_kcyc": round(st[:, 3].mean() / 1e3, 1), "iters_per_wave": round(st[:, 4].mean() / 16, 1),
                       "w1_kcyc": round(st[:, 5].mean() / 1e3, 1), "w1w3_kcyc": round(st[:, 6].mean() / 1e3, 1),
-                      "total_kcyc": round(st[:, 7].mean() / 1e3, 1)}))
+                      "total_kcyc": round(st[:, 7].mean() / 1e3, 1),
+                      "p0_staged_kcyc": round(st[:, 8].mean() / 1e3, 1), "p0_pass1_end_kcyc": round(st[:, 9].mean() / 1e3, 1),
+                      "p0_pass2_end_kcyc": round(st[:, 10].mean() / 1e3, 1)}))
 
 cfgs = [("text", 1), ("text", 16), ("text", 0), ("random", 0), ("zeros", 0)]
 if len(sys.argv) > 1:
