@@ -151,19 +151,30 @@ __device__ __forceinline__ uint32_t match_bytes(uint64_t x) {   // equal leading
 __device__ __forceinline__ uint32_t wshr(uint32_t v, uint32_t lane0) {   // lane l <- lane l-1; lane 0 <- lane0
     return (uint32_t)__builtin_amdgcn_update_dpp((int)lane0, (int)v, 0x138, 0xF, 0xF, false);
 }
-// Length of a candidate known to match bytes [0, kk): 32 more bytes per LDS round trip
-// (four independent 8-byte reads per side).
+// Length of a candidate known to match bytes [0, kk): 32 more bytes per LDS round trip.
+// Each side is read as 9 aligned words and realigned with v_alignbyte (one VALU per 4
+// bytes); the first differing word comes from a mask of non-zero xors.
 __device__ __forceinline__ uint32_t ext_len(const MatchLDS& L, uint32_t i, uint32_t q, uint32_t kk, uint32_t lim) {
     for (;;) {
-        uint64_t a[4], b[4];
+        const uint32_t a = (i + kk) >> 2, sa = (i + kk) & 3, c = (q + kk) >> 2, sc = (q + kk) & 3;
+        uint32_t wa[9], wc[9];
 #pragma unroll
-        for (int j = 0; j < 4; j++) { a[j] = ld8(L.data, i + kk + 8 * j); b[j] = ld8(L.data, q + kk + 8 * j); }
+        for (int t = 0; t < 9; t++) { wa[t] = L.data[a + t]; wc[t] = L.data[c + t]; }
+        uint32_t x[8], nz = 0;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t mb = match_bytes(a[j] ^ b[j]);
-            kk += mb;
-            if (mb < 8 || kk >= lim) return kk;
+        for (int t = 0; t < 8; t++) {
+            x[t] = __builtin_amdgcn_alignbyte(wa[t + 1], wa[t], sa) ^ __builtin_amdgcn_alignbyte(wc[t + 1], wc[t], sc);
+            nz |= (x[t] != 0 ? 1u : 0u) << t;
         }
+        if (nz) {
+            const uint32_t t0 = (uint32_t)__builtin_ctz(nz);
+            uint32_t xv = x[0];
+#pragma unroll
+            for (int t = 1; t < 8; t++) xv = (t0 == (uint32_t)t) ? x[t] : xv;
+            return kk + 4 * t0 + ((uint32_t)__builtin_ctz(xv) >> 3);
+        }
+        kk += 32;
+        if (kk >= lim) return kk;
     }
 }
 // Could candidate q (known to match [0, 16)) be strictly longer than best (>= 16)? Only if
