@@ -218,6 +218,45 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     return x + (row >= 1 ? t0 : 0u) + (row >= 2 ? t1 : 0u) + (row >= 3 ? t2 : 0u);
 }
 
+// The candidate steps of one chunk.  Step j: every register stream moves down one lane
+// (lane 0 takes halo entry j-1), so lane l holds entry k-j, its j-th chain candidate.
+// Key = (equal bytes, max 8) << 8 | (255 - j): the max over j is the longest match, then
+// the smallest j = the nearest (positions increase along a bucket).  No per-step validity
+// test: an entry before the bucket start has another bucket, hence another trigram, so it
+// never reaches 3 equal bytes, and candidates < 3 bytes are discarded once after the max.
+// Only the first chunk of the block (GUARD) has halo lanes without entries.
+template <bool GUARD>
+__device__ __forceinline__ void cand_step(uint32_t j, uint32_t& x0, uint32_t& x1, uint32_t i0, uint32_t i1,
+                                          uint32_t h0, uint32_t h1, uint32_t nc, uint32_t lim_eff,
+                                          uint32_t& jkey, uint32_t& full) {
+    const int src = (int)j - 1;
+    x0 = wshr(x0, __builtin_amdgcn_readlane(h0, src));
+    x1 = wshr(x1, __builtin_amdgcn_readlane(h1, src));
+    // equal leading bits of the 8-byte window, 64 = all (ffbl(0) = ~0)
+    const uint32_t mb = min(ffbl(i0 ^ x0), min(ffbl(i1 ^ x1), 32u) + 32u);
+    uint32_t m = min(mb >> 3, lim_eff);
+    bool fl = mb == 64u;
+    if (GUARD) {
+        m = j <= nc ? m : 0u;
+        fl = fl && j <= nc;
+    }
+    jkey = max(jkey, (m << 8) | (255u - j));
+    full |= fl ? (1u << src) : 0u;
+}
+template <bool GUARD>
+__device__ __forceinline__ void cand_steps(uint32_t jmax, uint32_t i0, uint32_t i1, uint32_t h0, uint32_t h1,
+                                           uint32_t nc, uint32_t lim_eff, uint32_t& jkey, uint32_t& full) {
+    uint32_t x0 = i0, x1 = i1, y0, y1;
+    uint32_t j = 1;
+    for (; j + 1 <= jmax; j += 2) {   // two steps per trip, alternating registers (no copies)
+        y0 = x0; y1 = x1;
+        cand_step<GUARD>(j, y0, y1, i0, i1, h0, h1, nc, lim_eff, jkey, full);
+        x0 = y0; x1 = y1;
+        cand_step<GUARD>(j + 1, x0, x1, i0, i1, h0, h1, nc, lim_eff, jkey, full);
+    }
+    if (j <= jmax) cand_step<GUARD>(j, x0, x1, i0, i1, h0, h1, nc, lim_eff, jkey, full);
+}
+
 __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint16_t* __restrict__ pg,
                                      uint32_t tid, bool stamp, uint64_t& tdef) {
     const uint32_t lane = tid & 63, wave = tid >> 6;
@@ -227,7 +266,7 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
     for (uint32_t k0 = wave << 6; k0 < nvalid; k0 += MT) {
         const uint32_t k = k0 + lane;
         const bool act = k < nvalid;
-        uint32_t i = 0, nc = 0, lim = 0, bestkey = 0;
+        uint32_t i = 0, nc = 0, lim = 0;
         uint64_t iv0 = 0;
         if (act) {
             i = L.sorted[k];
@@ -243,7 +282,6 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
             hq = L.sorted[k0 - 1 - lane];
             hv0 = ld8(L.data, hq);
         }
-        uint32_t xq = i, x0 = (uint32_t)iv0, x1 = (uint32_t)(iv0 >> 32);
         const uint32_t i0 = (uint32_t)iv0, i1 = (uint32_t)(iv0 >> 32);
         const uint32_t h0 = (uint32_t)hv0, h1 = (uint32_t)(hv0 >> 32);
         // wave-uniform bound: the largest chain length of the chunk, capped at KD
@@ -254,21 +292,15 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
         jmax = max(jmax, dpp_shr(jmax, 8));
         jmax = max(max(__builtin_amdgcn_readlane(jmax, 15), __builtin_amdgcn_readlane(jmax, 31)),
                    max(__builtin_amdgcn_readlane(jmax, 47), __builtin_amdgcn_readlane(jmax, 63)));
+        iters += jmax;
         const uint32_t lim_eff = act ? lim : 0;
-        uint32_t full = 0;   // bit j-1: candidate j matches all 8 bytes (length still open)
-        for (uint32_t j = 1; j <= jmax; j++) {
-            iters++;
-            const int src = (int)j - 1;
-            xq = wshr(xq, __builtin_amdgcn_readlane(hq, src));
-            x0 = wshr(x0, __builtin_amdgcn_readlane(h0, src));
-            x1 = wshr(x1, __builtin_amdgcn_readlane(h1, src));
-            // equal leading bytes of the 8-byte window, branch-free: ffbl(0) = ~0
-            const uint32_t m8 = min(ffbl(i0 ^ x0), min(ffbl(i1 ^ x1), 32u) + 32u) >> 3;
-            const bool valid = j <= nc;
-            const uint32_t m = min(m8, lim_eff);
-            bestkey = max(bestkey, (valid && m >= 3) ? ((m << 15) | xq) : 0u);
-            full |= (valid && m8 == 8 && lim_eff > 8) ? (1u << src) : 0u;
-        }
+        uint32_t jkey = 0, full = 0;   // full: bit j-1 = candidate j matches all 8 bytes
+        if (k0 == 0) cand_steps<true>(jmax, i0, i1, h0, h1, nc, lim_eff, jkey, full);
+        else cand_steps<false>(jmax, i0, i1, h0, h1, nc, lim_eff, jkey, full);
+        if (lim_eff <= 8) full = 0;
+        // position form of the best key: (len << 15) | source position
+        uint32_t bestkey = 0;
+        if (act && (jkey >> 8) >= 3) bestkey = ((jkey >> 8) << 15) | (uint32_t)L.sorted[k - (255u - (jkey & 255u))];
         const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
         // Candidates matching all 8 bytes (any of them beats every key above): exact length
         // from LDS.  Round 1: each lane's nearest one; a lane whose best is then the longest
