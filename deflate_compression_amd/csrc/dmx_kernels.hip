@@ -141,6 +141,7 @@ __device__ __forceinline__ uint32_t adv_of(const MatchLDS& L, uint32_t p) {
 // longest, then nearest (largest q) -- the reference's newest-first walk with strict >
 // (:249-263).  A lane stops comparing once its best is the longest possible length.
 #define KD 32
+#define JR 8    // Jacobi rounds of the walk before the serial fallback
 #define CW 4
 __device__ __forceinline__ uint32_t ffbl(uint32_t x) {   // lowest set bit, ~0 for 0 (v_ffbl_b32)
     return x ? (uint32_t)__builtin_ctz(x) : 0xFFFFFFFFu;
@@ -455,7 +456,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
                                                        uint32_t* __restrict__ tok_g, uint32_t* __restrict__ hist_g,
                                                        dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg) {
     __shared__ MatchLDS L;
-    __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def, tp0[3];
+    __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def, tp0[3], st_rounds;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t b = blockIdx.x;
     const uint64_t off = (uint64_t)b * sw;
@@ -693,39 +694,68 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         }
     }
     if (dbg && tid == 0) st_w1 = __builtin_amdgcn_s_memtime() - t1;
-    {   // W2: each wave resolves its 64 segments assuming it is entered at 2048*wave.
-        // Segment words live one per lane; the serial loop runs on uniform values.
-        uint32_t myw = L.tsm[tid];
-        const uint32_t myx = L.exitp[tid], myl = L.lit[tid];
-        uint32_t e = wave << 11;
-        for (uint32_t j = 0; j < 64; j++) {
-            const uint32_t m = __builtin_amdgcn_readlane(myw, (int)j), x = __builtin_amdgcn_readlane(myx, (int)j),
-                           lw = __builtin_amdgcn_readlane(myl, (int)j);
-            uint32_t nm;
-            bool mg;
-            e = resolve_word(L, ((wave << 6) + j) << 5, e, bn, m, lw, x, nm, mg);
-            if (lane == j) myw = nm;
-        }
-        L.tsm[tid] = myw;
-        if (lane == 0) L.wexit[wave] = e;
-    }
-    __syncthreads();
-    if (tid == 0) {   // W3: fix the waves whose true entry differs, until the paths merge
-        uint32_t E = L.wexit[0];
-        for (uint32_t w = 1; w < MW; w++) {
-            if (E == (w << 11)) { E = L.wexit[w]; continue; }
-            uint32_t e = E;
-            for (uint32_t s = w << 6; s < (w << 6) + 64; s++) {
+    // W2 (parallel): Jacobi rounds.  Every segment takes the exit of its predecessor's
+    // current path as its entry and, if that changed, re-walks from it until it meets its
+    // own current path (the rest then coincides: the next-function is deterministic) or
+    // leaves the segment.  A round where no entry changes is a fixed point, i.e. the
+    // sequential path.  Typical text converges in a few rounds; a run of long matches moves
+    // the true entry one segment per round, so after JR rounds the serial resolution below
+    // finishes from the current (valid) segment paths.
+    bool conv = false;
+    {
+        uint32_t entry = tid << 5;   // what W1 assumed
+        uint32_t r = 0;
+        for (; r < JR; r++) {
+            const uint32_t e = tid == 0 ? 0u : L.exitp[tid - 1];
+            __syncthreads();
+            const bool ch = (tid << 5) < bn && e != entry;   // segments past the block end stay empty
+            if (ch) {
                 uint32_t nm;
                 bool mg;
-                e = resolve_word(L, s << 5, e, bn, L.tsm[s], L.lit[s], 0, nm, mg);
-                L.tsm[s] = nm;
-                if (mg) { e = L.wexit[w]; break; }
+                const uint32_t x = resolve_word(L, tid << 5, e, bn, L.tsm[tid], L.lit[tid], L.exitp[tid], nm, mg);
+                L.tsm[tid] = nm;
+                L.exitp[tid] = x;
+                entry = e;
             }
-            E = e;
+            if (!__syncthreads_or(ch)) { conv = true; break; }
         }
+        if (dbg && tid == 0) st_rounds = r;
     }
-    __syncthreads();
+    if (!conv) {
+        {   // W2: each wave resolves its 64 segments assuming it is entered at 2048*wave.
+            // Segment words live one per lane; the serial loop runs on uniform values.
+            uint32_t myw = L.tsm[tid];
+            const uint32_t myx = L.exitp[tid], myl = L.lit[tid];
+            uint32_t e = wave << 11;
+            for (uint32_t j = 0; j < 64; j++) {
+                const uint32_t m = __builtin_amdgcn_readlane(myw, (int)j), x = __builtin_amdgcn_readlane(myx, (int)j),
+                               lw = __builtin_amdgcn_readlane(myl, (int)j);
+                uint32_t nm;
+                bool mg;
+                e = resolve_word(L, ((wave << 6) + j) << 5, e, bn, m, lw, x, nm, mg);
+                if (lane == j) myw = nm;
+            }
+            L.tsm[tid] = myw;
+            if (lane == 0) L.wexit[wave] = e;
+        }
+        __syncthreads();
+        if (tid == 0) {   // W3: fix the waves whose true entry differs, until the paths merge
+            uint32_t E = L.wexit[0];
+            for (uint32_t w = 1; w < MW; w++) {
+                if (E == (w << 11)) { E = L.wexit[w]; continue; }
+                uint32_t e = E;
+                for (uint32_t s = w << 6; s < (w << 6) + 64; s++) {
+                    uint32_t nm;
+                    bool mg;
+                    e = resolve_word(L, s << 5, e, bn, L.tsm[s], L.lit[s], 0, nm, mg);
+                    L.tsm[s] = nm;
+                    if (mg) { e = L.wexit[w]; break; }
+                }
+                E = e;
+            }
+        }
+        __syncthreads();
+    }
     if (dbg && tid == 0) st_w23 = __builtin_amdgcn_s_memtime() - t1;
 
     // ---- P3: compaction + histograms ----
@@ -789,6 +819,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         dbg[(uint64_t)b * DMX_STAMPS + 8] = tp0[0] - tbeg;   // P0 sub-phases: block staged
         dbg[(uint64_t)b * DMX_STAMPS + 9] = tp0[1] - tbeg;   //   pass 1 done
         dbg[(uint64_t)b * DMX_STAMPS + 10] = tp0[2] - tbeg;  //   pass 2 done
+        dbg[(uint64_t)b * DMX_STAMPS + 11] = st_rounds;      // walk: Jacobi rounds (JR = not converged)
     }
     if (tid == 0) {
         info[b].ntok = L.ntok;

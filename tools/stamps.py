@@ -19,7 +19,8 @@ def run(kind, n, mc):
                       "w1_kcyc": round(st[:, 5].mean() / 1e3, 1), "w1w3_kcyc": round(st[:, 6].mean() / 1e3, 1),
                       "total_kcyc": round(st[:, 7].mean() / 1e3, 1),
                       "p0_staged_kcyc": round(st[:, 8].mean() / 1e3, 1), "p0_pass1_end_kcyc": round(st[:, 9].mean() / 1e3, 1),
-                      "p0_pass2_end_kcyc": round(st[:, 10].mean() / 1e3, 1)}))
+                      "p0_pass2_end_kcyc": round(st[:, 10].mean() / 1e3, 1),
+                      "walk_rounds": round(st[:, 11].mean(), 2), "walk_fallback_frac": round(float((st[:, 11] >= 8).mean()), 3)}))
 
 cfgs = [("text", 1), ("text", 16), ("text", 0), ("random", 0), ("zeros", 0)]
 if len(sys.argv) > 1:
