@@ -272,8 +272,10 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
         if (act) {
             i = L.sorted[k];
             iv0 = ld8(L.data, i);
-            const uint32_t rank = k - (uint32_t)L.bstart[dmx_hash((uint32_t)iv0 & 0xFFFFFFu)];
-            nc = min(rank, K);
+            // bounded mode (K <= KD) needs no bucket rank: the K entries below k are examined
+            // and those of other buckets never reach 3 equal bytes (cand_steps); only the
+            // first K entries of the block lack K predecessors.  Longer chains need the rank.
+            nc = K <= KD ? min(k, K) : min(k - (uint32_t)L.bstart[dmx_hash((uint32_t)iv0 & 0xFFFFFFu)], K);
             lim = (bn - i) < MAXLEN ? (bn - i) : MAXLEN;
         }
         // halo: lane l < KD holds entry k0-1-l
@@ -497,6 +499,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
     // Bucket starts = exclusive scan of a bucket histogram taken in pass 1.
     {
         const uint32_t nvalid = bn > 2 ? bn - 2 : 0;   // positions with a full trigram
+        const bool need_starts = max_chain <= 0 || max_chain > KD;
         uint32_t* C = L.tsm;                              // 16 x 128 digit counters (tsm + exitp)
         uint32_t* H = reinterpret_cast<uint32_t*>(L.len8);   // 8192 bucket counts, u16 pairs
         unsigned long long* G = reinterpret_cast<unsigned long long*>(L.len8 + DMX_BLK / 2);   // 16 x 128 lane masks
@@ -524,7 +527,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         for (int st = 0; st < 32; st++) {
             const uint32_t x = x0 + ((uint32_t)st << 6);
             const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
-            count_add(H, h, x < nvalid, true);
+            if (need_starts) count_add(H, h, x < nvalid, true);
             count_add(C + (wave << 7), h & 127u, x < nvalid, false);
         }
         __syncthreads();
@@ -581,12 +584,14 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
             const uint32_t i0 = ((tid & 15) << 6) + (tid >> 4);
             const uint32_t v0 = C[i0];
             const uint32_t ex = block_excl_scan(L, v0, tid);
-            uint32_t hv[8], hs = 0;
+            if (need_starts) {   // bucket starts: only chains longer than KD use them
+                uint32_t hv[8], hs = 0;
 #pragma unroll
-            for (int j = 0; j < 8; j++) { hv[j] = (H[tid * 4 + (j >> 1)] >> (16 * (j & 1))) & 0xFFFFu; hs += hv[j]; }
-            uint32_t hx = block_excl_scan(L, hs, tid);
+                for (int j = 0; j < 8; j++) { hv[j] = (H[tid * 4 + (j >> 1)] >> (16 * (j & 1))) & 0xFFFFu; hs += hv[j]; }
+                uint32_t hx = block_excl_scan(L, hs, tid);
 #pragma unroll
-            for (int j = 0; j < 8; j++) { L.bstart[tid * 8 + j] = (uint16_t)hx; hx += hv[j]; }
+                for (int j = 0; j < 8; j++) { L.bstart[tid * 8 + j] = (uint16_t)hx; hx += hv[j]; }
+            }
             C[i0] = ex;
         }
         __syncthreads();
