@@ -838,154 +838,287 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
 // K2: Huffman codes + block type (one wave per block)
 // ------------------------------------------------------------------------------------
 
-struct HuffLDS {
-    uint32_t f[320];
-    uint32_t fs[320];
-    uint32_t nodew[320];
-    uint16_t sym[320];
-    uint16_t lpar[320];
-    uint16_t npar[320];
-    uint8_t ndep[320];
-    int32_t blc[64];
-    int32_t m;
-};
-
 struct K2LDS {
-    HuffLDS H;
     uint32_t fll[288];
     uint32_t fd[32];
     uint32_t fcl[20];
     uint8_t lll[288];
     uint8_t ld[32];
     uint8_t lcl[20];
+    // Huffman construction (one alphabet at a time)
+    uint32_t fs[320];     // used symbols' weights sorted by (weight, symbol)
+    uint16_t sym[320];    //   and their symbols
+    uint32_t nodew[320];  // internal node weights, in creation order
+    uint16_t lpar[320];   // sorted leaf -> parent node
+    uint16_t up[320];     // node -> ancestor (pointer jumping)
+    uint16_t dd[320];     // node -> distance to that ancestor (-> depth)
+    int32_t blc[64];      // leaves per code length
+    int32_t lstart[16];   // first sorted index that gets length d
+    int32_t cnt[16];      // canonical codes: codes handed out per length so far
+    uint32_t next[16];    // canonical codes: first code of each length
+    uint32_t code[320];   // canonical codes (bit-reversed) | len << 16
+    // run-length coding of the code lengths (RFC 1951 §3.2.7)
     uint8_t rle_sym[320];
     uint8_t rle_ext[320];
-    uint32_t code[320];  // canonical codes (bit-reversed) | len << 16
     uint32_t hdr[DMX_HDR_WORDS];
     int32_t rle_n, hlit, hdist, hclen;
-    uint32_t hdr_pos;
 };
 
 __constant__ uint8_t c_clorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 __constant__ uint8_t c_cl_eb[19] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 3, 7};
 
-// Code lengths for freq H.f[0..n) limited to maxbits: symbols sorted
-// by (freq, symbol); two-queue merge (ties take the leaf); depths; overflow
-// redistribution; longest lengths to the least frequent symbols.
-__device__ void huff_lengths(HuffLDS& H, int n, int maxbits, uint8_t* len, uint32_t lane) {
+// Exclusive prefix sum over one wave (64 lanes).
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v) { return wave_incl_scan(v) - v; }
+
+// Code lengths for the weights f[0..n) limited to maxbits (restated in
+// oracle/dmx_oracle.c dmx_oracle_huff_lengths): used symbols sorted by (weight, symbol);
+// two-queue merge (ties take the leaf); depths; overflow redistribution; the longest
+// lengths to the least frequent symbols.  One wave; NR = symbol registers (64 each).
+// Sorting, depths and the length assignment are lane-parallel; only the merge is serial
+// (lane 0, one LDS round trip per node: both heads of both queues are read together).
+template <int NR>
+__device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, uint8_t* len, uint32_t lane) {
+    uint32_t key[NR];
     uint32_t m = 0;
-    for (int j = 0; j < n; j += 64) {
-        const int s = j + (int)lane;
-        const bool used = s < n && H.f[s] != 0;
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+        const int s = r * 64 + (int)lane;
+        const uint32_t fv = s < n ? f[s] : 0u;
+        key[r] = fv ? ((fv << 9) | (uint32_t)s) : 0xFFFFFFFFu;
         if (s < n) len[s] = 0;
-        m += __popcll(__ballot(used));
+        m += (uint32_t)__popcll(__ballot(fv != 0));
     }
     __syncthreads();
     if (m == 0) return;
-    if (m == 1) {
-        if (lane == 0) {
-            int s0 = 0;
-            while (H.f[s0] == 0) s0++;
-            len[s0] = 1;
-            len[s0 == 0 ? 1 : 0] = 1;
-        }
+    if (m == 1) {   // one used symbol: one more code of length 1 (RFC 1951 allows it)
+#pragma unroll
+        for (int r = 0; r < NR; r++)
+            if (key[r] != 0xFFFFFFFFu) {
+                const uint32_t s0 = key[r] & 511u;
+                len[s0] = 1;
+                len[s0 == 0 ? 1 : 0] = 1;
+            }
         __syncthreads();
         return;
     }
-    // rank of each used symbol among used symbols by key (freq << 9 | sym)
-    {
-        uint32_t key[5];
+    // rank among the used symbols: compare with every key, broadcast by readlane
+    uint32_t rk[NR];
 #pragma unroll
-        for (int j = 0; j < 5; j++) {
-            const int s = j * 64 + (int)lane;
-            key[j] = (s < n && H.f[s]) ? ((H.f[s] << 9) | (uint32_t)s) : 0xFFFFFFFFu;
-        }
-        uint32_t r[5] = {0, 0, 0, 0, 0};
-        for (int s2 = 0; s2 < n; s2++) {
-            const uint32_t f2 = H.f[s2];
-            const uint32_t k2 = f2 ? ((f2 << 9) | (uint32_t)s2) : 0xFFFFFFFFu;
+    for (int r = 0; r < NR; r++) rk[r] = 0;
 #pragma unroll
-            for (int j = 0; j < 5; j++) r[j] += (k2 < key[j]) ? 1u : 0u;
-        }
+    for (int r2 = 0; r2 < NR; r2++) {
+        for (int l2 = 0; l2 < 64; l2++) {
+            const uint32_t k2 = __builtin_amdgcn_readlane(key[r2], l2);
 #pragma unroll
-        for (int j = 0; j < 5; j++) {
-            if (key[j] != 0xFFFFFFFFu) {
-                H.sym[r[j]] = (uint16_t)(key[j] & 511u);
-                H.fs[r[j]] = key[j] >> 9;
-            }
+            for (int r = 0; r < NR; r++) rk[r] += k2 < key[r] ? 1u : 0u;
         }
     }
-    for (int k = (int)lane; k < 64; k += 64) H.blc[k] = 0;
+#pragma unroll
+    for (int r = 0; r < NR; r++)
+        if (key[r] != 0xFFFFFFFFu) {
+            S.fs[rk[r]] = key[r] >> 9;
+            S.sym[rk[r]] = (uint16_t)(key[r] & 511u);
+        }
+    for (int k = (int)lane; k < 64; k += 64) S.blc[k] = 0;
+    __syncthreads();
+    const int mm = (int)m, nn = mm - 1, root = nn - 1;
+    if (lane == 0) {   // two-queue merge
+        int li = 0, ni = 0;
+        for (int k = 0; k < nn; k++) {
+            const uint32_t a0 = li < mm ? S.fs[li] : 0xFFFFFFFFu, a1 = li + 1 < mm ? S.fs[li + 1] : 0xFFFFFFFFu;
+            const uint32_t b0 = ni < k ? S.nodew[ni] : 0xFFFFFFFFu, b1 = ni + 1 < k ? S.nodew[ni + 1] : 0xFFFFFFFFu;
+            uint32_t w;
+            uint32_t A, B;
+            if (li < mm && a0 <= b0) { w = a0; S.lpar[li++] = (uint16_t)k; A = a1; B = b0; }
+            else { w = b0; S.up[ni++] = (uint16_t)k; A = a0; B = b1; }
+            if (li < mm && A <= B) { w += A; S.lpar[li++] = (uint16_t)k; }
+            else { w += B; S.up[ni++] = (uint16_t)k; }
+            S.nodew[k] = w;
+        }
+        S.up[root] = (uint16_t)root;
+    }
+    __syncthreads();
+    // node depths by pointer jumping: dd = distance to up, up = an ancestor, doubling
+    uint32_t u[5], d[5];
+#pragma unroll
+    for (int r = 0; r < 5; r++) {
+        const int j = r * 64 + (int)lane;
+        u[r] = j < nn ? S.up[j] : 0u;
+        d[r] = (j < nn && j != root) ? 1u : 0u;
+        if (j < nn) S.dd[j] = (uint16_t)d[r];
+    }
+    __syncthreads();
+    for (int round = 0; round < 9; round++) {   // 2^9 > 320 nodes
+        uint32_t du[5], uu[5];
+#pragma unroll
+        for (int r = 0; r < 5; r++) {
+            const int j = r * 64 + (int)lane;
+            du[r] = j < nn ? S.dd[u[r]] : 0u;
+            uu[r] = j < nn ? S.up[u[r]] : 0u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 5; r++) {
+            const int j = r * 64 + (int)lane;
+            d[r] += du[r];
+            u[r] = uu[r];
+            if (j < nn) { S.dd[j] = (uint16_t)d[r]; S.up[j] = (uint16_t)u[r]; }
+        }
+        __syncthreads();
+    }
+    // leaf depths -> leaves per length
+    uint32_t maxd = 0;
+#pragma unroll
+    for (int r = 0; r < 5; r++) {
+        const int i = r * 64 + (int)lane;
+        if (i < mm) {
+            const uint32_t dl = S.dd[S.lpar[i]] + 1u;
+            atomicAdd(&S.blc[dl], 1);
+            maxd = max(maxd, dl);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) maxd = max(maxd, (uint32_t)__shfl_xor((int)maxd, o));
     __syncthreads();
     if (lane == 0) {
-        int li = 0, ni = 0, nn = 0;
-        const int mm = (int)m;
-        for (int k = 0; k < mm - 1; k++) {
-            uint32_t w = 0;
-#pragma unroll
-            for (int pick = 0; pick < 2; pick++) {
-                if (li < mm && (ni >= nn || H.fs[li] <= H.nodew[ni])) {
-                    w += H.fs[li];
-                    H.lpar[li++] = (uint16_t)nn;
-                } else {
-                    w += H.nodew[ni];
-                    H.npar[ni++] = (uint16_t)nn;
-                }
-            }
-            H.nodew[nn++] = w;
-        }
-        H.ndep[nn - 1] = 0;
-        for (int j = nn - 2; j >= 0; j--) H.ndep[j] = (uint8_t)(H.ndep[H.npar[j]] + 1);
-        int maxd = 0;
-        for (int k = 0; k < mm; k++) {
-            const int dpt = H.ndep[H.lpar[k]] + 1;
-            H.blc[dpt]++;
-            if (dpt > maxd) maxd = dpt;
-        }
-        if (maxd > maxbits) {
-            for (int dd = maxbits + 1; dd <= maxd; dd++) { H.blc[maxbits] += H.blc[dd]; H.blc[dd] = 0; }
+        if ((int)maxd > maxbits) {   // overflow redistribution (miniz style)
+            for (int e = maxbits + 1; e <= (int)maxd; e++) { S.blc[maxbits] += S.blc[e]; S.blc[e] = 0; }
             uint32_t total = 0;
-            for (int dd = 1; dd <= maxbits; dd++) total += (uint32_t)H.blc[dd] << (maxbits - dd);
+            for (int e = 1; e <= maxbits; e++) total += (uint32_t)S.blc[e] << (maxbits - e);
             while (total != (1u << maxbits)) {
-                H.blc[maxbits]--;
-                for (int dd = maxbits - 1; dd >= 1; dd--) {
-                    if (H.blc[dd]) { H.blc[dd]--; H.blc[dd + 1] += 2; break; }
+                S.blc[maxbits]--;
+                for (int e = maxbits - 1; e >= 1; e--) {
+                    if (S.blc[e]) { S.blc[e]--; S.blc[e + 1] += 2; break; }
                 }
                 total--;
             }
         }
-        int k = 0;
-        for (int dd = maxbits; dd >= 1; dd--)
-            for (int c = 0; c < H.blc[dd]; c++) len[H.sym[k++]] = (uint8_t)dd;
+        int k = 0;   // sorted index where length e starts: longest lengths first
+        for (int e = maxbits; e >= 1; e--) { S.lstart[e] = k; k += S.blc[e]; }
     }
     __syncthreads();
-}
-
-// canonical codes (RFC 1951 §3.2.2), bit-reversed, packed code | len << 16
-__device__ void canon_codes(const uint8_t* len, int n, uint32_t* out, uint32_t lane) {
-    if (lane == 0) {
-        int bl[16] = {0};
-        for (int s = 0; s < n; s++) bl[len[s]]++;
-        bl[0] = 0;
-        uint32_t next[16], c = 0;
-        for (int b = 1; b < 16; b++) { c = (c + bl[b - 1]) << 1; next[b] = c; }
-        for (int s = 0; s < n; s++) {
-            const uint32_t l = len[s];
-            if (!l) { out[s] = 0; continue; }
-            const uint32_t v = next[l]++;
-            out[s] = (__brev(v) >> (32 - l)) | (l << 16);
+#pragma unroll
+    for (int r = 0; r < 5; r++) {
+        const int i = r * 64 + (int)lane;
+        if (i < mm) {
+            int e = maxbits;
+            while (e > 1 && i >= S.lstart[e] + S.blc[e]) e--;
+            len[S.sym[i]] = (uint8_t)e;
         }
     }
     __syncthreads();
 }
 
-__device__ __forceinline__ void hdr_put(K2LDS& S, uint32_t v, uint32_t nb) {  // lane 0 only
-    if (!nb) return;
-    const uint32_t p = S.hdr_pos;
-    const uint32_t w = p >> 5, sh = p & 31;
-    S.hdr[w] |= v << sh;
-    if (sh + nb > 32) S.hdr[w + 1] |= v >> (32 - sh);
-    S.hdr_pos = p + nb;
+// Canonical codes (RFC 1951 §3.2.2), bit-reversed, packed code | len << 16.  Lane-parallel:
+// a symbol's code = first code of its length + number of earlier symbols of that length.
+template <int NR>
+__device__ void canon_codes(K2LDS& S, const uint8_t* len, int n, uint32_t* out, uint32_t lane) {
+    if (lane < 16) S.cnt[lane] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+        const int s = r * 64 + (int)lane;
+        if (s < n && len[s]) atomicAdd(&S.cnt[len[s]], 1);
+    }
+    __syncthreads();
+    if (lane == 0) {
+        uint32_t c = 0;
+        for (int b2 = 1; b2 < 16; b2++) { c = (c + (b2 > 1 ? (uint32_t)S.cnt[b2 - 1] : 0u)) << 1; S.next[b2] = c; }
+        for (int b2 = 0; b2 < 16; b2++) S.cnt[b2] = 0;
+    }
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+        const int s = r * 64 + (int)lane;
+        const uint32_t l = s < n ? len[s] : 0u;
+        uint64_t eq = __ballot(l != 0);
+#pragma unroll
+        for (int bit = 0; bit < 4; bit++) {
+            const bool hb = (l >> bit) & 1u;
+            const uint64_t mk = __ballot(hb);
+            eq &= hb ? mk : ~mk;
+        }
+        if (l) {
+            const uint32_t base = (uint32_t)S.cnt[l];
+            const uint32_t v = S.next[l] + base + (uint32_t)__popcll(eq & lt);
+            out[s] = (__brev(v) >> (32 - l)) | (l << 16);
+            if ((eq >> lane) == 1ull) S.cnt[l] = (int32_t)(base + (uint32_t)__popcll(eq));
+        } else if (s < n) {
+            out[s] = 0;
+        }
+        __syncthreads();
+    }
+}
+
+// Run-length coding of the concatenated lit/len + distance code lengths (DESIGN.md §4.3,
+// oracle orc_plan_block): runs are found lane-parallel, every run's symbol count has a
+// closed form, and a prefix sum places each run's symbols.
+__device__ void rle_lengths(K2LDS& S, uint32_t lane) {
+    const int hl = S.hlit, ns = hl + S.hdist;
+    uint32_t v[5];
+    uint64_t sm[5];
+#pragma unroll
+    for (int r = 0; r < 5; r++) {
+        const int k = r * 64 + (int)lane;
+        v[r] = k < ns ? (k < hl ? S.lll[k] : S.ld[k - hl]) : 0xFFu;
+        const uint32_t pv = (k >= 1 && k - 1 < ns) ? (k - 1 < hl ? S.lll[k - 1] : S.ld[k - 1 - hl]) : 0x1FFu;
+        sm[r] = __ballot(k < ns && v[r] != pv);
+    }
+    uint32_t cntr[5], runl[5];
+#pragma unroll
+    for (int r = 0; r < 5; r++) {
+        const int k = r * 64 + (int)lane;
+        cntr[r] = 0;
+        runl[r] = 0;
+        if ((sm[r] >> lane) & 1ull) {
+            int nx = ns;   // next run start
+            const uint64_t above = lane == 63 ? 0ull : (sm[r] & ~((2ull << lane) - 1ull));
+            if (above) nx = r * 64 + (int)__builtin_ctzll(above);
+            else {
+#pragma unroll
+                for (int r2 = r + 1; r2 < 5; r2++)
+                    if (nx == ns && sm[r2]) nx = r2 * 64 + (int)__builtin_ctzll(sm[r2]);
+            }
+            const uint32_t R = (uint32_t)(nx - k);
+            runl[r] = R;
+            if (v[r] == 0) {
+                uint32_t n18 = R / 138, rem = R % 138;
+                if (rem >= 11) { n18++; rem = 0; }
+                cntr[r] = n18 + (rem >= 3 ? 1u : rem);
+            } else {
+                uint32_t rr = R - 1, n16 = rr / 6, rem = rr % 6;
+                if (rem >= 3) { n16++; rem = 0; }
+                cntr[r] = 1 + n16 + rem;
+            }
+        }
+    }
+    uint32_t carry = 0;
+#pragma unroll
+    for (int r = 0; r < 5; r++) {
+        const uint32_t incl = wave_incl_scan(cntr[r]);
+        uint32_t o = carry + incl - cntr[r];
+        carry += __builtin_amdgcn_readlane(incl, 63);
+        if (cntr[r]) {   // emit this run's symbols exactly as the sequential rule does
+            uint32_t rr = runl[r];
+            const uint32_t val = v[r];
+            if (val == 0) {
+                while (rr >= 11) { const uint32_t c = rr < 138 ? rr : 138; S.rle_sym[o] = 18; S.rle_ext[o] = (uint8_t)(c - 11); o++; rr -= c; }
+                if (rr >= 3) { S.rle_sym[o] = 17; S.rle_ext[o] = (uint8_t)(rr - 3); o++; rr = 0; }
+                while (rr > 0) { S.rle_sym[o] = 0; S.rle_ext[o] = 0; o++; rr--; }
+            } else {
+                S.rle_sym[o] = (uint8_t)val; S.rle_ext[o] = 0; o++;
+                rr--;
+                while (rr >= 3) { const uint32_t c = rr < 6 ? rr : 6; S.rle_sym[o] = 16; S.rle_ext[o] = (uint8_t)(c - 3); o++; rr -= c; }
+                while (rr > 0) { S.rle_sym[o] = (uint8_t)val; S.rle_ext[o] = 0; o++; rr--; }
+            }
+        }
+    }
+    if (lane < 20) S.fcl[lane] = 0;
+    __syncthreads();
+    if (lane == 0) S.rle_n = (int32_t)carry;
+    for (uint32_t t = lane; t < carry; t += 64) atomicAdd(&S.fcl[S.rle_sym[t]], 1u);
+    __syncthreads();
 }
 
 __global__ __launch_bounds__(64) void dmx_huff_kernel(const uint32_t* __restrict__ hist_g, dmx_blkinfo* __restrict__ info,
@@ -998,67 +1131,39 @@ __global__ __launch_bounds__(64) void dmx_huff_kernel(const uint32_t* __restrict
     const uint32_t bn = info[b].n;
     const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1) ? 1u : 0u;
 
-    for (int s = (int)lane; s < 288; s += 64) S.fll[s] = s < 286 ? hg[s] : 0;
-    for (int s = (int)lane; s < 32; s += 64) S.fd[s] = s < 30 ? hg[DMX_DIST0 + s] : 0;
+    for (int s = (int)lane; s < 288; s += 64) S.fll[s] = s < 286 ? (s == 256 ? 1u : hg[s]) : 0u;   // + end of block
+    for (int s = (int)lane; s < 32; s += 64) S.fd[s] = s < 30 ? hg[DMX_DIST0 + s] : 0u;
     for (int k = (int)lane; k < DMX_HDR_WORDS; k += 64) S.hdr[k] = 0;
-    __syncthreads();
-    if (lane == 0) S.fll[256] = 1;  // end of block
     __syncthreads();
 
     // lit/len and distance code lengths
-    for (int s = (int)lane; s < 286; s += 64) S.H.f[s] = S.fll[s];
-    __syncthreads();
-    huff_lengths(S.H, 286, 15, S.lll, lane);
-    for (int s = (int)lane; s < 30; s += 64) S.H.f[s] = S.fd[s];
-    __syncthreads();
-    huff_lengths(S.H, 30, 15, S.ld, lane);
-    if (lane == 0) {
-        int any = 0;
-        for (int s = 0; s < 30; s++) any |= S.ld[s];
-        if (!any) { S.ld[0] = 1; S.ld[1] = 1; }   // no matches: two 1-bit codes
-        int hl = 286;
-        while (hl > 257 && S.lll[hl - 1] == 0) hl--;
-        int hd = 30;
-        while (hd > 1 && S.ld[hd - 1] == 0) hd--;
-        S.hlit = hl;
-        S.hdist = hd;
-        // RLE of the concatenated length sequence
-        for (int k = 0; k < 20; k++) S.fcl[k] = 0;
-        const int ns = hl + hd;
-        int i = 0, rn = 0;
-#define SEQ(k) ((k) < hl ? S.lll[(k)] : S.ld[(k) - hl])
-#define EMIT(SY, EX) do { S.rle_sym[rn] = (uint8_t)(SY); S.rle_ext[rn] = (uint8_t)(EX); rn++; S.fcl[(SY)]++; } while (0)
-        while (i < ns) {
-            const int v = SEQ(i);
-            int run = 1;
-            while (i + run < ns && SEQ(i + run) == v) run++;
-            if (v == 0) {
-                int r = run;
-                while (r >= 11) { const int c = r < 138 ? r : 138; EMIT(18, c - 11); r -= c; }
-                if (r >= 3) { EMIT(17, r - 3); r = 0; }
-                while (r > 0) { EMIT(0, 0); r--; }
-            } else {
-                EMIT(v, 0);
-                int r = run - 1;
-                while (r >= 3) { const int c = r < 6 ? r : 6; EMIT(16, c - 3); r -= c; }
-                while (r > 0) { EMIT(v, 0); r--; }
-            }
-            i += run;
+    huff_lengths<5>(S, S.fll, 286, 15, S.lll, lane);
+    huff_lengths<1>(S, S.fd, 30, 15, S.ld, lane);
+    {
+        const uint64_t anyd = __ballot(lane < 30 && S.ld[lane] != 0);
+        if (anyd == 0 && lane < 2) S.ld[lane] = 1;   // no matches: two 1-bit codes
+        // HLIT / HDIST: trailing zero lengths dropped (>= 257 / >= 1)
+        int hl = 257;
+#pragma unroll
+        for (int r = 0; r < 5; r++) {
+            const int s = r * 64 + (int)lane;
+            const uint64_t nz = __ballot(s < 286 && S.lll[s] != 0);
+            if (nz) hl = max(hl, r * 64 + 64 - (int)__builtin_clzll(nz));
         }
-#undef EMIT
-#undef SEQ
-        S.rle_n = rn;
+        const uint64_t nzd = __ballot(lane < 30 && S.ld[lane] != 0);
+        if (lane == 0) {
+            S.hlit = hl;
+            S.hdist = nzd ? max(1, 64 - (int)__builtin_clzll(nzd)) : 1;
+        }
+        __syncthreads();
     }
-    __syncthreads();
-    for (int s = (int)lane; s < 19; s += 64) S.H.f[s] = S.fcl[s];
-    __syncthreads();
-    huff_lengths(S.H, 19, 7, S.lcl, lane);
-    if (lane == 0) {
-        int hc = 19;
-        while (hc > 4 && S.lcl[c_clorder[hc - 1]] == 0) hc--;
-        S.hclen = hc;
+    rle_lengths(S, lane);
+    huff_lengths<1>(S, S.fcl, 19, 7, S.lcl, lane);
+    {
+        const uint64_t nzc = __ballot(lane < 19 && S.lcl[c_clorder[lane < 19 ? lane : 0]] != 0);
+        if (lane == 0) S.hclen = nzc ? max(4, 64 - (int)__builtin_clzll(nzc)) : 4;
+        __syncthreads();
     }
-    __syncthreads();
 
     // exact costs
     uint64_t dyn_body = 0, fix_body = 0, extra = 0;
@@ -1095,35 +1200,46 @@ __global__ __launch_bounds__(64) void dmx_huff_kernel(const uint32_t* __restrict
         for (int s = (int)lane; s < 30; s += 64) S.ld[s] = 5;
         __syncthreads();
     }
-    canon_codes(S.lll, 286, S.code, lane);
-    canon_codes(S.ld, 30, S.code + DMX_DIST0, lane);
+    canon_codes<5>(S, S.lll, 286, S.code, lane);
+    canon_codes<1>(S, S.ld, 30, S.code + DMX_DIST0, lane);
     uint32_t* cg = codes_g + (uint64_t)b * DMX_HIST;
     for (int s = (int)lane; s < 316; s += 64) cg[s] = S.code[s];
+    __syncthreads();
 
-    // header bits
-    if (lane == 0) {
-        S.hdr_pos = 0;
-        hdr_put(S, final_bit | (bt << 1), 3);
-        if (bt == 2) {
-            hdr_put(S, (uint32_t)(S.hlit - 257), 5);
-            hdr_put(S, (uint32_t)(S.hdist - 1), 5);
-            hdr_put(S, (uint32_t)(S.hclen - 4), 4);
-            for (int k = 0; k < S.hclen; k++) hdr_put(S, S.lcl[c_clorder[k]], 3);
+    // header bits: items (value, bits) placed by a prefix sum over their bit counts
+    uint32_t nitems = 1;
+    if (bt == 2) {
+        canon_codes<1>(S, S.lcl, 19, S.code, lane);   // code-length codes (lit/dist codes are out)
+        nitems = 4 + (uint32_t)S.hclen + (uint32_t)S.rle_n;
+    }
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nitems; base += 64) {
+        const uint32_t it = base + lane;
+        uint32_t val = 0, nb = 0;
+        if (it < nitems) {
+            if (it == 0) { val = final_bit | (bt << 1); nb = 3; }
+            else if (it == 1) { val = (uint32_t)(S.hlit - 257); nb = 5; }
+            else if (it == 2) { val = (uint32_t)(S.hdist - 1); nb = 5; }
+            else if (it == 3) { val = (uint32_t)(S.hclen - 4); nb = 4; }
+            else if (it < 4 + (uint32_t)S.hclen) { val = S.lcl[c_clorder[it - 4]]; nb = 3; }
+            else {
+                const uint32_t t = it - 4 - (uint32_t)S.hclen, sy = S.rle_sym[t], cw = S.code[sy];
+                const uint32_t cl = cw >> 16;
+                val = (cw & 0xFFFFu) | ((uint32_t)S.rle_ext[t] << cl);
+                nb = cl + c_cl_eb[sy];
+            }
+        }
+        const uint32_t incl = wave_incl_scan(nb);
+        const uint32_t pos = carry + incl - nb;
+        carry += __builtin_amdgcn_readlane(incl, 63);
+        if (nb) {
+            const uint32_t w = pos >> 5, sh = pos & 31;
+            atomicOr(&S.hdr[w], val << sh);
+            if (sh + nb > 32) atomicOr(&S.hdr[w + 1], val >> (32 - sh));
         }
     }
     __syncthreads();
-    if (bt == 2) {
-        canon_codes(S.lcl, 19, S.code, lane);   // reuse: cl codes
-        if (lane == 0) {
-            for (int k = 0; k < S.rle_n; k++) {
-                const uint32_t sy = S.rle_sym[k], cw = S.code[sy];
-                hdr_put(S, cw & 0xFFFFu, cw >> 16);
-                hdr_put(S, S.rle_ext[k], c_cl_eb[sy]);
-            }
-        }
-        __syncthreads();
-    }
-    const uint32_t hbits = S.hdr_pos;
+    const uint32_t hbits = carry;
     uint32_t* hgout = hdr_g + (uint64_t)b * DMX_HDR_WORDS;
     for (uint32_t k = lane; k < (hbits + 31) / 32; k += 64) hgout[k] = S.hdr[k];
     if (lane == 0) {
