@@ -141,6 +141,7 @@ __device__ __forceinline__ uint32_t adv_of(const MatchLDS& L, uint32_t p) {
 // longest, then nearest (largest q) -- the reference's newest-first walk with strict >
 // (:249-263).  A lane stops comparing once its best is the longest possible length.
 #define KD 32
+#define CB 12   // bytes compared in registers per candidate step; longer matches extend from LDS
 #define JR 8    // Jacobi rounds of the walk before the serial fallback
 #define CW 4
 __device__ __forceinline__ uint32_t ffbl(uint32_t x) {   // lowest set bit, ~0 for 0 (v_ffbl_b32)
@@ -227,16 +228,18 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
 // never reaches 3 equal bytes, and candidates < 3 bytes are discarded once after the max.
 // Only the first chunk of the block (GUARD) has halo lanes without entries.
 template <bool GUARD>
-__device__ __forceinline__ void cand_step(uint32_t j, uint32_t& x0, uint32_t& x1, uint32_t i0, uint32_t i1,
-                                          uint32_t h0, uint32_t h1, uint32_t nc, uint32_t lim_eff,
-                                          uint32_t& jkey, uint32_t& full) {
+__device__ __forceinline__ void cand_step(uint32_t j, uint32_t& x0, uint32_t& x1, uint32_t& x2, uint32_t i0, uint32_t i1,
+                                          uint32_t i2, uint32_t h0, uint32_t h1, uint32_t h2, uint32_t nc,
+                                          uint32_t lim_eff, uint32_t& jkey, uint32_t& full) {
     const int src = (int)j - 1;
     x0 = wshr(x0, __builtin_amdgcn_readlane(h0, src));
     x1 = wshr(x1, __builtin_amdgcn_readlane(h1, src));
-    // equal leading bits of the 8-byte window, 64 = all (ffbl(0) = ~0)
-    const uint32_t mb = min(ffbl(i0 ^ x0), min(ffbl(i1 ^ x1), 32u) + 32u);
+    x2 = wshr(x2, __builtin_amdgcn_readlane(h2, src));
+    // equal leading bits of the 12-byte window, 96 = all (ffbl(0) = ~0)
+    const uint32_t t = min(ffbl(i1 ^ x1), min(ffbl(i2 ^ x2), 32u) + 32u) + 32u;
+    const uint32_t mb = min(ffbl(i0 ^ x0), t);
     uint32_t m = min(mb >> 3, lim_eff);
-    bool fl = mb == 64u;
+    bool fl = mb == 96u;
     if (GUARD) {
         m = j <= nc ? m : 0u;
         fl = fl && j <= nc;
@@ -245,17 +248,18 @@ __device__ __forceinline__ void cand_step(uint32_t j, uint32_t& x0, uint32_t& x1
     full |= fl ? (1u << src) : 0u;
 }
 template <bool GUARD>
-__device__ __forceinline__ void cand_steps(uint32_t jmax, uint32_t i0, uint32_t i1, uint32_t h0, uint32_t h1,
-                                           uint32_t nc, uint32_t lim_eff, uint32_t& jkey, uint32_t& full) {
-    uint32_t x0 = i0, x1 = i1, y0, y1;
+__device__ __forceinline__ void cand_steps(uint32_t jmax, uint32_t i0, uint32_t i1, uint32_t i2, uint32_t h0,
+                                           uint32_t h1, uint32_t h2, uint32_t nc, uint32_t lim_eff, uint32_t& jkey,
+                                           uint32_t& full) {
+    uint32_t x0 = i0, x1 = i1, x2 = i2, y0, y1, y2;
     uint32_t j = 1;
     for (; j + 1 <= jmax; j += 2) {   // two steps per trip, alternating registers (no copies)
-        y0 = x0; y1 = x1;
-        cand_step<GUARD>(j, y0, y1, i0, i1, h0, h1, nc, lim_eff, jkey, full);
-        x0 = y0; x1 = y1;
-        cand_step<GUARD>(j + 1, x0, x1, i0, i1, h0, h1, nc, lim_eff, jkey, full);
+        y0 = x0; y1 = x1; y2 = x2;
+        cand_step<GUARD>(j, y0, y1, y2, i0, i1, i2, h0, h1, h2, nc, lim_eff, jkey, full);
+        x0 = y0; x1 = y1; x2 = y2;
+        cand_step<GUARD>(j + 1, x0, x1, x2, i0, i1, i2, h0, h1, h2, nc, lim_eff, jkey, full);
     }
-    if (j <= jmax) cand_step<GUARD>(j, x0, x1, i0, i1, h0, h1, nc, lim_eff, jkey, full);
+    if (j <= jmax) cand_step<GUARD>(j, x0, x1, x2, i0, i1, i2, h0, h1, h2, nc, lim_eff, jkey, full);
 }
 
 __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint16_t* __restrict__ pg,
@@ -269,9 +273,11 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
         const bool act = k < nvalid;
         uint32_t i = 0, nc = 0, lim = 0;
         uint64_t iv0 = 0;
+        uint32_t i2 = 0;
         if (act) {
             i = L.sorted[k];
             iv0 = ld8(L.data, i);
+            i2 = ld4(L.data, i + 8);
             // bounded mode (K <= KD) needs no bucket rank: the K entries below k are examined
             // and those of other buckets never reach 3 equal bytes (cand_steps); only the
             // first K entries of the block lack K predecessors.  Longer chains need the rank.
@@ -281,9 +287,11 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
         // halo: lane l < KD holds entry k0-1-l
         uint32_t hq = 0;
         uint64_t hv0 = 0;
+        uint32_t h2 = 0;
         if (lane < KD && k0 >= lane + 1) {
             hq = L.sorted[k0 - 1 - lane];
             hv0 = ld8(L.data, hq);
+            h2 = ld4(L.data, hq + 8);
         }
         const uint32_t i0 = (uint32_t)iv0, i1 = (uint32_t)(iv0 >> 32);
         const uint32_t h0 = (uint32_t)hv0, h1 = (uint32_t)(hv0 >> 32);
@@ -297,10 +305,10 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
                    max(__builtin_amdgcn_readlane(jmax, 47), __builtin_amdgcn_readlane(jmax, 63)));
         iters += jmax;
         const uint32_t lim_eff = act ? lim : 0;
-        uint32_t jkey = 0, full = 0;   // full: bit j-1 = candidate j matches all 8 bytes
-        if (k0 == 0) cand_steps<true>(jmax, i0, i1, h0, h1, nc, lim_eff, jkey, full);
-        else cand_steps<false>(jmax, i0, i1, h0, h1, nc, lim_eff, jkey, full);
-        if (lim_eff <= 8) full = 0;
+        uint32_t jkey = 0, full = 0;   // full: bit j-1 = candidate j matches all CB bytes
+        if (k0 == 0) cand_steps<true>(jmax, i0, i1, i2, h0, h1, h2, nc, lim_eff, jkey, full);
+        else cand_steps<false>(jmax, i0, i1, i2, h0, h1, h2, nc, lim_eff, jkey, full);
+        if (lim_eff <= CB) full = 0;
         // position form of the best key: (len << 15) | source position
         uint32_t bestkey = 0;
         if (act && (jkey >> 8) >= 3) bestkey = ((jkey >> 8) << 15) | (uint32_t)L.sorted[k - (255u - (jkey & 255u))];
@@ -315,7 +323,7 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
                 const uint32_t j = (uint32_t)__builtin_ctz(full) + 1u;
                 full &= full - 1u;
                 const uint32_t q = L.sorted[k - j];
-                const uint32_t len = min(ext_len(L, i, q, 8, lim_eff), lim_eff);
+                const uint32_t len = min(ext_len(L, i, q, CB, lim_eff), lim_eff);
                 bestkey = max(bestkey, (len << 15) | q);
             }
             if ((bestkey >> 15) >= lim_eff) full = 0;
@@ -338,7 +346,7 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
                     const uint32_t it = lds_ld(&Q[lane]), o = it >> 16;
                     const uint32_t q = L.sorted[it & 0xFFFFu], ii = L.sorted[k0 + o];
                     const uint32_t lo = min(bn - ii, (uint32_t)MAXLEN);
-                    const uint32_t len = min(ext_len(L, ii, q, 8, lo), lo);
+                    const uint32_t len = min(ext_len(L, ii, q, CB, lo), lo);
                     __hip_atomic_fetch_max(&B[o], (len << 15) | q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
                 __builtin_amdgcn_wave_barrier();
