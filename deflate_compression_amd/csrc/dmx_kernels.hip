@@ -495,32 +495,33 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         }
         *reinterpret_cast<uint4*>(&L.data[k << 2]) = v;
     }
-    // Bucket-sorted positions S (stable by position inside a bucket) and bucket starts,
-    // built here instead of by a separate chain pass: a two-pass LSD radix sort of the
-    // positions by bucket, digit 1 = bucket & 127, digit 2 = bucket >> 7.  Wave w owns the
-    // 2048 entries [2048w, 2048w+2048) of a pass.  Sweep A counts (digit, wave) with LDS
-    // atomics (order-free); an exclusive scan, digit-major, turns the counts into
-    // destinations; sweep B walks the entries again, 64 per step, groups the lanes with
-    // equal digits by ballots (stable in lane order) and writes entry -> destination +
-    // earlier lanes of its group, advancing the (digit, wave) destination.  Pass 2 reads
-    // its source (the pass-1 order) into registers first, so it can write S in place.
-    // Bucket starts = exclusive scan of a bucket histogram taken in pass 1.
+    // Bucket-sorted positions S (stable by position inside a bucket), built here instead of
+    // by a separate chain pass: a two-pass LSD radix sort of the positions by bucket,
+    // digit 1 = bucket & 127, digit 2 = bucket >> 7.  Wave w owns the 2048 entries
+    // [2048w, 2048w+2048) of a pass.  Pass 1: sweep A counts (digit, wave) with LDS atomics
+    // (order-free), an exclusive scan (digit-major) turns counts into destinations, sweep B
+    // walks the entries again 64 per step, groups lanes with equal digits (LDS match-any,
+    // stable in lane order) and writes entry -> destination + earlier lanes of its group.
+    // Sweep B also stores each entry's digit 2 at its destination and counts pass 2's
+    // (digit, wave) totals, so pass 2 is a sequential read, one scan and the scatter; it
+    // reads its source into registers first, so it can write S in place.  Chains longer
+    // than KD need bucket starts: found afterwards where the bucket changes along S.
     {
         const uint32_t nvalid = bn > 2 ? bn - 2 : 0;   // positions with a full trigram
         const bool need_starts = max_chain <= 0 || max_chain > KD;
-        uint32_t* C = L.tsm;                              // 16 x 128 digit counters (tsm + exitp)
-        uint32_t* H = reinterpret_cast<uint32_t*>(L.len8);   // 8192 bucket counts, u16 pairs
+        uint32_t* C = L.tsm;                                   // 16 x 128 pass-1 counters (tsm + exitp)
+        uint32_t* C2 = L.lit;                                  // 16 x 64 pass-2 counters (lit: zeroed after P0)
+        uint8_t* D2 = reinterpret_cast<uint8_t*>(L.bstart);    // digit 2 per pass-1 entry (bstart + len8[0, 16K))
         unsigned long long* G = reinterpret_cast<unsigned long long*>(L.len8 + DMX_BLK / 2);   // 16 x 128 lane masks
         unsigned long long* Gw = G + (wave << 7);
         for (uint32_t k = tid; k < 2 * (DMX_BLK / 32); k += MT) C[k] = 0;
-        for (uint32_t k = tid; k < DMX_NBUCKET / 2; k += MT) H[k] = 0;
+        for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) C2[k] = 0;
         for (uint32_t k = tid; k < 16 * 128; k += MT) G[k] = 0;
         __syncthreads();
         if (dbg && tid == 0) tp0[0] = __builtin_amdgcn_s_memtime();
         const uint64_t lt = (1ull << lane) - 1ull;
         const uint32_t x0 = (wave << 11) + lane;
-        // bucket of each of this lane's 32 entries, two 13-bit values per register; all
-        // 32 loads in flight at once
+        // bucket of each of this lane's 32 entries, two 13-bit values per register
         uint32_t hh[16];
 #pragma unroll
         for (int st = 0; st < 32; st += 2) {
@@ -535,7 +536,6 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         for (int st = 0; st < 32; st++) {
             const uint32_t x = x0 + ((uint32_t)st << 6);
             const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
-            if (need_starts) count_add(H, h, x < nvalid, true);
             count_add(C + (wave << 7), h & 127u, x < nvalid, false);
         }
         __syncthreads();
@@ -552,55 +552,38 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         for (int st = 0; st < 32; st++) {
             const uint32_t x = x0 + ((uint32_t)st << 6);
             const bool valid = x < nvalid;
-            const uint32_t dg = (hh[st >> 1] >> (16 * (st & 1))) & 127u;
+            const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
+            const uint32_t dg = h & 127u;
             const uint64_t eq = group_of(Gw, dg, valid);
             const uint32_t c = valid ? C[(wave << 7) + dg] : 0u;
+            const uint32_t dst = c + (uint32_t)__popcll(eq & lt);
             if (valid) {
-                L.sorted[c + (uint32_t)__popcll(eq & lt)] = (uint16_t)x;
+                L.sorted[dst] = (uint16_t)x;
+                D2[dst] = (uint8_t)(h >> 7);
                 if ((eq >> lane) == 1ull) C[(wave << 7) + dg] = c + (uint32_t)__popcll(eq);
             }
+            count_add(C2, ((dst >> 11) << 6) | (h >> 7), valid, false);   // pass 2: (wave, digit)
         }
         __syncthreads();
         if (dbg && tid == 0) tp0[1] = __builtin_amdgcn_s_memtime();
         // ---- pass 2: pass-1 order, digit = bucket >> 7
-        for (uint32_t k = tid; k < 16 * 64; k += MT) C[k] = 0;
-        uint32_t pk[16];   // this lane's 32 source entries, two u16 per register
+        uint32_t pk[16], dk[8];   // this lane's 32 source entries (u16 pairs) and digits (u8 quads)
 #pragma unroll
         for (int st = 0; st < 32; st += 2) {
             const uint32_t xa = x0 + ((uint32_t)st << 6), xb = xa + 64;
             const uint32_t pa = xa < nvalid ? (uint32_t)L.sorted[xa] : 0u;
             const uint32_t pb = xb < nvalid ? (uint32_t)L.sorted[xb] : 0u;
+            const uint32_t da = xa < nvalid ? (uint32_t)D2[xa] : 0u;
+            const uint32_t db = xb < nvalid ? (uint32_t)D2[xb] : 0u;
             pk[st >> 1] = pa | (pb << 16);
+            if ((st & 3) == 0) dk[st >> 2] = da | (db << 8);
+            else dk[st >> 2] |= (da << 16) | (db << 24);
         }
-#pragma unroll
-        for (int st = 0; st < 32; st += 2) {
-            const uint32_t xa = x0 + ((uint32_t)st << 6), xb = xa + 64;
-            const uint32_t pa = pk[st >> 1] & 0xFFFFu, pb = pk[st >> 1] >> 16;
-            const uint32_t ha = xa < nvalid ? dmx_hash(ld4(L.data, pa) & 0xFFFFFFu) : 0u;
-            const uint32_t hb = xb < nvalid ? dmx_hash(ld4(L.data, pb) & 0xFFFFFFu) : 0u;
-            hh[st >> 1] = ha | (hb << 16);
-            if ((st & 7) == 6) __builtin_amdgcn_sched_barrier(0);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int st = 0; st < 32; st++) {
-            const uint32_t x = x0 + ((uint32_t)st << 6);
-            count_add(C + (wave << 6), ((hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu) >> 7, x < nvalid, false);
-        }
-        __syncthreads();
-        {   // destinations (dg, w) at order 16*dg + w, one per thread; bucket starts
+        {   // destinations (dg, w) at order 16*dg + w, one per thread
             const uint32_t i0 = ((tid & 15) << 6) + (tid >> 4);
-            const uint32_t v0 = C[i0];
-            const uint32_t ex = block_excl_scan(L, v0, tid);
-            if (need_starts) {   // bucket starts: only chains longer than KD use them
-                uint32_t hv[8], hs = 0;
-#pragma unroll
-                for (int j = 0; j < 8; j++) { hv[j] = (H[tid * 4 + (j >> 1)] >> (16 * (j & 1))) & 0xFFFFu; hs += hv[j]; }
-                uint32_t hx = block_excl_scan(L, hs, tid);
-#pragma unroll
-                for (int j = 0; j < 8; j++) { L.bstart[tid * 8 + j] = (uint16_t)hx; hx += hv[j]; }
-            }
-            C[i0] = ex;
+            const uint32_t v0 = C2[i0];
+            const uint32_t ex = block_excl_scan(L, v0, tid);   // (its barriers also order the reads above)
+            C2[i0] = ex;
         }
         __syncthreads();
 #pragma unroll
@@ -608,12 +591,21 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
             const uint32_t x = x0 + ((uint32_t)st << 6);
             const bool valid = x < nvalid;
             const uint32_t p = (pk[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
-            const uint32_t dg = ((hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu) >> 7;
+            const uint32_t dg = (dk[st >> 2] >> (8 * (st & 3))) & 0xFFu;
             const uint64_t eq = group_of(Gw, dg, valid);
-            const uint32_t c = valid ? C[(wave << 6) + dg] : 0u;
+            const uint32_t c = valid ? C2[(wave << 6) + dg] : 0u;
             if (valid) {
                 L.sorted[c + (uint32_t)__popcll(eq & lt)] = (uint16_t)p;
-                if ((eq >> lane) == 1ull) C[(wave << 6) + dg] = c + (uint32_t)__popcll(eq);
+                if ((eq >> lane) == 1ull) C2[(wave << 6) + dg] = c + (uint32_t)__popcll(eq);
+            }
+        }
+        __syncthreads();
+        for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) L.lit[k] = 0;
+        if (need_starts) {   // bucket starts: entries whose bucket differs from the previous one
+            for (uint32_t k = tid; k < nvalid; k += MT) {
+                const uint32_t h = dmx_hash(ld4(L.data, L.sorted[k]) & 0xFFFFFFu);
+                const uint32_t hp = k ? dmx_hash(ld4(L.data, L.sorted[k - 1]) & 0xFFFFFFu) : 0xFFFFFFFFu;
+                if (h != hp) L.bstart[h] = (uint16_t)k;
             }
         }
         __syncthreads();
