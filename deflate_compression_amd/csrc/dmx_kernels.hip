@@ -422,6 +422,10 @@ __device__ __forceinline__ uint32_t resolve_word(const MatchLDS& L, uint32_t lo,
 // instructions in order, so the read sees all ORs), then the slot is cleared for reuse.
 // 3 LDS instructions instead of one ballot per bit of v.
 __device__ __forceinline__ uint64_t group_of(unsigned long long* G, uint32_t v, bool valid) {
+    const uint64_t vm = __ballot(valid);
+    if (vm == 0) return 0;
+    const uint32_t v0 = __builtin_amdgcn_readlane(v, (int)__builtin_ctzll(vm));
+    if (__ballot(valid && v != v0) == 0) return valid ? vm : 0;   // one group (runs): no LDS traffic
     uint64_t eq = 0;
     if (valid) {
         __hip_atomic_fetch_or(&G[v], 1ull << (threadIdx.x & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
