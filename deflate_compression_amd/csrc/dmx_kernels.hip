@@ -142,6 +142,7 @@ __device__ __forceinline__ uint32_t adv_of(const MatchLDS& L, uint32_t p) {
 // (:249-263).  A lane stops comparing once its best is the longest possible length.
 #define KD 32
 #define CB 12   // bytes compared in registers per candidate step; longer matches extend from LDS
+#define KE 8    // chains up to KE candidates use chunks with the halo embedded (64-K owned entries)
 #define JR 8    // Jacobi rounds of the walk before the serial fallback
 #define CW 4
 __device__ __forceinline__ uint32_t ffbl(uint32_t x) {   // lowest set bit, ~0 for 0 (v_ffbl_b32)
@@ -262,12 +263,134 @@ __device__ __forceinline__ void cand_steps(uint32_t jmax, uint32_t i0, uint32_t 
     if (j <= jmax) cand_step<GUARD>(j, x0, x1, x2, i0, i1, i2, h0, h1, h2, nc, lim_eff, jkey, full);
 }
 
+// Candidates matching all CB register bytes (any of them beats every key found in
+// registers): exact length from LDS.  Round 1: each lane's nearest one; a lane whose best
+// is then the longest possible is done (runs end here).  The rest are spread over the
+// wave's lanes through an LDS queue (one round for typical text instead of max-popcount
+// rounds) and merged with atomicMax on the key, which orders longest, then nearest.
+// kb = entry of lane 0 of the chunk (owner lane o has entry kb + o).
+__device__ __forceinline__ uint32_t resolve_full(MatchLDS& L, uint32_t bn, uint32_t lane, uint32_t wave, uint32_t k,
+                                                 uint32_t i, uint32_t lim_eff, uint32_t bestkey, uint32_t full,
+                                                 uint32_t kb) {
+    if (__ballot(full != 0) == 0) return bestkey;
+    if (full) {
+        const uint32_t j = (uint32_t)__builtin_ctz(full) + 1u;
+        full &= full - 1u;
+        const uint32_t q = L.sorted[k - j];
+        const uint32_t len = min(ext_len(L, i, q, CB, lim_eff), lim_eff);
+        bestkey = max(bestkey, (len << 15) | q);
+    }
+    if ((bestkey >> 15) >= lim_eff) full = 0;
+    const uint32_t cnt = __popc(full);
+    const uint32_t incl = wave_incl_scan(cnt);
+    const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
+    uint32_t* Q = L.tsm + (wave << 6);     // P2 arrays, free during the search
+    uint32_t* B = L.exitp + (wave << 6);
+    for (uint32_t base = 0; base < T; base += 64) {
+        lds_st(&B[lane], 0u);
+        uint32_t f = full, idx = incl - cnt;
+        while (f) {
+            const uint32_t j = (uint32_t)__builtin_ctz(f) + 1u;
+            f &= f - 1u;
+            if (idx >= base && idx < base + 64) lds_st(&Q[idx - base], (k - j) | (lane << 16));
+            idx++;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (base + lane < T) {
+            const uint32_t it = lds_ld(&Q[lane]), o = it >> 16;
+            const uint32_t q = L.sorted[it & 0xFFFFu], ii = L.sorted[kb + o];
+            const uint32_t lo = min(bn - ii, (uint32_t)MAXLEN);
+            const uint32_t len = min(ext_len(L, ii, q, CB, lo), lo);
+            __hip_atomic_fetch_max(&B[o], (len << 15) | q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __builtin_amdgcn_wave_barrier();
+        bestkey = max(bestkey, lds_ld(&B[lane]));
+        __builtin_amdgcn_wave_barrier();
+    }
+    return bestkey;
+}
+
+// Result of one position: length (len8, literal bit) in position order, distance in bucket
+// order -- one coalesced 128-byte store per wave (a store to pg[i] would scatter 2-byte
+// partial-line writes over the block).
+__device__ __forceinline__ void store_result(MatchLDS& L, uint16_t* __restrict__ pg, uint32_t k, uint32_t i,
+                                             uint32_t bestkey) {
+    if (bestkey == 0) {
+        atomicOr(&L.lit[i >> 5], 1u << (i & 31));
+        L.len8[i] = 0;
+    } else {
+        L.len8[i] = (uint8_t)((bestkey >> 15) - 3);
+    }
+    pg[k] = (uint16_t)(bestkey ? i - (bestkey & 0x7FFFu) : 0u);
+}
+
+// Candidate steps with the halo embedded in the chunk (K <= KE): lanes 0..K-1 hold the K
+// entries before the chunk's owned entries, so a plain wave_shr feeds every owned lane.
+template <bool GUARD>
+__device__ __forceinline__ void cand_step_emb(uint32_t j, uint32_t& x0, uint32_t& x1, uint32_t& x2, uint32_t i0,
+                                              uint32_t i1, uint32_t i2, uint32_t nc, uint32_t lim_eff,
+                                              uint32_t& jkey, uint32_t& full) {
+    x0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x0, 0x138, 0xF, 0xF, true);
+    x1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x1, 0x138, 0xF, 0xF, true);
+    x2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x2, 0x138, 0xF, 0xF, true);
+    const uint32_t t = min(ffbl(i1 ^ x1), min(ffbl(i2 ^ x2), 32u) + 32u) + 32u;
+    const uint32_t mb = min(ffbl(i0 ^ x0), t);
+    uint32_t m = min(mb >> 3, lim_eff);
+    bool fl = mb == 96u;
+    if (GUARD) {
+        m = j <= nc ? m : 0u;
+        fl = fl && j <= nc;
+    }
+    jkey = max(jkey, (m << 8) | (255u - j));
+    full |= fl ? (1u << (j - 1)) : 0u;
+}
+template <bool GUARD>
+__device__ __forceinline__ void cand_steps_emb(uint32_t K, uint32_t i0, uint32_t i1, uint32_t i2, uint32_t nc,
+                                               uint32_t lim_eff, uint32_t& jkey, uint32_t& full) {
+    uint32_t x0 = i0, x1 = i1, x2 = i2;
+    for (uint32_t j = 1; j <= K; j++) cand_step_emb<GUARD>(j, x0, x1, x2, i0, i1, i2, nc, lim_eff, jkey, full);
+}
+
 __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint16_t* __restrict__ pg,
                                      uint32_t tid, bool stamp, uint64_t& tdef) {
     const uint32_t lane = tid & 63, wave = tid >> 6;
     const uint32_t K = max_chain > 0 ? (uint32_t)max_chain : 0xFFFFFFFFu;
     const uint32_t nvalid = bn > 2 ? bn - 2 : 0;   // positions with a full trigram = entries of S
     uint32_t iters = 0;
+    if (K <= KE) {
+        // bounded mode with a short chain: chunks of 64-K owned entries, halo embedded
+        const uint32_t own = 64 - K;
+        for (uint32_t base = wave * own; base < nvalid; base += MW * own) {
+            const int ei = (int)(base + lane) - (int)K;   // entry of this lane
+            const uint32_t k = (uint32_t)ei;
+            const bool load = ei >= 0 && k < nvalid;
+            const bool act = lane >= K && k < nvalid;
+            uint32_t i = 0, nc = 0, lim_eff = 0;
+            uint64_t iv0 = 0;
+            uint32_t i2 = 0;
+            if (load) {
+                i = L.sorted[k];
+                iv0 = ld8(L.data, i);
+                i2 = ld4(L.data, i + 8);
+            }
+            if (act) {
+                nc = min(k, K);
+                lim_eff = (bn - i) < MAXLEN ? (bn - i) : MAXLEN;
+            }
+            iters += K;
+            uint32_t jkey = 0, full = 0;
+            const uint32_t i0 = (uint32_t)iv0, i1 = (uint32_t)(iv0 >> 32);
+            if (base == 0) cand_steps_emb<true>(K, i0, i1, i2, nc, lim_eff, jkey, full);
+            else cand_steps_emb<false>(K, i0, i1, i2, nc, lim_eff, jkey, full);
+            if (lim_eff <= CB) full = 0;
+            uint32_t bestkey = 0;
+            if (act && (jkey >> 8) >= 3) bestkey = ((jkey >> 8) << 15) | (uint32_t)L.sorted[k - (255u - (jkey & 255u))];
+            const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
+            bestkey = resolve_full(L, bn, lane, wave, k, i, lim_eff, bestkey, full, base - K);
+            if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
+            if (act) store_result(L, pg, k, i, bestkey);
+        }
+    } else
     for (uint32_t k0 = wave << 6; k0 < nvalid; k0 += MT) {
         const uint32_t k = k0 + lane;
         const bool act = k < nvalid;
@@ -313,47 +436,7 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
         uint32_t bestkey = 0;
         if (act && (jkey >> 8) >= 3) bestkey = ((jkey >> 8) << 15) | (uint32_t)L.sorted[k - (255u - (jkey & 255u))];
         const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
-        // Candidates matching all 8 bytes (any of them beats every key above): exact length
-        // from LDS.  Round 1: each lane's nearest one; a lane whose best is then the longest
-        // possible is done (runs end here).  The rest are spread over the wave's lanes through
-        // an LDS queue (one round for typical text instead of max-popcount rounds) and merged
-        // with atomicMax on the key, which orders longest, then nearest.
-        if (__ballot(full != 0)) {
-            if (full) {
-                const uint32_t j = (uint32_t)__builtin_ctz(full) + 1u;
-                full &= full - 1u;
-                const uint32_t q = L.sorted[k - j];
-                const uint32_t len = min(ext_len(L, i, q, CB, lim_eff), lim_eff);
-                bestkey = max(bestkey, (len << 15) | q);
-            }
-            if ((bestkey >> 15) >= lim_eff) full = 0;
-            const uint32_t cnt = __popc(full);
-            const uint32_t incl = wave_incl_scan(cnt);
-            const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
-            uint32_t* Q = L.tsm + (wave << 6);     // P2 arrays, free during the search
-            uint32_t* B = L.exitp + (wave << 6);
-            for (uint32_t base = 0; base < T; base += 64) {
-                lds_st(&B[lane], 0u);
-                uint32_t f = full, idx = incl - cnt;
-                while (f) {
-                    const uint32_t j = (uint32_t)__builtin_ctz(f) + 1u;
-                    f &= f - 1u;
-                    if (idx >= base && idx < base + 64) lds_st(&Q[idx - base], (k - j) | (lane << 16));
-                    idx++;
-                }
-                __builtin_amdgcn_wave_barrier();
-                if (base + lane < T) {
-                    const uint32_t it = lds_ld(&Q[lane]), o = it >> 16;
-                    const uint32_t q = L.sorted[it & 0xFFFFu], ii = L.sorted[k0 + o];
-                    const uint32_t lo = min(bn - ii, (uint32_t)MAXLEN);
-                    const uint32_t len = min(ext_len(L, ii, q, CB, lo), lo);
-                    __hip_atomic_fetch_max(&B[o], (len << 15) | q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-                __builtin_amdgcn_wave_barrier();
-                bestkey = max(bestkey, lds_ld(&B[lane]));
-                __builtin_amdgcn_wave_barrier();
-            }
-        }
+        bestkey = resolve_full(L, bn, lane, wave, k, i, lim_eff, bestkey, full, k0);
         if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
         // chains longer than KD (exhaustive mode): continue from LDS, CW candidates per iteration
         for (uint32_t c = KD;; c += CW) {
@@ -378,17 +461,7 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
                 }
             }
         }
-        if (act) {
-            if (bestkey == 0) {
-                atomicOr(&L.lit[i >> 5], 1u << (i & 31));
-                L.len8[i] = 0;
-            } else {
-                L.len8[i] = (uint8_t)((bestkey >> 15) - 3);
-            }
-            // distance in bucket order: one coalesced 128-byte store per wave (a store to
-            // pg[i] would scatter 2-byte partial-line writes over the block)
-            pg[k] = (uint16_t)(bestkey ? i - (bestkey & 0x7FFFu) : 0u);
-        }
+        if (act) store_result(L, pg, k, i, bestkey);
     }
     // the last two positions have no trigram: literals
     if (tid < 2 && bn >= 1 + tid) {
@@ -525,22 +598,27 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         if (dbg && tid == 0) tp0[0] = __builtin_amdgcn_s_memtime();
         const uint64_t lt = (1ull << lane) - 1ull;
         const uint32_t x0 = (wave << 11) + lane;
+        // per-sweep copies, laundered through an empty asm: the compiler otherwise keeps the
+        // 32 step addresses and validity masks of one sweep live into the next (spills)
+        uint32_t x0l = x0, nvl = nvalid;
         // bucket of each of this lane's 32 entries, two 13-bit values per register
         uint32_t hh[16];
+        asm volatile("" : "+v"(x0l), "+v"(nvl));
 #pragma unroll
         for (int st = 0; st < 32; st += 2) {
-            const uint32_t xa = x0 + ((uint32_t)st << 6), xb = xa + 64;
-            const uint32_t ha = xa < nvalid ? dmx_hash(ld4(L.data, xa) & 0xFFFFFFu) : 0u;
-            const uint32_t hb = xb < nvalid ? dmx_hash(ld4(L.data, xb) & 0xFFFFFFu) : 0u;
+            const uint32_t xa = x0l + ((uint32_t)st << 6), xb = xa + 64;
+            const uint32_t ha = xa < nvl ? dmx_hash(ld4(L.data, xa) & 0xFFFFFFu) : 0u;
+            const uint32_t hb = xb < nvl ? dmx_hash(ld4(L.data, xb) & 0xFFFFFFu) : 0u;
             hh[st >> 1] = ha | (hb << 16);
             if ((st & 7) == 6) __builtin_amdgcn_sched_barrier(0);   // 8 loads in flight per group
         }
         // ---- pass 1: position order, digit = bucket & 127
+        asm volatile("" : "+v"(x0l), "+v"(nvl));
 #pragma unroll
         for (int st = 0; st < 32; st++) {
-            const uint32_t x = x0 + ((uint32_t)st << 6);
+            const uint32_t x = x0l + ((uint32_t)st << 6);
             const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
-            count_add(C + (wave << 7), h & 127u, x < nvalid, false);
+            count_add(C + (wave << 7), h & 127u, x < nvl, false);
         }
         __syncthreads();
         {   // destinations, digit-major: entry (dg, w) at order 16*dg + w; two per thread
@@ -552,10 +630,11 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
             C[i1] = ex + v0;
         }
         __syncthreads();
+        asm volatile("" : "+v"(x0l), "+v"(nvl));
 #pragma unroll
         for (int st = 0; st < 32; st++) {
-            const uint32_t x = x0 + ((uint32_t)st << 6);
-            const bool valid = x < nvalid;
+            const uint32_t x = x0l + ((uint32_t)st << 6);
+            const bool valid = x < nvl;
             const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
             const uint32_t dg = h & 127u;
             const uint64_t eq = group_of(Gw, dg, valid);
@@ -567,21 +646,24 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
                 if ((eq >> lane) == 1ull) C[(wave << 7) + dg] = c + (uint32_t)__popcll(eq);
             }
             count_add(C2, ((dst >> 11) << 6) | (h >> 7), valid, false);   // pass 2: (wave, digit)
+            __builtin_amdgcn_sched_barrier(0);   // keep the unrolled steps apart (register pressure)
         }
         __syncthreads();
         if (dbg && tid == 0) tp0[1] = __builtin_amdgcn_s_memtime();
         // ---- pass 2: pass-1 order, digit = bucket >> 7
         uint32_t pk[16], dk[8];   // this lane's 32 source entries (u16 pairs) and digits (u8 quads)
+        asm volatile("" : "+v"(x0l), "+v"(nvl));
 #pragma unroll
         for (int st = 0; st < 32; st += 2) {
-            const uint32_t xa = x0 + ((uint32_t)st << 6), xb = xa + 64;
-            const uint32_t pa = xa < nvalid ? (uint32_t)L.sorted[xa] : 0u;
-            const uint32_t pb = xb < nvalid ? (uint32_t)L.sorted[xb] : 0u;
-            const uint32_t da = xa < nvalid ? (uint32_t)D2[xa] : 0u;
-            const uint32_t db = xb < nvalid ? (uint32_t)D2[xb] : 0u;
+            const uint32_t xa = x0l + ((uint32_t)st << 6), xb = xa + 64;
+            const uint32_t pa = xa < nvl ? (uint32_t)L.sorted[xa] : 0u;
+            const uint32_t pb = xb < nvl ? (uint32_t)L.sorted[xb] : 0u;
+            const uint32_t da = xa < nvl ? (uint32_t)D2[xa] : 0u;
+            const uint32_t db = xb < nvl ? (uint32_t)D2[xb] : 0u;
             pk[st >> 1] = pa | (pb << 16);
             if ((st & 3) == 0) dk[st >> 2] = da | (db << 8);
             else dk[st >> 2] |= (da << 16) | (db << 24);
+            if ((st & 7) == 6) __builtin_amdgcn_sched_barrier(0);
         }
         {   // destinations (dg, w) at order 16*dg + w, one per thread
             const uint32_t i0 = ((tid & 15) << 6) + (tid >> 4);
@@ -590,10 +672,11 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
             C2[i0] = ex;
         }
         __syncthreads();
+        asm volatile("" : "+v"(x0l), "+v"(nvl));
 #pragma unroll
         for (int st = 0; st < 32; st++) {
-            const uint32_t x = x0 + ((uint32_t)st << 6);
-            const bool valid = x < nvalid;
+            const uint32_t x = x0l + ((uint32_t)st << 6);
+            const bool valid = x < nvl;
             const uint32_t p = (pk[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
             const uint32_t dg = (dk[st >> 2] >> (8 * (st & 3))) & 0xFFu;
             const uint64_t eq = group_of(Gw, dg, valid);
@@ -602,6 +685,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
                 L.sorted[c + (uint32_t)__popcll(eq & lt)] = (uint16_t)p;
                 if ((eq >> lane) == 1ull) C2[(wave << 6) + dg] = c + (uint32_t)__popcll(eq);
             }
+            __builtin_amdgcn_sched_barrier(0);
         }
         __syncthreads();
         for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) L.lit[k] = 0;
