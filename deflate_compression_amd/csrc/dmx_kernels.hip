@@ -148,6 +148,13 @@ __device__ __forceinline__ uint32_t adv_of(const MatchLDS& L, uint32_t p) {
 __device__ __forceinline__ uint32_t ffbl(uint32_t x) {   // lowest set bit, ~0 for 0 (v_ffbl_b32)
     return x ? (uint32_t)__builtin_ctz(x) : 0xFFFFFFFFu;
 }
+// v_ffbl_b32 as the hardware defines it (lowest set bit, ~0 for 0), opaque to the
+// optimizer so it does not re-derive the zero case with compares and selects.
+__device__ __forceinline__ uint32_t ffbl_hw(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
 __device__ __forceinline__ uint32_t match_bytes(uint64_t x) {   // equal leading bytes of an 8-byte xor
     return x ? ((uint32_t)__builtin_ctzll(x) >> 3) : 8u;
 }
@@ -326,29 +333,35 @@ __device__ __forceinline__ void store_result(MatchLDS& L, uint16_t* __restrict__
 
 // Candidate steps with the halo embedded in the chunk (K <= KE): lanes 0..K-1 hold the K
 // entries before the chunk's owned entries, so a plain wave_shr feeds every owned lane.
-template <bool GUARD>
-__device__ __forceinline__ void cand_step_emb(uint32_t j, uint32_t& x0, uint32_t& x1, uint32_t& x2, uint32_t i0,
-                                              uint32_t i1, uint32_t i2, uint32_t nc, uint32_t lim_eff,
+template <bool GUARD, bool CLAMP>
+__device__ __forceinline__ void cand_step_emb(uint32_t j, uint32_t sj, uint32_t& x0, uint32_t& x1, uint32_t& x2,
+                                              uint32_t i0, uint32_t i1, uint32_t i2, uint32_t nc, uint32_t lim_eff,
                                               uint32_t& jkey, uint32_t& full) {
     x0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x0, 0x138, 0xF, 0xF, true);
     x1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x1, 0x138, 0xF, 0xF, true);
     x2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x2, 0x138, 0xF, 0xF, true);
-    const uint32_t t = min(ffbl(i1 ^ x1), min(ffbl(i2 ^ x2), 32u) + 32u) + 32u;
-    const uint32_t mb = min(ffbl(i0 ^ x0), t);
-    uint32_t m = min(mb >> 3, lim_eff);
-    bool fl = mb == 96u;
+    // equal leading bits, 96 = all CB bytes: ffbl(0) = ~0 and the saturating adds keep it
+    // there, so one min3 picks the first differing word (v_add_u32 clamp + v_min3_u32)
+    const uint32_t mb = min(min(ffbl_hw(i0 ^ x0), __builtin_elementwise_add_sat(ffbl_hw(i1 ^ x1), 32u)),
+                            min(ffbl_hw(i2 ^ x2), 32u) + 64u);
+    uint32_t m;   // bytes (mb <= 96); opaque, else it is folded into a 3-op shift/mask/or
+    asm("v_bfe_u32 %0, %1, 3, 4" : "=v"(m) : "v"(mb));
+    if (CLAMP) m = min(m, lim_eff);   // only chunks holding one of the last CB-1 positions
     if (GUARD) {
         m = j <= nc ? m : 0u;
-        fl = fl && j <= nc;
+        full |= (mb == 96u && j <= nc) ? (1u << (j - 1)) : 0u;
+    } else {
+        full |= ((mb + 32u) >> 7) << (j - 1);   // 1 iff mb == 96
     }
-    jkey = max(jkey, (m << 8) | (255u - j));
-    full |= fl ? (1u << (j - 1)) : 0u;
+    jkey = max(jkey, (m << 8) | sj);
 }
-template <bool GUARD>
+template <bool GUARD, bool CLAMP>
 __device__ __forceinline__ void cand_steps_emb(uint32_t K, uint32_t i0, uint32_t i1, uint32_t i2, uint32_t nc,
                                                uint32_t lim_eff, uint32_t& jkey, uint32_t& full) {
     uint32_t x0 = i0, x1 = i1, x2 = i2;
-    for (uint32_t j = 1; j <= K; j++) cand_step_emb<GUARD>(j, x0, x1, x2, i0, i1, i2, nc, lim_eff, jkey, full);
+    uint32_t sj = 254u;   // 255 - j, kept as its own uniform counter
+    for (uint32_t j = 1; j <= K; j++, sj--)
+        cand_step_emb<GUARD, CLAMP>(j, sj, x0, x1, x2, i0, i1, i2, nc, lim_eff, jkey, full);
 }
 
 __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint16_t* __restrict__ pg,
@@ -380,8 +393,9 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
             iters += K;
             uint32_t jkey = 0, full = 0;
             const uint32_t i0 = (uint32_t)iv0, i1 = (uint32_t)(iv0 >> 32);
-            if (base == 0) cand_steps_emb<true>(K, i0, i1, i2, nc, lim_eff, jkey, full);
-            else cand_steps_emb<false>(K, i0, i1, i2, nc, lim_eff, jkey, full);
+            if (base == 0) cand_steps_emb<true, true>(K, i0, i1, i2, nc, lim_eff, jkey, full);
+            else if (__ballot(act && lim_eff < CB)) cand_steps_emb<false, true>(K, i0, i1, i2, nc, lim_eff, jkey, full);
+            else cand_steps_emb<false, false>(K, i0, i1, i2, nc, lim_eff, jkey, full);
             if (lim_eff <= CB) full = 0;
             uint32_t bestkey = 0;
             if (act && (jkey >> 8) >= 3) bestkey = ((jkey >> 8) << 15) | (uint32_t)L.sorted[k - (255u - (jkey & 255u))];
