@@ -23,7 +23,7 @@ import struct
 __all__ = [
     "DeflateError", "Opts", "Result", "Encoder", "lib", "compress", "deflate_compress",
     "deflate_decompress", "max_compressed", "adler32_combine", "gen_text", "gen_random",
-    "COMPRESS_STATS", "E", "DMX_F_HEADER", "DMX_F_TRAILER", "DMX_F_FINAL", "DMX_ZLIB", "DMX_F_LAZY",
+    "COMPRESS_STATS", "E", "DMX_F_HEADER", "DMX_F_TRAILER", "DMX_F_FINAL", "DMX_ZLIB", "DMX_F_LAZY", "DMX_F_EXACT_SORT",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -34,6 +34,7 @@ DEFLATE_NULLTERM = 1
 DMX_F_HEADER, DMX_F_TRAILER, DMX_F_FINAL = 1, 2, 4
 DMX_ZLIB = 7
 DMX_F_LAZY = 8
+DMX_F_EXACT_SORT = 16
 _M = 1 << 24
 # global_errors.h:64-75 and deflate_errors.h:134-147
 E = {

@@ -105,6 +105,7 @@ struct __attribute__((aligned(16))) MatchLDS {
     uint32_t wexit[MW];
     uint32_t wsum[MW];
     uint32_t ntok;
+    uint32_t sortbad;   // the search saw two entries of one bucket out of position order
     unsigned long long adl_s, adl_t;
 };
 
@@ -393,6 +394,12 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
             iters += K;
             uint32_t jkey = 0, full = 0;
             const uint32_t i0 = (uint32_t)iv0, i1 = (uint32_t)(iv0 >> 32);
+            {   // sort check: the predecessor entry (lane - 1) must be earlier if same bucket
+                const uint32_t pn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)i, 0x138, 0xF, 0xF, true);
+                const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)i0, 0x138, 0xF, 0xF, true);
+                const bool bad = act && ei >= 1 && pn > i && dmx_hash(dn & 0xFFFFFFu) == dmx_hash(i0 & 0xFFFFFFu);
+                if (__ballot(bad)) L.sortbad = 1;
+            }
             if (base == 0) cand_steps_emb<true, true>(K, i0, i1, i2, nc, lim_eff, jkey, full);
             else if (__ballot(act && lim_eff < CB)) cand_steps_emb<false, true>(K, i0, i1, i2, nc, lim_eff, jkey, full);
             else cand_steps_emb<false, false>(K, i0, i1, i2, nc, lim_eff, jkey, full);
@@ -432,6 +439,12 @@ __device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain
         }
         const uint32_t i0 = (uint32_t)iv0, i1 = (uint32_t)(iv0 >> 32);
         const uint32_t h0 = (uint32_t)hv0, h1 = (uint32_t)(hv0 >> 32);
+        {   // sort check: the predecessor entry (lane - 1, lane 0: halo 0) earlier if same bucket
+            const uint32_t pn = wshr(i, __builtin_amdgcn_readlane(hq, 0));
+            const uint32_t dn = wshr(i0, __builtin_amdgcn_readlane(h0, 0));
+            const bool bad = act && k >= 1 && pn > i && dmx_hash(dn & 0xFFFFFFu) == dmx_hash(i0 & 0xFFFFFFu);
+            if (__ballot(bad)) L.sortbad = 1;
+        }
         // wave-uniform bound: the largest chain length of the chunk, capped at KD
         uint32_t jmax = act ? min(nc, (uint32_t)KD) : 0;
         jmax = max(jmax, dpp_shr(jmax, 1));
@@ -541,6 +554,23 @@ __device__ __forceinline__ void count_add(uint32_t* T, uint32_t v, bool valid, b
     }
 }
 
+// Stable rank in T[v] (a running destination): the old value of an LDS atomicAdd, which
+// same-address lanes of one instruction get in lane order on gfx950 (verified at run time
+// by the search, see sort_positions).  A step whose valid lanes share v (runs) takes one
+// add of the group size instead of a 64-way conflicting atomic.
+__device__ __forceinline__ uint32_t atomic_rank(uint32_t* T, uint32_t v, bool valid, uint64_t lt) {
+    const uint64_t vm = __ballot(valid);
+    if (vm == 0) return 0;
+    const uint32_t first = (uint32_t)__builtin_ctzll(vm);
+    const uint32_t v0 = __builtin_amdgcn_readlane(v, (int)first);
+    if (__ballot(valid && v != v0) == 0) {
+        uint32_t base = 0;
+        if ((threadIdx.x & 63) == first) base = atomicAdd(&T[v0], (uint32_t)__popcll(vm));
+        return __builtin_amdgcn_readlane(base, (int)first) + (uint32_t)__popcll(vm & lt);
+    }
+    return valid ? atomicAdd(&T[v], 1u) : 0u;
+}
+
 // Exclusive prefix sum over the 1024 threads of the workgroup (all threads call it).
 __device__ __forceinline__ uint32_t block_excl_scan(MatchLDS& L, uint32_t v, uint32_t tid) {
     const uint32_t incl = wave_incl_scan(v);
@@ -552,8 +582,154 @@ __device__ __forceinline__ uint32_t block_excl_scan(MatchLDS& L, uint32_t v, uin
     return base + incl - v;
 }
 
+// Bucket-sorted positions S (stable by position inside a bucket), built here instead of
+// by a separate chain pass: a two-pass LSD radix sort of the positions by bucket,
+// digit 1 = bucket & 127, digit 2 = bucket >> 7.  Wave w owns the 2048 entries
+// [2048w, 2048w+2048) of a pass.  Pass 1: sweep A counts (digit, wave) with LDS atomics
+// (order-free), an exclusive scan (digit-major) turns counts into destinations, sweep B
+// walks the entries again 64 per step, groups lanes with equal digits (LDS match-any,
+// stable in lane order) and writes entry -> destination + earlier lanes of its group.
+// Sweep B also stores each entry's digit 2 at its destination and counts pass 2's
+// (digit, wave) totals, so pass 2 is a sequential read, one scan and the scatter; it
+// reads its source into registers first, so it can write S in place.  Chains longer
+// than KD need bucket starts: found afterwards where the bucket changes along S.
+// Ranks inside a (digit, wave) group: EXACT = LDS match-any (order by construction); else
+// the return value of an LDS atomicAdd per lane, which gfx950 serves in lane order for
+// same-address lanes of one instruction (tools/atomic_order.hip: 0 of ~5e9 pairs out of
+// order).  That order is not a documented guarantee, so the search verifies the result
+// (every entry against its predecessor, sortbad) and the block falls back to EXACT.
+template <bool EXACT>
+__device__ __forceinline__ void sort_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint32_t tid, bool stamp,
+                                               uint64_t* tp0) {
+    const uint32_t lane = tid & 63, wave = tid >> 6;
+    const uint32_t nvalid = bn > 2 ? bn - 2 : 0;   // positions with a full trigram
+    const bool need_starts = max_chain <= 0 || max_chain > KD;
+    uint32_t* C = L.tsm;                                   // 16 x 128 pass-1 counters (tsm + exitp)
+    uint32_t* C2 = L.lit;                                  // 16 x 64 pass-2 counters (lit: zeroed after P0)
+    uint8_t* D2 = reinterpret_cast<uint8_t*>(L.bstart);    // digit 2 per pass-1 entry (bstart + len8[0, 16K))
+    unsigned long long* G = reinterpret_cast<unsigned long long*>(L.len8 + DMX_BLK / 2);   // 16 x 128 lane masks
+    unsigned long long* Gw = G + (wave << 7);
+    for (uint32_t k = tid; k < 2 * (DMX_BLK / 32); k += MT) C[k] = 0;
+    for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) C2[k] = 0;
+    for (uint32_t k = tid; k < 16 * 128; k += MT) G[k] = 0;
+    __syncthreads();
+    if (stamp && tid == 0) tp0[0] = __builtin_amdgcn_s_memtime();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint32_t x0 = (wave << 11) + lane;
+    // per-sweep copies, laundered through an empty asm: the compiler otherwise keeps the
+    // 32 step addresses and validity masks of one sweep live into the next (spills)
+    uint32_t x0l = x0, nvl = nvalid;
+    // bucket of each of this lane's 32 entries, two 13-bit values per register
+    uint32_t hh[16];
+    asm volatile("" : "+v"(x0l), "+v"(nvl));
+#pragma unroll
+    for (int st = 0; st < 32; st += 2) {
+        const uint32_t xa = x0l + ((uint32_t)st << 6), xb = xa + 64;
+        const uint32_t ha = xa < nvl ? dmx_hash(ld4(L.data, xa) & 0xFFFFFFu) : 0u;
+        const uint32_t hb = xb < nvl ? dmx_hash(ld4(L.data, xb) & 0xFFFFFFu) : 0u;
+        hh[st >> 1] = ha | (hb << 16);
+        if ((st & 7) == 6) __builtin_amdgcn_sched_barrier(0);   // 8 loads in flight per group
+    }
+    // ---- pass 1: position order, digit = bucket & 127
+    asm volatile("" : "+v"(x0l), "+v"(nvl));
+#pragma unroll
+    for (int st = 0; st < 32; st++) {
+        const uint32_t x = x0l + ((uint32_t)st << 6);
+        const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
+        count_add(C + (wave << 7), h & 127u, x < nvl, false);
+    }
+    __syncthreads();
+    {   // destinations, digit-major: entry (dg, w) at order 16*dg + w; two per thread
+        const uint32_t o0 = tid * 2, o1 = o0 + 1;
+        const uint32_t i0 = ((o0 & 15) << 7) + (o0 >> 4), i1 = ((o1 & 15) << 7) + (o1 >> 4);
+        const uint32_t v0 = C[i0], v1 = C[i1];
+        const uint32_t ex = block_excl_scan(L, v0 + v1, tid);
+        C[i0] = ex;
+        C[i1] = ex + v0;
+    }
+    __syncthreads();
+    asm volatile("" : "+v"(x0l), "+v"(nvl));
+#pragma unroll
+    for (int st = 0; st < 32; st++) {
+        const uint32_t x = x0l + ((uint32_t)st << 6);
+        const bool valid = x < nvl;
+        const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
+        const uint32_t dg = h & 127u;
+        uint32_t dst = 0;
+        if (EXACT) {   // rank = destination + earlier lanes of the same digit (LDS match-any)
+            const uint32_t c = valid ? C[(wave << 7) + dg] : 0u;
+            const uint64_t eq = group_of(Gw, dg, valid);
+            dst = c + (uint32_t)__popcll(eq & lt);
+            if (valid && (eq >> lane) == 1ull) C[(wave << 7) + dg] = c + (uint32_t)__popcll(eq);
+        } else {   // same-address LDS atomics return in lane order (checked, see above)
+            dst = atomic_rank(&C[wave << 7], dg, valid, lt);
+        }
+        if (valid) {
+            L.sorted[dst] = (uint16_t)x;
+            D2[dst] = (uint8_t)(h >> 7);
+        }
+        count_add(C2, ((dst >> 11) << 6) | (h >> 7), valid, false);   // pass 2: (wave, digit)
+        __builtin_amdgcn_sched_barrier(0);   // keep the unrolled steps apart (register pressure)
+    }
+    __syncthreads();
+    if (stamp && tid == 0) tp0[1] = __builtin_amdgcn_s_memtime();
+    // ---- pass 2: pass-1 order, digit = bucket >> 7
+    uint32_t pk[16], dk[8];   // this lane's 32 source entries (u16 pairs) and digits (u8 quads)
+    asm volatile("" : "+v"(x0l), "+v"(nvl));
+#pragma unroll
+    for (int st = 0; st < 32; st += 2) {
+        const uint32_t xa = x0l + ((uint32_t)st << 6), xb = xa + 64;
+        const uint32_t pa = xa < nvl ? (uint32_t)L.sorted[xa] : 0u;
+        const uint32_t pb = xb < nvl ? (uint32_t)L.sorted[xb] : 0u;
+        const uint32_t da = xa < nvl ? (uint32_t)D2[xa] : 0u;
+        const uint32_t db = xb < nvl ? (uint32_t)D2[xb] : 0u;
+        pk[st >> 1] = pa | (pb << 16);
+        if ((st & 3) == 0) dk[st >> 2] = da | (db << 8);
+        else dk[st >> 2] |= (da << 16) | (db << 24);
+        if ((st & 7) == 6) __builtin_amdgcn_sched_barrier(0);
+    }
+    {   // destinations (dg, w) at order 16*dg + w, one per thread
+        const uint32_t i0 = ((tid & 15) << 6) + (tid >> 4);
+        const uint32_t v0 = C2[i0];
+        const uint32_t ex = block_excl_scan(L, v0, tid);   // (its barriers also order the reads above)
+        C2[i0] = ex;
+    }
+    __syncthreads();
+    asm volatile("" : "+v"(x0l), "+v"(nvl));
+#pragma unroll
+    for (int st = 0; st < 32; st++) {
+        const uint32_t x = x0l + ((uint32_t)st << 6);
+        const bool valid = x < nvl;
+        const uint32_t p = (pk[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
+        const uint32_t dg = (dk[st >> 2] >> (8 * (st & 3))) & 0xFFu;
+        if (EXACT) {
+            const uint32_t c = valid ? C2[(wave << 6) + dg] : 0u;
+            const uint64_t eq = group_of(Gw, dg, valid);
+            if (valid) {
+                L.sorted[c + (uint32_t)__popcll(eq & lt)] = (uint16_t)p;
+                if ((eq >> lane) == 1ull) C2[(wave << 6) + dg] = c + (uint32_t)__popcll(eq);
+            }
+        } else {
+            const uint32_t dst = atomic_rank(&C2[wave << 6], dg, valid, lt);
+            if (valid) L.sorted[dst] = (uint16_t)p;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) L.lit[k] = 0;
+    if (need_starts) {   // bucket starts: entries whose bucket differs from the previous one
+        for (uint32_t k = tid; k < nvalid; k += MT) {
+            const uint32_t h = dmx_hash(ld4(L.data, L.sorted[k]) & 0xFFFFFFu);
+            const uint32_t hp = k ? dmx_hash(ld4(L.data, L.sorted[k - 1]) & 0xFFFFFFu) : 0xFFFFFFFFu;
+            if (h != hp) L.bstart[h] = (uint16_t)k;
+        }
+    }
+    __syncthreads();
+    if (stamp && tid == 0) tp0[2] = __builtin_amdgcn_s_memtime();
+}
+
 __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
-                                                       int32_t max_chain, uint32_t lazy, uint16_t* __restrict__ dist_g,
+                                                       int32_t max_chain, uint32_t mflags, uint16_t* __restrict__ dist_g,
                                                        uint32_t* __restrict__ tok_g, uint32_t* __restrict__ hist_g,
                                                        dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg) {
     __shared__ MatchLDS L;
@@ -568,7 +744,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
 
     // ---- P0: stage the block, the bucket starts and the bucket-sorted positions in LDS ----
     const uint64_t tbeg = dbg ? __builtin_amdgcn_s_memtime() : 0;
-    if (tid == 0) { L.adl_s = 0; L.adl_t = 0; }
+    if (tid == 0) { L.adl_s = 0; L.adl_t = 0; L.sortbad = (mflags & 2u) ? 1u : 0u; }   // 2: test hook
     if (dbg && tid == 0) { st_search = 0; st_iters = 0; st_def = 0; }
     for (uint32_t k = tid; k < DMX_HIST; k += MT) L.hist[k] = 0;
     for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) L.lit[k] = 0;
@@ -586,133 +762,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         }
         *reinterpret_cast<uint4*>(&L.data[k << 2]) = v;
     }
-    // Bucket-sorted positions S (stable by position inside a bucket), built here instead of
-    // by a separate chain pass: a two-pass LSD radix sort of the positions by bucket,
-    // digit 1 = bucket & 127, digit 2 = bucket >> 7.  Wave w owns the 2048 entries
-    // [2048w, 2048w+2048) of a pass.  Pass 1: sweep A counts (digit, wave) with LDS atomics
-    // (order-free), an exclusive scan (digit-major) turns counts into destinations, sweep B
-    // walks the entries again 64 per step, groups lanes with equal digits (LDS match-any,
-    // stable in lane order) and writes entry -> destination + earlier lanes of its group.
-    // Sweep B also stores each entry's digit 2 at its destination and counts pass 2's
-    // (digit, wave) totals, so pass 2 is a sequential read, one scan and the scatter; it
-    // reads its source into registers first, so it can write S in place.  Chains longer
-    // than KD need bucket starts: found afterwards where the bucket changes along S.
-    {
-        const uint32_t nvalid = bn > 2 ? bn - 2 : 0;   // positions with a full trigram
-        const bool need_starts = max_chain <= 0 || max_chain > KD;
-        uint32_t* C = L.tsm;                                   // 16 x 128 pass-1 counters (tsm + exitp)
-        uint32_t* C2 = L.lit;                                  // 16 x 64 pass-2 counters (lit: zeroed after P0)
-        uint8_t* D2 = reinterpret_cast<uint8_t*>(L.bstart);    // digit 2 per pass-1 entry (bstart + len8[0, 16K))
-        unsigned long long* G = reinterpret_cast<unsigned long long*>(L.len8 + DMX_BLK / 2);   // 16 x 128 lane masks
-        unsigned long long* Gw = G + (wave << 7);
-        for (uint32_t k = tid; k < 2 * (DMX_BLK / 32); k += MT) C[k] = 0;
-        for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) C2[k] = 0;
-        for (uint32_t k = tid; k < 16 * 128; k += MT) G[k] = 0;
-        __syncthreads();
-        if (dbg && tid == 0) tp0[0] = __builtin_amdgcn_s_memtime();
-        const uint64_t lt = (1ull << lane) - 1ull;
-        const uint32_t x0 = (wave << 11) + lane;
-        // per-sweep copies, laundered through an empty asm: the compiler otherwise keeps the
-        // 32 step addresses and validity masks of one sweep live into the next (spills)
-        uint32_t x0l = x0, nvl = nvalid;
-        // bucket of each of this lane's 32 entries, two 13-bit values per register
-        uint32_t hh[16];
-        asm volatile("" : "+v"(x0l), "+v"(nvl));
-#pragma unroll
-        for (int st = 0; st < 32; st += 2) {
-            const uint32_t xa = x0l + ((uint32_t)st << 6), xb = xa + 64;
-            const uint32_t ha = xa < nvl ? dmx_hash(ld4(L.data, xa) & 0xFFFFFFu) : 0u;
-            const uint32_t hb = xb < nvl ? dmx_hash(ld4(L.data, xb) & 0xFFFFFFu) : 0u;
-            hh[st >> 1] = ha | (hb << 16);
-            if ((st & 7) == 6) __builtin_amdgcn_sched_barrier(0);   // 8 loads in flight per group
-        }
-        // ---- pass 1: position order, digit = bucket & 127
-        asm volatile("" : "+v"(x0l), "+v"(nvl));
-#pragma unroll
-        for (int st = 0; st < 32; st++) {
-            const uint32_t x = x0l + ((uint32_t)st << 6);
-            const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
-            count_add(C + (wave << 7), h & 127u, x < nvl, false);
-        }
-        __syncthreads();
-        {   // destinations, digit-major: entry (dg, w) at order 16*dg + w; two per thread
-            const uint32_t o0 = tid * 2, o1 = o0 + 1;
-            const uint32_t i0 = ((o0 & 15) << 7) + (o0 >> 4), i1 = ((o1 & 15) << 7) + (o1 >> 4);
-            const uint32_t v0 = C[i0], v1 = C[i1];
-            const uint32_t ex = block_excl_scan(L, v0 + v1, tid);
-            C[i0] = ex;
-            C[i1] = ex + v0;
-        }
-        __syncthreads();
-        asm volatile("" : "+v"(x0l), "+v"(nvl));
-#pragma unroll
-        for (int st = 0; st < 32; st++) {
-            const uint32_t x = x0l + ((uint32_t)st << 6);
-            const bool valid = x < nvl;
-            const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
-            const uint32_t dg = h & 127u;
-            const uint64_t eq = group_of(Gw, dg, valid);
-            const uint32_t c = valid ? C[(wave << 7) + dg] : 0u;
-            const uint32_t dst = c + (uint32_t)__popcll(eq & lt);
-            if (valid) {
-                L.sorted[dst] = (uint16_t)x;
-                D2[dst] = (uint8_t)(h >> 7);
-                if ((eq >> lane) == 1ull) C[(wave << 7) + dg] = c + (uint32_t)__popcll(eq);
-            }
-            count_add(C2, ((dst >> 11) << 6) | (h >> 7), valid, false);   // pass 2: (wave, digit)
-            __builtin_amdgcn_sched_barrier(0);   // keep the unrolled steps apart (register pressure)
-        }
-        __syncthreads();
-        if (dbg && tid == 0) tp0[1] = __builtin_amdgcn_s_memtime();
-        // ---- pass 2: pass-1 order, digit = bucket >> 7
-        uint32_t pk[16], dk[8];   // this lane's 32 source entries (u16 pairs) and digits (u8 quads)
-        asm volatile("" : "+v"(x0l), "+v"(nvl));
-#pragma unroll
-        for (int st = 0; st < 32; st += 2) {
-            const uint32_t xa = x0l + ((uint32_t)st << 6), xb = xa + 64;
-            const uint32_t pa = xa < nvl ? (uint32_t)L.sorted[xa] : 0u;
-            const uint32_t pb = xb < nvl ? (uint32_t)L.sorted[xb] : 0u;
-            const uint32_t da = xa < nvl ? (uint32_t)D2[xa] : 0u;
-            const uint32_t db = xb < nvl ? (uint32_t)D2[xb] : 0u;
-            pk[st >> 1] = pa | (pb << 16);
-            if ((st & 3) == 0) dk[st >> 2] = da | (db << 8);
-            else dk[st >> 2] |= (da << 16) | (db << 24);
-            if ((st & 7) == 6) __builtin_amdgcn_sched_barrier(0);
-        }
-        {   // destinations (dg, w) at order 16*dg + w, one per thread
-            const uint32_t i0 = ((tid & 15) << 6) + (tid >> 4);
-            const uint32_t v0 = C2[i0];
-            const uint32_t ex = block_excl_scan(L, v0, tid);   // (its barriers also order the reads above)
-            C2[i0] = ex;
-        }
-        __syncthreads();
-        asm volatile("" : "+v"(x0l), "+v"(nvl));
-#pragma unroll
-        for (int st = 0; st < 32; st++) {
-            const uint32_t x = x0l + ((uint32_t)st << 6);
-            const bool valid = x < nvl;
-            const uint32_t p = (pk[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
-            const uint32_t dg = (dk[st >> 2] >> (8 * (st & 3))) & 0xFFu;
-            const uint64_t eq = group_of(Gw, dg, valid);
-            const uint32_t c = valid ? C2[(wave << 6) + dg] : 0u;
-            if (valid) {
-                L.sorted[c + (uint32_t)__popcll(eq & lt)] = (uint16_t)p;
-                if ((eq >> lane) == 1ull) C2[(wave << 6) + dg] = c + (uint32_t)__popcll(eq);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        __syncthreads();
-        for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) L.lit[k] = 0;
-        if (need_starts) {   // bucket starts: entries whose bucket differs from the previous one
-            for (uint32_t k = tid; k < nvalid; k += MT) {
-                const uint32_t h = dmx_hash(ld4(L.data, L.sorted[k]) & 0xFFFFFFu);
-                const uint32_t hp = k ? dmx_hash(ld4(L.data, L.sorted[k - 1]) & 0xFFFFFFu) : 0xFFFFFFFFu;
-                if (h != hp) L.bstart[h] = (uint16_t)k;
-            }
-        }
-        __syncthreads();
-        if (dbg && tid == 0) tp0[2] = __builtin_amdgcn_s_memtime();
-    }
+    sort_positions<false>(L, bn, max_chain, tid, dbg != nullptr, tp0);
 
     {   // Adler-32 partial sums of this block
         uint64_t s = 0, t = 0;
@@ -741,13 +791,18 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         atomicMax((unsigned long long*)&st_def, (unsigned long long)tdef);
     }
     __syncthreads();
+    if (L.sortbad) {   // never observed on gfx950: redo the block with the match-any sort
+        sort_positions<true>(L, bn, max_chain, tid, dbg != nullptr, tp0);
+        search_positions(L, bn, max_chain, pg, tid, false, tdef);
+        __syncthreads();
+    }
     const uint64_t t1 = dbg ? __builtin_amdgcn_s_memtime() : 0;
 
     // ---- P1b (DMX_F_LAZY): lazy evaluation as a per-position rule on the search results.
     // Position p (a match) becomes a literal when p+1 holds a strictly longer match; the
     // walk below then emits the literal and re-decides at p+1 -- exactly the sequential
-    // rule of dmx_oracle_parse_block_ex.  Each thread owns one 32-position literal word.
-    if (lazy) {
+    // sequential rule (bounded/lazy modes).  Each thread owns one literal word.
+    if (mflags & 1u) {   // DMX_F_LAZY
         const uint32_t lw = L.lit[tid];
         const uint32_t nb0 = (tid + 1 < DMX_BLK / 32) ? (L.lit[tid + 1] & 1u) : 1u;
         const uint32_t* l32 = reinterpret_cast<const uint32_t*>(L.len8);
@@ -972,8 +1027,8 @@ __constant__ uint8_t c_cl_eb[19] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
 // Exclusive prefix sum over one wave (64 lanes).
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v) { return wave_incl_scan(v) - v; }
 
-// Code lengths for the weights f[0..n) limited to maxbits (restated in
-// oracle/dmx_oracle.c dmx_oracle_huff_lengths): used symbols sorted by (weight, symbol);
+// Code lengths for the weights f[0..n) limited to maxbits:
+// used symbols sorted by (weight, symbol);
 // two-queue merge (ties take the leaf); depths; overflow redistribution; the longest
 // lengths to the least frequent symbols.  One wave; NR = symbol registers (64 each).
 // Sorting, depths and the length assignment are lane-parallel; only the merge is serial
@@ -1153,8 +1208,8 @@ __device__ void canon_codes(K2LDS& S, const uint8_t* len, int n, uint32_t* out, 
     }
 }
 
-// Run-length coding of the concatenated lit/len + distance code lengths (DESIGN.md §4.3,
-// oracle orc_plan_block): runs are found lane-parallel, every run's symbol count has a
+// Run-length coding of the concatenated lit/len + distance code lengths:
+// runs are found lane-parallel, every run's symbol count has a
 // closed form, and a prefix sum places each run's symbols.
 __device__ void rle_lengths(K2LDS& S, uint32_t lane) {
     const int hl = S.hlit, ns = hl + S.hdist;
@@ -1789,7 +1844,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         }
         if (ev) (void)hipEventRecord(ev[1], s);   // stage "chain": folded into the match kernel (P0)
         hipLaunchKernelGGL(dmx_match_kernel, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw,
-                           o.max_chain, (o.flags & DMX_F_LAZY) ? 1u : 0u, c->dist, c->tok, c->hist, c->info, dbg);
+                           o.max_chain, ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u), c->dist, c->tok, c->hist, c->info, dbg);
         if (ev) (void)hipEventRecord(ev[2], s);
         hipLaunchKernelGGL(dmx_huff_kernel, dim3(nblk), dim3(64), 0, s, c->hist, c->info, c->codes, c->hdr, nblk, o.flags);
         if (ev) (void)hipEventRecord(ev[3], s);

@@ -114,6 +114,8 @@ struct compress_stats {
                             an empty stored block (sync flush) so it is byte-aligned
                             and another shard can be appended */
 #define DMX_ZLIB (DMX_F_HEADER | DMX_F_TRAILER | DMX_F_FINAL)
+#define DMX_F_EXACT_SORT 16u  /* test hook: sort positions with the match-any grouping instead
+                                of lane-ordered LDS atomics (same result; used by the tests) */
 #define DMX_F_LAZY 8u    /* parse option: lazy evaluation, one position of
                             lookahead -- a match at i becomes a literal when the match at
                             i+1 is strictly longer.  Off = the reference's greedy parse. */

@@ -118,6 +118,18 @@ def test_lazy_parity(enc, golden_cases, k):
     check_stream(z, data)
 
 
+@pytest.mark.parametrize("k", [0, 8, 16])
+def test_exact_sort_fallback_parity(enc, golden_cases, k):
+    """The match-any sort (the fallback if lane-ordered LDS atomics ever misorder) gives the
+    same stream as the fast sort and the oracle."""
+    data = golden_cases["bee0"] + D.gen_text(150000, 21).tobytes() + bytes(3000) + golden_cases["runs32k"]
+    for lazy in (False, True):
+        f = D.DMX_ZLIB | (D.DMX_F_LAZY if lazy else 0)
+        z_fast, _ = enc.compress_bytes(data, max_chain=k, flags=f)
+        z_exact, _ = enc.compress_bytes(data, max_chain=k, flags=f | D.DMX_F_EXACT_SORT)
+        assert z_fast == z_exact == O.compress(data, max_chain=k, lazy=lazy)
+
+
 def test_lazy_tokens_and_edges(enc, golden_cases):
     for n in (0, 1, 2, 3, 4, 9, 258, 259, 32767, 32768, 32771):
         data = ((golden_cases["bee0"] + golden_cases["bee1"]) * 2)[:n]

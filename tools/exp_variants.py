@@ -1,0 +1,65 @@
+"""Diagnostic: build copies of the match kernel with one part knocked out (output is wrong
+by construction) to see what a phase's time is made of.  Usage (build, CPU):
+  python tools/exp_variants.py build      -> build/exp/libdmx_<name>.so
+and on the GPU box:
+  python tools/exp_variants.py run        -> P0 / search / walk cycles per variant
+"""
+import os, subprocess, sys, json
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(R, "deflate_compression_amd", "csrc")
+OUT = os.path.join(R, "build", "exp")
+
+VARIANTS = {
+    "base": [],
+    "nogroup": [("    const uint64_t vm = __ballot(valid);\n    if (vm == 0) return 0;\n    const uint32_t v0 = __builtin_amdgcn_readlane(v, (int)__builtin_ctzll(vm));",
+                 "    const uint64_t vm = __ballot(valid);\n    return valid ? (1ull << (threadIdx.x & 63)) : 0ull;\n    const uint32_t v0 = __builtin_amdgcn_readlane(v, (int)__builtin_ctzll(vm));")],
+    "ballot7": [("    uint64_t eq = 0;\n    if (valid) {\n        __hip_atomic_fetch_or(",
+                 "    uint64_t eq = vm;\n#pragma unroll\n    for (int bit = 0; bit < 7; bit++) { const bool hb = (v >> bit) & 1u; const uint64_t mk = __ballot(hb); eq &= hb ? mk : ~mk; }\n    return valid ? eq : 0ull;\n    if (valid) {\n        __hip_atomic_fetch_or(")],
+    "nocount": [("__device__ __forceinline__ void count_add(uint32_t* T, uint32_t v, bool valid, bool pair16) {\n",
+                 "__device__ __forceinline__ void count_add(uint32_t* T, uint32_t v, bool valid, bool pair16) {\n    return;\n")],
+    "noscatter": [("                L.sorted[dst] = (uint16_t)x;\n                D2[dst] = (uint8_t)(h >> 7);\n", ""),
+                  ("                L.sorted[c + (uint32_t)__popcll(eq & lt)] = (uint16_t)p;\n", "")],
+}
+
+def build():
+    os.makedirs(OUT, exist_ok=True)
+    base = open(os.path.join(SRC, "dmx_kernels.hip")).read()
+    for name, reps in VARIANTS.items():
+        s = base
+        for a, b in reps:
+            assert a in s, (name, a[:60])
+            s = s.replace(a, b)
+        src = os.path.join(OUT, f"k_{name}.hip")
+        open(src, "w").write(s)
+        obj = os.path.join(OUT, f"k_{name}.o")
+        subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-fPIC", "--offload-arch=gfx950", "-std=c++17",
+                               "-I", SRC, "-I", os.path.join(R, "include"), "-c", "-o", obj, src])
+        objs = [os.path.join(R, "build", "dmx", f) for f in ("dmx_host.o", "dmx_inflate.o", "dmx_gen.o")]
+        subprocess.check_call(["/opt/rocm/bin/hipcc", "-shared", "-fPIC", "--offload-arch=gfx950", "-o",
+                               os.path.join(OUT, f"libdmx_{name}.so"), obj] + objs + ["-lm", "-lpthread"])
+        print("built", name)
+
+def run():
+    for name in VARIANTS:
+        r = subprocess.run([sys.executable, __file__, "one", name], capture_output=True, text=True, timeout=300)
+        print(name, r.stdout.strip() or r.stderr[-300:])
+
+def one(name):
+    os.environ["DMX_STAMPS"] = "1"
+    sys.path.insert(0, R)
+    import numpy as np, torch
+    import deflate_compression_amd as D
+    D.LIB_PATH = os.path.join(OUT, f"libdmx_{name}.so")
+    n = 20_000_000
+    t = torch.from_numpy(D.gen_text(n, 0xE5818)).cuda()
+    e = D.Encoder(0, n, max_chain=8, flags=D.DMX_ZLIB | D.DMX_F_LAZY)
+    for _ in range(2):
+        out, r = e.compress_tensor(t)
+    st = e.stamps(r.nblocks).astype(np.float64)
+    e.close()
+    print(json.dumps({"p0": round(st[:, 0].mean() / 1e3, 1), "pass1_end": round(st[:, 9].mean() / 1e3, 1),
+                      "pass2_end": round(st[:, 10].mean() / 1e3, 1), "search": round(st[:, 1].mean() / 1e3, 1),
+                      "total": round(st[:, 7].mean() / 1e3, 1)}))
+
+if __name__ == "__main__":
+    {"build": build, "run": run}.get(sys.argv[1], lambda: one(sys.argv[2]))()
