@@ -365,7 +365,7 @@ __device__ __forceinline__ void cand_steps_emb(uint32_t K, uint32_t i0, uint32_t
         cand_step_emb<GUARD, CLAMP>(j, sj, x0, x1, x2, i0, i1, i2, nc, lim_eff, jkey, full);
 }
 
-__device__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint16_t* __restrict__ pg,
+__device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint16_t* __restrict__ pg,
                                      uint32_t tid, bool stamp, uint64_t& tdef) {
     const uint32_t lane = tid & 63, wave = tid >> 6;
     const uint32_t K = max_chain > 0 ? (uint32_t)max_chain : 0xFFFFFFFFu;
@@ -784,17 +784,17 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
     // ---- P1: longest match of every position ----
     const uint64_t t0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t tdef = 0;
-    const uint32_t its = search_positions(L, bn, max_chain, pg, tid, dbg != nullptr, tdef);
-    if (dbg && lane == 0) {
-        atomicAdd((unsigned long long*)&st_iters, (unsigned long long)its);
-        atomicMax((unsigned long long*)&st_search, (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
-        atomicMax((unsigned long long*)&st_def, (unsigned long long)tdef);
-    }
-    __syncthreads();
-    if (L.sortbad) {   // never observed on gfx950: redo the block with the match-any sort
-        sort_positions<true>(L, bn, max_chain, tid, dbg != nullptr, tp0);
-        search_positions(L, bn, max_chain, pg, tid, false, tdef);
+    for (uint32_t attempt = 0;; attempt++) {   // one call site keeps the search inlined
+        const uint32_t its = search_positions(L, bn, max_chain, pg, tid, dbg != nullptr, tdef);
+        if (dbg && lane == 0 && attempt == 0) {
+            atomicAdd((unsigned long long*)&st_iters, (unsigned long long)its);
+            atomicMax((unsigned long long*)&st_search, (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
+            atomicMax((unsigned long long*)&st_def, (unsigned long long)tdef);
+        }
         __syncthreads();
+        if (!L.sortbad || attempt) break;
+        // never observed on gfx950: redo the block with the match-any sort (stable by construction)
+        sort_positions<true>(L, bn, max_chain, tid, dbg != nullptr, tp0);
     }
     const uint64_t t1 = dbg ? __builtin_amdgcn_s_memtime() : 0;
 
