@@ -277,6 +277,7 @@ __device__ __forceinline__ void cand_steps(uint32_t jmax, uint32_t i0, uint32_t 
 // wave's lanes through an LDS queue (one round for typical text instead of max-popcount
 // rounds) and merged with atomicMax on the key, which orders longest, then nearest.
 // kb = entry of lane 0 of the chunk (owner lane o has entry kb + o).
+template <bool SHORT>
 __device__ __forceinline__ uint32_t resolve_full(MatchLDS& L, uint32_t bn, uint32_t lane, uint32_t wave, uint32_t k,
                                                  uint32_t i, uint32_t lim_eff, uint32_t bestkey, uint32_t full,
                                                  uint32_t kb) {
@@ -289,13 +290,34 @@ __device__ __forceinline__ uint32_t resolve_full(MatchLDS& L, uint32_t bn, uint3
         bestkey = max(bestkey, (len << 15) | q);
     }
     if ((bestkey >> 15) >= lim_eff) full = 0;
+    if (SHORT) {   // chains <= 8: filter the rest in place, extend the (rare) survivors per lane
+        const uint32_t bl = bestkey >> 15;
+        const uint8_t* D8 = reinterpret_cast<const uint8_t*>(L.data);
+        uint32_t surv = 0;
+        if (full) {
+            const uint32_t ib = D8[i + bl];
+#pragma unroll
+            for (uint32_t j = 1; j <= KE; j++)
+                if ((full >> (j - 1)) & 1u) surv |= (D8[(uint32_t)L.sorted[k - j] + bl] == ib ? 1u : 0u) << (j - 1);
+        }
+        while (__ballot(surv != 0)) {
+            if (surv) {
+                const uint32_t j = (uint32_t)__builtin_ctz(surv) + 1u;
+                surv &= surv - 1u;
+                const uint32_t q = L.sorted[k - j];
+                const uint32_t len = min(ext_len(L, i, q, CB, lim_eff), lim_eff);
+                bestkey = max(bestkey, (len << 15) | q);
+            }
+        }
+        return bestkey;
+    }
     const uint32_t cnt = __popc(full);
     const uint32_t incl = wave_incl_scan(cnt);
     const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
     uint32_t* Q = L.tsm + (wave << 6);     // P2 arrays, free during the search
     uint32_t* B = L.exitp + (wave << 6);
     for (uint32_t base = 0; base < T; base += 64) {
-        lds_st(&B[lane], 0u);
+        lds_st(&B[lane], bestkey);   // owners' best so far: filters the queued candidates
         uint32_t f = full, idx = incl - cnt;
         while (f) {
             const uint32_t j = (uint32_t)__builtin_ctz(f) + 1u;
@@ -308,8 +330,12 @@ __device__ __forceinline__ uint32_t resolve_full(MatchLDS& L, uint32_t bn, uint3
             const uint32_t it = lds_ld(&Q[lane]), o = it >> 16;
             const uint32_t q = L.sorted[it & 0xFFFFu], ii = L.sorted[kb + o];
             const uint32_t lo = min(bn - ii, (uint32_t)MAXLEN);
-            const uint32_t len = min(ext_len(L, ii, q, CB, lo), lo);
-            __hip_atomic_fetch_max(&B[o], (len << 15) | q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t bl = lds_ld(&B[o]) >> 15;   // >= CB: the owner's round-1 length
+            // only a candidate that also matches byte bl can be strictly longer
+            if (bl < lo && may_beat(L, ii, q, bl)) {
+                const uint32_t len = min(ext_len(L, ii, q, CB, lo), lo);
+                __hip_atomic_fetch_max(&B[o], (len << 15) | q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
         }
         __builtin_amdgcn_wave_barrier();
         bestkey = max(bestkey, lds_ld(&B[lane]));
@@ -407,7 +433,7 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
             uint32_t bestkey = 0;
             if (act && (jkey >> 8) >= 3) bestkey = ((jkey >> 8) << 15) | (uint32_t)L.sorted[k - (255u - (jkey & 255u))];
             const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
-            bestkey = resolve_full(L, bn, lane, wave, k, i, lim_eff, bestkey, full, base - K);
+            bestkey = resolve_full<true>(L, bn, lane, wave, k, i, lim_eff, bestkey, full, base - K);
             if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
             if (act) store_result(L, pg, k, i, bestkey);
         }
@@ -463,7 +489,7 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
         uint32_t bestkey = 0;
         if (act && (jkey >> 8) >= 3) bestkey = ((jkey >> 8) << 15) | (uint32_t)L.sorted[k - (255u - (jkey & 255u))];
         const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
-        bestkey = resolve_full(L, bn, lane, wave, k, i, lim_eff, bestkey, full, k0);
+        bestkey = resolve_full<false>(L, bn, lane, wave, k, i, lim_eff, bestkey, full, k0);
         if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
         // chains longer than KD (exhaustive mode): continue from LDS, CW candidates per iteration
         for (uint32_t c = KD;; c += CW) {

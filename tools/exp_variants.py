@@ -16,6 +16,8 @@ VARIANTS = {
     "_ballot7": [("    uint64_t eq = 0;\n    if (valid) {\n        __hip_atomic_fetch_or(",
                  "    uint64_t eq = vm;\n#pragma unroll\n    for (int bit = 0; bit < 7; bit++) { const bool hb = (v >> bit) & 1u; const uint64_t mk = __ballot(hb); eq &= hb ? mk : ~mk; }\n    return valid ? eq : 0ull;\n    if (valid) {\n        __hip_atomic_fetch_or(")],
     "nocheck": [("                const bool bad = act && ei >= 1 && pn > i && dmx_hash(dn & 0xFFFFFFu) == dmx_hash(i0 & 0xFFFFFFu);\n                if (__ballot(bad)) L.sortbad = 1;\n", "")],
+    "noqueue": [("    const uint32_t cnt = __popc(full);\n    const uint32_t incl = wave_incl_scan(cnt);", "    return bestkey;\n    const uint32_t cnt = __popc(full);\n    const uint32_t incl = wave_incl_scan(cnt);")],
+    "nodeferred": [("    if (__ballot(full != 0) == 0) return bestkey;", "    return bestkey;")],
     "nocount": [("__device__ __forceinline__ void count_add(uint32_t* T, uint32_t v, bool valid, bool pair16) {\n",
                  "__device__ __forceinline__ void count_add(uint32_t* T, uint32_t v, bool valid, bool pair16) {\n    return;\n")],
     "noscatter": [("                L.sorted[dst] = (uint16_t)x;\n                D2[dst] = (uint8_t)(h >> 7);\n", ""),
