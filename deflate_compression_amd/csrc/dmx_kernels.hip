@@ -1591,6 +1591,7 @@ __global__ __launch_bounds__(ST) void dmx_scan_kernel(dmx_blkinfo* __restrict__ 
 // ------------------------------------------------------------------------------------
 
 #define PT 256
+#define TPT 8   // tokens per thread per packing round
 
 __device__ __forceinline__ void st_or64(uint32_t* st, uint32_t pos, uint64_t v, uint32_t nb) {
     if (!nb) return;
@@ -1637,37 +1638,41 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
             const uint32_t nb = (hb - 32 * k) < 32 ? (hb - 32 * k) : 32;
             st_or64(stage, s0 + 32 * k, hg[k], nb);
         }
+        // tokens: TPT consecutive tokens per thread; a per-thread bit accumulator flushes
+        // whole words -- plain stores inside the thread's own bit range, atomicOr only on
+        // the first and last word, which it shares with its neighbours
         const uint32_t* tb = tok_g + (uint64_t)b * DMX_BLK;
         uint32_t pos = s0 + hb;
-        for (uint32_t c = 0; c < bi.ntok; c += PT) {
-            const uint32_t j = c + tid;
-            uint64_t v = 0;
-            uint32_t nb = 0;
-            if (j < bi.ntok) {
-                const uint32_t t = tb[j];
-                if ((t >> 9) == 0) {
-                    const uint32_t cw = code[t];
-                    v = cw & 0xFFFFu;
-                    nb = cw >> 16;
-                } else {
-                    uint32_t s, eb, ev;
-                    len_sym(t & 0x1FFu, s, eb, ev);
-                    uint32_t cw = code[s];
-                    v = (cw & 0xFFFFu) | ((uint64_t)ev << (cw >> 16));
-                    nb = (cw >> 16) + eb;
-                    dist_sym(t >> 9, s, eb, ev);
-                    cw = code[DMX_DIST0 + s];
-                    v |= ((uint64_t)(cw & 0xFFFFu) | ((uint64_t)ev << (cw >> 16))) << nb;
-                    nb += (cw >> 16) + eb;
+        for (uint32_t c = 0; c < bi.ntok; c += PT * TPT) {
+            const uint32_t j0 = c + tid * TPT;
+            uint32_t pv[2 * TPT], pb[2 * TPT];   // up to two pieces per token, <= 28 bits each
+            uint32_t mybits = 0;
+#pragma unroll
+            for (int t = 0; t < TPT; t++) {
+                pv[2 * t] = pb[2 * t] = pv[2 * t + 1] = pb[2 * t + 1] = 0;
+                if (j0 + t < bi.ntok) {
+                    const uint32_t tk = tb[j0 + t];
+                    if ((tk >> 9) == 0) {
+                        const uint32_t cw = code[tk];
+                        pv[2 * t] = cw & 0xFFFFu;
+                        pb[2 * t] = cw >> 16;
+                    } else {
+                        uint32_t sy, eb, ev;
+                        len_sym(tk & 0x1FFu, sy, eb, ev);
+                        uint32_t cw = code[sy];
+                        pv[2 * t] = (cw & 0xFFFFu) | (ev << (cw >> 16));
+                        pb[2 * t] = (cw >> 16) + eb;
+                        dist_sym(tk >> 9, sy, eb, ev);
+                        cw = code[DMX_DIST0 + sy];
+                        pv[2 * t + 1] = (cw & 0xFFFFu) | (ev << (cw >> 16));
+                        pb[2 * t + 1] = (cw >> 16) + eb;
+                    }
+                    mybits += pb[2 * t] + pb[2 * t + 1];
                 }
             }
-            uint32_t x = nb;   // exclusive scan of bit counts over the workgroup
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(x, o);
-                if (lane >= (uint32_t)o) x += y;
-            }
-            if (lane == 63) wsum[wave] = x;
+            // exclusive scan of the threads' bit counts over the workgroup
+            const uint32_t incl = wave_incl_scan(mybits);
+            if (lane == 63) wsum[wave] = incl;
             __syncthreads();
             uint32_t wbase = 0, tot = 0;
 #pragma unroll
@@ -1676,7 +1681,26 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
                 if ((uint32_t)w < wave) wbase += t;
                 tot += t;
             }
-            st_or64(stage, pos + wbase + x - nb, v, nb);
+            if (mybits) {
+                const uint32_t p0 = pos + wbase + incl - mybits;
+                uint32_t w = p0 >> 5, ab = p0 & 31;
+                uint64_t acc = 0;
+                bool first = true;
+#pragma unroll
+                for (int q = 0; q < 2 * TPT; q++) {
+                    acc |= (uint64_t)pv[q] << ab;
+                    ab += pb[q];
+                    if (ab >= 32) {
+                        if (first) atomicOr(&stage[w], (uint32_t)acc);
+                        else stage[w] = (uint32_t)acc;
+                        first = false;
+                        acc >>= 32;
+                        ab -= 32;
+                        w++;
+                    }
+                }
+                if (ab) atomicOr(&stage[w], (uint32_t)acc);   // shared with the next thread
+            }
             pos += tot;
             __syncthreads();
         }
