@@ -23,7 +23,7 @@ import struct
 __all__ = [
     "DeflateError", "Opts", "Result", "Encoder", "lib", "compress", "deflate_compress",
     "deflate_decompress", "max_compressed", "adler32_combine", "gen_text", "gen_random",
-    "COMPRESS_STATS", "E", "DMX_F_HEADER", "DMX_F_TRAILER", "DMX_F_FINAL", "DMX_ZLIB", "DMX_F_LAZY", "DMX_F_EXACT_SORT",
+    "COMPRESS_STATS", "E", "DMX_F_HEADER", "DMX_F_TRAILER", "DMX_F_FINAL", "DMX_ZLIB", "DMX_F_LAZY", "DMX_F_EXACT_SORT", "inflate_gpu",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -111,6 +111,8 @@ def lib() -> ctypes.CDLL:
         "dmx_ctx_stage_times": ([vp, ctypes.POINTER(ctypes.c_double), u32p], ctypes.c_int),
         "dmx_adler32_combine": ([u32, u32, u64], u32),
         "dmx_debug_stamps": ([vp, ctypes.POINTER(u64), u32], ctypes.c_int),
+        "dmx_block_index": ([vp, vp, u32, vp], ctypes.c_int),
+        "dmx_inflate_async": ([vp, u64, vp, u32, vp, u64, vp, vp], ctypes.c_int),
         "dmx_gen_text": ([vp, u64, u64], None),
         "dmx_gen_random": ([vp, u64, u64], None),
     }
@@ -177,6 +179,28 @@ def deflate_decompress(data, ops: int = 0) -> bytes:
     res = ctypes.string_at(cout.str, n)
     _libc.free(ctypes.cast(cout.str, ctypes.c_void_p))
     return res
+
+
+def inflate_gpu(z, out_cap: int, index=None, nblk: int = 0, stream=None):
+    """Inflate on the GPU (csrc/dmx_inflate_dev.hip).  z: uint8 CUDA tensor.  index=None:
+    z is a whole zlib stream, decoded in one workgroup with the Adler-32 check.  index:
+    the encoder's block index (Encoder.block_index), every block decoded in parallel.
+    Returns (uint8 tensor of out_len bytes, status) -- status 0 or -E_*."""
+    import numpy as np
+    import torch
+    L = lib()
+    dev = z.device
+    out = torch.empty(max(out_cap, 1), dtype=torch.uint8, device=dev)
+    st = torch.zeros(16, dtype=torch.uint8, device=dev)
+    s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    r = L.dmx_inflate_async(z.data_ptr(), z.numel(), index.data_ptr() if index is not None else None,
+                            nblk, out.data_ptr(), out_cap, st.data_ptr(), s)
+    _check(r, "dmx_inflate_async")
+    torch.cuda.synchronize(dev)
+    h = st.cpu().numpy()
+    status = int(np.frombuffer(h[:4].tobytes(), np.int32)[0])
+    olen = int(np.frombuffer(h[8:16].tobytes(), np.uint64)[0])
+    return out[:olen], status
 
 
 def adler32_combine(a: int, b: int, len_b: int) -> int:
@@ -277,6 +301,21 @@ class Encoder:
         _check(self._L.dmx_debug_stamps(self._ctx, a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), nblk),
                "dmx_debug_stamps")
         return a
+
+    def block_index(self, stream=None):
+        """Device block index of the last encode (uint8 tensor of nblk x 24 B dmx_iblock
+        records) for inflate_gpu's parallel mode."""
+        import torch
+        n = self.last_nblk()
+        ix = torch.empty(max(n, 1) * 24, dtype=torch.uint8, device=f"cuda:{self.device}")
+        s = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+        r = self._L.dmx_block_index(self._ctx, ix.data_ptr(), n, s)
+        if r < 0:
+            raise DeflateError(r, "dmx_block_index")
+        return ix, n
+
+    def last_nblk(self) -> int:
+        return int(self._L.dmx_last_blocks(self._ctx, None, None, None, 1 << 30))
 
     def set_timing(self, on: bool) -> None:
         self._L.dmx_ctx_set_timing(self._ctx, 1 if on else 0)

@@ -1741,6 +1741,7 @@ struct dmx_ctx {
     uint64_t dbg_cap;
     // last encode (introspection)
     uint32_t last_nblk;
+    uint32_t last_sw;
     // host staging for dmx_encode_host
     void* d_in;
     uint64_t d_in_cap;
@@ -1912,6 +1913,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
     if (ev) (void)hipEventRecord(ev[5], s);
     HIPCHK(hipGetLastError());
     c->last_nblk = nblk;
+    c->last_sw = (uint32_t)o.sw;
     return 0;
 }
 
@@ -1938,6 +1940,30 @@ extern "C" int dmx_ctx_stage_times(dmx_ctx* c, double* ms6, uint32_t* count) {
     for (int k = 0; k < 6; k++) ms6[k] = c->stage_n ? c->stage_ms[k] / c->stage_n : 0.0;
     *count = c->stage_n;
     return 0;
+}
+
+__global__ void dmx_index_kernel(const dmx_blkinfo* __restrict__ info, uint32_t nblk, uint32_t sw,
+                                 dmx_iblock* __restrict__ ix) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblk) return;
+    dmx_iblock e;
+    e.bit = info[b].off_bits;
+    e.out_off = (uint64_t)b * sw;
+    e.out_len = info[b].n;
+    e.reserved = 0;
+    ix[b] = e;
+}
+
+extern "C" int dmx_block_index(dmx_ctx* c, dmx_iblock* d_index, uint32_t cap, void* stream) {
+    if (!c || !d_index) return -(int)E_INVAL;
+    if (cap < c->last_nblk) return -(int)E_RANGE;
+    if (!c->last_nblk) return 0;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipLaunchKernelGGL(dmx_index_kernel, dim3((c->last_nblk + 255) / 256), dim3(256), 0, s, c->info, c->last_nblk,
+                       c->last_sw, d_index);
+    HIPCHK(hipGetLastError());
+    return (int)c->last_nblk;
 }
 
 extern "C" int dmx_last_blocks(dmx_ctx* c, uint32_t* ntok, uint8_t* btype, uint32_t* hdr_bits, uint32_t cap) {

@@ -163,6 +163,29 @@ int dmx_encode_result(dmx_ctx* ctx, dmx_result* r, void* stream);
 int dmx_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t out_cap,
                     uint64_t* out_len, const dmx_opts* opts);
 
+/* ---- GPU inflate, csrc/dmx_inflate_dev.hip ---- */
+/* One entry per independently decodable DEFLATE block: start bit in the stream, output
+ * offset and length.  Blocks of a dmx stream never reference earlier blocks. */
+typedef struct {
+    uint64_t bit;
+    uint64_t out_off;
+    uint32_t out_len;
+    uint32_t reserved;
+} dmx_iblock;
+typedef struct {
+    int32_t status;     /* 0 or -E_* (first error) */
+    uint32_t reserved;
+    uint64_t out_len;   /* bytes produced */
+} dmx_inflate_status;
+/* Device block index of the last encode of ctx (nblk entries into d_index, on stream). */
+int dmx_block_index(dmx_ctx* ctx, dmx_iblock* d_index, uint32_t cap, void* stream);
+/* Inflate on the GPU.  d_index != NULL: decode the nblk listed blocks in parallel (one
+ * wave each) into d_out + out_off.  d_index == NULL: decode the whole zlib stream d_z
+ * (header, blocks until BFINAL, Adler-32 check) in one workgroup.  Status in the device
+ * record d_status.  Returns 0 or -E_* (launch errors). */
+int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_iblock* d_index, uint32_t nblk, void* d_out,
+                      uint64_t out_cap, dmx_inflate_status* d_status, void* stream);
+
 /* Introspection of the last encode of ctx (tests / fd_stats): per-block token
  * counts and the token stream (t = byte | dist << 9 | len),
  * per-block BTYPE, and the lit/len + distance code lengths (286 + 30 per block). */
