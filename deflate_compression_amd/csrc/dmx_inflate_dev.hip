@@ -1,17 +1,24 @@
 // dmx_inflate_dev.hip -- RFC 1950/1951 inflate on the MI355X.
 //
-// Two modes, one kernel:
-//   * indexed: one workgroup (one wave) per DEFLATE block listed in a block index
-//     {start bit, output offset, output length}.  Blocks of a dmx stream never reference
-//     earlier blocks (every sw-sized block is its own window), so all blocks
-//     decode in parallel; the encoder exports the index (dmx_block_index).
-//   * stream: index == NULL, one workgroup decodes a whole zlib stream (header, blocks
-//     until BFINAL, Adler-32 check) sequentially -- any RFC 1950 stream, e.g. PNG IDAT.
-// Decoding is wave-uniform: every lane runs the same bit reader and table lookups, lane 0
-// stores literals, the whole wave copies matches (rounds of min(dist, 64) bytes, so an
-// overlapping source is always already written).  Output is assembled in a 32 KiB LDS
-// window and written to HBM in coalesced chunks.  Tables: a 10-bit first-level lookup
-// (len << 12 | sym) plus canonical counts for longer codes.
+// Two kernels over one decoder:
+//   * indexed (dmx_inflate_index_kernel): one single-wave workgroup per DEFLATE block listed
+//     in a block index {start bit, output offset, output length}.  Blocks of a dmx stream
+//     never reference earlier blocks (every sw-sized block is its own window),
+//     so all blocks decode in parallel; the encoder exports the index (dmx_block_index).
+//   * stream (dmx_inflate_stream_kernel): one workgroup decodes a whole zlib stream
+//     (header, blocks until BFINAL, Adler-32 check) -- any RFC 1950 stream, e.g. PNG IDAT.
+//
+// The decoder is wave-uniform and lives in scalar registers: the 64-bit bit buffer, the
+// stream word index and the output position are SGPRs (table entries come back through
+// readfirstlane), the stream is read with scalar loads, and the whole decode is one inlined
+// loop -- no calls, no scratch.  Lane 0 stores literals; a match is copied by the whole wave
+// from the periodic extension of its source (byte i of a match at distance d is the byte at
+// op - d + i mod d), so every lane reads data that existed before the match and a match of
+// up to 258 bytes is at most five independent LDS read/write rounds.  Output is assembled
+// in a 32 KiB LDS window and written to HBM in 16-byte-per-lane coalesced stores (stream
+// mode flushes every 16 KiB and folds the Adler-32 sums into the same pass).
+// Tables: 10-bit first-level lookup of 16-bit entries (symbol << 4 | code length); codes
+// longer than 10 bits take a canonical slow path (first code / count / offset per length).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -19,322 +26,471 @@
 #include "../../include/dmx.h"
 
 #define IW 32768          // window = LDS ring
+#define IM (IW - 1)
 #define IFB 10            // first-level table bits
 #define IFLUSH 16384      // stream mode: flush to HBM every IFLUSH bytes
 
 struct ITable {
-    uint16_t fast[1 << IFB];   // (len << 12) | sym, 0 = longer than IFB
-    uint16_t count[16];
-    uint16_t sym[320];         // symbols sorted by (length, symbol)
+    uint16_t fast[1 << IFB];   // sym << 4 | len; ISLOW = code longer than IFB (or none)
+    uint16_t first[16];        // first canonical code of each length
+    uint16_t cnt[16];
+    uint16_t offs[16];         // index into sym[] of the first symbol of each length
+    uint16_t sym[288];         // symbols sorted by (length, symbol)
 };
 
 struct InfLDS {
     uint8_t win[IW];
     ITable lt, dt;
     uint8_t len[320];
-    uint16_t rev[320];
+    uint8_t seq[320];
 };
 
-struct IBits {   // wave-uniform bit reader over the stream in global memory
-    const uint8_t* z;
-    uint64_t zbytes, pos;   // next byte to load
-    uint64_t bb;
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+    return ((uint64_t)rfl((uint32_t)(v >> 32)) << 32) | rfl((uint32_t)v);
+}
+
+// ---------------------------------------------------------------------------------------
+// Bit reader.  Coordinates are relative to the dword-aligned address at or below z, so the
+// fast refill is one aligned scalar dword load; words that are not wholly inside the
+// stream go through the byte path (zeros past the end, counted as overrun).
+// ---------------------------------------------------------------------------------------
+typedef __attribute__((address_space(4))) const uint32_t cu32;   // constant space: scalar loads
+
+struct IBits {
+    cu32* w;
+    const uint8_t* zb;     // aligned base as bytes
+    uint32_t lo, hi;       // valid byte range [lo, hi) relative to zb
+    uint32_t wi, wfast;    // next word; words < wfast are wholly inside the stream
     uint32_t bc;
+    uint64_t bb;
     bool over;
 };
 
-__device__ __forceinline__ void ib_refill(IBits& r) {
-    while (r.bc <= 32) {
-        uint32_t w;
-        if (r.pos + 4 <= r.zbytes) {
-            __builtin_memcpy(&w, r.z + r.pos, 4);
-        } else {
-            w = 0;
-            for (uint32_t j = 0; j < 4; j++)
-                if (r.pos + j < r.zbytes) w |= (uint32_t)r.z[r.pos + j] << (8 * j);
-            if (r.pos + 4 > r.zbytes + 8) r.over = true;   // far past the end: corrupt stream
-        }
-        r.bb |= (uint64_t)w << r.bc;
-        r.pos += 4;
+__device__ __forceinline__ uint32_t ib_word(IBits& r, uint32_t wi) {
+    if (wi < r.wfast) return r.w[wi];
+    uint32_t v = 0;
+    for (uint32_t j = 0; j < 4; j++) {
+        const uint32_t b = wi * 4 + j;
+        if (b >= r.lo && b < r.hi) v |= (uint32_t)r.zb[b] << (8 * j);
+    }
+    if (wi * 4 >= r.hi + 8) r.over = true;
+    return rfl(v);
+}
+__device__ __forceinline__ void ib_refill(IBits& r) {   // afterwards bc >= 32
+    if (r.bc <= 32) {
+        r.bb |= (uint64_t)ib_word(r, r.wi) << r.bc;
+        r.wi++;
         r.bc += 32;
     }
 }
-__device__ __forceinline__ uint32_t ib_bits(IBits& r, uint32_t n) {   // n <= 32
-    if (n == 0) return 0;
-    ib_refill(r);
-    const uint32_t v = (uint32_t)(r.bb & ((1ull << n) - 1));
+__device__ __forceinline__ void ib_seek(IBits& r, uint64_t bit) {   // bit: relative to z
+    const uint64_t ab = bit + (uint64_t)r.lo * 8;
+    r.wi = (uint32_t)(ab >> 5);
+    r.bb = (uint64_t)ib_word(r, r.wi) >> (ab & 31);
+    r.bc = 32 - (uint32_t)(ab & 31);
+    r.wi++;
+}
+__device__ __forceinline__ void ib_init(IBits& r, const uint8_t* z, uint64_t zbytes) {
+    const uintptr_t a = (uintptr_t)z;
+    r.zb = (const uint8_t*)(a & ~(uintptr_t)3);
+    r.w = (cu32*)r.zb;
+    r.lo = (uint32_t)(a & 3);
+    r.hi = r.lo + (uint32_t)zbytes;
+    r.wfast = r.hi >> 2;
+    r.over = false;
+    r.wi = 0;
+    r.bb = 0;
+    r.bc = 0;
+}
+__device__ __forceinline__ uint32_t ib_peek(const IBits& r, uint32_t n) { return (uint32_t)r.bb & ((1u << n) - 1); }
+__device__ __forceinline__ void ib_drop(IBits& r, uint32_t n) {
     r.bb >>= n;
     r.bc -= n;
+}
+__device__ __forceinline__ uint32_t ib_bits(IBits& r, uint32_t n) {   // n <= 32
+    ib_refill(r);
+    const uint32_t v = n ? ib_peek(r, n) : 0;
+    ib_drop(r, n);
     return v;
 }
-__device__ __forceinline__ void ib_align(IBits& r) {   // to a byte boundary
-    const uint32_t d = r.bc & 7;
-    r.bb >>= d;
-    r.bc -= d;
+__device__ __forceinline__ uint64_t ib_bytepos(const IBits& r) {   // after ib_align; relative to z
+    return (uint64_t)r.wi * 4 - r.bc / 8 - r.lo;
 }
-__device__ __forceinline__ uint64_t ib_bitpos(const IBits& r) { return r.pos * 8 - r.bc; }
 
-// Build a table from len[0..n): lane 0 sorts (counts, offsets, canonical codes), all
-// lanes fill the first-level entries.  Returns 0 ok, <0 over-subscribed, >0 incomplete.
-__device__ int itable_build(InfLDS& S, ITable& T, int n, uint32_t lane) {
-    __shared__ int res;
-    for (int k = (int)lane; k < (1 << IFB); k += 64) T.fast[k] = 0;
-    if (lane == 0) {
-        uint16_t offs[16];
-        for (int l = 0; l < 16; l++) T.count[l] = 0;
-        for (int s = 0; s < n; s++) T.count[S.len[s]]++;
-        int left = 1, r = 0;
-        for (int l = 1; l < 16; l++) {
-            left <<= 1;
-            left -= T.count[l];
-            if (left < 0) { r = -1; break; }
+// ---------------------------------------------------------------------------------------
+// Huffman tables.  Lane l (1..15) owns code length l: it counts its symbols, then assigns
+// their canonical codes in symbol order and fills their first-level entries.  Entries are
+// sym << 4 | len; ISLOW marks a code longer than IFB bits (or no code), so "literal" is the
+// single test e < 256 << 4.  Returns 0 complete, 1 incomplete, -1 over-subscribed.
+// ---------------------------------------------------------------------------------------
+#define ISLOW 0xFFFFu
+#define ILIT (256u << 4)
+
+__device__ __forceinline__ int itable_build(InfLDS& S, ITable& T, int n, uint32_t lane) {
+    for (int k = (int)lane; k < (1 << IFB); k += 64) T.fast[k] = (uint16_t)ISLOW;
+    uint32_t c = 0;
+    if (lane >= 1 && lane < 16)
+        for (int s = 0; s < n; s++) c += S.len[s] == lane;
+    // Kraft check, first codes and offsets (uniform, unrolled)
+    int left = 1, res = 0;
+    uint32_t code = 0, off = 0, firstl = 0, offl = 0, cprev = 0;
+    for (int l = 1; l < 16; l++) {
+        const uint32_t cl = rfl(__builtin_amdgcn_readlane(c, l));
+        left = 2 * left - (int)cl;
+        if (left < 0) res = -1;
+        code = (code + cprev) << 1;
+        if ((uint32_t)l == lane) { firstl = code; offl = off; }
+        if (lane == 0) {
+            T.first[l] = (uint16_t)code;
+            T.cnt[l] = (uint16_t)cl;
+            T.offs[l] = (uint16_t)off;
         }
-        if (r == 0) r = left;   // > 0: incomplete
-        offs[1] = 0;
-        for (int l = 1; l < 15; l++) offs[l + 1] = offs[l] + T.count[l];
-        uint32_t code = 0;
-        uint32_t next[16];
-        for (int l = 1; l < 16; l++) { code = (code + (l > 1 ? T.count[l - 1] : 0)) << 1; next[l] = code; }
-        for (int s = 0; s < n; s++) {
-            const int l = S.len[s];
-            if (!l) continue;
-            T.sym[offs[l]++] = (uint16_t)s;
-            const uint32_t c = next[l]++;
-            S.rev[s] = (uint16_t)(__brev(c) >> (32 - l));
-        }
-        res = T.count[0] == n ? 0 : r;
+        off += cl;
+        cprev = cl;
     }
+    if (res == 0 && left > 0) res = 1;
+    if (off == 0) res = 1;   // no codes at all
     __syncthreads();
-    for (int s = (int)lane; s < n; s += 64) {
-        const int l = S.len[s];
-        if (l == 0 || l > IFB) continue;
-        const uint32_t rv = S.rev[s];
-        for (uint32_t k = 0; k < (1u << (IFB - l)); k++) T.fast[rv | (k << l)] = (uint16_t)((l << 12) | s);
+    if (res >= 0 && lane >= 1 && lane < 16 && c) {
+        uint32_t k = 0;
+        for (int s = 0; s < n; s++) {
+            if (S.len[s] != lane) continue;
+            T.sym[offl + k] = (uint16_t)s;
+            if (lane <= IFB) {
+                const uint32_t rv = __brev(firstl + k) >> (32 - lane);
+                const uint16_t e = (uint16_t)((s << 4) | lane);
+                for (uint32_t j = 0; j < (1u << (IFB - lane)); j++) T.fast[rv | (j << lane)] = e;
+            }
+            k++;
+        }
     }
     __syncthreads();
     return res;
 }
 
-// One symbol (wave-uniform).  -1: invalid code.
-__device__ __forceinline__ int isym(IBits& r, const ITable& T) {
-    ib_refill(r);
-    const uint32_t e = T.fast[r.bb & ((1u << IFB) - 1)];
-    if (e) {
-        const uint32_t l = e >> 12;
-        r.bb >>= l;
-        r.bc -= l;
-        return (int)(e & 0xFFFu);
+// Entry for the code at the reader (caller refilled: bc >= 15): the first-level entry, or
+// for longer codes the canonical decode; ISLOW = no valid code.
+__device__ __forceinline__ uint32_t ientry_slow(const IBits& r, const ITable& T) {
+    const uint32_t cr = __brev((uint32_t)r.bb);   // next bits, first bit in the MSB
+    for (uint32_t l = IFB + 1; l < 16; l++) {
+        const uint32_t code = cr >> (32 - l);
+        const uint32_t d = code - rfl(T.first[l]);
+        if (d < rfl(T.cnt[l])) return (rfl(T.sym[rfl(T.offs[l]) + d]) << 4) | l;
     }
-    // canonical decode, one bit at a time (codes longer than IFB; rare)
-    int code = 0, first = 0, index = 0;
-    for (int l = 1; l < 16; l++) {
-        code |= (int)(r.bb & 1u);
-        r.bb >>= 1;
-        r.bc -= 1;
-        const int c = T.count[l];
-        if (code - c < first) return T.sym[index + (code - first)];
-        index += c;
-        first += c;
-        first <<= 1;
-        code <<= 1;
-    }
-    return -1;
+    return ISLOW;
+}
+__device__ __forceinline__ uint32_t ientry(const IBits& r, const ITable& T) {
+    const uint32_t e = rfl(T.fast[ib_peek(r, IFB)]);
+    return e != ISLOW ? e : ientry_slow(r, T);
 }
 
-__constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
-                                     35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__constant__ uint8_t c_lext[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t c_dbase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385,
-                                     513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-__constant__ uint8_t c_dext[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+// DEFLATE length / distance bases by arithmetic (RFC 1951 3.2.5), no table loads.
+__device__ __forceinline__ uint32_t len_extra(uint32_t li) { return li < 8 || li == 28 ? 0 : (li - 4) >> 2; }
+__device__ __forceinline__ uint32_t len_base(uint32_t li) {
+    return li < 8 ? li + 3 : li == 28 ? 258 : ((4 + (li & 3)) << ((li - 4) >> 2)) + 3;
+}
+__device__ __forceinline__ uint32_t dist_extra(uint32_t d) { return d < 4 ? 0 : (d - 2) >> 1; }
+__device__ __forceinline__ uint32_t dist_base(uint32_t d) { return d < 4 ? d + 1 : ((2 + (d & 1)) << ((d - 2) >> 1)) + 1; }
+
 __constant__ uint8_t c_iclorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-// Output state of one workgroup: op = bytes produced (absolute), fl = bytes flushed to HBM.
+// ---------------------------------------------------------------------------------------
+// Output.  Positions are 32-bit and relative to ob (a multiple of IW, so the window index
+// of a position is pos & IM); stream mode moves ob forward as it flushes.
+// ---------------------------------------------------------------------------------------
 struct IOut {
-    uint8_t* out;
-    uint64_t base, cap, op, fl;
-    bool ring;   // stream mode: the window wraps and is flushed as it fills
+    uint8_t* out;     // + base + ob = position 0
+    uint64_t base, ob, cap;   // cap: absolute output capacity
+    uint32_t op, fl;  // produced / flushed (relative)
+    uint32_t a, b;    // stream mode: Adler-32 of everything flushed
 };
+#define IRENORM (1u << 30)
 
-__device__ __forceinline__ void io_flush(InfLDS& S, IOut& o, uint64_t upto, uint32_t lane) {
-    for (uint64_t p = o.fl + lane; p < upto; p += 64) o.out[o.base + p] = S.win[p & (IW - 1)];
+__device__ __forceinline__ uint32_t io_caprel(const IOut& o) {
+    const uint64_t c = o.cap - o.ob;
+    return c > 0x80000000ull ? 0x80000000u : (uint32_t)c;
+}
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+    for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s, 64);
+    return v;
+}
+
+// Write window bytes [fl, upto) to HBM (upto - fl <= IW).  ADLER: fold them into (a, b).
+template <bool ADLER>
+__device__ __forceinline__ void io_flush(InfLDS& S, IOut& o, uint32_t upto, uint32_t lane) {
+    __syncthreads();
+    uint8_t* dst = o.out + o.base + o.ob;
+    const uint32_t n = upto - o.fl;
+    uint64_t ss = 0, tt = 0;
+    uint32_t p = o.fl;
+    // byte head up to a 16-byte aligned destination
+    const uint32_t head = min(n, (uint32_t)((16 - (((uintptr_t)dst + p) & 15)) & 15));
+    if (lane < head) {
+        const uint32_t x = S.win[(p + lane) & IM];
+        dst[p + lane] = (uint8_t)x;
+        if (ADLER) { ss += x; tt += (uint64_t)(n - lane) * x; }
+    }
+    p += head;
+    // 16 bytes per lane
+    for (; p + 16 <= upto; p += 1024) {
+        const uint32_t q = p + lane * 16;
+        if (q + 16 <= upto) {
+            uint32_t w[4];
+            const uint32_t wp = q & IM;
+            if ((wp & 15) == 0) {
+                const uint4 v = *(const uint4*)&S.win[wp];
+                w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+            } else {
+                for (int k = 0; k < 4; k++) {
+                    uint32_t x = 0;
+                    for (int j = 0; j < 4; j++) x |= (uint32_t)S.win[(q + 4 * k + j) & IM] << (8 * j);
+                    w[k] = x;
+                }
+            }
+            *(uint4*)&dst[q] = make_uint4(w[0], w[1], w[2], w[3]);
+            if (ADLER) {
+                const uint32_t rem = upto - q;   // weight of the first byte
+                for (int k = 0; k < 16; k++) {
+                    const uint32_t x = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+                    ss += x;
+                    tt += (uint64_t)(rem - k) * x;
+                }
+            }
+        } else if (q < upto) {   // the last partial stride: bytes
+            for (uint32_t t = q; t < upto; t++) {
+                const uint32_t x = S.win[t & IM];
+                dst[t] = (uint8_t)x;
+                if (ADLER) { ss += x; tt += (uint64_t)(upto - t) * x; }
+            }
+        }
+    }
+    if (p < upto && lane == 0) {   // fewer than 16 bytes left after the loop
+        for (uint32_t t = p; t < upto; t++) {
+            const uint32_t x = S.win[t & IM];
+            dst[t] = (uint8_t)x;
+            if (ADLER) { ss += x; tt += (uint64_t)(upto - t) * x; }
+        }
+    }
+    if (ADLER) {
+        ss = wave_sum64(ss);
+        tt = wave_sum64(tt);
+        // a' = a + S; b' = b + n * a + T  (mod 65521)
+        const uint64_t b2 = (o.b + (uint64_t)(n % 65521) * o.a + tt % 65521) % 65521;
+        o.a = rfl((uint32_t)((o.a + ss % 65521) % 65521));
+        o.b = rfl((uint32_t)b2);
+    }
     o.fl = upto;
+    if (o.fl >= IRENORM) {   // keep relative positions small (ob stays a multiple of IW)
+        o.ob += IRENORM;
+        o.op -= IRENORM;
+        o.fl -= IRENORM;
+    }
     __syncthreads();
 }
 
-// Decode the symbols of one Huffman block.  Returns 0 or -E_*.
-__device__ int icodes(InfLDS& S, IBits& r, IOut& o, uint32_t lane, bool fixed_dist) {
-    for (;;) {
-        const int sy = isym(r, S.lt);
-        if (sy < 0) return -(int)E_HUFINV;
-        if (sy < 256) {
-            if (o.op >= o.cap) return -(int)E_SZ;
-            if (lane == 0) S.win[o.op & (IW - 1)] = (uint8_t)sy;
-            o.op++;
-        } else if (sy == 256) {
-            return 0;
-        } else {
-            const int li = sy - 257;
-            if (li >= 29) return -(int)E_HUFVAL;
-            const uint32_t len = c_lbase[li] + ib_bits(r, c_lext[li]);
-            int ds;
-            if (fixed_dist) ds = (int)(__brev(ib_bits(r, 5)) >> 27);
-            else ds = isym(r, S.dt);
-            if (ds < 0 || ds >= 30) return -(int)E_HUFVAL;
-            const uint32_t dist = c_dbase[ds] + ib_bits(r, c_dext[ds]);
-            if (dist > o.op || dist > IW) return -(int)E_HUFDIS;
-            if (o.op + len > o.cap) return -(int)E_SZ;
-            const uint32_t step = dist < 64 ? dist : 64;
-            __builtin_amdgcn_wave_barrier();
-            for (uint32_t t = 0; t < len; t += step) {
-                const uint32_t m = min(step, len - t);
-                if (lane < m) {
-                    const uint64_t d = o.op + t + lane;
-                    S.win[d & (IW - 1)] = S.win[(d - dist) & (IW - 1)];
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
-            o.op += len;
-        }
-        if (o.ring && o.op - o.fl >= IFLUSH) io_flush(S, o, o.fl + IFLUSH, lane);
-        if (r.over) return -(int)E_LEN;
-    }
-}
-
-// One DEFLATE block at the reader.  Returns 0 / -E_*; *last = BFINAL.
-__device__ int iblock(InfLDS& S, IBits& r, IOut& o, uint32_t lane, bool* last) {
-    *last = ib_bits(r, 1) != 0;
+// ---------------------------------------------------------------------------------------
+// One DEFLATE block at the reader.  Returns 0 / -E_*; last = BFINAL.
+// ---------------------------------------------------------------------------------------
+template <bool RING>
+__device__ __forceinline__ int iblock(InfLDS& S, IBits& r, IOut& o, uint32_t lane, bool& last) {
+    last = ib_bits(r, 1) != 0;
     const uint32_t bt = ib_bits(r, 2);
     if (bt == 0) {   // stored
-        ib_align(r);
+        ib_drop(r, r.bc & 7);
         const uint32_t len = ib_bits(r, 16), nlen = ib_bits(r, 16);
         if (len != (~nlen & 0xFFFFu)) return -(int)E_ZNLEN;
-        if (o.op + len > o.cap) return -(int)E_SZ;
-        // bytes still in the bit buffer first, then straight from the stream
-        uint32_t k = 0;
-        while (k < len && r.bc >= 8) {
-            if (lane == 0) S.win[(o.op + k) & (IW - 1)] = (uint8_t)(r.bb & 0xFFu);
-            r.bb >>= 8;
-            r.bc -= 8;
-            k++;
+        if (len > io_caprel(o) - o.op) return -(int)E_SZ;
+        const uint64_t src = ib_bytepos(r);   // relative to z
+        if (src + len + r.lo > r.hi) return -(int)E_LEN;
+        const uint8_t* zs = r.zb + r.lo + src;
+        for (uint32_t c0 = 0; c0 < len; c0 += IFLUSH) {   // pieces the ring can hold
+            if (RING && o.op - o.fl > IW - IFLUSH) io_flush<true>(S, o, o.op, lane);
+            const uint32_t ce = min(len, c0 + (uint32_t)IFLUSH);
+            for (uint32_t j = c0 + lane; j < ce; j += 64) S.win[(o.op + (j - c0)) & IM] = zs[j];
+            o.op += ce - c0;
         }
-        __builtin_amdgcn_wave_barrier();
-        if (k < len) {   // the bit buffer is empty now: copy the rest from memory
-            const uint64_t src = r.pos;
-            if (src + (len - k) > r.zbytes) return -(int)E_LEN;
-            for (uint32_t c0 = k; c0 < len; c0 += IFLUSH) {   // pieces the ring can hold
-                if (o.ring) io_flush(S, o, o.op + c0, lane);
-                const uint32_t ce = min(len, c0 + (uint32_t)IFLUSH);
-                for (uint32_t j = c0 + lane; j < ce; j += 64) S.win[(o.op + j) & (IW - 1)] = r.z[src + (j - k)];
-                __syncthreads();
-            }
-            r.pos = src + (len - k);
-            r.bb = 0;
-            r.bc = 0;
-        }
-        o.op += len;
+        __syncthreads();
+        ib_seek(r, (src + len) * 8);
         return 0;
     }
+    if (bt == 3) return -(int)E_ZBTYPE;
+    int nlen = 288, ndist = 30;
     if (bt == 1) {   // fixed codes
-        for (int s = (int)lane; s < 288; s += 64) S.len[s] = (uint8_t)(s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8);
+        for (int s = (int)lane; s < 320; s += 64)
+            S.seq[s] = (uint8_t)(s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5);
+    } else {
+        nlen = (int)ib_bits(r, 5) + 257;
+        ndist = (int)ib_bits(r, 5) + 1;
+        const int ncode = (int)ib_bits(r, 4) + 4;
+        if (nlen > 286 || ndist > 30) return -(int)E_ZINV;
+        if (lane < 19) S.len[lane] = 0;
         __syncthreads();
-        itable_build(S, S.lt, 288, lane);
-        return icodes(S, r, o, lane, true);
-    }
-    if (bt != 2) return -(int)E_ZBTYPE;
-    const int nlen = (int)ib_bits(r, 5) + 257, ndist = (int)ib_bits(r, 5) + 1, ncode = (int)ib_bits(r, 4) + 4;
-    if (nlen > 286 || ndist > 30) return -(int)E_ZINV;
-    for (int s = (int)lane; s < 19; s += 64) S.len[s] = 0;
-    __syncthreads();
-    uint32_t clv[19];
-    for (int k = 0; k < ncode; k++) clv[k] = ib_bits(r, 3);
-    if (lane == 0)
-        for (int k = 0; k < ncode; k++) S.len[c_iclorder[k]] = (uint8_t)clv[k];
-    __syncthreads();
-    if (itable_build(S, S.lt, 19, lane) != 0) return -(int)E_HUFAMB;
-    // code lengths with runs (wave-uniform decode, lane 0 stores)
-    uint8_t lens_prev = 0;
-    int idx = 0;
-    __shared__ uint8_t seq[320];
-    while (idx < nlen + ndist) {
-        const int sy = isym(r, S.lt);
-        if (sy < 0) return -(int)E_HUFINV;
-        if (sy < 16) {
-            if (lane == 0) seq[idx] = (uint8_t)sy;
-            lens_prev = (uint8_t)sy;
-            idx++;
-        } else {
-            uint32_t rep;
-            uint8_t v = 0;
-            if (sy == 16) {
-                if (idx == 0) return -(int)E_ZINV;
-                v = lens_prev;
-                rep = 3 + ib_bits(r, 2);
-            } else if (sy == 17) {
-                rep = 3 + ib_bits(r, 3);
-            } else {
-                rep = 11 + ib_bits(r, 7);
-            }
-            if (idx + (int)rep > nlen + ndist) return -(int)E_ZINV;
-            for (uint32_t q = lane; q < rep; q += 64) seq[idx + q] = v;
-            lens_prev = v;
-            idx += (int)rep;
+        for (int k = 0; k < ncode; k++) {
+            const uint32_t v = ib_bits(r, 3);
+            if (lane == 0) S.len[c_iclorder[k]] = (uint8_t)v;
         }
-        __builtin_amdgcn_wave_barrier();
+        __syncthreads();
+        if (itable_build(S, S.lt, 19, lane) != 0) return -(int)E_HUFAMB;
+        uint32_t prev = 0;
+        int idx = 0, err = 0;
+        while (idx < nlen + ndist) {
+            ib_refill(r);
+            const uint32_t e = ientry(r, S.lt);
+            if (e == ISLOW) { err = -(int)E_HUFINV; break; }
+            ib_drop(r, e & 15u);
+            const uint32_t sy = e >> 4;
+            if (sy < 16) {
+                if (lane == 0) S.seq[idx] = (uint8_t)sy;
+                prev = sy;
+                idx++;
+            } else {
+                uint32_t rep, v = 0;
+                if (sy == 16) {
+                    if (idx == 0) { err = -(int)E_ZINV; break; }
+                    v = prev;
+                    rep = 3 + ib_bits(r, 2);
+                } else if (sy == 17) {
+                    rep = 3 + ib_bits(r, 3);
+                } else {
+                    rep = 11 + ib_bits(r, 7);
+                }
+                if (idx + (int)rep > nlen + ndist) { err = -(int)E_ZINV; break; }
+                for (uint32_t q = lane; q < rep; q += 64) S.seq[idx + q] = (uint8_t)v;
+                prev = v;
+                idx += (int)rep;
+            }
+        }
+        if (err) return err;
+        __syncthreads();
+        if (rfl(S.seq[256]) == 0) return -(int)E_ZINV;
     }
+    // literal/length table from seq[0, nlen), distance table from seq[nlen, nlen + ndist)
+    for (int s = (int)lane; s < 288; s += 64) S.len[s] = s < nlen ? S.seq[s] : 0;
     __syncthreads();
-    for (int s = (int)lane; s < 288; s += 64) S.len[s] = s < nlen ? seq[s] : 0;
-    __syncthreads();
-    if (S.len[256] == 0) return -(int)E_ZINV;
     int e = itable_build(S, S.lt, nlen, lane);
-    if (e < 0 || (e > 0 && nlen - S.lt.count[0] != 1)) return -(int)E_HUFAMB;
-    for (int s = (int)lane; s < 30; s += 64) S.len[s] = s < ndist ? seq[nlen + s] : 0;
+    if (e < 0 || (e > 0 && bt == 2 && rfl(S.lt.offs[15] + S.lt.cnt[15]) != 1)) return -(int)E_HUFAMB;
+    for (int s = (int)lane; s < 32; s += 64) S.len[s] = s < ndist ? S.seq[nlen + s] : 0;
     __syncthreads();
     e = itable_build(S, S.dt, ndist, lane);
-    if (e < 0 || (e > 0 && ndist - S.dt.count[0] != 1)) return -(int)E_HUFAMB;
-    return icodes(S, r, o, lane, false);
+    if (e < 0 || (e > 0 && bt == 2 && rfl(S.dt.offs[15] + S.dt.cnt[15]) > 1)) return -(int)E_HUFAMB;
+
+    // symbols.  The inner loop is the literal run: one lookup, one compare, one byte store.
+    uint32_t op = o.op;
+    uint32_t capr = io_caprel(o);
+    int err = 0;
+    for (;;) {
+        const uint32_t lim = RING ? min(capr, o.fl + IFLUSH) : capr;
+        uint32_t en;
+        for (;;) {
+            ib_refill(r);
+            en = rfl(S.lt.fast[ib_peek(r, IFB)]);
+            if (en >= ILIT || op >= lim) break;
+            ib_drop(r, en & 15u);
+            if (lane == 0) S.win[op & IM] = (uint8_t)(en >> 4);
+            op++;
+        }
+        if (RING && op - o.fl >= IFLUSH) {
+            o.op = op;
+            io_flush<true>(S, o, o.fl + IFLUSH, lane);
+            op = o.op;
+            capr = io_caprel(o);
+            continue;
+        }
+        if (en == ISLOW) en = ientry_slow(r, S.lt);
+        if (en == ISLOW) { err = -(int)E_HUFINV; break; }
+        ib_drop(r, en & 15u);
+        const uint32_t sy = en >> 4;
+        if (sy < 256) {   // a literal at the capacity limit
+            if (op >= capr) { err = -(int)E_SZ; break; }
+            if (lane == 0) S.win[op & IM] = (uint8_t)sy;
+            op++;
+            continue;
+        }
+        if (sy == 256) break;
+        const uint32_t li = sy - 257;
+        if (li >= 29) { err = -(int)E_HUFVAL; break; }
+        const uint32_t len = len_base(li) + ib_bits(r, len_extra(li));
+        ib_refill(r);
+        const uint32_t ed = ientry(r, S.dt);
+        const uint32_t ds = ed >> 4;
+        if (ed == ISLOW || ds >= 30) { err = -(int)E_HUFVAL; break; }
+        ib_drop(r, ed & 15u);
+        const uint32_t dist = dist_base(ds) + ib_bits(r, dist_extra(ds));
+        if (o.ob == 0 && dist > op) { err = -(int)E_HUFDIS; break; }
+        if (len > capr - op) { err = -(int)E_SZ; break; }
+        const uint32_t src = op - dist;
+        if (dist >= 64 || dist >= len) {   // every read is of bytes written before its round
+            for (uint32_t t = lane; t < len; t += 64) S.win[(op + t) & IM] = S.win[(src + t) & IM];
+        } else {   // short period: byte t repeats byte t mod dist
+            const float inv = 1.0f / (float)dist;
+            for (uint32_t t = lane; t < len; t += 64) {
+                int q = (int)((float)t * inv);
+                int rm = (int)t - q * (int)dist;
+                if (rm >= (int)dist) rm -= (int)dist;
+                if (rm < 0) rm += (int)dist;
+                S.win[(op + t) & IM] = S.win[(src + (uint32_t)rm) & IM];
+            }
+        }
+        op += len;
+    }
+    o.op = op;
+    if (err) return err;
+    if (r.over) return -(int)E_LEN;
+    return 0;
 }
 
-__global__ __launch_bounds__(64) void dmx_inflate_kernel(const uint8_t* __restrict__ z, uint64_t zbytes,
-                                                         const dmx_iblock* __restrict__ index, uint32_t nblk,
-                                                         uint8_t* __restrict__ out, uint64_t out_cap,
-                                                         dmx_inflate_status* __restrict__ st) {
+__global__ __launch_bounds__(64) void dmx_inflate_index_kernel(const uint8_t* __restrict__ z, uint64_t zbytes,
+                                                               const dmx_iblock* __restrict__ index,
+                                                               uint8_t* __restrict__ out, uint64_t out_cap,
+                                                               dmx_inflate_status* __restrict__ st) {
     __shared__ InfLDS S;
     const uint32_t lane = threadIdx.x;
     IBits r;
-    r.z = z;
-    r.zbytes = zbytes;
-    r.bb = 0;
-    r.bc = 0;
-    r.over = false;
+    ib_init(r, z, zbytes);
+    const uint64_t bit = rfl64(index[blockIdx.x].bit);
+    const uint64_t off = rfl64(index[blockIdx.x].out_off);
+    const uint32_t olen = rfl(index[blockIdx.x].out_len);
     IOut o;
     o.out = out;
+    o.base = off;
+    o.ob = 0;
+    o.cap = olen;
     o.op = 0;
     o.fl = 0;
+    o.a = 1;
+    o.b = 0;
     int err = 0;
-    if (index) {   // one DEFLATE block per workgroup, no history
-        const dmx_iblock ix = index[blockIdx.x];
-        if (ix.out_len > IW || ix.out_off + ix.out_len > out_cap) err = -(int)E_RANGE;
-        r.pos = ix.bit >> 3;
-        o.base = ix.out_off;
-        o.cap = ix.out_len;
-        o.ring = false;
-        if (!err) {
-            ib_bits(r, (uint32_t)(ix.bit & 7));
-            bool last;
-            err = iblock(S, r, o, lane, &last);
-            if (!err && o.op != ix.out_len) err = -(int)E_SZ;
-            if (!err) io_flush(S, o, o.op, lane);
-        }
-        if (lane == 0 && err) atomicCAS(&st->status, 0, err);
-        if (lane == 0 && !err) atomicAdd((unsigned long long*)&st->out_len, (unsigned long long)o.op);
-        return;
+    if (olen > IW || off + olen > out_cap || (bit >> 3) >= zbytes) err = -(int)E_RANGE;
+    if (!err) {
+        ib_seek(r, bit);
+        bool last;
+        err = iblock<false>(S, r, o, lane, last);
+        if (!err && o.op != olen) err = -(int)E_SZ;
+        if (!err) io_flush<false>(S, o, o.op, lane);
     }
-    // whole zlib stream in this workgroup
+    if (lane == 0 && err) atomicCAS(&st->status, 0, err);
+    if (lane == 0 && !err) atomicAdd((unsigned long long*)&st->out_len, (unsigned long long)o.op);
+}
+
+__global__ __launch_bounds__(64) void dmx_inflate_stream_kernel(const uint8_t* __restrict__ z, uint64_t zbytes,
+                                                                uint8_t* __restrict__ out, uint64_t out_cap,
+                                                                dmx_inflate_status* __restrict__ st) {
+    __shared__ InfLDS S;
+    const uint32_t lane = threadIdx.x;
+    IBits r;
+    ib_init(r, z, zbytes);
+    IOut o;
+    o.out = out;
     o.base = 0;
+    o.ob = 0;
     o.cap = out_cap;
-    o.ring = true;
-    r.pos = 0;
+    o.op = 0;
+    o.fl = 0;
+    o.a = 1;
+    o.b = 0;
+    int err = 0;
     if (zbytes < 6) err = -(int)E_ZHEAD;
     if (!err) {
         const uint32_t cmf = z[0], flg = z[1];
@@ -343,43 +499,22 @@ __global__ __launch_bounds__(64) void dmx_inflate_kernel(const uint8_t* __restri
         else if (((cmf << 8) | flg) % 31) err = -(int)E_ZFCHCK;
         else if (flg & 0x20) err = -(int)E_ZPDICT;
     }
-    r.pos = 2;
-    bool last = false;
-    while (!err && !last) err = iblock(S, r, o, lane, &last);
-    if (!err) io_flush(S, o, o.op, lane);
-    if (!err) {   // Adler-32 trailer (RFC 1950, MSB first) over the output in HBM
-        ib_align(r);
+    if (!err) {
+        ib_seek(r, 16);
+        bool last = false;
+        while (!err && !last) err = iblock<true>(S, r, o, lane, last);
+    }
+    if (!err) {
+        io_flush<true>(S, o, o.op, lane);
+        ib_drop(r, r.bc & 7);   // Adler-32 trailer, MSB first
         uint32_t want = 0;
         for (int k = 0; k < 4; k++) want = (want << 8) | ib_bits(r, 8);
-        // per-lane sums over interleaved 4 KiB pieces, combined in order by lane 0
-        __shared__ unsigned long long ps[64], pt[64];
-        const uint64_t n = o.op;
-        const uint64_t piece = 4096;
-        uint32_t a = 1, bsum = 0;
-        for (uint64_t p0 = 0; p0 < n; p0 += 64 * piece) {
-            const uint64_t lo = p0 + lane * piece, hi = min(n, lo + piece);
-            uint64_t s = 0, t = 0;
-            for (uint64_t p = lo; p < hi; p++) { s += out[p]; t += (uint64_t)(hi - p) * out[p]; }
-            ps[lane] = s;
-            pt[lane] = t;
-            __syncthreads();
-            if (lane == 0) {
-                for (uint32_t l = 0; l < 64; l++) {
-                    const uint64_t plo = p0 + l * piece, phi = min(n, plo + piece);
-                    if (plo >= n) break;
-                    const uint64_t len = phi - plo;
-                    // a' = a + s, b' = b + len * a + t   (mod 65521)
-                    bsum = (uint32_t)((bsum + (len % 65521) * a + (pt[l] % 65521)) % 65521);
-                    a = (uint32_t)((a + ps[l] % 65521) % 65521);
-                }
-            }
-            __syncthreads();
-        }
-        if (lane == 0 && ((bsum << 16) | a) != want) err = -(int)E_ZADL32;
+        if (r.over) err = -(int)E_LEN;
+        else if (((o.b << 16) | o.a) != want) err = -(int)E_ZADL32;
     }
     if (lane == 0) {
         if (err) atomicCAS(&st->status, 0, err);
-        else st->out_len = o.op;
+        else st->out_len = o.ob + o.op;
     }
 }
 
@@ -390,11 +525,15 @@ __global__ __launch_bounds__(64) void dmx_inflate_kernel(const uint8_t* __restri
 extern "C" int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_iblock* d_index, uint32_t nblk,
                                  void* d_out, uint64_t out_cap, dmx_inflate_status* d_status, void* stream) {
     if (!d_z || !d_out || !d_status || (d_index && !nblk)) return -(int)E_INVAL;
+    if (zbytes > 0xFFFFFFF0ull) return -(int)E_RANGE;   // reader word indices are 32-bit
     hipStream_t s = (hipStream_t)stream;
     if (hipMemsetAsync(d_status, 0, sizeof(dmx_inflate_status), s) != hipSuccess) return -(int)E_DEVICE;
-    const uint32_t grid = d_index ? nblk : 1u;
-    hipLaunchKernelGGL(dmx_inflate_kernel, dim3(grid), dim3(64), 0, s, (const uint8_t*)d_z, zbytes, d_index, nblk,
-                       (uint8_t*)d_out, out_cap, d_status);
+    if (d_index)
+        hipLaunchKernelGGL(dmx_inflate_index_kernel, dim3(nblk), dim3(64), 0, s, (const uint8_t*)d_z, zbytes,
+                           d_index, (uint8_t*)d_out, out_cap, d_status);
+    else
+        hipLaunchKernelGGL(dmx_inflate_stream_kernel, dim3(1), dim3(64), 0, s, (const uint8_t*)d_z, zbytes,
+                           (uint8_t*)d_out, out_cap, d_status);
     if (hipGetLastError() != hipSuccess) return -(int)E_DEVICE;
     return 0;
 }
