@@ -95,6 +95,8 @@ def main() -> int:
                     help="0 = exhaustive (reference parse); K = K newest chain entries (default 8)")
     ap.add_argument("--lazy", type=int, default=int(os.environ.get("DMX_LAZY", "1")),
                     help="1 = lazy evaluation parse (DMX_F_LAZY, SURVEY §8 f2)")
+    ap.add_argument("--split", type=int, default=int(os.environ.get("DMX_SPLIT", "0")),
+                    help="1 = adaptive block splitting (DMX_F_SPLIT, SURVEY §8 f3)")
     ap.add_argument("--exhaustive-steps", type=int, default=3,
                     help="also time this many exhaustive-parse steps (reported under 'exhaustive')")
     ap.add_argument("--gather", default="root", choices=["root", "all", "none"])
@@ -135,6 +137,8 @@ def main() -> int:
     flags = D.DMX_ZLIB if world == 1 else S.shard_flags(rank, world)
     if args.lazy:
         flags |= D.DMX_F_LAZY
+    if args.split:
+        flags |= D.DMX_F_SPLIT
     enc = D.Encoder(local, n, 32768, args.max_chain, flags)
     d_in = torch.from_numpy(host).to(dev)
     cap = D.max_compressed(n)
@@ -157,6 +161,38 @@ def main() -> int:
         ok = zlib.decompress(z) == host.tobytes()
         if not ok:
             log("ERROR: stream does not inflate to the input")
+    # GPU inflate of the same stream: every block decoded in parallel from the
+    # encoder's block index, compared bit for bit with the input; timed with events
+    ix, nblk = enc.block_index()
+    dec = torch.empty(n, dtype=torch.uint8, device=dev)
+    ist = torch.zeros(16, dtype=torch.uint8, device=dev)
+    Lib = D.lib()
+
+    def inflate():
+        rc = Lib.dmx_inflate_async(d_out.data_ptr(), out_len, ix.data_ptr(), nblk, dec.data_ptr(), n,
+                                   ist.data_ptr(), stream)
+        if rc != 0:
+            raise RuntimeError(f"dmx_inflate_async: {rc}")
+
+    inflate()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(3):
+        inflate()
+    ev1.record()
+    torch.cuda.synchronize(dev)
+    inf_ms = ev0.elapsed_time(ev1) / 3
+    h = ist.cpu().numpy()
+    inf_status = int(np.frombuffer(h[:4].tobytes(), np.int32)[0])
+    inf_len = int(np.frombuffer(h[8:16].tobytes(), np.uint64)[0])
+    inf_ok = inf_status == 0 and inf_len == n and bool(torch.equal(dec, d_in))
+    if not inf_ok:
+        log(f"ERROR: GPU inflate status {inf_status}, {inf_len} of {n} bytes, or a byte mismatch")
+        ok = False
+    gpu_inflate = {"GBps_out": round(n / inf_ms / 1e6, 3), "ms": round(inf_ms, 4), "bit_exact": inf_ok,
+                   "mode": "indexed: one single-wave workgroup per block", "kernel": "dmx_inflate_index_kernel"}
+    del dec
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -243,7 +279,7 @@ def main() -> int:
                 "bytes_per_rank": n,
                 "block": 32768,
                 "parse": ("exhaustive (reference semantics)" if args.max_chain == 0 else f"max_chain={args.max_chain}")
-                         + (", lazy" if args.lazy else ", greedy"),
+                         + (", lazy" if args.lazy else ", greedy") + (", split" if args.split else ""),
                 "parallelism": f"blocks sharded over {world} GPU(s)" + (f", gather={args.gather}" if world > 1 else ""),
             },
             "ratio": round(out_len / n, 5),
@@ -252,6 +288,7 @@ def main() -> int:
             "exhaustive": exh,
             "compressed_bytes_rank0": out_len,
             "inflate_ok": ok,
+            "gpu_inflate": gpu_inflate,
             "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
             "roofline": {
                 "bound": "hbm",

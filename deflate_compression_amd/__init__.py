@@ -23,7 +23,7 @@ import struct
 __all__ = [
     "DeflateError", "Opts", "Result", "Encoder", "lib", "compress", "deflate_compress",
     "deflate_decompress", "max_compressed", "adler32_combine", "gen_text", "gen_random",
-    "COMPRESS_STATS", "E", "DMX_F_HEADER", "DMX_F_TRAILER", "DMX_F_FINAL", "DMX_ZLIB", "DMX_F_LAZY", "DMX_F_EXACT_SORT", "inflate_gpu",
+    "COMPRESS_STATS", "E", "DMX_F_HEADER", "DMX_F_TRAILER", "DMX_F_FINAL", "DMX_ZLIB", "DMX_F_LAZY", "DMX_F_EXACT_SORT", "DMX_F_SPLIT", "inflate_gpu",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -35,6 +35,7 @@ DMX_F_HEADER, DMX_F_TRAILER, DMX_F_FINAL = 1, 2, 4
 DMX_ZLIB = 7
 DMX_F_LAZY = 8
 DMX_F_EXACT_SORT = 16
+DMX_F_SPLIT = 32
 _M = 1 << 24
 # global_errors.h:64-75 and deflate_errors.h:134-147
 E = {
@@ -107,6 +108,7 @@ def lib() -> ctypes.CDLL:
         "dmx_last_blocks": ([vp, u32p, u8p, u32p, u32], ctypes.c_int),
         "dmx_last_tokens": ([vp, u32, u32p, u32], ctypes.c_int),
         "dmx_last_code_lengths": ([vp, u32, u8p], ctypes.c_int),
+        "dmx_last_subblock": ([vp, u32, u32, u32p, u32p, u32p, u8p], ctypes.c_int),
         "dmx_ctx_set_timing": ([vp, ctypes.c_int], ctypes.c_int),
         "dmx_ctx_stage_times": ([vp, ctypes.POINTER(ctypes.c_double), u32p], ctypes.c_int),
         "dmx_adler32_combine": ([u32, u32, u64], u32),
@@ -147,14 +149,16 @@ def max_compressed(n: int, sw: int = 32768) -> int:
     return int(lib().dmx_max_compressed(n, sw))
 
 
-def compress(data, sw: int = 32768, max_chain: int = 0, flags: int = DMX_ZLIB, lazy: bool = False) -> bytes:
-    """Encode a host buffer on the GPU; returns the zlib stream (or raw DEFLATE with flags)."""
+def compress(data, sw: int = 32768, max_chain: int = 0, flags: int = DMX_ZLIB, lazy: bool = False,
+             split: bool = False) -> bytes:
+    """Encode a host buffer on the GPU; returns the zlib stream (or raw DEFLATE with flags).
+    lazy = f2 lazy parse (DMX_F_LAZY), split = f3 adaptive block splitting (DMX_F_SPLIT)."""
     L = lib()
     p, n, keep = _buf(data)
     cap = max_compressed(n, sw)
     out = ctypes.create_string_buffer(cap)
     olen = ctypes.c_uint64(0)
-    o = Opts(sw, max_chain, flags | (DMX_F_LAZY if lazy else 0), 0)
+    o = Opts(sw, max_chain, flags | (DMX_F_LAZY if lazy else 0) | (DMX_F_SPLIT if split else 0), 0)
     _check(L.dmx_encode_host(p, n, out, cap, ctypes.byref(olen), ctypes.byref(o)), "dmx_encode_host")
     del keep
     return out.raw[:olen.value]
@@ -291,6 +295,26 @@ class Encoder:
         _check(self._L.dmx_last_code_lengths(self._ctx, blk, ln.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))),
                "dmx_last_code_lengths")
         return ln
+
+    def subblocks(self, blk: int):
+        """DEFLATE blocks of sw block `blk` in the last encode (f3 split: up to 4):
+        list of (t0, t1, btype, hdr_bits, code lengths[316])."""
+        import numpy as np
+        out = []
+        nsub, k = 1, 0
+        while k < nsub:
+            rg = np.zeros(2, np.uint32)
+            bt = np.zeros(1, np.uint32)
+            hb = np.zeros(1, np.uint32)
+            ln = np.zeros(316, np.uint8)
+            P = ctypes.POINTER(ctypes.c_uint32)
+            nsub = self._L.dmx_last_subblock(self._ctx, blk, k, rg.ctypes.data_as(P), bt.ctypes.data_as(P),
+                                             hb.ctypes.data_as(P), ln.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+            if nsub < 0:
+                raise DeflateError(nsub, "dmx_last_subblock")
+            out.append((int(rg[0]), int(rg[1]), int(bt[0]), int(hb[0]), ln))
+            k += 1
+        return out
 
     def stamps(self, nblk: int):
         """[nblk, 16] match-kernel phase cycles (needs DMX_STAMPS=1): P0, search, walk+compaction,

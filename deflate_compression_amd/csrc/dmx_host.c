@@ -99,56 +99,58 @@ static void h_dist_sym(int dist, int* sym, int* eb) {
 }
 
 /* One compress_stats record per token (deflate_compress.c:290-309) with exact costs:
- * tree_bits = header bits of the token's block, ll_bits/d_bits = running lit/len and
- * distance bits inside the block. */
+ * tree_bits = header bits of the token's DEFLATE block, ll_bits/d_bits = running lit/len
+ * and distance bits inside that block.  With DMX_F_SPLIT an sw block holds up to four
+ * DEFLATE blocks, each with its own codes; the running sums restart at each. */
 static int write_stats(dmx_ctx* c, int fd, uint64_t n, int sw) {
     const uint32_t nblk = (uint32_t)((n + (uint64_t)sw - 1) / (uint64_t)sw);
     if (!nblk) return 0;
-    uint32_t* ntok = (uint32_t*)malloc(sizeof(uint32_t) * nblk);
-    uint8_t* bt = (uint8_t*)malloc(nblk);
-    uint32_t* hb = (uint32_t*)malloc(sizeof(uint32_t) * nblk);
     uint32_t* tok = (uint32_t*)malloc(sizeof(uint32_t) * DMX_BLK);
     struct compress_stats* rec = (struct compress_stats*)malloc(sizeof(struct compress_stats) * DMX_BLK);
     int r = 0;
-    if (!ntok || !bt || !hb || !tok || !rec) r = -E_MALLOC;
-    if (!r && dmx_last_blocks(c, ntok, bt, hb, nblk) != (int)nblk) r = -E_DEVICE;
+    if (!tok || !rec) r = -E_MALLOC;
     for (uint32_t b = 0; !r && b < nblk; b++) {
-        uint8_t lens[316];
         int nt = dmx_last_tokens(c, b, tok, DMX_BLK);
         if (nt < 0) { r = nt; break; }
-        if (dmx_last_code_lengths(c, b, lens)) { r = -E_DEVICE; break; }
-        int ll_bits = 0, d_bits = 0;
         uint64_t pos = (uint64_t)b * (uint64_t)sw;
-        for (int k = 0; k < nt; k++) {
-            uint32_t t = tok[k];
-            struct compress_stats* cs = rec + k;
-            cs->bytes = (int)(pos + 1);
-            cs->tree_bits = bt[b] == 2 ? (int)hb[b] : 3;
-            if ((t >> 9) == 0) {
-                cs->ll = (int)(t & 0xFF);
-                cs->d = 0;
-                ll_bits += bt[b] == 0 ? 8 : lens[t & 0xFF];
-                pos += 1;
-            } else {
-                int len = (int)(t & 0x1FF), dist = (int)(t >> 9), s, eb;
-                cs->ll = len;
-                cs->d = dist;
-                if (bt[b] == 0) {          /* stored block: the bytes themselves */
-                    ll_bits += 8 * len;
+        int nsub = 1;
+        for (int sb = 0; !r && sb < nsub; sb++) {
+            uint8_t lens[316];
+            uint32_t range[2], bt = 0, hb = 0;
+            nsub = dmx_last_subblock(c, b, (uint32_t)sb, range, &bt, &hb, lens);
+            if (nsub < 0) { r = nsub; break; }
+            int ll_bits = 0, d_bits = 0;
+            for (uint32_t k = range[0]; k < range[1]; k++) {
+                uint32_t t = tok[k];
+                struct compress_stats* cs = rec + k;
+                cs->bytes = (int)(pos + 1);
+                cs->tree_bits = bt == 2 ? (int)hb : 3;
+                if ((t >> 9) == 0) {
+                    cs->ll = (int)(t & 0xFF);
+                    cs->d = 0;
+                    ll_bits += bt == 0 ? 8 : lens[t & 0xFF];
+                    pos += 1;
                 } else {
-                    h_len_sym(len, &s, &eb);
-                    ll_bits += lens[s] + eb;
-                    h_dist_sym(dist, &s, &eb);
-                    d_bits += lens[DMX_DIST0 + s] + eb;
+                    int len = (int)(t & 0x1FF), dist = (int)(t >> 9), sy, eb;
+                    cs->ll = len;
+                    cs->d = dist;
+                    if (bt == 0) {          /* stored block: the bytes themselves */
+                        ll_bits += 8 * len;
+                    } else {
+                        h_len_sym(len, &sy, &eb);
+                        ll_bits += lens[sy] + eb;
+                        h_dist_sym(dist, &sy, &eb);
+                        d_bits += lens[DMX_DIST0 + sy] + eb;
+                    }
+                    pos += (uint64_t)len;
                 }
-                pos += (uint64_t)len;
+                cs->ll_bits = ll_bits;
+                cs->d_bits = d_bits;
             }
-            cs->ll_bits = ll_bits;
-            cs->d_bits = d_bits;
         }
-        r = write_all(fd, rec, sizeof(struct compress_stats) * (uint64_t)nt);
+        if (!r) r = write_all(fd, rec, sizeof(struct compress_stats) * (uint64_t)nt);
     }
-    free(ntok); free(bt); free(hb); free(tok); free(rec);
+    free(tok); free(rec);
     return r;
 }
 
@@ -163,6 +165,8 @@ int deflate_compress(int fd_in, int fd_out, int fd_stats, swi sw, int ops) {
     o.flags = DMX_ZLIB;
     const char* lz = getenv("DMX_LAZY");   /* 1 = lazy evaluation (DMX_F_LAZY); default greedy */
     if (lz && atoi(lz) > 0) o.flags |= DMX_F_LAZY;
+    const char* sp = getenv("DMX_SPLIT");  /* 1 = adaptive block splitting (DMX_F_SPLIT) */
+    if (sp && atoi(sp) > 0) o.flags |= DMX_F_SPLIT;
     o.reserved = 0;
     uint8_t* in = NULL;
     uint64_t n = 0;

@@ -1,8 +1,9 @@
 // dmx_inflate_dev.hip -- RFC 1950/1951 inflate on the MI355X.
 //
 // Two kernels over one decoder:
-//   * indexed (dmx_inflate_index_kernel): one single-wave workgroup per DEFLATE block listed
-//     in a block index {start bit, output offset, output length}.  Blocks of a dmx stream
+//   * indexed (dmx_inflate_index_kernel): one single-wave workgroup per sw block listed in a
+//     block index {start bit, output offset, output length}; it decodes DEFLATE blocks until
+//     the sw block's output is complete (one, or up to four with DMX_F_SPLIT).  Blocks of a dmx stream
 //     never reference earlier blocks (every sw-sized block is its own window),
 //     so all blocks decode in parallel; the encoder exports the index (dmx_block_index).
 //   * stream (dmx_inflate_stream_kernel): one workgroup decodes a whole zlib stream
@@ -465,8 +466,10 @@ __global__ __launch_bounds__(64) void dmx_inflate_index_kernel(const uint8_t* __
     if (olen > IW || off + olen > out_cap || (bit >> 3) >= zbytes) err = -(int)E_RANGE;
     if (!err) {
         ib_seek(r, bit);
-        bool last;
-        err = iblock<false>(S, r, o, lane, last);
+        bool last = false;
+        do {   // one sw block may be several DEFLATE blocks (DMX_F_SPLIT)
+            err = iblock<false>(S, r, o, lane, last);
+        } while (!err && o.op < olen && !last);
         if (!err && o.op != olen) err = -(int)E_SZ;
         if (!err) io_flush<false>(S, o, o.op, lane);
     }

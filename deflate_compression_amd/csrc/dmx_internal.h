@@ -25,6 +25,17 @@ typedef struct {
     uint64_t body_bits; /* bits of the coded tokens + EOB (fixed/dynamic) */
     uint64_t off_bits;  /* scan kernel: absolute bit offset of the block in the output */
     uint64_t len_bits;  /* scan kernel: bits the block occupies (stored: incl. padding) */
+    uint32_t nsub;      /* huff kernel: DEFLATE blocks emitted for this block (1..4, f3 split) */
+    uint32_t pad_;
 } dmx_blkinfo;
+
+/* One emitted DEFLATE block inside an sw block (DMX_NSUB per block; f3 split). */
+#define DMX_NSUB 4
+typedef struct {
+    uint32_t t0, t1;    /* token range [t0, t1) */
+    uint32_t btype;     /* 1 fixed, 2 dynamic (a stored block is never split) */
+    uint32_t hdr_bits;  /* header bits incl. the 3-bit BFINAL/BTYPE */
+    uint64_t body_bits; /* coded tokens + extra bits + EOB */
+} dmx_subinfo;
 
 #endif

@@ -1040,12 +1040,21 @@ struct K2LDS {
     int32_t cnt[16];      // canonical codes: codes handed out per length so far
     uint32_t next[16];    // canonical codes: first code of each length
     uint32_t code[320];   // canonical codes (bit-reversed) | len << 16
+    uint32_t ccode[20];   // code-length codes, same packing
     // run-length coding of the code lengths (RFC 1951 §3.2.7)
     uint8_t rle_sym[320];
     uint8_t rle_ext[320];
     uint32_t hdr[DMX_HDR_WORDS];
     int32_t rle_n, hlit, hdist, hclen;
 };
+
+// K2 helpers run on one wave (one wave per alphabet / per split group), so they
+// synchronise the wave, never the workgroup: LDS writes of this wave done, then a
+// compiler barrier.
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
 
 __constant__ uint8_t c_clorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 __constant__ uint8_t c_cl_eb[19] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 3, 7};
@@ -1071,7 +1080,7 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
         if (s < n) len[s] = 0;
         m += (uint32_t)__popcll(__ballot(fv != 0));
     }
-    __syncthreads();
+    wsync();
     if (m == 0) return;
     if (m == 1) {   // one used symbol: one more code of length 1 (RFC 1951 allows it)
 #pragma unroll
@@ -1081,7 +1090,7 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
                 len[s0] = 1;
                 len[s0 == 0 ? 1 : 0] = 1;
             }
-        __syncthreads();
+        wsync();
         return;
     }
     // rank among the used symbols: compare with every key, broadcast by readlane
@@ -1103,7 +1112,7 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
             S.sym[rk[r]] = (uint16_t)(key[r] & 511u);
         }
     for (int k = (int)lane; k < 64; k += 64) S.blc[k] = 0;
-    __syncthreads();
+    wsync();
     const int mm = (int)m, nn = mm - 1, root = nn - 1;
     if (lane == 0) {   // two-queue merge
         int li = 0, ni = 0;
@@ -1120,7 +1129,7 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
         }
         S.up[root] = (uint16_t)root;
     }
-    __syncthreads();
+    wsync();
     // node depths by pointer jumping: dd = distance to up, up = an ancestor, doubling
     uint32_t u[5], d[5];
 #pragma unroll
@@ -1130,7 +1139,7 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
         d[r] = (j < nn && j != root) ? 1u : 0u;
         if (j < nn) S.dd[j] = (uint16_t)d[r];
     }
-    __syncthreads();
+    wsync();
     for (int round = 0; round < 9; round++) {   // 2^9 > 320 nodes
         uint32_t du[5], uu[5];
 #pragma unroll
@@ -1139,7 +1148,7 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
             du[r] = j < nn ? S.dd[u[r]] : 0u;
             uu[r] = j < nn ? S.up[u[r]] : 0u;
         }
-        __syncthreads();
+        wsync();
 #pragma unroll
         for (int r = 0; r < 5; r++) {
             const int j = r * 64 + (int)lane;
@@ -1147,7 +1156,7 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
             u[r] = uu[r];
             if (j < nn) { S.dd[j] = (uint16_t)d[r]; S.up[j] = (uint16_t)u[r]; }
         }
-        __syncthreads();
+        wsync();
     }
     // leaf depths -> leaves per length
     uint32_t maxd = 0;
@@ -1162,7 +1171,7 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) maxd = max(maxd, (uint32_t)__shfl_xor((int)maxd, o));
-    __syncthreads();
+    wsync();
     if (lane == 0) {
         if ((int)maxd > maxbits) {   // overflow redistribution (miniz style)
             for (int e = maxbits + 1; e <= (int)maxd; e++) { S.blc[maxbits] += S.blc[e]; S.blc[e] = 0; }
@@ -1179,7 +1188,7 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
         int k = 0;   // sorted index where length e starts: longest lengths first
         for (int e = maxbits; e >= 1; e--) { S.lstart[e] = k; k += S.blc[e]; }
     }
-    __syncthreads();
+    wsync();
 #pragma unroll
     for (int r = 0; r < 5; r++) {
         const int i = r * 64 + (int)lane;
@@ -1189,7 +1198,7 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
             len[S.sym[i]] = (uint8_t)e;
         }
     }
-    __syncthreads();
+    wsync();
 }
 
 // Canonical codes (RFC 1951 §3.2.2), bit-reversed, packed code | len << 16.  Lane-parallel:
@@ -1197,19 +1206,19 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
 template <int NR>
 __device__ void canon_codes(K2LDS& S, const uint8_t* len, int n, uint32_t* out, uint32_t lane) {
     if (lane < 16) S.cnt[lane] = 0;
-    __syncthreads();
+    wsync();
 #pragma unroll
     for (int r = 0; r < NR; r++) {
         const int s = r * 64 + (int)lane;
         if (s < n && len[s]) atomicAdd(&S.cnt[len[s]], 1);
     }
-    __syncthreads();
+    wsync();
     if (lane == 0) {
         uint32_t c = 0;
         for (int b2 = 1; b2 < 16; b2++) { c = (c + (b2 > 1 ? (uint32_t)S.cnt[b2 - 1] : 0u)) << 1; S.next[b2] = c; }
         for (int b2 = 0; b2 < 16; b2++) S.cnt[b2] = 0;
     }
-    __syncthreads();
+    wsync();
     const uint64_t lt = (1ull << lane) - 1ull;
 #pragma unroll
     for (int r = 0; r < NR; r++) {
@@ -1230,7 +1239,7 @@ __device__ void canon_codes(K2LDS& S, const uint8_t* len, int n, uint32_t* out, 
         } else if (s < n) {
             out[s] = 0;
         }
-        __syncthreads();
+        wsync();
     }
 }
 
@@ -1298,27 +1307,24 @@ __device__ void rle_lengths(K2LDS& S, uint32_t lane) {
         }
     }
     if (lane < 20) S.fcl[lane] = 0;
-    __syncthreads();
+    wsync();
     if (lane == 0) S.rle_n = (int32_t)carry;
     for (uint32_t t = lane; t < carry; t += 64) atomicAdd(&S.fcl[S.rle_sym[t]], 1u);
-    __syncthreads();
+    wsync();
 }
 
-__global__ __launch_bounds__(64) void dmx_huff_kernel(const uint32_t* __restrict__ hist_g, dmx_blkinfo* __restrict__ info,
-                                                      uint32_t* __restrict__ codes_g, uint32_t* __restrict__ hdr_g,
-                                                      uint32_t nblk, uint32_t flags) {
-    __shared__ K2LDS S;
-    const uint32_t lane = threadIdx.x;
-    const uint32_t b = blockIdx.x;
-    const uint32_t* hg = hist_g + (uint64_t)b * DMX_HIST;
-    const uint32_t bn = info[b].n;
-    const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1) ? 1u : 0u;
+struct HuffRes {
+    uint32_t bt, hbits;
+    uint64_t body, cost;
+};
 
-    for (int s = (int)lane; s < 288; s += 64) S.fll[s] = s < 286 ? (s == 256 ? 1u : hg[s]) : 0u;   // + end of block
-    for (int s = (int)lane; s < 32; s += 64) S.fd[s] = s < 30 ? hg[DMX_DIST0 + s] : 0u;
+// Plan one DEFLATE block from the frequencies in S.fll / S.fd (EOB included): code
+// lengths, exact stored / fixed / dynamic costs, the type (the cheapest; stored only if
+// allow_stored), canonical codes in S.code and the header bits (BFINAL/BTYPE + trees)
+// in S.hdr.  One wave.
+__device__ HuffRes huff_block(K2LDS& S, uint32_t bn, uint32_t final_bit, bool allow_stored, uint32_t lane) {
     for (int k = (int)lane; k < DMX_HDR_WORDS; k += 64) S.hdr[k] = 0;
-    __syncthreads();
-
+    wsync();
     // lit/len and distance code lengths
     huff_lengths<5>(S, S.fll, 286, 15, S.lll, lane);
     huff_lengths<1>(S, S.fd, 30, 15, S.ld, lane);
@@ -1338,14 +1344,14 @@ __global__ __launch_bounds__(64) void dmx_huff_kernel(const uint32_t* __restrict
             S.hlit = hl;
             S.hdist = nzd ? max(1, 64 - (int)__builtin_clzll(nzd)) : 1;
         }
-        __syncthreads();
+        wsync();
     }
     rle_lengths(S, lane);
     huff_lengths<1>(S, S.fcl, 19, 7, S.lcl, lane);
     {
         const uint64_t nzc = __ballot(lane < 19 && S.lcl[c_clorder[lane < 19 ? lane : 0]] != 0);
         if (lane == 0) S.hclen = nzc ? max(4, 64 - (int)__builtin_clzll(nzc)) : 4;
-        __syncthreads();
+        wsync();
     }
 
     // exact costs
@@ -1375,24 +1381,25 @@ __global__ __launch_bounds__(64) void dmx_huff_kernel(const uint32_t* __restrict
     uint32_t bt = 2;
     uint64_t best = dyn_bits;
     if (fix_bits <= best) { best = fix_bits; bt = 1; }
-    if (sto_bits < best) bt = 0;
+    if (allow_stored && sto_bits < best) { best = sto_bits; bt = 0; }
 
     // code table for the packer (fixed codes for BTYPE 1)
     if (bt == 1) {
         for (int s = (int)lane; s < 288; s += 64) S.lll[s] = (uint8_t)fixed_len((uint32_t)s);
         for (int s = (int)lane; s < 30; s += 64) S.ld[s] = 5;
-        __syncthreads();
+        wsync();
     }
-    canon_codes<5>(S, S.lll, 286, S.code, lane);
+    // fixed codes: the canonical assignment counts all 288 lit/len lengths (RFC 1951
+    // 3.2.6: 280..287 are 8-bit codes, so the 9-bit codes of 144..255 start after them);
+    // slots 286/287 are overwritten by the distance codes next (never emitted)
+    canon_codes<5>(S, S.lll, bt == 1 ? 288 : 286, S.code, lane);
     canon_codes<1>(S, S.ld, 30, S.code + DMX_DIST0, lane);
-    uint32_t* cg = codes_g + (uint64_t)b * DMX_HIST;
-    for (int s = (int)lane; s < 316; s += 64) cg[s] = S.code[s];
-    __syncthreads();
+    wsync();
 
     // header bits: items (value, bits) placed by a prefix sum over their bit counts
     uint32_t nitems = 1;
     if (bt == 2) {
-        canon_codes<1>(S, S.lcl, 19, S.code, lane);   // code-length codes (lit/dist codes are out)
+        canon_codes<1>(S, S.lcl, 19, S.ccode, lane);   // code-length codes
         nitems = 4 + (uint32_t)S.hclen + (uint32_t)S.rle_n;
     }
     uint32_t carry = 0;
@@ -1406,7 +1413,7 @@ __global__ __launch_bounds__(64) void dmx_huff_kernel(const uint32_t* __restrict
             else if (it == 3) { val = (uint32_t)(S.hclen - 4); nb = 4; }
             else if (it < 4 + (uint32_t)S.hclen) { val = S.lcl[c_clorder[it - 4]]; nb = 3; }
             else {
-                const uint32_t t = it - 4 - (uint32_t)S.hclen, sy = S.rle_sym[t], cw = S.code[sy];
+                const uint32_t t = it - 4 - (uint32_t)S.hclen, sy = S.rle_sym[t], cw = S.ccode[sy];
                 const uint32_t cl = cw >> 16;
                 val = (cw & 0xFFFFu) | ((uint32_t)S.rle_ext[t] << cl);
                 nb = cl + c_cl_eb[sy];
@@ -1421,14 +1428,227 @@ __global__ __launch_bounds__(64) void dmx_huff_kernel(const uint32_t* __restrict
             if (sh + nb > 32) atomicOr(&S.hdr[w + 1], val >> (32 - sh));
         }
     }
-    __syncthreads();
-    const uint32_t hbits = carry;
-    uint32_t* hgout = hdr_g + (uint64_t)b * DMX_HDR_WORDS;
-    for (uint32_t k = lane; k < (hbits + 31) / 32; k += 64) hgout[k] = S.hdr[k];
+    wsync();
+    HuffRes h;
+    h.bt = bt;
+    h.hbits = carry;
+    h.body = (bt == 2 ? dyn_body : fix_body) + extra;
+    h.cost = best;
+    return h;
+}
+
+__global__ __launch_bounds__(64) void dmx_huff_kernel(const uint32_t* __restrict__ hist_g, dmx_blkinfo* __restrict__ info,
+                                                      uint32_t* __restrict__ codes_g, uint32_t* __restrict__ hdr_g,
+                                                      dmx_subinfo* __restrict__ sub_g, uint32_t nblk, uint32_t flags) {
+    __shared__ K2LDS S;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    const uint32_t* hg = hist_g + (uint64_t)b * DMX_HIST;
+    const uint32_t bn = info[b].n;
+    const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1) ? 1u : 0u;
+
+    for (int s = (int)lane; s < 288; s += 64) S.fll[s] = s < 286 ? (s == 256 ? 1u : hg[s]) : 0u;   // + end of block
+    for (int s = (int)lane; s < 32; s += 64) S.fd[s] = s < 30 ? hg[DMX_DIST0 + s] : 0u;
+    wsync();
+    const HuffRes h = huff_block(S, bn, final_bit, true, lane);
+    uint32_t* cg = codes_g + (uint64_t)b * DMX_NSUB * DMX_HIST;
+    for (int s = (int)lane; s < 316; s += 64) cg[s] = S.code[s];
+    uint32_t* hgout = hdr_g + (uint64_t)b * DMX_NSUB * DMX_HDR_WORDS;
+    for (uint32_t k = lane; k < (h.hbits + 31) / 32; k += 64) hgout[k] = S.hdr[k];
     if (lane == 0) {
-        info[b].btype = bt;
-        info[b].hdr_bits = hbits;
-        info[b].body_bits = (bt == 2 ? dyn_body : fix_body) + extra;
+        info[b].btype = h.bt;
+        info[b].hdr_bits = h.hbits;
+        info[b].body_bits = h.body;
+        info[b].nsub = 1;
+        dmx_subinfo si;
+        si.t0 = 0;
+        si.t1 = info[b].ntok;
+        si.btype = h.bt;
+        si.hdr_bits = h.hbits;
+        si.body_bits = h.body;
+        sub_g[(uint64_t)b * DMX_NSUB] = si;
+    }
+}
+
+// K2s (DMX_F_SPLIT): adaptive block splitting.  Quarter k of a block holds
+// the tokens whose start lies in [(k*bn)>>2, ((k+1)*bn)>>2).  All 640 threads rebuild the
+// per-quarter histograms from the block's tokens (a prefix sum of token lengths gives the
+// starts); then wave g plans group g -- one of the 10 contiguous runs of quarters -- with
+// huff_block (fixed or dynamic; the whole block keeps the stored option); thread 0 picks
+// the cheapest of the 8 cut masks (ties: fewer blocks, then the smaller mask; no empty
+// group), and waves 0..nsub-1 write the chosen blocks' codes, headers and token ranges.
+// The rule is DESIGN.md §4.5.
+#define SPW 10
+__constant__ uint8_t c_gi[SPW] = {0, 1, 2, 3, 0, 1, 2, 0, 1, 0};
+__constant__ uint8_t c_gj[SPW] = {0, 1, 2, 3, 1, 2, 3, 2, 3, 3};
+
+struct SplitLDS {
+    uint32_t qh[4][DMX_HIST];
+    uint32_t qt[5];
+    uint32_t wsum[SPW];
+    uint32_t gbt[SPW], ghb[SPW], gempty[SPW];
+    uint64_t gbody[SPW], gcost[SPW];
+    uint32_t nsub, sg[DMX_NSUB];
+};
+
+__device__ __forceinline__ uint32_t grp_of(uint32_t i, uint32_t j) {   // inverse of c_gi / c_gj
+    const uint32_t len = j - i;   // 0: 0..3, 1: 4..6, 2: 7..8, 3: 9
+    return (len == 0 ? 0u : len == 1 ? 4u : len == 2 ? 7u : 9u) + i;
+}
+
+__global__ __launch_bounds__(64 * SPW) void dmx_huff_split_kernel(const uint32_t* __restrict__ tok_g,
+                                                                  dmx_blkinfo* __restrict__ info,
+                                                                  uint32_t* __restrict__ codes_g,
+                                                                  uint32_t* __restrict__ hdr_g,
+                                                                  dmx_subinfo* __restrict__ sub_g,
+                                                                  uint32_t nblk, uint32_t flags) {
+    __shared__ K2LDS K[SPW];
+    __shared__ SplitLDS Q;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t b = blockIdx.x;
+    const uint32_t ntok = info[b].ntok, bn = info[b].n;
+    const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1) ? 1u : 0u;
+    for (uint32_t k = tid; k < 4 * DMX_HIST; k += 64 * SPW) (&Q.qh[0][0])[k] = 0;
+    if (tid < 5) Q.qt[tid] = tid == 4 ? ntok : 0u;
+    __syncthreads();
+
+    // per-quarter histograms and quarter token boundaries
+    const uint32_t B1 = bn >> 2, B2 = (2 * bn) >> 2, B3 = (3 * bn) >> 2;
+    const uint32_t* tb = tok_g + (uint64_t)b * DMX_BLK;
+    uint32_t carry = 0, c1 = 0, c2 = 0, c3 = 0;
+    for (uint32_t base = 0; base < ntok; base += 64 * SPW) {
+        const uint32_t t = base + tid;
+        const uint32_t tk = t < ntok ? tb[t] : 0u;
+        const uint32_t adv = t < ntok ? ((tk >> 9) == 0 ? 1u : (tk & 0x1FFu)) : 0u;
+        const uint32_t incl = wave_incl_scan(adv);
+        if (lane == 63) Q.wsum[wave] = incl;
+        __syncthreads();
+        uint32_t wbase = 0, tot = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < SPW; w++) {
+            const uint32_t x = Q.wsum[w];
+            if (w < wave) wbase += x;
+            tot += x;
+        }
+        if (t < ntok) {
+            const uint32_t st = carry + wbase + incl - adv;
+            const uint32_t q = (st >= B1) + (st >= B2) + (st >= B3);
+            c1 += st < B1;
+            c2 += st < B2;
+            c3 += st < B3;
+            if ((tk >> 9) == 0) {
+                atomicAdd(&Q.qh[q][tk], 1u);
+            } else {
+                uint32_t sy, eb, ev;
+                len_sym(tk & 0x1FFu, sy, eb, ev);
+                atomicAdd(&Q.qh[q][sy], 1u);
+                dist_sym(tk >> 9, sy, eb, ev);
+                atomicAdd(&Q.qh[q][DMX_DIST0 + sy], 1u);
+            }
+        }
+        carry += tot;
+        __syncthreads();
+    }
+    c1 = wave_sum_u32(c1);
+    c2 = wave_sum_u32(c2);
+    c3 = wave_sum_u32(c3);
+    if (lane == 0) {
+        atomicAdd(&Q.qt[1], c1);
+        atomicAdd(&Q.qt[2], c2);
+        atomicAdd(&Q.qt[3], c3);
+    }
+    __syncthreads();
+
+    // one group per wave
+    {
+        K2LDS& S = K[wave];
+        const uint32_t i = c_gi[wave], j = c_gj[wave];
+        for (int s = (int)lane; s < 288; s += 64) {
+            uint32_t f = 0;
+            if (s == 256) f = 1;   // end of block
+            else if (s < 286)
+                for (uint32_t q = i; q <= j; q++) f += Q.qh[q][s];
+            S.fll[s] = f;
+        }
+        for (int s = (int)lane; s < 32; s += 64) {
+            uint32_t f = 0;
+            if (s < 30)
+                for (uint32_t q = i; q <= j; q++) f += Q.qh[q][DMX_DIST0 + s];
+            S.fd[s] = f;
+        }
+        wsync();
+        const HuffRes h = huff_block(S, bn, j == 3 ? final_bit : 0u, wave == SPW - 1, lane);
+        if (lane == 0) {
+            Q.gbt[wave] = h.bt;
+            Q.ghb[wave] = h.hbits;
+            Q.gbody[wave] = h.body;
+            Q.gcost[wave] = h.cost;
+            Q.gempty[wave] = Q.qt[j + 1] == Q.qt[i];
+        }
+    }
+    __syncthreads();
+
+    if (tid == 0) {   // cheapest cut mask: bit k = a cut after quarter k
+        int best = -1;
+        uint64_t bestc = 0;
+        for (uint32_t c = 0; c < 8; c++) {
+            uint64_t tot = 0;
+            bool ok = true;
+            uint32_t start = 0;
+            for (uint32_t k = 0; k < 4; k++)
+                if (k == 3 || ((c >> k) & 1u)) {
+                    const uint32_t g = grp_of(start, k);
+                    if (Q.gempty[g]) ok = false;
+                    tot += Q.gcost[g];
+                    start = k + 1;
+                }
+            if (!ok) continue;
+            if (best < 0 || tot < bestc || (tot == bestc && __popc(c) < __popc((uint32_t)best))) {
+                best = (int)c;
+                bestc = tot;
+            }
+        }
+        uint32_t ns = 0, start = 0;
+        for (uint32_t k = 0; k < 4; k++)
+            if (k == 3 || (((uint32_t)best >> k) & 1u)) {
+                Q.sg[ns++] = grp_of(start, k);
+                start = k + 1;
+            }
+        Q.nsub = ns;
+    }
+    __syncthreads();
+
+    const uint32_t nsub = Q.nsub;
+    if (wave < nsub) {
+        const uint32_t s = wave, g = Q.sg[s];
+        const uint64_t slot = (uint64_t)b * DMX_NSUB + s;
+        uint32_t* cg = codes_g + slot * DMX_HIST;
+        for (int k = (int)lane; k < 316; k += 64) cg[k] = K[g].code[k];
+        uint32_t* hg = hdr_g + slot * DMX_HDR_WORDS;
+        for (uint32_t k = lane; k < (Q.ghb[g] + 31) / 32; k += 64) hg[k] = K[g].hdr[k];
+        if (lane == 0) {
+            dmx_subinfo si;
+            si.t0 = Q.qt[c_gi[g]];
+            si.t1 = Q.qt[c_gj[g] + 1];
+            si.btype = Q.gbt[g];
+            si.hdr_bits = Q.ghb[g];
+            si.body_bits = Q.gbody[g];
+            sub_g[slot] = si;
+        }
+    }
+    if (tid == 0) {
+        uint32_t hb = 0, bt = 1;
+        uint64_t body = 0;
+        for (uint32_t s = 0; s < nsub; s++) {
+            const uint32_t g = Q.sg[s];
+            hb += Q.ghb[g];
+            body += Q.gbody[g];
+            if (Q.gbt[g] == 2) bt = 2;
+        }
+        info[b].btype = nsub == 1 ? Q.gbt[Q.sg[0]] : bt;
+        info[b].hdr_bits = hb;
+        info[b].body_bits = body;
+        info[b].nsub = nsub;
     }
 }
 
@@ -1605,6 +1825,7 @@ __device__ __forceinline__ void st_or64(uint32_t* st, uint32_t pos, uint64_t v, 
 __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict__ in, uint32_t sw,
                                                       const uint32_t* __restrict__ tok_g, const uint32_t* __restrict__ codes_g,
                                                       const uint32_t* __restrict__ hdr_g, const dmx_blkinfo* __restrict__ info,
+                                                      const dmx_subinfo* __restrict__ sub_g,
                                                       uint32_t nblk, uint32_t flags, uint32_t* __restrict__ out32,
                                                       dmx_result* __restrict__ res) {
     __shared__ uint32_t stage[DMX_STAGE_WORDS];
@@ -1619,7 +1840,7 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
     const uint32_t nwords = (uint32_t)((s0 + Lb + 31) >> 5);
     const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1) ? 1u : 0u;
     for (uint32_t k = tid; k < nwords; k += PT) stage[k] = 0;
-    for (uint32_t k = tid; k < 316; k += PT) code[k] = codes_g[(uint64_t)b * DMX_HIST + k];
+    for (uint32_t k = tid; k < 316; k += PT) code[k] = codes_g[(uint64_t)b * DMX_NSUB * DMX_HIST + k];
     __syncthreads();
     if (bi.btype == 0) {
         const uint8_t* d = in + (uint64_t)b * sw;
@@ -1632,81 +1853,91 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
         uint8_t* st8 = reinterpret_cast<uint8_t*>(stage) + ((P + 32) >> 3);
         for (uint32_t k = tid; k < bi.n; k += PT) st8[k] = d[k];
     } else {
-        const uint32_t* hg = hdr_g + (uint64_t)b * DMX_HDR_WORDS;
-        const uint32_t hb = bi.hdr_bits;
-        for (uint32_t k = tid; k < (hb + 31) / 32; k += PT) {
-            const uint32_t nb = (hb - 32 * k) < 32 ? (hb - 32 * k) : 32;
-            st_or64(stage, s0 + 32 * k, hg[k], nb);
-        }
-        // tokens: TPT consecutive tokens per thread; a per-thread bit accumulator flushes
-        // whole words -- plain stores inside the thread's own bit range, atomicOr only on
-        // the first and last word, which it shares with its neighbours
+        // one or more DEFLATE blocks (f3 split): header, tokens [t0, t1), end of block
         const uint32_t* tb = tok_g + (uint64_t)b * DMX_BLK;
-        uint32_t pos = s0 + hb;
-        for (uint32_t c = 0; c < bi.ntok; c += PT * TPT) {
-            const uint32_t j0 = c + tid * TPT;
-            uint32_t pv[2 * TPT], pb[2 * TPT];   // up to two pieces per token, <= 28 bits each
-            uint32_t mybits = 0;
-#pragma unroll
-            for (int t = 0; t < TPT; t++) {
-                pv[2 * t] = pb[2 * t] = pv[2 * t + 1] = pb[2 * t + 1] = 0;
-                if (j0 + t < bi.ntok) {
-                    const uint32_t tk = tb[j0 + t];
-                    if ((tk >> 9) == 0) {
-                        const uint32_t cw = code[tk];
-                        pv[2 * t] = cw & 0xFFFFu;
-                        pb[2 * t] = cw >> 16;
-                    } else {
-                        uint32_t sy, eb, ev;
-                        len_sym(tk & 0x1FFu, sy, eb, ev);
-                        uint32_t cw = code[sy];
-                        pv[2 * t] = (cw & 0xFFFFu) | (ev << (cw >> 16));
-                        pb[2 * t] = (cw >> 16) + eb;
-                        dist_sym(tk >> 9, sy, eb, ev);
-                        cw = code[DMX_DIST0 + sy];
-                        pv[2 * t + 1] = (cw & 0xFFFFu) | (ev << (cw >> 16));
-                        pb[2 * t + 1] = (cw >> 16) + eb;
-                    }
-                    mybits += pb[2 * t] + pb[2 * t + 1];
-                }
+        uint32_t pos = s0;
+        for (uint32_t sb = 0; sb < bi.nsub; sb++) {
+            const uint64_t slot = (uint64_t)b * DMX_NSUB + sb;
+            const dmx_subinfo si = sub_g[slot];
+            if (sb) {   // this block's codes (every thread is done with the previous ones)
+                __syncthreads();
+                for (uint32_t k = tid; k < 316; k += PT) code[k] = codes_g[slot * DMX_HIST + k];
+                __syncthreads();
             }
-            // exclusive scan of the threads' bit counts over the workgroup
-            const uint32_t incl = wave_incl_scan(mybits);
-            if (lane == 63) wsum[wave] = incl;
-            __syncthreads();
-            uint32_t wbase = 0, tot = 0;
-#pragma unroll
-            for (int w = 0; w < PT / 64; w++) {
-                const uint32_t t = wsum[w];
-                if ((uint32_t)w < wave) wbase += t;
-                tot += t;
+            const uint32_t* hg = hdr_g + slot * DMX_HDR_WORDS;
+            const uint32_t hb = si.hdr_bits;
+            for (uint32_t k = tid; k < (hb + 31) / 32; k += PT) {
+                const uint32_t nb = (hb - 32 * k) < 32 ? (hb - 32 * k) : 32;
+                st_or64(stage, pos + 32 * k, hg[k], nb);
             }
-            if (mybits) {
-                const uint32_t p0 = pos + wbase + incl - mybits;
-                uint32_t w = p0 >> 5, ab = p0 & 31;
-                uint64_t acc = 0;
-                bool first = true;
-#pragma unroll
-                for (int q = 0; q < 2 * TPT; q++) {
-                    acc |= (uint64_t)pv[q] << ab;
-                    ab += pb[q];
-                    if (ab >= 32) {
-                        if (first) atomicOr(&stage[w], (uint32_t)acc);
-                        else stage[w] = (uint32_t)acc;
-                        first = false;
-                        acc >>= 32;
-                        ab -= 32;
-                        w++;
+            pos += hb;
+            // tokens: TPT consecutive tokens per thread; a per-thread bit accumulator flushes
+            // whole words -- plain stores inside the thread's own bit range, atomicOr only on
+            // the first and last word, which it shares with its neighbours
+            for (uint32_t c = si.t0; c < si.t1; c += PT * TPT) {
+                const uint32_t j0 = c + tid * TPT;
+                uint32_t pv[2 * TPT], pb[2 * TPT];   // up to two pieces per token, <= 28 bits each
+                uint32_t mybits = 0;
+    #pragma unroll
+                for (int t = 0; t < TPT; t++) {
+                    pv[2 * t] = pb[2 * t] = pv[2 * t + 1] = pb[2 * t + 1] = 0;
+                    if (j0 + t < si.t1) {
+                        const uint32_t tk = tb[j0 + t];
+                        if ((tk >> 9) == 0) {
+                            const uint32_t cw = code[tk];
+                            pv[2 * t] = cw & 0xFFFFu;
+                            pb[2 * t] = cw >> 16;
+                        } else {
+                            uint32_t sy, eb, ev;
+                            len_sym(tk & 0x1FFu, sy, eb, ev);
+                            uint32_t cw = code[sy];
+                            pv[2 * t] = (cw & 0xFFFFu) | (ev << (cw >> 16));
+                            pb[2 * t] = (cw >> 16) + eb;
+                            dist_sym(tk >> 9, sy, eb, ev);
+                            cw = code[DMX_DIST0 + sy];
+                            pv[2 * t + 1] = (cw & 0xFFFFu) | (ev << (cw >> 16));
+                            pb[2 * t + 1] = (cw >> 16) + eb;
+                        }
+                        mybits += pb[2 * t] + pb[2 * t + 1];
                     }
                 }
-                if (ab) atomicOr(&stage[w], (uint32_t)acc);   // shared with the next thread
+                // exclusive scan of the threads' bit counts over the workgroup
+                const uint32_t incl = wave_incl_scan(mybits);
+                if (lane == 63) wsum[wave] = incl;
+                __syncthreads();
+                uint32_t wbase = 0, tot = 0;
+    #pragma unroll
+                for (int w = 0; w < PT / 64; w++) {
+                    const uint32_t t = wsum[w];
+                    if ((uint32_t)w < wave) wbase += t;
+                    tot += t;
+                }
+                if (mybits) {
+                    const uint32_t p0 = pos + wbase + incl - mybits;
+                    uint32_t w = p0 >> 5, ab = p0 & 31;
+                    uint64_t acc = 0;
+                    bool first = true;
+    #pragma unroll
+                    for (int q = 0; q < 2 * TPT; q++) {
+                        acc |= (uint64_t)pv[q] << ab;
+                        ab += pb[q];
+                        if (ab >= 32) {
+                            if (first) atomicOr(&stage[w], (uint32_t)acc);
+                            else stage[w] = (uint32_t)acc;
+                            first = false;
+                            acc >>= 32;
+                            ab -= 32;
+                            w++;
+                        }
+                    }
+                    if (ab) atomicOr(&stage[w], (uint32_t)acc);   // shared with the next thread
+                }
+                pos += tot;
+                __syncthreads();
             }
-            pos += tot;
-            __syncthreads();
-        }
-        if (tid == 0) {
             const uint32_t cw = code[256];
-            st_or64(stage, pos, cw & 0xFFFFu, cw >> 16);
+            if (tid == 0) st_or64(stage, pos, cw & 0xFFFFu, cw >> 16);
+            pos += cw >> 16;
         }
     }
     __syncthreads();
@@ -1734,7 +1965,8 @@ struct dmx_ctx {
     uint32_t* tok;    // cap_blocks * DMX_BLK
     uint32_t* hist;   // cap_blocks * DMX_HIST
     uint32_t* codes;  // cap_blocks * DMX_HIST
-    uint32_t* hdr;    // cap_blocks * DMX_HDR_WORDS
+    uint32_t* hdr;    // cap_blocks * DMX_NSUB * DMX_HDR_WORDS
+    dmx_subinfo* sub; // cap_blocks * DMX_NSUB
     dmx_blkinfo* info;
     dmx_result* res;
     uint64_t* dbg;        // optional per-block phase stamps (DMX_STAMPS=1)
@@ -1777,8 +2009,9 @@ static void ctx_free_ws(dmx_ctx* c) {
     if (c->hist) (void)hipFree(c->hist);
     if (c->codes) (void)hipFree(c->codes);
     if (c->hdr) (void)hipFree(c->hdr);
+    if (c->sub) (void)hipFree(c->sub);
     if (c->info) (void)hipFree(c->info);
-    c->dist = NULL; c->tok = NULL; c->hist = NULL; c->codes = NULL; c->hdr = NULL; c->info = NULL;
+    c->dist = NULL; c->tok = NULL; c->hist = NULL; c->codes = NULL; c->hdr = NULL; c->sub = NULL; c->info = NULL;
     c->cap_blocks = 0;
 }
 
@@ -1789,8 +2022,9 @@ static int ctx_reserve(dmx_ctx* c, uint64_t nblk) {
     HIPCHK(hipMalloc(&c->dist, cb * DMX_BLK * sizeof(uint16_t)));
     HIPCHK(hipMalloc(&c->tok, cb * DMX_BLK * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&c->hist, cb * DMX_HIST * sizeof(uint32_t)));
-    HIPCHK(hipMalloc(&c->codes, cb * DMX_HIST * sizeof(uint32_t)));
-    HIPCHK(hipMalloc(&c->hdr, cb * DMX_HDR_WORDS * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&c->codes, cb * DMX_NSUB * DMX_HIST * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&c->hdr, cb * DMX_NSUB * DMX_HDR_WORDS * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&c->sub, cb * DMX_NSUB * sizeof(dmx_subinfo)));
     HIPCHK(hipMalloc(&c->info, cb * sizeof(dmx_blkinfo)));
     c->cap_blocks = cb;
     return 0;
@@ -1897,7 +2131,12 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         hipLaunchKernelGGL(dmx_match_kernel, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw,
                            o.max_chain, ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u), c->dist, c->tok, c->hist, c->info, dbg);
         if (ev) (void)hipEventRecord(ev[2], s);
-        hipLaunchKernelGGL(dmx_huff_kernel, dim3(nblk), dim3(64), 0, s, c->hist, c->info, c->codes, c->hdr, nblk, o.flags);
+        if (o.flags & DMX_F_SPLIT)
+            hipLaunchKernelGGL(dmx_huff_split_kernel, dim3(nblk), dim3(64 * SPW), 0, s, c->tok, c->info, c->codes, c->hdr,
+                               c->sub, nblk, o.flags);
+        else
+            hipLaunchKernelGGL(dmx_huff_kernel, dim3(nblk), dim3(64), 0, s, c->hist, c->info, c->codes, c->hdr, c->sub,
+                               nblk, o.flags);
         if (ev) (void)hipEventRecord(ev[3], s);
     } else if (ev) {
         (void)hipEventRecord(ev[1], s);
@@ -1909,7 +2148,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
     if (ev) (void)hipEventRecord(ev[4], s);
     if (nblk)
         hipLaunchKernelGGL(dmx_pack_kernel, dim3(nblk), dim3(PT), 0, s, (const uint8_t*)d_in, (uint32_t)o.sw, c->tok,
-                           c->codes, c->hdr, c->info, nblk, o.flags, (uint32_t*)d_out, c->res);
+                           c->codes, c->hdr, c->info, c->sub, nblk, o.flags, (uint32_t*)d_out, c->res);
     if (ev) (void)hipEventRecord(ev[5], s);
     HIPCHK(hipGetLastError());
     c->last_nblk = nblk;
@@ -2000,9 +2239,31 @@ extern "C" int dmx_last_code_lengths(dmx_ctx* c, uint32_t blk, uint8_t* lens316)
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipDeviceSynchronize());
     uint32_t cw[316];
-    HIPCHK(hipMemcpy(cw, c->codes + (uint64_t)blk * DMX_HIST, sizeof(cw), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(cw, c->codes + (uint64_t)blk * DMX_NSUB * DMX_HIST, sizeof(cw), hipMemcpyDeviceToHost));
     for (int s = 0; s < 316; s++) lens316[s] = (uint8_t)(cw[s] >> 16);
     return 0;
+}
+
+extern "C" int dmx_last_subblock(dmx_ctx* c, uint32_t blk, uint32_t sub, uint32_t* tok_range, uint32_t* btype,
+                                 uint32_t* hdr_bits, uint8_t* lens316) {
+    if (blk >= c->last_nblk || sub >= DMX_NSUB) return -(int)E_RANGE;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipDeviceSynchronize());
+    dmx_blkinfo bi;
+    HIPCHK(hipMemcpy(&bi, c->info + blk, sizeof(bi), hipMemcpyDeviceToHost));
+    if (sub >= bi.nsub) return -(int)E_RANGE;
+    const uint64_t slot = (uint64_t)blk * DMX_NSUB + sub;
+    dmx_subinfo si;
+    HIPCHK(hipMemcpy(&si, c->sub + slot, sizeof(si), hipMemcpyDeviceToHost));
+    if (tok_range) { tok_range[0] = si.t0; tok_range[1] = si.t1; }
+    if (btype) *btype = si.btype;
+    if (hdr_bits) *hdr_bits = si.hdr_bits;
+    if (lens316) {
+        uint32_t cw[316];
+        HIPCHK(hipMemcpy(cw, c->codes + slot * DMX_HIST, sizeof(cw), hipMemcpyDeviceToHost));
+        for (int k = 0; k < 316; k++) lens316[k] = (uint8_t)(cw[k] >> 16);
+    }
+    return (int)bi.nsub;
 }
 
 // --- host-buffer convenience on a cached context per device ---

@@ -119,6 +119,9 @@ struct compress_stats {
 #define DMX_F_LAZY 8u    /* parse option: lazy evaluation, one position of
                             lookahead -- a match at i becomes a literal when the match at
                             i+1 is strictly longer.  Off = the reference's greedy parse. */
+#define DMX_F_SPLIT 32u  /* block option: an sw block may be emitted as up to
+                            four DEFLATE blocks cut at the token boundaries of its quarters,
+                            each with its own codes, when that is smaller */
 
 typedef struct {
     int32_t sw;        /* block size 1..32768 (0 = 32768) */
@@ -193,6 +196,11 @@ int dmx_last_blocks(dmx_ctx* ctx, uint32_t* ntok, uint8_t* btype, uint32_t* hdr_
                     uint32_t nblk_cap);
 int dmx_last_tokens(dmx_ctx* ctx, uint32_t blk, uint32_t* tok, uint32_t cap);
 int dmx_last_code_lengths(dmx_ctx* ctx, uint32_t blk, uint8_t* lens316);
+/* DEFLATE block `sub` of sw block `blk` (DMX_F_SPLIT emits up to 4 per sw block):
+ * token range [tok_range[0], tok_range[1]), BTYPE, header bits, and its 286 + 30 code
+ * lengths.  Returns the number of DEFLATE blocks of `blk`, or -E_RANGE. */
+int dmx_last_subblock(dmx_ctx* ctx, uint32_t blk, uint32_t sub, uint32_t* tok_range, uint32_t* btype,
+                      uint32_t* hdr_bits, uint8_t* lens316);
 
 /* Per-kernel HIP-event timing of subsequent encodes on the context's launches
  * (bench): enable, then read the mean milliseconds per launch of each stage

@@ -488,15 +488,87 @@ uint32_t dmx_oracle_adler32(const uint8_t* d, size_t n) {
     return (b << 16) | a;
 }
 
-/* ---- 7. whole stream ---------------------------------------------------------------- */
+/* ---- 7. adaptive block splitting ------------------
+ *
+ * A block of bn bytes may be emitted as up to four DEFLATE blocks.  The candidate cut
+ * points are the token boundaries at the quarters: quarter k holds the tokens whose start
+ * position lies in [(k*bn)>>2, ((k+1)*bn)>>2).  Every contiguous run of quarters (10
+ * groups) is planned on its own (fixed or dynamic, the usual rule, never stored); the
+ * whole block keeps the stored option.  Of the 8 cut masks the cheapest total wins, ties
+ * to fewer blocks, then to the smaller mask.  A group with no tokens is not allowed.
+ */
+static const int orc_grp[4][4] = {{0, 4, 7, 9}, {-1, 1, 5, 8}, {-1, -1, 2, 6}, {-1, -1, -1, 3}};
+
+typedef struct {
+    int nsub;
+    int t0[4], t1[4], g[4];
+    orc_plan P[10];
+} orc_split_plan;
+
+static void orc_plan_split(const uint32_t* tok, int ntok, int bn, orc_split_plan* SP) {
+    int qt[5] = {0, 0, 0, 0, ntok};   /* qt[q] = tokens that start before (q*bn)>>2 */
+    {
+        long long pos = 0;
+        for (int k = 0; k < ntok; k++) {
+            for (int q = 1; q < 4; q++)
+                if (pos < (((long long)q * bn) >> 2)) qt[q]++;
+            pos += (tok[k] >> 9) == 0 ? 1 : (long long)(tok[k] & 0x1FF);
+        }
+    }
+    uint64_t cost[10];
+    int empty[10];
+    for (int i = 0; i < 4; i++)
+        for (int j = i; j < 4; j++) {
+            const int g = orc_grp[i][j];
+            const int a = qt[i], b = qt[j + 1];
+            orc_plan_block(tok + a, b - a, bn, &SP->P[g]);
+            empty[g] = b == a;
+            if (g == 9) {
+                cost[g] = SP->P[g].btype == 0 ? SP->P[g].sto_bits
+                        : SP->P[g].btype == 1 ? SP->P[g].fix_bits : SP->P[g].dyn_bits;
+            } else {
+                SP->P[g].btype = SP->P[g].fix_bits <= SP->P[g].dyn_bits ? 1 : 2;
+                cost[g] = SP->P[g].btype == 1 ? SP->P[g].fix_bits : SP->P[g].dyn_bits;
+            }
+        }
+    int best = -1;
+    uint64_t bestc = 0;
+    for (int c = 0; c < 8; c++) {
+        uint64_t tot = 0;
+        int ok = 1, start = 0;
+        for (int k = 0; k < 4; k++)
+            if (k == 3 || ((c >> k) & 1)) {
+                const int g = orc_grp[start][k];
+                if (empty[g]) ok = 0;
+                tot += cost[g];
+                start = k + 1;
+            }
+        if (!ok) continue;
+        const int pc = __builtin_popcount((unsigned)c), pb = best < 0 ? 0 : __builtin_popcount((unsigned)best);
+        if (best < 0 || tot < bestc || (tot == bestc && pc < pb)) { best = c; bestc = tot; }
+    }
+    SP->nsub = 0;
+    int start = 0;
+    for (int k = 0; k < 4; k++)
+        if (k == 3 || ((best >> k) & 1)) {
+            const int s = SP->nsub++;
+            SP->g[s] = orc_grp[start][k];
+            SP->t0[s] = qt[start];
+            SP->t1[s] = qt[k + 1];
+            start = k + 1;
+        }
+}
+
+/* ---- 8. whole stream ---------------------------------------------------------------- */
 
 /*
  * Compress `in` (n bytes) into a zlib stream.  Returns the stream length, or
- * -1 if `cap` is too small.  sw = block size (1..32768), max_chain as above.
- * If btypes != NULL it receives the chosen BTYPE of every block.
+ * -1 if `cap` is too small.  sw = block size (1..32768), max_chain as above,
+ * lazy = f2 parse, split = f3 block splitting.  If btypes != NULL it receives the
+ * chosen BTYPE of every block (split blocks: the type of their first sub-block).
  */
-long long dmx_oracle_compress_ex(const uint8_t* in, size_t n, int sw, int max_chain, int hash_kind,
-                                 int lazy, uint8_t* out, size_t cap, uint8_t* btypes) {
+long long dmx_oracle_compress_ex2(const uint8_t* in, size_t n, int sw, int max_chain, int hash_kind,
+                                  int lazy, int split, uint8_t* out, size_t cap, uint8_t* btypes) {
     if (sw <= 0 || sw > 32768) return -2;
     if (cap < 8) return -1;
     memset(out, 0, cap);
@@ -511,16 +583,26 @@ long long dmx_oracle_compress_ex(const uint8_t* in, size_t n, int sw, int max_ch
     }
     uint32_t* tok = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)sw);
     orc_plan* P = (orc_plan*)malloc(sizeof(orc_plan));
+    orc_split_plan* SP = split ? (orc_split_plan*)malloc(sizeof(orc_split_plan)) : NULL;
     for (size_t b = 0; b < nblk; b++) {
         size_t off = b * (size_t)sw;
         int bn = (int)((n - off) < (size_t)sw ? (n - off) : (size_t)sw);
         int ntok = dmx_oracle_parse_block_ex(in + off, bn, max_chain, hash_kind, lazy, tok);
-        orc_plan_block(tok, ntok, bn, P);
-        if (btypes) btypes[b] = (uint8_t)P->btype;
-        orc_write_block(&w, in + off, bn, tok, ntok, P, b + 1 == nblk);
+        if (split) {
+            orc_plan_split(tok, ntok, bn, SP);
+            if (btypes) btypes[b] = (uint8_t)SP->P[SP->g[0]].btype;
+            for (int s = 0; s < SP->nsub; s++)
+                orc_write_block(&w, in + off, bn, tok + SP->t0[s], SP->t1[s] - SP->t0[s], &SP->P[SP->g[s]],
+                                b + 1 == nblk && s + 1 == SP->nsub);
+        } else {
+            orc_plan_block(tok, ntok, bn, P);
+            if (btypes) btypes[b] = (uint8_t)P->btype;
+            orc_write_block(&w, in + off, bn, tok, ntok, P, b + 1 == nblk);
+        }
     }
     free(tok);
     free(P);
+    free(SP);
     orc_align(&w);
     if (w.overflow) return -1;
     size_t nbytes = (size_t)(orc_bitpos(&w) >> 3);
@@ -532,6 +614,11 @@ long long dmx_oracle_compress_ex(const uint8_t* in, size_t n, int sw, int max_ch
     tail[2] = (uint8_t)(ad >> 8);
     tail[3] = (uint8_t)ad;
     return (long long)(2 + nbytes + 4);
+}
+
+long long dmx_oracle_compress_ex(const uint8_t* in, size_t n, int sw, int max_chain, int hash_kind,
+                                 int lazy, uint8_t* out, size_t cap, uint8_t* btypes) {
+    return dmx_oracle_compress_ex2(in, n, sw, max_chain, hash_kind, lazy, 0, out, cap, btypes);
 }
 
 long long dmx_oracle_compress(const uint8_t* in, size_t n, int sw, int max_chain, int hash_kind,

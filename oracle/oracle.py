@@ -50,6 +50,9 @@ def lib():
         L.dmx_oracle_compress_ex.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_int, ctypes.c_int, u8p, ctypes.c_size_t, u8p]
         L.dmx_oracle_compress_ex.restype = ctypes.c_longlong
+        L.dmx_oracle_compress_ex2.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_int, u8p, ctypes.c_size_t, u8p]
+        L.dmx_oracle_compress_ex2.restype = ctypes.c_longlong
         L.dmx_oracle_plan.argtypes = [u32p, ctypes.c_int, ctypes.c_int, u64p, u8p, u8p]
         L.dmx_oracle_plan.restype = ctypes.c_int
         _lib = L
@@ -94,13 +97,15 @@ def adler32(data) -> int:
 
 
 def compress(data, sw: int = 32768, max_chain: int = 0, hash_kind: int = HASH_MUL,
-             want_btypes: bool = False, lazy: bool = False):
+             want_btypes: bool = False, lazy: bool = False, split: bool = False):
+    """zlib stream of `data`; lazy = f2 parse, split = f3 adaptive block splitting."""
     a = _as_u8(data)
     nblk = (a.size + sw - 1) // sw
     cap = a.size + 5 * (nblk + 1) + 64
     out = np.zeros(cap, dtype=np.uint8)
     bt = np.zeros(max(nblk, 1), dtype=np.uint8)
-    r = lib().dmx_oracle_compress_ex(_u8(a), a.size, sw, max_chain, hash_kind, int(lazy), _u8(out), cap, _u8(bt))
+    r = lib().dmx_oracle_compress_ex2(_u8(a), a.size, sw, max_chain, hash_kind, int(lazy), int(split),
+                                      _u8(out), cap, _u8(bt))
     if r < 0:
         raise RuntimeError(f"oracle compress failed: {r}")
     z = out[:r].tobytes()

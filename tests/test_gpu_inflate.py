@@ -29,6 +29,7 @@ def _inputs(golden_cases):
         "mixed": golden_cases["runs32k"] + D.gen_random(5000, 2).tobytes() + golden_cases["period7"] + bytes(70000),
         "tiny": b"ab",
         "one": b"x",
+        "high": bytes([195, 250, 144, 143, 255]),   # fixed block, 9-bit literal codes
     }
 
 

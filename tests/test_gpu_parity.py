@@ -187,6 +187,19 @@ def test_shards_stitch(enc):
     assert adl == zlib.adler32(data)
 
 
+def test_fixed_blocks_high_literals(enc):
+    """Fixed-Huffman blocks with literals 144..255 (9-bit codes, RFC 1951 3.2.6): the
+    canonical assignment must count the 8-bit codes 280..287 too."""
+    cases = [bytes([195]), bytes([143, 144, 255, 0, 200]), bytes(range(256)), bytes(range(255, -1, -1)) * 2,
+             bytes([250]) * 5 + bytes([7, 251])]
+    for data in cases:
+        for sw in (1, 2, 7, 32768):
+            for f in (D.DMX_ZLIB, D.DMX_ZLIB | D.DMX_F_LAZY):
+                z, _ = enc.compress_bytes(data, sw=sw, max_chain=8, flags=f)
+                assert z == O.compress(data, sw=sw, max_chain=8, lazy=bool(f & D.DMX_F_LAZY)), (list(data[:4]), sw)
+                check_stream(z, data)
+
+
 def test_raw_deflate_flags(enc):
     data = D.gen_text(100000, 4).tobytes()
     z, _ = enc.compress_bytes(data, flags=D.DMX_F_FINAL)
