@@ -8,7 +8,7 @@ under torch.distributed.run): weak scaling, every rank encodes its own 100 MB sh
 (per-rank seed) framed as a shard of one stream, and the compressed chunks are
 gathered to rank 0 over RCCL (point-to-point over xGMI) inside the timed region.
 
-Prints ONE JSON line on rank 0 (see DESIGN.md §6 for the roofline accounting).
+Prints ONE JSON line on rank 0 (see DESIGN.md §5 for the roofline accounting).
 """
 from __future__ import annotations
 

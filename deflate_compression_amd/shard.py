@@ -1,4 +1,4 @@
-"""Multi-GPU sharding of one DEFLATE stream (DESIGN.md §5).
+"""Multi-GPU sharding of one DEFLATE stream (DESIGN.md §6).
 
 Blocks are independent, so rank r of N encodes a contiguous, block-aligned range
 of the input with no collective on the data path.  Shard framing makes the pieces

@@ -67,7 +67,7 @@ static unsigned orc_hash_morton(const uint8_t* p) {
     return (x | (y << 1) | (z << 2)) % 1024u;
 }
 
-/* 13-bit multiplicative hash of the 24-bit little-endian trigram. */
+/* 13-bit multiplicative hash of the 24-bit little-endian trigram (bounded mode). */
 static unsigned orc_hash_mul(const uint8_t* p) {
     uint32_t t = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
     return (uint32_t)(t * 0x9E3779B1u) >> 19;

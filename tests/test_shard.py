@@ -1,4 +1,4 @@
-"""Multi-rank shard framing + chunk gather (DESIGN.md §5), world_size 2 over gloo on CPU.
+"""Multi-rank shard framing + chunk gather (DESIGN.md §6), world_size 2 over gloo on CPU.
 
 The encoder itself needs a GPU, so on CPU each rank frames its shard with zlib's raw
 deflate in exactly the shape the HIP path emits (rank 0: zlib header; non-final:
