@@ -36,6 +36,7 @@ DMX_ZLIB = 7
 DMX_F_LAZY = 8
 DMX_F_EXACT_SORT = 16
 DMX_F_SPLIT = 32
+DMX_F_DICT = 64
 _M = 1 << 24
 # global_errors.h:64-75 and deflate_errors.h:134-147
 E = {
@@ -60,7 +61,7 @@ class DeflateError(RuntimeError):
 
 class Opts(ctypes.Structure):
     _fields_ = [("sw", ctypes.c_int32), ("max_chain", ctypes.c_int32), ("flags", ctypes.c_uint32),
-                ("reserved", ctypes.c_int32)]
+                ("reserved", ctypes.c_int32), ("dict", ctypes.c_void_p), ("dict_len", ctypes.c_uint64)]
 
 
 class Result(ctypes.Structure):
@@ -150,17 +151,23 @@ def max_compressed(n: int, sw: int = 32768) -> int:
 
 
 def compress(data, sw: int = 32768, max_chain: int = 0, flags: int = DMX_ZLIB, lazy: bool = False,
-             split: bool = False) -> bytes:
+             split: bool = False, dict: bool = False, pre=None) -> bytes:
     """Encode a host buffer on the GPU; returns the zlib stream (or raw DEFLATE with flags).
-    lazy = f2 lazy parse (DMX_F_LAZY), split = f3 adaptive block splitting (DMX_F_SPLIT)."""
+    lazy = f2 lazy parse (DMX_F_LAZY), split = f3 adaptive block splitting (DMX_F_SPLIT),
+    dict = f1 cross-block dictionary (DMX_F_DICT; pre = the bytes before `data`)."""
     L = lib()
     p, n, keep = _buf(data)
     cap = max_compressed(n, sw)
     out = ctypes.create_string_buffer(cap)
     olen = ctypes.c_uint64(0)
-    o = Opts(sw, max_chain, flags | (DMX_F_LAZY if lazy else 0) | (DMX_F_SPLIT if split else 0), 0)
+    o = Opts(sw, max_chain, flags | (DMX_F_LAZY if lazy else 0) | (DMX_F_SPLIT if split else 0) |
+             (DMX_F_DICT if dict else 0), 0)
+    pk = None
+    if dict and pre is not None and len(pre):
+        pk = ctypes.create_string_buffer(bytes(pre), len(pre))
+        o.dict, o.dict_len = ctypes.cast(pk, ctypes.c_void_p), len(pre)
     _check(L.dmx_encode_host(p, n, out, cap, ctypes.byref(olen), ctypes.byref(o)), "dmx_encode_host")
-    del keep
+    del keep, pk
     return out.raw[:olen.value]
 
 
@@ -348,7 +355,7 @@ class Encoder:
         ms = (ctypes.c_double * 6)()
         cnt = ctypes.c_uint32(0)
         self._L.dmx_ctx_stage_times(self._ctx, ms, ctypes.byref(cnt))
-        return dict(zip(["chain", "match", "huff", "scan", "pack", "total"], list(ms))), cnt.value
+        return {k: v for k, v in zip(["dict", "match", "huff", "scan", "pack", "total"], list(ms))}, cnt.value
 
     # -- host convenience on this context via torch tensors --
     def compress_tensor(self, t_in, stream=None, opts: Opts | None = None):
@@ -363,13 +370,18 @@ class Encoder:
         r = self.result(s)
         return out[:r.out_len], r
 
-    def compress_bytes(self, data, sw: int = 32768, max_chain: int = 0, flags: int = DMX_ZLIB):
-        """Host bytes -> HBM -> encode -> host bytes, on this context (keeps introspection)."""
+    def compress_bytes(self, data, sw: int = 32768, max_chain: int = 0, flags: int = DMX_ZLIB, pre=None):
+        """Host bytes -> HBM -> encode -> host bytes, on this context (keeps introspection).
+        pre: DMX_F_DICT history of block 0 (host bytes, staged in HBM here)."""
         import numpy as np
         import torch
+        dev = f"cuda:{self.device}"
         a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
-        t = torch.from_numpy(a.copy()).to(f"cuda:{self.device}") if a.size else \
-            torch.empty(0, dtype=torch.uint8, device=f"cuda:{self.device}")
+        t = torch.from_numpy(a.copy()).to(dev) if a.size else torch.empty(0, dtype=torch.uint8, device=dev)
         self.reserve(a.size, sw)
-        out, r = self.compress_tensor(t, opts=Opts(sw, max_chain, flags, 0))
+        o = Opts(sw, max_chain, flags, 0)
+        if pre is not None and len(pre):
+            tp = torch.from_numpy(np.frombuffer(bytes(pre), dtype=np.uint8).copy()).to(dev)
+            o.dict, o.dict_len = tp.data_ptr(), tp.numel()
+        out, r = self.compress_tensor(t, opts=o)
         return out.cpu().numpy().tobytes(), r

@@ -167,7 +167,11 @@ int deflate_compress(int fd_in, int fd_out, int fd_stats, swi sw, int ops) {
     if (lz && atoi(lz) > 0) o.flags |= DMX_F_LAZY;
     const char* sp = getenv("DMX_SPLIT");  /* 1 = adaptive block splitting (DMX_F_SPLIT) */
     if (sp && atoi(sp) > 0) o.flags |= DMX_F_SPLIT;
+    const char* dc = getenv("DMX_DICT");   /* 1 = cross-block dictionary (DMX_F_DICT) */
+    if (dc && atoi(dc) > 0) o.flags |= DMX_F_DICT;
     o.reserved = 0;
+    o.dict = NULL;
+    o.dict_len = 0;
     uint8_t* in = NULL;
     uint64_t n = 0;
     int r = read_all(fd_in, &in, &n);

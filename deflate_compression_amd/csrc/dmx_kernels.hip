@@ -91,7 +91,8 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #define MT 1024
 #define MW (MT / 64)
 #define DMX_STAMPS 16   // diagnostic u64 stamps per block (DMX_STAMPS=1 in the environment)
-#define DATA_WORDS 8208   // 32 KiB + slack for 32-byte extension reads past the end (zeroed)
+#define DATA_WORDS 8272   // 32 KiB + slack: 32-byte extension reads past the end (zeroed); the
+                          // history kernel keeps the first bytes of the block there (>= 258 + 40)
 
 struct __attribute__((aligned(16))) MatchLDS {
     uint32_t data[DATA_WORDS];    // the block, zero padded
@@ -754,6 +755,133 @@ __device__ __forceinline__ void sort_positions(MatchLDS& L, uint32_t bn, int32_t
     if (stamp && tid == 0) tp0[2] = __builtin_amdgcn_s_memtime();
 }
 
+// ------------------------------------------------------------------------------------
+// K0 (DMX_F_DICT): the cross-block dictionary.  For every position p of
+// block b, the longest match against the previous sw block (block 0: the caller's dict
+// bytes) -- the history of DESIGN.md §4.6:
+//   candidates = the K newest history positions q of p's bucket (all for K = 0) whose
+//                trigram lies inside the history (q + 2 < hn), with distance
+//                hn - q + p <= 32768; newest first, strict > (ties to the nearest);
+//   bytes are compared across the boundary (the source runs from the history into the
+//   block itself), up to min(258, bn - p).
+// One 1024-thread workgroup per block, MatchLDS reused: data = history + the first
+// DATA_WORDS*4 - hn bytes of the block (sources that cross the boundary), sorted = the
+// history's positions by (bucket, position) from the match kernel's own sort, bstart =
+// bucket ENDS (0 = empty), len8 = the block (targets).  Result per position:
+// len << 16 | dist (0 = none) into the block's token slots, which the match kernel reads
+// back after its search (P1h) and overwrites with tokens in P3.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(MT) void dmx_hist_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
+                                                      int32_t max_chain, const uint8_t* __restrict__ pre, uint32_t npre,
+                                                      uint32_t* __restrict__ hb_g) {
+    __shared__ MatchLDS L;
+    __shared__ uint64_t tp0[3];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    const uint64_t off = (uint64_t)b * sw;
+    const uint32_t bn = (uint32_t)((n - off) < sw ? (n - off) : sw);
+    const uint8_t* cur = in + off;
+    const uint8_t* hs = nullptr;
+    uint32_t hn = 0;
+    if (b > 0) { hs = cur - sw; hn = sw; }
+    else if (pre && npre) { hn = npre < sw ? npre : sw; hs = pre + (npre - hn); }
+    uint32_t* hb = hb_g + (uint64_t)b * DMX_BLK;
+    const uint32_t nvalid = bn > 2 ? bn - 2 : 0;
+    if (hn < 3) {   // no history entries
+        for (uint32_t p = tid; p < nvalid; p += MT) hb[p] = 0;
+        return;
+    }
+    // history bytes, then the block's first bytes, zero padded (16-byte chunks)
+    const bool ha = ((reinterpret_cast<uintptr_t>(hs) & 15) == 0);
+    for (uint32_t k = tid; k < DATA_WORDS / 4; k += MT) {
+        const uint32_t p = k << 4;
+        uint4 v;
+        if (ha && p + 16 <= hn) {
+            v = *reinterpret_cast<const uint4*>(hs + p);
+        } else {
+            uint32_t w[4] = {0, 0, 0, 0};
+            for (uint32_t j = 0; j < 16; j++) {
+                const uint32_t x = p + j;
+                const uint32_t c = x < hn ? hs[x] : (x - hn < bn ? cur[x - hn] : 0u);
+                w[j >> 2] |= c << (8 * (j & 3));
+            }
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        *reinterpret_cast<uint4*>(&L.data[k << 2]) = v;
+    }
+    const uint32_t nh = hn - 2;   // history entries
+    for (uint32_t attempt = 0;; attempt++) {
+        if (attempt == 0) sort_positions<false>(L, hn, 1, tid, false, tp0);
+        else sort_positions<true>(L, hn, 1, tid, false, tp0);
+        for (uint32_t k = tid; k < DMX_NBUCKET; k += MT) L.bstart[k] = 0;
+        __syncthreads();
+        bool bad = false;   // lane-ordered atomic ranks are checked here as in the search
+        for (uint32_t k = tid; k < nh; k += MT) {
+            const uint32_t q = L.sorted[k];
+            const uint32_t h = dmx_hash(ld4(L.data, q) & 0xFFFFFFu);
+            if (k + 1 < nh) {
+                const uint32_t q1 = L.sorted[k + 1];
+                const uint32_t h1 = dmx_hash(ld4(L.data, q1) & 0xFFFFFFu);
+                if (h1 != h) L.bstart[h] = (uint16_t)(k + 1);
+                else if (q1 < q) bad = true;
+            } else {
+                L.bstart[h] = (uint16_t)(k + 1);
+            }
+        }
+        if (!__syncthreads_or(bad) || attempt) break;
+    }
+    // the block itself (targets) into len8, zero padded
+    uint32_t* TW = reinterpret_cast<uint32_t*>(L.len8);
+    const bool ca = ((reinterpret_cast<uintptr_t>(cur) & 15) == 0);
+    for (uint32_t k = tid; k < DMX_BLK / 16; k += MT) {
+        const uint32_t p = k << 4;
+        uint4 v;
+        if (ca && p + 16 <= bn) {
+            v = *reinterpret_cast<const uint4*>(cur + p);
+        } else {
+            uint32_t w[4] = {0, 0, 0, 0};
+            for (uint32_t j = 0; j < 16; j++)
+                if (p + j < bn) w[j >> 2] |= (uint32_t)cur[p + j] << (8 * (j & 3));
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        *reinterpret_cast<uint4*>(&TW[k << 2]) = v;
+    }
+    __syncthreads();
+    const uint32_t K = max_chain > 0 ? (uint32_t)max_chain : 0xFFFFFFFFu;
+    for (uint32_t p = tid; p < nvalid; p += MT) {
+        const uint64_t tv = ld8(TW, p);
+        const uint32_t tri = (uint32_t)tv & 0xFFFFFFu;
+        const uint32_t h = dmx_hash(tri);
+        const uint32_t lim = min(bn - p, (uint32_t)MAXLEN);
+        const int32_t minq = (int32_t)(hn + p) - 32768;   // distance <= 32768
+        uint32_t best = 2, bq = 0, cnt = 0;
+        for (int32_t x = (int32_t)L.bstart[h] - 1; x >= 0 && cnt < K; x--, cnt++) {
+            const uint32_t q = L.sorted[x];
+            if ((int32_t)q < minq) break;   // older entries of the bucket are farther still
+            const uint64_t sv = ld8(L.data, q);
+            if (((uint32_t)sv ^ tri) & 0xFFFFFFu) {   // another trigram
+                if (K == 0xFFFFFFFFu && dmx_hash((uint32_t)sv & 0xFFFFFFu) != h) break;   // left the bucket
+                continue;
+            }
+            uint32_t t = match_bytes(sv ^ tv);
+            if (t == 8) {
+                while (t < lim) {
+                    const uint64_t xr = ld8(L.data, q + t) ^ ld8(TW, p + t);
+                    if (xr) { t += (uint32_t)__builtin_ctzll(xr) >> 3; break; }
+                    t += 8;
+                }
+            }
+            t = min(t, lim);
+            if (t > best) {
+                best = t;
+                bq = q;
+                if (t >= lim) break;
+            }
+        }
+        hb[p] = best >= 3 ? (best << 16) | (hn - bq + p) : 0u;
+    }
+}
+
 __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
                                                        int32_t max_chain, uint32_t mflags, uint16_t* __restrict__ dist_g,
                                                        uint32_t* __restrict__ tok_g, uint32_t* __restrict__ hist_g,
@@ -824,6 +952,37 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
     }
     const uint64_t t1 = dbg ? __builtin_amdgcn_s_memtime() : 0;
 
+    // ---- P1h (DMX_F_DICT): merge the history kernel's results (K0, in tok_g until P3).
+    // The history is older than every position of the block, so its match replaces the
+    // block's own only when strictly longer.  Thread t owns the 32
+    // positions of lit word t; `hov` remembers which of them took a history distance.
+    uint32_t hov = 0;
+    const uint32_t* hbp = tok_g + (uint64_t)b * DMX_BLK;
+    if (mflags & 4u) {
+        const uint32_t nvalid = bn > 2 ? bn - 2 : 0;
+        const uint32_t lo = tid << 5;
+        if (lo < nvalid) {
+            const uint32_t lw = L.lit[tid];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint4 v = reinterpret_cast<const uint4*>(hbp + lo)[j];
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const uint32_t bit = 4 * j + e, p = lo + bit;
+                    const uint32_t hl = w[e] >> 16;
+                    const uint32_t cl = ((lw >> bit) & 1u) ? 0u : (uint32_t)L.len8[p] + 3u;
+                    if (p < nvalid && hl > cl) {
+                        L.len8[p] = (uint8_t)(hl - 3u);
+                        hov |= 1u << bit;
+                    }
+                }
+            }
+            L.lit[tid] = lw & ~hov;
+        }
+        __syncthreads();
+    }
+
     // ---- P1b (DMX_F_LAZY): lazy evaluation as a per-position rule on the search results.
     // Position p (a match) becomes a literal when p+1 holds a strictly longer match; the
     // walk below then emits the literal and re-decides at p+1 -- exactly the sequential
@@ -879,6 +1038,16 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
                 if (kk < nvalid)
                     L.sorted[(pw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu] = (uint16_t)(dw[e >> 1] >> (16 * (e & 1)));
             }
+        }
+    }
+    if (mflags & 4u) {   // history distances over the permuted ones (DMX_F_DICT)
+        __syncthreads();
+        uint32_t m = hov;
+        while (m) {
+            const uint32_t bit = (uint32_t)__builtin_ctz(m);
+            m &= m - 1u;
+            const uint32_t p = (tid << 5) + bit;
+            L.sorted[p] = (uint16_t)(hbp[p] & 0xFFFFu);
         }
     }
     if (dbg && tid == 0) st_w1 = __builtin_amdgcn_s_memtime() - t1;
@@ -1979,6 +2148,7 @@ struct dmx_ctx {
     uint64_t d_in_cap;
     void* d_out;
     uint64_t d_out_cap;
+    void* d_dict;         // DMX_F_DICT history of block 0 (DMX_BLK bytes)
     // timing: a ring of event sets so timed encodes never block the host
     int timing;
     hipEvent_t ev[DMX_EV_RING][6];
@@ -2074,6 +2244,7 @@ extern "C" void dmx_ctx_destroy(dmx_ctx* c) {
     if (c->dbg) (void)hipFree(c->dbg);
     if (c->d_in) (void)hipFree(c->d_in);
     if (c->d_out) (void)hipFree(c->d_out);
+    if (c->d_dict) (void)hipFree(c->d_dict);
     for (int j = 0; j < DMX_EV_RING; j++)
         for (int k = 0; k < 6; k++) if (c->ev[j][k]) (void)hipEventDestroy(c->ev[j][k]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -2097,12 +2268,17 @@ static void ctx_collect_set(dmx_ctx* c, int j) {
 extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* d_out, uint64_t out_cap,
                                 const dmx_opts* opts, void* stream) {
     if (!c || !d_out || (!d_in && n)) return -(int)E_INVAL;
-    dmx_opts o = {0, 0, DMX_ZLIB, 0};
+    dmx_opts o = {0, 0, DMX_ZLIB, 0, NULL, 0};
     if (opts) o = *opts;
     if (o.sw == 0) o.sw = DMX_BLK;
     if (o.sw < 1 || o.sw > DMX_BLK) return -(int)E_RANGE;
     if (o.max_chain < 0) return -(int)E_RANGE;
     if ((reinterpret_cast<uintptr_t>(d_out) & 3) != 0) return -(int)E_INVAL;
+    uint32_t dict_len = 0;   // DMX_F_DICT: history of block 0 (the last sw bytes are used)
+    if ((o.flags & DMX_F_DICT) && o.dict && o.dict_len) {
+        dict_len = o.dict_len < (uint64_t)o.sw ? (uint32_t)o.dict_len : (uint32_t)o.sw;
+        o.dict = (const uint8_t*)o.dict + (o.dict_len - dict_len);
+    }
     const uint64_t nblk64 = (n + (uint64_t)o.sw - 1) / (uint64_t)o.sw;
     if (nblk64 > c->cap_blocks || nblk64 > 0x7FFFFFFFull) return -(int)E_SZ;
     const uint32_t nblk = (uint32_t)nblk64;
@@ -2127,9 +2303,14 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
             }
             dbg = c->dbg;
         }
-        if (ev) (void)hipEventRecord(ev[1], s);   // stage "chain": folded into the match kernel (P0)
+        // stage 0 "dict": the history kernel (DMX_F_DICT only; the chains are built inside the match kernel)
+        if (o.flags & DMX_F_DICT)
+            hipLaunchKernelGGL(dmx_hist_kernel, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw,
+                               o.max_chain, (const uint8_t*)o.dict, dict_len, c->tok);
+        if (ev) (void)hipEventRecord(ev[1], s);
         hipLaunchKernelGGL(dmx_match_kernel, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw,
-                           o.max_chain, ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u), c->dist, c->tok, c->hist, c->info, dbg);
+                           o.max_chain, ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u) |
+                           ((o.flags & DMX_F_DICT) ? 4u : 0u), c->dist, c->tok, c->hist, c->info, dbg);
         if (ev) (void)hipEventRecord(ev[2], s);
         if (o.flags & DMX_F_SPLIT)
             hipLaunchKernelGGL(dmx_huff_split_kernel, dim3(nblk), dim3(64 * SPW), 0, s, c->tok, c->info, c->codes, c->hdr,
@@ -2294,7 +2475,7 @@ static int ensure_buf(void** p, uint64_t* cap, uint64_t need) {
 
 extern "C" int dmx_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t out_cap, uint64_t* out_len,
                                const dmx_opts* opts) {
-    dmx_opts o = {0, 0, DMX_ZLIB, 0};
+    dmx_opts o = {0, 0, DMX_ZLIB, 0, NULL, 0};
     if (opts) o = *opts;
     if (o.sw == 0) o.sw = DMX_BLK;
     if (o.sw < 1 || o.sw > DMX_BLK) return -(int)E_RANGE;
@@ -2313,6 +2494,14 @@ extern "C" int dmx_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint
     if (!r) r = ensure_buf(&c->d_out, &c->d_out_cap, dcap);
     if (!r && hip_fail(hipSetDevice(c->device), "hipSetDevice")) r = -(int)E_DEVICE;
     if (!r && n && hip_fail(hipMemcpyAsync(c->d_in, in, n, hipMemcpyHostToDevice, c->stream), "H2D")) r = -(int)E_DEVICE;
+    if (!r && (o.flags & DMX_F_DICT) && o.dict && o.dict_len) {   // host dictionary -> device
+        const uint64_t dl = o.dict_len < (uint64_t)o.sw ? o.dict_len : (uint64_t)o.sw;
+        if (!c->d_dict && hip_fail(hipMalloc(&c->d_dict, DMX_BLK), "hipMalloc(dict)")) r = -(int)E_DEVICE;
+        if (!r && hip_fail(hipMemcpyAsync(c->d_dict, (const uint8_t*)o.dict + (o.dict_len - dl), dl,
+                                          hipMemcpyHostToDevice, c->stream), "H2D(dict)")) r = -(int)E_DEVICE;
+        o.dict = c->d_dict;
+        o.dict_len = dl;
+    }
     if (!r) r = dmx_encode_async(c, c->d_in, n, c->d_out, c->d_out_cap, &o, NULL);
     dmx_result res;
     if (!r) r = dmx_encode_result(c, &res, NULL);

@@ -123,11 +123,22 @@ struct compress_stats {
                             four DEFLATE blocks cut at the token boundaries of its quarters,
                             each with its own codes, when that is smaller */
 
+#define DMX_F_DICT 64u   /* parse option: cross-block dictionary -- every block
+                            also searches the previous sw block (the K newest entries of its
+                            hash chain, distance <= 32768); a history match is taken only when
+                            strictly longer than the block's own.  Block 0
+                            uses dmx_opts.dict when given.  Blocks then depend on their
+                            predecessor: inflate with the stream mode, not the block index. */
+
 typedef struct {
     int32_t sw;        /* block size 1..32768 (0 = 32768) */
     int32_t max_chain; /* 0 = exhaustive (reference semantics); K > 0 = the K newest chain entries */
     uint32_t flags;    /* DMX_F_* */
     int32_t reserved;
+    const void* dict;  /* DMX_F_DICT: the bytes just before the input (device memory for
+                          dmx_encode_async, host memory for dmx_encode_host), history of
+                          block 0; the last min(dict_len, sw) bytes are used.  NULL: none */
+    uint64_t dict_len;
 } dmx_opts;
 
 /* Result of one encode, filled on the device, fetched by dmx_encode_result(). */

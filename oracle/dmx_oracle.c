@@ -126,27 +126,90 @@ static int orc_search(orc_chains* C, int i, int* pos) {
     return best_pos < 0 ? 0 : best_len;
 }
 
+/* History of one block for the cross-block dictionary:
+ * the hn bytes before the block (the previous sw block), with its own chains over the
+ * positions whose trigram lies inside it (q + 2 < hn) -- the previous block's chains. */
+typedef struct {
+    orc_chains C;   /* over the history bytes; every position inserted */
+    int hn;
+} orc_hist;
+
+/* Best history match at block position i: candidates are the K newest history entries
+ * of i's bucket (all of them for K = 0) whose distance hn - q + i is at most 32768
+ * (DEFLATE's window); they are the oldest of the window, so a candidate only counts
+ * when strictly longer than best_len (the in-block result, 2 if none); ties inside the
+ * history go to the nearest (newest first, strict >).  Bytes are compared across the
+ * history/block boundary: the source runs from the history into the block. */
+static int orc_search_hist(const orc_hist* H, const uint8_t* d, int n, int i, int best_len, int* pos) {
+    int lim = n - i < ORC_MAXLEN ? n - i : ORC_MAXLEN;
+    *pos = -1;
+    if (!H || H->hn <= 0 || lim < 3 || best_len >= lim) return 0;
+    const orc_chains* C = &H->C;
+    const uint8_t* hd = C->d;
+    const int hn = H->hn;
+    int found = 0;
+    uint32_t c = C->head[orc_hash_mul(d + i)];
+    int steps = 0;
+    while (c != ORC_NONE) {
+        if (C->max_chain > 0 && steps >= C->max_chain) break;
+        steps++;
+        if ((long)hn - (long)c + i > 32768) break;   /* older entries are farther still */
+        int t = 0;
+        while (t < lim) {
+            long sp = (long)c + t;   /* source byte: history, then the block itself */
+            uint8_t sb = sp < hn ? hd[sp] : d[sp - hn];
+            if (sb != d[i + t]) break;
+            t++;
+        }
+        if (t > best_len) {
+            best_len = t;
+            *pos = (int)c;
+            found = 1;
+            if (t == lim) break;
+        }
+        c = C->prev[c];
+    }
+    return found ? best_len : 0;
+}
+
 /* Parse one block; returns the number of tokens written to tok (<= n).
  * lazy = 0: the reference's greedy parse.  lazy = 1 (RFC 1951 §4
  * "lazy evaluation", one position of lookahead): a match at i is deferred -- i becomes
  * a literal -- when the match at i+1 is strictly longer; the same rule then applies at
- * i+1.  Both matches are searched with the same chains (all positions before them). */
-int dmx_oracle_parse_block_ex(const uint8_t* d, int n, int max_chain, int hash_kind, int lazy,
-                              uint32_t* tok) {
+ * i+1.  Both matches are searched with the same chains (all positions before them).
+ * hist/hn (f1): the hn bytes before the block as a dictionary (hn = 0: none); a history
+ * match is taken only when strictly longer than the block's own best. */
+int dmx_oracle_parse_block_hist(const uint8_t* hist, int hn, const uint8_t* d, int n, int max_chain,
+                                int hash_kind, int lazy, uint32_t* tok) {
     int ntok = 0;
     if (n <= 0) return 0;
     const int nb = hash_kind == DMX_HASH_MORTON ? 1024 : 8192;
     orc_chains C = {d, n, max_chain, hash_kind, 0, (uint32_t*)malloc(sizeof(uint32_t) * nb),
                     (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n)};
     for (int b = 0; b < nb; b++) C.head[b] = ORC_NONE;
+    orc_hist H, *HP = NULL;
+    if (hist && hn > 0) {   /* the history's chains: every position of it inserted */
+        H.hn = hn;
+        H.C = (orc_chains){hist, hn, max_chain, DMX_HASH_MUL, 0, (uint32_t*)malloc(sizeof(uint32_t) * 8192),
+                           (uint32_t*)malloc(sizeof(uint32_t) * (size_t)hn)};
+        for (int b = 0; b < 8192; b++) H.C.head[b] = ORC_NONE;
+        orc_insert_upto(&H.C, hn);
+        HP = &H;
+    }
     int i = 0;
     int cached = -1, cached_len = 0, cached_pos = -1;   /* the lookahead result at i+1 */
     while (i < n) {
         int pos, len;
         if (cached == i) { len = cached_len; pos = cached_pos; }
-        else len = orc_search(&C, i, &pos);
+        else {
+            len = orc_search(&C, i, &pos);
+            int hp, hl = orc_search_hist(HP, d, n, i, len < 3 ? 2 : len, &hp);
+            if (hl > len) { len = hl; pos = hp - hn; }   /* pos < 0: in the history */
+        }
         if (len >= 3 && lazy && i + 1 < n) {
             int pos1, len1 = orc_search(&C, i + 1, &pos1);
+            int hp, hl = orc_search_hist(HP, d, n, i + 1, len1 < 3 ? 2 : len1, &hp);
+            if (hl > len1) { len1 = hl; pos1 = hp - hn; }
             cached = i + 1; cached_len = len1; cached_pos = pos1;
             if (len1 > len) len = 0;                  /* defer: literal at i */
         }
@@ -160,7 +223,16 @@ int dmx_oracle_parse_block_ex(const uint8_t* d, int n, int max_chain, int hash_k
     }
     free(C.head);
     free(C.prev);
+    if (HP) {
+        free(H.C.head);
+        free(H.C.prev);
+    }
     return ntok;
+}
+
+int dmx_oracle_parse_block_ex(const uint8_t* d, int n, int max_chain, int hash_kind, int lazy,
+                              uint32_t* tok) {
+    return dmx_oracle_parse_block_hist(NULL, 0, d, n, max_chain, hash_kind, lazy, tok);
 }
 
 int dmx_oracle_parse_block(const uint8_t* d, int n, int max_chain, int hash_kind, uint32_t* tok) {
@@ -567,8 +639,9 @@ static void orc_plan_split(const uint32_t* tok, int ntok, int bn, orc_split_plan
  * lazy = f2 parse, split = f3 block splitting.  If btypes != NULL it receives the
  * chosen BTYPE of every block (split blocks: the type of their first sub-block).
  */
-long long dmx_oracle_compress_ex2(const uint8_t* in, size_t n, int sw, int max_chain, int hash_kind,
-                                  int lazy, int split, uint8_t* out, size_t cap, uint8_t* btypes) {
+long long dmx_oracle_compress_ex3(const uint8_t* in, size_t n, int sw, int max_chain, int hash_kind,
+                                  int lazy, int split, int dict, const uint8_t* pre, size_t npre,
+                                  uint8_t* out, size_t cap, uint8_t* btypes) {
     if (sw <= 0 || sw > 32768) return -2;
     if (cap < 8) return -1;
     memset(out, 0, cap);
@@ -587,7 +660,12 @@ long long dmx_oracle_compress_ex2(const uint8_t* in, size_t n, int sw, int max_c
     for (size_t b = 0; b < nblk; b++) {
         size_t off = b * (size_t)sw;
         int bn = (int)((n - off) < (size_t)sw ? (n - off) : (size_t)sw);
-        int ntok = dmx_oracle_parse_block_ex(in + off, bn, max_chain, hash_kind, lazy, tok);
+        /* f1: the previous sw block is the history (block 0: the last sw bytes of pre) */
+        const uint8_t* hist = NULL;
+        int hn = 0;
+        if (dict && b > 0) { hist = in + off - (size_t)sw; hn = sw; }
+        else if (dict && pre && npre > 0) { hn = npre < (size_t)sw ? (int)npre : sw; hist = pre + npre - (size_t)hn; }
+        int ntok = dmx_oracle_parse_block_hist(hist, hn, in + off, bn, max_chain, hash_kind, lazy, tok);
         if (split) {
             orc_plan_split(tok, ntok, bn, SP);
             if (btypes) btypes[b] = (uint8_t)SP->P[SP->g[0]].btype;
@@ -614,6 +692,11 @@ long long dmx_oracle_compress_ex2(const uint8_t* in, size_t n, int sw, int max_c
     tail[2] = (uint8_t)(ad >> 8);
     tail[3] = (uint8_t)ad;
     return (long long)(2 + nbytes + 4);
+}
+
+long long dmx_oracle_compress_ex2(const uint8_t* in, size_t n, int sw, int max_chain, int hash_kind,
+                                  int lazy, int split, uint8_t* out, size_t cap, uint8_t* btypes) {
+    return dmx_oracle_compress_ex3(in, n, sw, max_chain, hash_kind, lazy, split, 0, NULL, 0, out, cap, btypes);
 }
 
 long long dmx_oracle_compress_ex(const uint8_t* in, size_t n, int sw, int max_chain, int hash_kind,

@@ -53,6 +53,13 @@ def lib():
         L.dmx_oracle_compress_ex2.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                               ctypes.c_int, ctypes.c_int, u8p, ctypes.c_size_t, u8p]
         L.dmx_oracle_compress_ex2.restype = ctypes.c_longlong
+        L.dmx_oracle_compress_ex3.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p, ctypes.c_size_t,
+                                              u8p, ctypes.c_size_t, u8p]
+        L.dmx_oracle_compress_ex3.restype = ctypes.c_longlong
+        L.dmx_oracle_parse_block_hist.argtypes = [u8p, ctypes.c_int, u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                  ctypes.c_int, u32p]
+        L.dmx_oracle_parse_block_hist.restype = ctypes.c_int
         L.dmx_oracle_plan.argtypes = [u32p, ctypes.c_int, ctypes.c_int, u64p, u8p, u8p]
         L.dmx_oracle_plan.restype = ctypes.c_int
         _lib = L
@@ -68,19 +75,24 @@ def _as_u8(data) -> np.ndarray:
         data, np.ndarray) else np.ascontiguousarray(data, dtype=np.uint8)
 
 
-def parse_block(data, max_chain: int = 0, hash_kind: int = HASH_MUL, lazy: bool = False) -> np.ndarray:
-    """Token stream (uint32, see dmx_oracle.c header) of one block (<= 32768 bytes)."""
+def parse_block(data, max_chain: int = 0, hash_kind: int = HASH_MUL, lazy: bool = False,
+                hist=None) -> np.ndarray:
+    """Token stream (uint32, see dmx_oracle.c header) of one block (<= 32768 bytes).
+    hist: the bytes before the block as a dictionary (f1), or None."""
     a = _as_u8(data)
     assert a.size <= 32768
     tok = np.zeros(max(a.size, 1), dtype=np.uint32)
-    n = lib().dmx_oracle_parse_block_ex(_u8(a), a.size, max_chain, hash_kind, int(lazy),
-                                        tok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+    h = _as_u8(hist if hist is not None else b"")
+    n = lib().dmx_oracle_parse_block_hist(_u8(h), h.size, _u8(a), a.size, max_chain, hash_kind, int(lazy),
+                                          tok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
     return tok[:n].copy()
 
 
-def parse(data, sw: int = 32768, max_chain: int = 0, hash_kind: int = HASH_MUL, lazy: bool = False) -> list:
+def parse(data, sw: int = 32768, max_chain: int = 0, hash_kind: int = HASH_MUL, lazy: bool = False,
+          dict: bool = False) -> list:
     a = _as_u8(data)
-    return [parse_block(a[o:o + sw], max_chain, hash_kind, lazy) for o in range(0, a.size, sw)]
+    return [parse_block(a[o:o + sw], max_chain, hash_kind, lazy, a[o - sw:o] if dict and o else None)
+            for o in range(0, a.size, sw)]
 
 
 def huff_lengths(freq, maxbits: int) -> np.ndarray:
@@ -97,15 +109,18 @@ def adler32(data) -> int:
 
 
 def compress(data, sw: int = 32768, max_chain: int = 0, hash_kind: int = HASH_MUL,
-             want_btypes: bool = False, lazy: bool = False, split: bool = False):
-    """zlib stream of `data`; lazy = f2 parse, split = f3 adaptive block splitting."""
+             want_btypes: bool = False, lazy: bool = False, split: bool = False, dict: bool = False,
+             pre=None):
+    """zlib stream of `data`; lazy = f2 parse, split = f3 adaptive block splitting,
+    dict = f1 cross-block dictionary (pre: the bytes before `data`, history of block 0)."""
     a = _as_u8(data)
     nblk = (a.size + sw - 1) // sw
     cap = a.size + 5 * (nblk + 1) + 64
     out = np.zeros(cap, dtype=np.uint8)
     bt = np.zeros(max(nblk, 1), dtype=np.uint8)
-    r = lib().dmx_oracle_compress_ex2(_u8(a), a.size, sw, max_chain, hash_kind, int(lazy), int(split),
-                                      _u8(out), cap, _u8(bt))
+    pa = _as_u8(pre if pre is not None else b"")
+    r = lib().dmx_oracle_compress_ex3(_u8(a), a.size, sw, max_chain, hash_kind, int(lazy), int(split),
+                                      int(dict), _u8(pa), pa.size, _u8(out), cap, _u8(bt))
     if r < 0:
         raise RuntimeError(f"oracle compress failed: {r}")
     z = out[:r].tobytes()

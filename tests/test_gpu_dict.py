@@ -1,0 +1,155 @@
+"""SURVEY §8 f1 on the MI355X: the cross-block dictionary (DMX_F_DICT) through the C-ABI.
+
+Bar: bit-exact.  Streams byte-identical to the oracle's dict streams (tests/test_dict.py
+pins the oracle against an independent statement of DESIGN.md §4.6); tokens equal per
+block; every stream inflates with zlib, our deflate_decompress and the GPU stream inflate.
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import deflate_compression_amd as D  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def enc():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    e = D.Encoder(0, 8 << 20)
+    yield e
+    e.close()
+
+
+def _inputs():
+    text = D.gen_text(300000, 21).tobytes()
+    rnd = D.gen_random(70000, 2).tobytes()
+    return {
+        "text": text,
+        "zeros": bytes(200000),
+        "mixed": text[:50000] + bytes(40000) + rnd + text[:60000] + b"abc" * 9000,
+        "repeat_blocks": (text[:32768] * 5)[:150000],   # every block equals the previous one
+        "random": rnd,
+        "small": text[:40000],
+    }
+
+
+def gpu_inflate_stream(z: bytes, n: int) -> bytes:
+    dz = torch.frombuffer(bytearray(z), dtype=torch.uint8).cuda()
+    out, st = D.inflate_gpu(dz, n)
+    return out.cpu().numpy().tobytes(), st
+
+
+@pytest.mark.parametrize("K", [0, 1, 4, 8, 16, 64])
+@pytest.mark.parametrize("lazy", [False, True])
+def test_dict_streams_match_oracle(enc, K, lazy):
+    flags = D.DMX_ZLIB | D.DMX_F_DICT | (D.DMX_F_LAZY if lazy else 0)
+    for name, data in _inputs().items():
+        z, r = enc.compress_bytes(data, max_chain=K, flags=flags)
+        zo = O.compress(data, max_chain=K, lazy=lazy, dict=True)
+        assert z == zo, (name, K, lazy, len(z), len(zo))
+        assert zlib.decompress(z) == data
+
+
+def test_dict_tokens_per_block(enc):
+    data = _inputs()["mixed"]
+    flags = D.DMX_ZLIB | D.DMX_F_DICT | D.DMX_F_LAZY
+    z, r = enc.compress_bytes(data, max_chain=8, flags=flags)
+    ref = O.parse(data, max_chain=8, lazy=True, dict=True)
+    assert r.nblocks == len(ref)
+    for b, t in enumerate(ref):
+        assert np.array_equal(enc.tokens(b), t), b
+
+
+@pytest.mark.parametrize("sw", [1, 2, 3, 100, 1000, 4096, 16384, 32767])
+def test_dict_small_windows(enc, sw):
+    data = _inputs()["mixed"][:120000]
+    for K in (0, 8):
+        flags = D.DMX_ZLIB | D.DMX_F_DICT | D.DMX_F_LAZY
+        z, _ = enc.compress_bytes(data, sw=sw, max_chain=K, flags=flags)
+        assert z == O.compress(data, sw=sw, max_chain=K, lazy=True, dict=True), (sw, K)
+        assert zlib.decompress(z) == data
+
+
+def test_dict_edge_sizes(enc):
+    text = D.gen_text(100000, 5).tobytes()
+    for n in (0, 1, 2, 3, 258, 32767, 32768, 32769, 32770, 32771, 65536, 65537):
+        data = text[:n]
+        z, _ = enc.compress_bytes(data, max_chain=8, flags=D.DMX_ZLIB | D.DMX_F_DICT)
+        assert z == O.compress(data, max_chain=8, dict=True), n
+        assert zlib.decompress(z) == data
+
+
+def test_dict_pre_history(enc):
+    """Block 0 with the caller's preceding bytes (device dict), and dmx_encode_host (host dict)."""
+    full = D.gen_text(250000, 8).tobytes()
+    pre, data = full[:70000], full[70000:]
+    flags = D.DMX_ZLIB | D.DMX_F_DICT | D.DMX_F_LAZY
+    z, _ = enc.compress_bytes(data, max_chain=8, flags=flags, pre=pre)
+    zo = O.compress(data, max_chain=8, lazy=True, dict=True, pre=pre)
+    assert z == zo
+    assert D.compress(data, max_chain=8, lazy=True, dict=True, pre=pre) == zo
+    for short in (b"", b"a", b"ab", full[69000:70000]):   # shorter than a window
+        z, _ = enc.compress_bytes(data[:50000], max_chain=4, flags=flags, pre=short)
+        assert z == O.compress(data[:50000], max_chain=4, lazy=True, dict=True, pre=short), len(short)
+
+
+def test_dict_exact_sort_fallback(enc):
+    data = _inputs()["text"]
+    f = D.DMX_ZLIB | D.DMX_F_DICT | D.DMX_F_LAZY
+    z1, _ = enc.compress_bytes(data, max_chain=8, flags=f)
+    z2, _ = enc.compress_bytes(data, max_chain=8, flags=f | D.DMX_F_EXACT_SORT)
+    assert z1 == z2 == O.compress(data, max_chain=8, lazy=True, dict=True)
+
+
+def test_dict_split(enc):
+    data = _inputs()["mixed"]
+    f = D.DMX_ZLIB | D.DMX_F_DICT | D.DMX_F_LAZY | D.DMX_F_SPLIT
+    z, _ = enc.compress_bytes(data, max_chain=8, flags=f)
+    assert z == O.compress(data, max_chain=8, lazy=True, dict=True, split=True)
+    assert zlib.decompress(z) == data
+
+
+def test_dict_gpu_inflate_stream_mode(enc):
+    """Dict streams reference the previous block (distances up to 32768, across block
+    boundaries): the GPU stream inflate decodes them bit-exactly."""
+    for name in ("text", "repeat_blocks", "mixed"):
+        data = _inputs()[name]
+        z, _ = enc.compress_bytes(data, max_chain=8, flags=D.DMX_ZLIB | D.DMX_F_DICT | D.DMX_F_LAZY)
+        out, st = gpu_inflate_stream(z, len(data))
+        assert st == 0 and out == data, name
+        assert D.deflate_decompress(z) == data
+
+
+def test_dict_max_distance_tokens(enc):
+    """A block equal to its predecessor: position 0 matches at distance exactly 32768."""
+    text = D.gen_text(40000, 13).tobytes()
+    data = text[:32768] * 2
+    z, _ = enc.compress_bytes(data, max_chain=0, flags=D.DMX_ZLIB | D.DMX_F_DICT)
+    t = enc.tokens(1).astype(np.int64)
+    assert (t >> 9).max() == 32768
+    assert int(np.where(t >> 9, t & 0x1FF, 1).sum()) == 32768
+    assert z == O.compress(data, max_chain=0, dict=True)
+    out, st = gpu_inflate_stream(z, len(data))
+    assert st == 0 and out == data
+    assert zlib.decompress(z) == data
+
+
+def test_dict_c3_scale_roundtrip(enc):
+    """Full C3 size (100 MB of text): the dict stream inflates (zlib) and is smaller."""
+    n = 100_000_000
+    t = torch.from_numpy(D.gen_text(n)).cuda()
+    big = D.Encoder(0, n)
+    try:
+        o = D.Opts(32768, 8, D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_DICT, 0)
+        out, r = big.compress_tensor(t, opts=o)
+        zd = out.cpu().numpy().tobytes()
+        o2 = D.Opts(32768, 8, D.DMX_ZLIB | D.DMX_F_LAZY, 0)
+        out2, r2 = big.compress_tensor(t, opts=o2)
+        assert len(zd) < 0.97 * r2.out_len
+    finally:
+        big.close()
+    assert zlib.decompress(zd) == t.cpu().numpy().tobytes()
