@@ -97,6 +97,9 @@ def main() -> int:
                     help="1 = lazy evaluation parse (DMX_F_LAZY, SURVEY §8 f2)")
     ap.add_argument("--split", type=int, default=int(os.environ.get("DMX_SPLIT", "0")),
                     help="1 = adaptive block splitting (DMX_F_SPLIT, SURVEY §8 f3)")
+    ap.add_argument("--dict", type=int, default=int(os.environ.get("DMX_DICT", "0")),
+                    help="1 = cross-block dictionary (DMX_F_DICT, SURVEY §8 f1); N > 1: halo exchange of "
+                         "the block before each shard inside the step")
     ap.add_argument("--exhaustive-steps", type=int, default=3,
                     help="also time this many exhaustive-parse steps (reported under 'exhaustive')")
     ap.add_argument("--gather", default="root", choices=["root", "all", "none"])
@@ -139,20 +142,29 @@ def main() -> int:
         flags |= D.DMX_F_LAZY
     if args.split:
         flags |= D.DMX_F_SPLIT
+    if args.dict:
+        flags |= D.DMX_F_DICT
     enc = D.Encoder(local, n, 32768, args.max_chain, flags)
     d_in = torch.from_numpy(host).to(dev)
     cap = D.max_compressed(n)
     d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
+    lens = S.shard_lengths(n, dev) if (world > 1 and args.dict) else None
+    halo = [None]
+
     def step():
+        if lens is not None:   # f1 across shards: the block before this shard, from the previous rank
+            halo[0] = S.exchange_history(d_in, n, lens=lens, out=halo[0])
+            enc.opts.dict, enc.opts.dict_len = (halo[0].data_ptr(), halo[0].numel()) if halo[0] is not None \
+                else (None, 0)
         enc.encode_async(d_in.data_ptr(), n, d_out.data_ptr(), cap, stream)
         if world > 1 and args.gather != "none":
             r = enc.result(stream)   # chunk length (device -> host) before the exchange
             S.gather_chunks(d_out, int(r.out_len), root=0 if args.gather == "root" else None)
 
     # correctness of the measured configuration (outside the timed region)
-    enc.encode_async(d_in.data_ptr(), n, d_out.data_ptr(), cap, stream)
+    step()
     res = enc.result(stream)
     out_len = int(res.out_len)
     ok = True
@@ -163,35 +175,43 @@ def main() -> int:
             log("ERROR: stream does not inflate to the input")
     # GPU inflate of the same stream: every block decoded in parallel from the
     # encoder's block index, compared bit for bit with the input; timed with events
-    ix, nblk = enc.block_index()
+    # (dict streams reference the previous block: the whole-stream decoder, one timed run)
+    indexed = not args.dict
+    ix, nblk = enc.block_index() if indexed else (None, 0)
     dec = torch.empty(n, dtype=torch.uint8, device=dev)
     ist = torch.zeros(16, dtype=torch.uint8, device=dev)
     Lib = D.lib()
 
     def inflate():
-        rc = Lib.dmx_inflate_async(d_out.data_ptr(), out_len, ix.data_ptr(), nblk, dec.data_ptr(), n,
-                                   ist.data_ptr(), stream)
+        rc = Lib.dmx_inflate_async(d_out.data_ptr(), out_len, ix.data_ptr() if indexed else None, nblk,
+                                   dec.data_ptr(), n, ist.data_ptr(), stream)
         if rc != 0:
             raise RuntimeError(f"dmx_inflate_async: {rc}")
 
-    inflate()
+    if world == 1 or indexed:
+        inflate()
     torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
-    for _ in range(3):
+    inf_reps = 3 if indexed else (1 if world == 1 else 0)
+    for _ in range(inf_reps):
         inflate()
     ev1.record()
     torch.cuda.synchronize(dev)
-    inf_ms = ev0.elapsed_time(ev1) / 3
-    h = ist.cpu().numpy()
-    inf_status = int(np.frombuffer(h[:4].tobytes(), np.int32)[0])
-    inf_len = int(np.frombuffer(h[8:16].tobytes(), np.uint64)[0])
-    inf_ok = inf_status == 0 and inf_len == n and bool(torch.equal(dec, d_in))
-    if not inf_ok:
-        log(f"ERROR: GPU inflate status {inf_status}, {inf_len} of {n} bytes, or a byte mismatch")
-        ok = False
-    gpu_inflate = {"GBps_out": round(n / inf_ms / 1e6, 3), "ms": round(inf_ms, 4), "bit_exact": inf_ok,
-                   "mode": "indexed: one single-wave workgroup per block", "kernel": "dmx_inflate_index_kernel"}
+    gpu_inflate = None
+    if inf_reps:
+        inf_ms = ev0.elapsed_time(ev1) / inf_reps
+        h = ist.cpu().numpy()
+        inf_status = int(np.frombuffer(h[:4].tobytes(), np.int32)[0])
+        inf_len = int(np.frombuffer(h[8:16].tobytes(), np.uint64)[0])
+        inf_ok = inf_status == 0 and inf_len == n and bool(torch.equal(dec, d_in))
+        if not inf_ok:
+            log(f"ERROR: GPU inflate status {inf_status}, {inf_len} of {n} bytes, or a byte mismatch")
+            ok = False
+        gpu_inflate = {"GBps_out": round(n / inf_ms / 1e6, 3), "ms": round(inf_ms, 4), "bit_exact": inf_ok,
+                       "mode": "indexed: one single-wave workgroup per block" if indexed else
+                               "stream: one wave decodes the whole zlib stream (dict blocks chain)",
+                       "kernel": "dmx_inflate_index_kernel" if indexed else "dmx_inflate_stream_kernel"}
     del dec
     for _ in range(args.warmup):
         step()
@@ -214,7 +234,7 @@ def main() -> int:
     exh = None
     if world == 1 and args.max_chain != 0 and args.exhaustive_steps > 0:
         # the reference's own parse (every earlier position of the bucket), same input
-        ex = D.Encoder(local, n, 32768, 0, flags & ~D.DMX_F_LAZY)
+        ex = D.Encoder(local, n, 32768, 0, flags & ~(D.DMX_F_LAZY | D.DMX_F_DICT | D.DMX_F_SPLIT))
         ex.encode_async(d_in.data_ptr(), n, d_out.data_ptr(), cap, stream)
         ex_len = int(ex.result(stream).out_len)
         torch.cuda.synchronize(dev)
@@ -240,6 +260,8 @@ def main() -> int:
         ms_step = dt / args.steps * 1e3
         value = tot_in * args.steps / dt / 1e9
         dom = max((k for k in stage_ms if k != "total"), key=stage_ms.get)
+        kname = {"dict": "dmx_hist_kernel", "huff": "dmx_huff_split_kernel" if args.split else "dmx_huff_kernel"}.get(
+            dom, f"dmx_{dom}_kernel")
         dom_ms = stage_ms[dom]
         algo_bytes = n + out_len   # per launch on this rank: input read + stream written
         achieved = algo_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
@@ -250,7 +272,7 @@ def main() -> int:
                 spec = importlib.util.spec_from_file_location("pmc", os.path.join(REPO, "tools", "pmc.py"))
                 pmc = importlib.util.module_from_spec(spec)
                 spec.loader.exec_module(pmc)
-                traffic = pmc.traffic_per_launch(args.traffic_csv, f"dmx_{dom}_kernel")
+                traffic = pmc.traffic_per_launch(args.traffic_csv, kname)
             except Exception as e:  # pragma: no cover
                 log("traffic csv unreadable:", e)
         cpu = {}
@@ -279,7 +301,8 @@ def main() -> int:
                 "bytes_per_rank": n,
                 "block": 32768,
                 "parse": ("exhaustive (reference semantics)" if args.max_chain == 0 else f"max_chain={args.max_chain}")
-                         + (", lazy" if args.lazy else ", greedy") + (", split" if args.split else ""),
+                         + (", lazy" if args.lazy else ", greedy") + (", split" if args.split else "")
+                         + (", dict" if args.dict else ""),
                 "parallelism": f"blocks sharded over {world} GPU(s)" + (f", gather={args.gather}" if world > 1 else ""),
             },
             "ratio": round(out_len / n, 5),
@@ -292,7 +315,7 @@ def main() -> int:
             "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
             "roofline": {
                 "bound": "hbm",
-                "kernel": f"dmx_{dom}_kernel",
+                "kernel": kname,
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -7,6 +7,10 @@ empty stored block (sync flush, byte-aligned), the last shard carries BFINAL; th
 Adler-32 trailer is combined on the host from the per-shard Adler values
 (RFC 1950 arithmetic, dmx_adler32_combine).  The exchange step is a gather of the
 variable-size compressed chunks to one rank (or all ranks) over RCCL/xGMI.
+
+With the cross-block dictionary (DMX_F_DICT) the first block of a shard
+needs the block before it, which the previous rank holds: exchange_history is that
+neighbour halo exchange (one sw-byte point-to-point message per rank boundary).
 """
 from __future__ import annotations
 
@@ -77,3 +81,51 @@ def gather_chunks(chunk: torch.Tensor, length: int, root: int | None = 0, group=
         for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, chunk[:length].contiguous(), root, group=group)]):
             w.wait()
     return None, lens
+
+
+def shard_lengths(n: int, dev, group=None) -> list:
+    """Every rank's shard length (one all_gather)."""
+    world = dist.get_world_size(group)
+    ln = torch.tensor([n], dtype=torch.int64, device=dev)
+    lens = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(lens, ln, group=group)
+    return [int(x.item()) for x in lens]
+
+
+def exchange_history(d_in: torch.Tensor, n: int, sw: int = BLOCK, group=None, lens=None,
+                     out: torch.Tensor | None = None) -> torch.Tensor | None:
+    """DMX_F_DICT across shards: the history of this rank's first block is the last block
+    of the nearest lower rank with a non-empty shard (shards are block-aligned, so that
+    is its last min(sw, len) bytes).  One all_gather of the lengths, then point-to-point
+    sends of each tail to the rank(s) that follow it.  Returns the received bytes (a
+    uint8 tensor on d_in's device) or None when there is no earlier data.  `lens` (all
+    shard lengths, from an earlier call's shard_lengths) and `out` (a receive buffer
+    of the right size) let a repeated exchange skip the length all_gather."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = d_in.device
+    if lens is None:
+        lens = shard_lengths(n, dev, group)
+
+    def src_of(t):
+        for r in range(t - 1, -1, -1):
+            if lens[r] > 0:
+                return r
+        return None
+
+    ops = []
+    if n > 0:
+        tail = d_in[n - min(sw, n):n].contiguous()
+        for t in range(rank + 1, world):
+            if lens[t] > 0 and src_of(t) == rank:
+                ops.append(dist.P2POp(dist.isend, tail, t, group=group))
+    src = src_of(rank) if n > 0 else None
+    if src is None:
+        out = None
+    else:
+        if out is None or out.numel() != min(sw, lens[src]):
+            out = torch.empty(min(sw, lens[src]), dtype=torch.uint8, device=dev)
+        ops.append(dist.P2POp(dist.irecv, out, src, group=group))
+    for w in dist.batch_isend_irecv(ops) if ops else []:
+        w.wait()
+    return out

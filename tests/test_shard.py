@@ -102,3 +102,43 @@ def test_combine_adler_matches_whole():
     cuts = [0, 1, 65536, 65537, 200_000, len(data)]
     parts = [data[a:b] for a, b in zip(cuts, cuts[1:])]
     assert S.combine_adler([zlib.adler32(p) for p in parts], [len(p) for p in parts]) == zlib.adler32(data)
+
+
+def _hist_worker(rank, world, port, n, q):
+    from oracle import oracle as O
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        full = gen_text(n, 17).tobytes()
+        lo, hi = S.shard_range(n, rank, world)
+        mine = torch.frombuffer(bytearray(full[lo:hi] + b"\0" * 16), dtype=torch.uint8)
+        h = S.exchange_history(mine, hi - lo)
+        hb = None if h is None else bytes(h.numpy())
+        ok_hist = hb == (full[max(0, lo - 32768):lo] if (lo > 0 and hi > lo) else None)
+        # the shard's dict parse with the received history == the whole stream's blocks
+        ok_tok = True
+        if hi > lo:
+            mine_t = O.parse(full[lo:hi], max_chain=8, lazy=True, dict=True)
+            whole = O.parse(full, max_chain=8, lazy=True, dict=True)[lo // 32768:(hi + 32767) // 32768]
+            mine_t[0] = O.parse_block(full[lo:lo + 32768], 8, lazy=True, hist=hb)
+            ok_tok = all(np.array_equal(a, b) for a, b in zip(mine_t, whole)) and len(mine_t) == len(whole)
+        q.put((rank, ok_hist, ok_tok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 5 * 32768 + 77), (3, 2 * 32768), (3, 7 * 32768)])
+def test_exchange_history_halo(world, n):
+    """DMX_F_DICT across shards: every rank receives the block before its shard (empty
+    shards skipped), and parsing the shard with it reproduces the whole stream's blocks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_hist_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    assert all(r[1] and r[2] for r in res), res
