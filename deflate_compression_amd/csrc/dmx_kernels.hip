@@ -348,15 +348,23 @@ __device__ __forceinline__ uint32_t resolve_full(MatchLDS& L, uint32_t bn, uint3
 // Result of one position: length (len8, literal bit) in position order, distance in bucket
 // order -- one coalesced 128-byte store per wave (a store to pg[i] would scatter 2-byte
 // partial-line writes over the block).
+// DMX_F_DICT: hbk = the history kernel's result of entry k (len << 16 | dist, 0 = none, in
+// the same bucket order); the history is older than the whole block, so it replaces the
+// block's own match only when strictly longer.
 __device__ __forceinline__ void store_result(MatchLDS& L, uint16_t* __restrict__ pg, uint32_t k, uint32_t i,
-                                             uint32_t bestkey) {
-    if (bestkey == 0) {
+                                             uint32_t bestkey, const uint32_t* __restrict__ hbk) {
+    uint32_t len = bestkey >> 15, dist = bestkey ? i - (bestkey & 0x7FFFu) : 0u;
+    if (hbk) {
+        const uint32_t hw = hbk[k];
+        if ((hw >> 16) > len) { len = hw >> 16; dist = hw & 0xFFFFu; }
+    }
+    if (len == 0) {
         atomicOr(&L.lit[i >> 5], 1u << (i & 31));
         L.len8[i] = 0;
     } else {
-        L.len8[i] = (uint8_t)((bestkey >> 15) - 3);
+        L.len8[i] = (uint8_t)(len - 3);
     }
-    pg[k] = (uint16_t)(bestkey ? i - (bestkey & 0x7FFFu) : 0u);
+    pg[k] = (uint16_t)dist;
 }
 
 // Candidate steps with the halo embedded in the chunk (K <= KE): lanes 0..K-1 hold the K
@@ -393,7 +401,7 @@ __device__ __forceinline__ void cand_steps_emb(uint32_t K, uint32_t i0, uint32_t
 }
 
 __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint16_t* __restrict__ pg,
-                                     uint32_t tid, bool stamp, uint64_t& tdef) {
+                                     uint32_t tid, bool stamp, uint64_t& tdef, const uint32_t* __restrict__ hbk) {
     const uint32_t lane = tid & 63, wave = tid >> 6;
     const uint32_t K = max_chain > 0 ? (uint32_t)max_chain : 0xFFFFFFFFu;
     const uint32_t nvalid = bn > 2 ? bn - 2 : 0;   // positions with a full trigram = entries of S
@@ -436,7 +444,7 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
             const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
             bestkey = resolve_full<true>(L, bn, lane, wave, k, i, lim_eff, bestkey, full, base - K);
             if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
-            if (act) store_result(L, pg, k, i, bestkey);
+            if (act) store_result(L, pg, k, i, bestkey, hbk);
         }
     } else
     for (uint32_t k0 = wave << 6; k0 < nvalid; k0 += MT) {
@@ -515,7 +523,7 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
                 }
             }
         }
-        if (act) store_result(L, pg, k, i, bestkey);
+        if (act) store_result(L, pg, k, i, bestkey, hbk);
     }
     // the last two positions have no trigram: literals
     if (tid < 2 && bn >= 1 + tid) {
@@ -756,70 +764,92 @@ __device__ __forceinline__ void sort_positions(MatchLDS& L, uint32_t bn, int32_t
 }
 
 // ------------------------------------------------------------------------------------
-// K0 (DMX_F_DICT): the cross-block dictionary.  For every position p of
-// block b, the longest match against the previous sw block (block 0: the caller's dict
-// bytes) -- the history of DESIGN.md §4.6:
-//   candidates = the K newest history positions q of p's bucket (all for K = 0) whose
+// K0 (DMX_F_DICT): the cross-block dictionary, DESIGN.md §4.6.  For every
+// position i of block b, the longest match against the history (the previous sw block;
+// block 0: the caller's dict bytes):
+//   candidates = the K newest history positions q of i's bucket (all for K = 0) whose
 //                trigram lies inside the history (q + 2 < hn), with distance
-//                hn - q + p <= 32768; newest first, strict > (ties to the nearest);
+//                hn - q + i <= 32768; newest first, strict > (ties to the nearest);
 //   bytes are compared across the boundary (the source runs from the history into the
-//   block itself), up to min(258, bn - p).
-// One 1024-thread workgroup per block, MatchLDS reused: data = history + the first
-// DATA_WORDS*4 - hn bytes of the block (sources that cross the boundary), sorted = the
-// history's positions by (bucket, position) from the match kernel's own sort, bstart =
-// bucket ENDS (0 = empty), len8 = the block (targets).  Result per position:
-// len << 16 | dist (0 = none) into the block's token slots, which the match kernel reads
-// back after its search (P1h) and overwrites with tokens in P3.
+//   block itself), up to min(258, bn - i).
+// Two launches before the match kernel:
+//   K0a dmx_chain_kernel  the bucket-sorted chains of every block (and of the dict), the
+//                         match kernel's own sort, exported: S (positions by (bucket,
+//                         position)) and the bucket ends.  The match kernel then loads
+//                         its S instead of sorting (each block is sorted once).
+//   K0b dmx_hist_kernel   the history search in the block's bucket order: lanes of one
+//                         bucket share their candidates (the history's bucket tail), so
+//                         their LDS reads are broadcasts.  Result per entry k of S:
+//                         len << 16 | dist (0 = none) into the block's token slots, which
+//                         the match kernel merges as it stores its own result
+//                         (store_result) and overwrites with tokens in P3.
+// Chain slots: slot 0 = the dict (block "-1"), slot b + 1 = block b.
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(MT) void dmx_hist_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
-                                                      int32_t max_chain, const uint8_t* __restrict__ pre, uint32_t npre,
-                                                      uint32_t* __restrict__ hb_g) {
-    __shared__ MatchLDS L;
-    __shared__ uint64_t tp0[3];
-    const uint32_t tid = threadIdx.x;
-    const uint32_t b = blockIdx.x;
-    const uint64_t off = (uint64_t)b * sw;
-    const uint32_t bn = (uint32_t)((n - off) < sw ? (n - off) : sw);
-    const uint8_t* cur = in + off;
-    const uint8_t* hs = nullptr;
-    uint32_t hn = 0;
-    if (b > 0) { hs = cur - sw; hn = sw; }
-    else if (pre && npre) { hn = npre < sw ? npre : sw; hs = pre + (npre - hn); }
-    uint32_t* hb = hb_g + (uint64_t)b * DMX_BLK;
-    const uint32_t nvalid = bn > 2 ? bn - 2 : 0;
-    if (hn < 3) {   // no history entries
-        for (uint32_t p = tid; p < nvalid; p += MT) hb[p] = 0;
-        return;
-    }
-    // history bytes, then the block's first bytes, zero padded (16-byte chunks)
-    const bool ha = ((reinterpret_cast<uintptr_t>(hs) & 15) == 0);
-    for (uint32_t k = tid; k < DATA_WORDS / 4; k += MT) {
+#define HG 8   // history candidates per group
+#define TB8(W, i) (reinterpret_cast<const uint8_t*>(W)[i])
+
+// Stage bytes src[0, len) at LDS word array W (16-byte chunks, zero padded to nwords).
+__device__ __forceinline__ void stage_bytes(uint32_t* W, uint32_t nwords, const uint8_t* src, uint32_t len,
+                                            const uint8_t* src2, uint32_t len2, uint32_t tid) {
+    // bytes [0, len) from src, then [len, len + len2) from src2, then zeros
+    const bool al = ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
+    for (uint32_t k = tid; k < nwords / 4; k += MT) {
         const uint32_t p = k << 4;
         uint4 v;
-        if (ha && p + 16 <= hn) {
-            v = *reinterpret_cast<const uint4*>(hs + p);
+        if (al && p + 16 <= len) {
+            v = *reinterpret_cast<const uint4*>(src + p);
         } else {
             uint32_t w[4] = {0, 0, 0, 0};
             for (uint32_t j = 0; j < 16; j++) {
                 const uint32_t x = p + j;
-                const uint32_t c = x < hn ? hs[x] : (x - hn < bn ? cur[x - hn] : 0u);
+                const uint32_t c = x < len ? src[x] : (x - len < len2 ? src2[x - len] : 0u);
                 w[j >> 2] |= c << (8 * (j & 3));
             }
             v = make_uint4(w[0], w[1], w[2], w[3]);
         }
-        *reinterpret_cast<uint4*>(&L.data[k << 2]) = v;
+        *reinterpret_cast<uint4*>(&W[k << 2]) = v;
     }
-    const uint32_t nh = hn - 2;   // history entries
+}
+
+// History of block b: its bytes and length (0 = none).
+__device__ __forceinline__ const uint8_t* hist_of(const uint8_t* in, uint32_t sw, uint32_t b, const uint8_t* pre,
+                                                  uint32_t npre, uint32_t& hn) {
+    if (b > 0) { hn = sw; return in + (uint64_t)(b - 1) * sw; }
+    hn = (pre && npre) ? (npre < sw ? npre : sw) : 0u;
+    return hn ? pre + (npre - hn) : nullptr;
+}
+
+__global__ __launch_bounds__(MT) void dmx_chain_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
+                                                       const uint8_t* __restrict__ pre, uint32_t npre,
+                                                       uint16_t* __restrict__ chs, uint16_t* __restrict__ che) {
+    __shared__ MatchLDS L;
+    __shared__ uint64_t tp0[3];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t slot = blockIdx.x;
+    const uint8_t* src;
+    uint32_t len;
+    if (slot == 0) {
+        src = hist_of(in, sw, 0, pre, npre, len);
+    } else {
+        const uint64_t off = (uint64_t)(slot - 1) * sw;
+        len = (uint32_t)((n - off) < sw ? (n - off) : sw);
+        src = in + off;
+    }
+    if (len < 3) return;   // no entries (slot 0 without a dict)
+    stage_bytes(L.data, DATA_WORDS, src, len, nullptr, 0, tid);
+    const uint32_t nv = len - 2;
+    uint16_t* S = chs + (uint64_t)slot * DMX_BLK;
+    uint16_t* E = che + (uint64_t)slot * DMX_NBUCKET;
     for (uint32_t attempt = 0;; attempt++) {
-        if (attempt == 0) sort_positions<false>(L, hn, 1, tid, false, tp0);
-        else sort_positions<true>(L, hn, 1, tid, false, tp0);
+        if (attempt == 0) sort_positions<false>(L, len, 1, tid, false, tp0);
+        else sort_positions<true>(L, len, 1, tid, false, tp0);
         for (uint32_t k = tid; k < DMX_NBUCKET; k += MT) L.bstart[k] = 0;
         __syncthreads();
-        bool bad = false;   // lane-ordered atomic ranks are checked here as in the search
-        for (uint32_t k = tid; k < nh; k += MT) {
+        bool bad = false;   // the lane-ordered atomic ranks are verified here, as in the search
+        for (uint32_t k = tid; k < nv; k += MT) {
             const uint32_t q = L.sorted[k];
             const uint32_t h = dmx_hash(ld4(L.data, q) & 0xFFFFFFu);
-            if (k + 1 < nh) {
+            if (k + 1 < nv) {
                 const uint32_t q1 = L.sorted[k + 1];
                 const uint32_t h1 = dmx_hash(ld4(L.data, q1) & 0xFFFFFFu);
                 if (h1 != h) L.bstart[h] = (uint16_t)(k + 1);
@@ -830,61 +860,122 @@ __global__ __launch_bounds__(MT) void dmx_hist_kernel(const uint8_t* __restrict_
         }
         if (!__syncthreads_or(bad) || attempt) break;
     }
-    // the block itself (targets) into len8, zero padded
-    uint32_t* TW = reinterpret_cast<uint32_t*>(L.len8);
-    const bool ca = ((reinterpret_cast<uintptr_t>(cur) & 15) == 0);
-    for (uint32_t k = tid; k < DMX_BLK / 16; k += MT) {
-        const uint32_t p = k << 4;
-        uint4 v;
-        if (ca && p + 16 <= bn) {
-            v = *reinterpret_cast<const uint4*>(cur + p);
-        } else {
-            uint32_t w[4] = {0, 0, 0, 0};
-            for (uint32_t j = 0; j < 16; j++)
-                if (p + j < bn) w[j >> 2] |= (uint32_t)cur[p + j] << (8 * (j & 3));
-            v = make_uint4(w[0], w[1], w[2], w[3]);
-        }
-        *reinterpret_cast<uint4*>(&TW[k << 2]) = v;
+    for (uint32_t k = tid; k < (nv + 7) / 8; k += MT)   // 8 entries per 16-byte store
+        reinterpret_cast<uint4*>(S)[k] = reinterpret_cast<const uint4*>(L.sorted)[k];
+    for (uint32_t k = tid; k < DMX_NBUCKET / 8; k += MT)
+        reinterpret_cast<uint4*>(E)[k] = reinterpret_cast<const uint4*>(L.bstart)[k];
+}
+
+// 66 KB: two workgroups per CU; the chains (S, bucket ends) are read through the caches
+struct __attribute__((aligned(16))) HistLDS {
+    uint32_t data[DATA_WORDS];        // the history, then the block's first bytes (sources crossing over)
+    uint32_t cur[DMX_BLK / 4 + 80];   // the block (targets), zero padded
+};
+
+__global__ __launch_bounds__(MT) void dmx_hist_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
+                                                      int32_t max_chain, const uint8_t* __restrict__ pre, uint32_t npre,
+                                                      const uint16_t* __restrict__ chs, const uint16_t* __restrict__ che,
+                                                      uint32_t* __restrict__ hb_g, uint64_t* __restrict__ dbg) {
+    __shared__ HistLDS L;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    const uint64_t off = (uint64_t)b * sw;
+    const uint32_t bn = (uint32_t)((n - off) < sw ? (n - off) : sw);
+    const uint8_t* cur = in + off;
+    uint32_t hn;
+    const uint8_t* hs = hist_of(in, sw, b, pre, npre, hn);
+    uint32_t* hb = hb_g + (uint64_t)b * DMX_BLK;
+    const uint32_t nvalid = bn > 2 ? bn - 2 : 0;
+    if (hn < 3) {   // no history entries
+        for (uint32_t k = tid; k < nvalid; k += MT) hb[k] = 0;
+        return;
     }
+    const uint64_t tbeg = dbg ? __builtin_amdgcn_s_memtime() : 0;
+    stage_bytes(L.data, DATA_WORDS, hs, hn, cur, bn, tid);
+    stage_bytes(L.cur, DMX_BLK / 4 + 80, cur, bn, nullptr, 0, tid);
     __syncthreads();
+    const uint64_t ts0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
+    const uint16_t* Sc = chs + (uint64_t)(b + 1) * DMX_BLK;   // the block's entries in bucket order
+    const uint16_t* Sp = chs + (uint64_t)b * DMX_BLK;         // the history's
+    const uint16_t* Ep = che + (uint64_t)b * DMX_NBUCKET;     // the history's bucket ends
     const uint32_t K = max_chain > 0 ? (uint32_t)max_chain : 0xFFFFFFFFu;
-    for (uint32_t p = tid; p < nvalid; p += MT) {
-        const uint64_t tv = ld8(TW, p);
-        const uint32_t tri = (uint32_t)tv & 0xFFFFFFu;
-        const uint32_t h = dmx_hash(tri);
-        const uint32_t lim = min(bn - p, (uint32_t)MAXLEN);
-        const int32_t minq = (int32_t)(hn + p) - 32768;   // distance <= 32768
-        uint32_t best = 2, bq = 0, cnt = 0;
-        for (int32_t x = (int32_t)L.bstart[h] - 1; x >= 0 && cnt < K; x--, cnt++) {
-            const uint32_t q = L.sorted[x];
-            if ((int32_t)q < minq) break;   // older entries of the bucket are farther still
-            const uint64_t sv = ld8(L.data, q);
-            if (((uint32_t)sv ^ tri) & 0xFFFFFFu) {   // another trigram
-                if (K == 0xFFFFFFFFu && dmx_hash((uint32_t)sv & 0xFFFFFFu) != h) break;   // left the bucket
-                continue;
+    uint32_t inext = tid < nvalid ? (uint32_t)Sc[tid] : 0u;
+    for (uint32_t k = tid; k < nvalid; k += MT) {
+        const uint32_t i = inext;
+        if (k + MT < nvalid) inext = Sc[k + MT];   // next entry in flight during this one
+        const uint64_t tv = ld8(L.cur, i);
+        const uint32_t t0 = (uint32_t)tv, t1 = (uint32_t)(tv >> 32), t2 = ld4(L.cur, i + 8);
+        const uint32_t h = dmx_hash(t0 & 0xFFFFFFu);
+        const uint32_t lim = min(bn - i, (uint32_t)MAXLEN);
+        const int32_t minq = (int32_t)(hn + i) - 32768;   // distance <= 32768
+        uint32_t best = 0, bq = 0, cnt = 0;
+        // Candidates newest first in groups of HG, loaded together and compared branch-free
+        // in registers on 12 bytes (longest, then nearest); only candidates equal in all 12
+        // are extended, those farther than the best so far only if they match its last byte.  An entry older than the distance limit, or of another bucket, can
+        // never win (a bucket's older entries are farther still; another bucket is another
+        // trigram), so it is masked, and the walk ends after its group; the exhaustive walk
+        // also ends where the bucket does.
+        for (int32_t x = (int32_t)Ep[h] - 1; x >= 0 && cnt < K && best < lim; x -= HG, cnt += HG) {
+            uint32_t q[HG], s0[HG], s1[HG], s2[HG];
+#pragma unroll
+            for (int g = 0; g < HG; g++) q[g] = (x - g >= 0) ? (uint32_t)Sp[x - g] : 0u;
+#pragma unroll
+            for (int g = 0; g < HG; g++) {
+                const uint64_t v = ld8(L.data, q[g]);
+                s0[g] = (uint32_t)v;
+                s1[g] = (uint32_t)(v >> 32);
+                s2[g] = ld4(L.data, q[g] + 8);
             }
-            uint32_t t = match_bytes(sv ^ tv);
-            if (t == 8) {
-                while (t < lim) {
-                    const uint64_t xr = ld8(L.data, q + t) ^ ld8(TW, p + t);
-                    if (xr) { t += (uint32_t)__builtin_ctzll(xr) >> 3; break; }
-                    t += 8;
+            uint32_t key = 0, full = 0;
+            bool left = false;
+#pragma unroll
+            for (int g = 0; g < HG; g++) {
+                const bool ok = x - g >= 0 && cnt + (uint32_t)g < K && (int32_t)q[g] >= minq;
+                const uint32_t mb = min(min(ffbl_hw(t0 ^ s0[g]), __builtin_elementwise_add_sat(ffbl_hw(t1 ^ s1[g]), 32u)),
+                                        min(ffbl_hw(t2 ^ s2[g]), 32u) + 64u);
+                const uint32_t m = ok ? min(mb >> 3, lim) : 0u;
+                key = max(key, (m << 8) | (255u - (uint32_t)g));
+                full |= (ok && mb == 96u && lim > CB) ? (1u << g) : 0u;
+                left = left || (x - g >= 0 && (int32_t)q[g] < minq);
+                if (K == 0xFFFFFFFFu)   // exhaustive: the walk ends at the bucket's start
+                    left = left || (x - g >= 0 && dmx_hash(s0[g] & 0xFFFFFFu) != h);
+            }
+            if ((key >> 8) > best) { best = key >> 8; bq = q[255u - (key & 255u)]; }
+            while (full) {   // nearest first; a farther one must be strictly longer
+                const uint32_t g = (uint32_t)__builtin_ctz(full);
+                full &= full - 1u;
+                if (best >= lim) break;
+                uint32_t qg = q[0];
+#pragma unroll
+                for (int gg = 1; gg < HG; gg++) qg = (uint32_t)gg == g ? q[gg] : qg;
+                if (best > CB && TB8(L.data, qg + best) != TB8(L.cur, i + best)) continue;
+                uint32_t kk = CB;
+                for (;;) {
+                    const uint64_t xr = ld8(L.data, qg + kk) ^ ld8(L.cur, i + kk);
+                    if (xr) { kk += (uint32_t)__builtin_ctzll(xr) >> 3; break; }
+                    kk += 8;
+                    if (kk >= lim) break;
                 }
+                kk = min(kk, lim);
+                if (kk > best) { best = kk; bq = qg; }
             }
-            t = min(t, lim);
-            if (t > best) {
-                best = t;
-                bq = q;
-                if (t >= lim) break;
-            }
+            if (left) break;
         }
-        hb[p] = best >= 3 ? (best << 16) | (hn - bq + p) : 0u;
+        hb[k] = best >= 3 ? (best << 16) | (hn - bq + i) : 0u;
+    }
+    if (dbg) {   // stamps 12..15: staged, searched
+        __syncthreads();
+        if (tid == 0) {
+            dbg[(uint64_t)b * DMX_STAMPS + 12] = ts0 - tbeg;
+            dbg[(uint64_t)b * DMX_STAMPS + 13] = __builtin_amdgcn_s_memtime() - tbeg;
+        }
     }
 }
 
 __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
                                                        int32_t max_chain, uint32_t mflags, uint16_t* __restrict__ dist_g,
-                                                       uint32_t* __restrict__ tok_g, uint32_t* __restrict__ hist_g,
+                                                       const uint16_t* __restrict__ chs, uint32_t* __restrict__ tok_g,
+                                                       uint32_t* __restrict__ hist_g,
                                                        dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg) {
     __shared__ MatchLDS L;
     __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def, tp0[3], st_rounds;
@@ -916,7 +1007,27 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         }
         *reinterpret_cast<uint4*>(&L.data[k << 2]) = v;
     }
-    sort_positions<false>(L, bn, max_chain, tid, dbg != nullptr, tp0);
+    // DMX_F_DICT: the chain kernel already sorted this block; the history kernel's
+    // results (bucket order) wait in the block's token slots until P3
+    const uint32_t* hbk = (mflags & 4u) ? tok_g + (uint64_t)b * DMX_BLK : nullptr;
+    if (hbk) {
+        const uint32_t nv = bn > 2 ? bn - 2 : 0;
+        const uint16_t* Sg = chs + (uint64_t)(b + 1) * DMX_BLK;
+        for (uint32_t k = tid; k < (nv + 7) / 8; k += MT)
+            reinterpret_cast<uint4*>(L.sorted)[k] = reinterpret_cast<const uint4*>(Sg)[k];
+        for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) L.lit[k] = 0;
+        __syncthreads();
+        if (max_chain <= 0 || max_chain > KD) {   // bucket starts, as sort_positions finds them
+            for (uint32_t k = tid; k < nv; k += MT) {
+                const uint32_t h = dmx_hash(ld4(L.data, L.sorted[k]) & 0xFFFFFFu);
+                const uint32_t hp = k ? dmx_hash(ld4(L.data, L.sorted[k - 1]) & 0xFFFFFFu) : 0xFFFFFFFFu;
+                if (h != hp) L.bstart[h] = (uint16_t)k;
+            }
+        }
+        __syncthreads();
+    } else {
+        sort_positions<false>(L, bn, max_chain, tid, dbg != nullptr, tp0);
+    }
 
     {   // Adler-32 partial sums of this block
         uint64_t s = 0, t = 0;
@@ -939,7 +1050,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
     const uint64_t t0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t tdef = 0;
     for (uint32_t attempt = 0;; attempt++) {   // one call site keeps the search inlined
-        const uint32_t its = search_positions(L, bn, max_chain, pg, tid, dbg != nullptr, tdef);
+        const uint32_t its = search_positions(L, bn, max_chain, pg, tid, dbg != nullptr, tdef, hbk);
         if (dbg && lane == 0 && attempt == 0) {
             atomicAdd((unsigned long long*)&st_iters, (unsigned long long)its);
             atomicMax((unsigned long long*)&st_search, (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
@@ -951,37 +1062,6 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         sort_positions<true>(L, bn, max_chain, tid, dbg != nullptr, tp0);
     }
     const uint64_t t1 = dbg ? __builtin_amdgcn_s_memtime() : 0;
-
-    // ---- P1h (DMX_F_DICT): merge the history kernel's results (K0, in tok_g until P3).
-    // The history is older than every position of the block, so its match replaces the
-    // block's own only when strictly longer.  Thread t owns the 32
-    // positions of lit word t; `hov` remembers which of them took a history distance.
-    uint32_t hov = 0;
-    const uint32_t* hbp = tok_g + (uint64_t)b * DMX_BLK;
-    if (mflags & 4u) {
-        const uint32_t nvalid = bn > 2 ? bn - 2 : 0;
-        const uint32_t lo = tid << 5;
-        if (lo < nvalid) {
-            const uint32_t lw = L.lit[tid];
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const uint4 v = reinterpret_cast<const uint4*>(hbp + lo)[j];
-                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const uint32_t bit = 4 * j + e, p = lo + bit;
-                    const uint32_t hl = w[e] >> 16;
-                    const uint32_t cl = ((lw >> bit) & 1u) ? 0u : (uint32_t)L.len8[p] + 3u;
-                    if (p < nvalid && hl > cl) {
-                        L.len8[p] = (uint8_t)(hl - 3u);
-                        hov |= 1u << bit;
-                    }
-                }
-            }
-            L.lit[tid] = lw & ~hov;
-        }
-        __syncthreads();
-    }
 
     // ---- P1b (DMX_F_LAZY): lazy evaluation as a per-position rule on the search results.
     // Position p (a match) becomes a literal when p+1 holds a strictly longer match; the
@@ -1038,16 +1118,6 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
                 if (kk < nvalid)
                     L.sorted[(pw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu] = (uint16_t)(dw[e >> 1] >> (16 * (e & 1)));
             }
-        }
-    }
-    if (mflags & 4u) {   // history distances over the permuted ones (DMX_F_DICT)
-        __syncthreads();
-        uint32_t m = hov;
-        while (m) {
-            const uint32_t bit = (uint32_t)__builtin_ctz(m);
-            m &= m - 1u;
-            const uint32_t p = (tid << 5) + bit;
-            L.sorted[p] = (uint16_t)(hbp[p] & 0xFFFFu);
         }
     }
     if (dbg && tid == 0) st_w1 = __builtin_amdgcn_s_memtime() - t1;
@@ -2149,6 +2219,9 @@ struct dmx_ctx {
     void* d_out;
     uint64_t d_out_cap;
     void* d_dict;         // DMX_F_DICT history of block 0 (DMX_BLK bytes)
+    uint16_t* chs;        // DMX_F_DICT: (cap_chain) x DMX_BLK bucket-sorted positions per block (+ the dict)
+    uint16_t* che;        // DMX_F_DICT: (cap_chain) x DMX_NBUCKET bucket ends
+    uint64_t cap_chain;
     // timing: a ring of event sets so timed encodes never block the host
     int timing;
     hipEvent_t ev[DMX_EV_RING][6];
@@ -2245,6 +2318,8 @@ extern "C" void dmx_ctx_destroy(dmx_ctx* c) {
     if (c->d_in) (void)hipFree(c->d_in);
     if (c->d_out) (void)hipFree(c->d_out);
     if (c->d_dict) (void)hipFree(c->d_dict);
+    if (c->chs) (void)hipFree(c->chs);
+    if (c->che) (void)hipFree(c->che);
     for (int j = 0; j < DMX_EV_RING; j++)
         for (int k = 0; k < 6; k++) if (c->ev[j][k]) (void)hipEventDestroy(c->ev[j][k]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -2283,6 +2358,16 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
     if (nblk64 > c->cap_blocks || nblk64 > 0x7FFFFFFFull) return -(int)E_SZ;
     const uint32_t nblk = (uint32_t)nblk64;
     HIPCHK(hipSetDevice(c->device));
+    if ((o.flags & DMX_F_DICT) && c->cap_chain < c->cap_blocks + 1) {   // chain export buffers, on first use
+        if (c->chs) (void)hipFree(c->chs);
+        if (c->che) (void)hipFree(c->che);
+        c->chs = NULL;
+        c->che = NULL;
+        c->cap_chain = 0;
+        HIPCHK(hipMalloc(&c->chs, (c->cap_blocks + 1) * DMX_BLK * sizeof(uint16_t)));
+        HIPCHK(hipMalloc(&c->che, (c->cap_blocks + 1) * DMX_NBUCKET * sizeof(uint16_t)));
+        c->cap_chain = c->cap_blocks + 1;
+    }
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     hipEvent_t* ev = NULL;
     if (c->timing) {
@@ -2303,14 +2388,18 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
             }
             dbg = c->dbg;
         }
-        // stage 0 "dict": the history kernel (DMX_F_DICT only; the chains are built inside the match kernel)
-        if (o.flags & DMX_F_DICT)
+        // stage 0 "dict" (DMX_F_DICT only): the chain kernel (every block's sorted chains, and
+        // the dict's) and the history search; otherwise the match kernel sorts its own block
+        if (o.flags & DMX_F_DICT) {
+            hipLaunchKernelGGL(dmx_chain_kernel, dim3(nblk + 1), dim3(MT), 0, s, (const uint8_t*)d_in, n,
+                               (uint32_t)o.sw, (const uint8_t*)o.dict, dict_len, c->chs, c->che);
             hipLaunchKernelGGL(dmx_hist_kernel, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw,
-                               o.max_chain, (const uint8_t*)o.dict, dict_len, c->tok);
+                               o.max_chain, (const uint8_t*)o.dict, dict_len, c->chs, c->che, c->tok, dbg);
+        }
         if (ev) (void)hipEventRecord(ev[1], s);
         hipLaunchKernelGGL(dmx_match_kernel, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw,
                            o.max_chain, ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u) |
-                           ((o.flags & DMX_F_DICT) ? 4u : 0u), c->dist, c->tok, c->hist, c->info, dbg);
+                           ((o.flags & DMX_F_DICT) ? 4u : 0u), c->dist, c->chs, c->tok, c->hist, c->info, dbg);
         if (ev) (void)hipEventRecord(ev[2], s);
         if (o.flags & DMX_F_SPLIT)
             hipLaunchKernelGGL(dmx_huff_split_kernel, dim3(nblk), dim3(64 * SPW), 0, s, c->tok, c->info, c->codes, c->hdr,

@@ -4,11 +4,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ["DMX_STAMPS"] = "1"
 import numpy as np, torch
 import deflate_compression_amd as D
+if os.environ.get("DMX_LIBV"): D.LIB_PATH = os.environ["DMX_LIBV"]
 
-def run(kind, n, mc):
+def run(kind, n, mc, flags=D.DMX_ZLIB | D.DMX_F_LAZY):
     a = D.gen_text(n, 0xE5818) if kind == "text" else (D.gen_random(n, 1) if kind == "random" else np.zeros(n, np.uint8))
     t = torch.from_numpy(a).cuda()
-    e = D.Encoder(0, n, max_chain=mc)
+    e = D.Encoder(0, n, max_chain=mc, flags=flags)
     for _ in range(2):
         out, r = e.compress_tensor(t)
     st = e.stamps(r.nblocks).astype(np.float64)
@@ -20,10 +21,14 @@ def run(kind, n, mc):
                       "total_kcyc": round(st[:, 7].mean() / 1e3, 1),
                       "p0_staged_kcyc": round(st[:, 8].mean() / 1e3, 1), "p0_pass1_end_kcyc": round(st[:, 9].mean() / 1e3, 1),
                       "p0_pass2_end_kcyc": round(st[:, 10].mean() / 1e3, 1),
-                      "walk_rounds": round(st[:, 11].mean(), 2), "walk_fallback_frac": round(float((st[:, 11] >= 8).mean()), 3)}))
+                      "walk_rounds": round(st[:, 11].mean(), 2), "walk_fallback_frac": round(float((st[:, 11] >= 8).mean()), 3),
+                      **({"hist_staged_kcyc": round(st[1:, 12].mean() / 1e3, 1), "hist_total_kcyc": round(st[1:, 13].mean() / 1e3, 1)}
+                         if flags & D.DMX_F_DICT else {})}))
 
-cfgs = [("text", 1), ("text", 16), ("text", 0), ("random", 0), ("zeros", 0)]
+# args: kind:max_chain[:d]  (d = with the cross-block dictionary, DMX_F_DICT)
+cfgs = [("text", 1, ""), ("text", 16, ""), ("text", 0, ""), ("random", 0, ""), ("zeros", 0, "")]
 if len(sys.argv) > 1:
-    cfgs = [(a.split(":")[0], int(a.split(":")[1])) for a in sys.argv[1:]]
-for kind, mc in cfgs:
-    run(kind, 20_000_000 if kind == "text" else 64 << 20, mc)
+    cfgs = [(a.split(":") + [""])[:3] for a in sys.argv[1:]]
+for kind, mc, opt in cfgs:
+    fl = D.DMX_ZLIB | D.DMX_F_LAZY | (D.DMX_F_DICT if "d" in opt else 0)
+    run(kind, 20_000_000 if kind == "text" else 64 << 20, int(mc), fl)
