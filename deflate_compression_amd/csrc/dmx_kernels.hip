@@ -146,6 +146,7 @@ __device__ __forceinline__ uint32_t adv_of(const MatchLDS& L, uint32_t p) {
 #define CB 12   // bytes compared in registers per candidate step; longer matches extend from LDS
 #define KE 8    // chains up to KE candidates use chunks with the halo embedded (64-K owned entries)
 #define JR 8    // Jacobi rounds of the walk before the serial fallback
+#define WALK_SERIAL 1024   // fallback: at most this many tokens (approximate path) -> one-lane token walk
 #define CW 4
 __device__ __forceinline__ uint32_t ffbl(uint32_t x) {   // lowest set bit, ~0 for 0 (v_ffbl_b32)
     return x ? (uint32_t)__builtin_ctz(x) : 0xFFFFFFFFu;
@@ -189,6 +190,54 @@ __device__ __forceinline__ uint32_t ext_len(const MatchLDS& L, uint32_t i, uint3
         if (kk >= lim) return kk;
     }
 }
+// Change bitmap (bounded mode, K <= KD: bucket starts are not needed, so it lives in
+// bstart): bit p = data[p] != data[p+1] (set for p >= bn - 1).  Built at the start of the
+// search (search_positions); gives a distance-1 candidate's exact length in a few word reads.
+__device__ __forceinline__ uint32_t* chg_bits(MatchLDS& L) { return reinterpret_cast<uint32_t*>(L.bstart); }
+__device__ __forceinline__ uint32_t* chg_bits(const MatchLDS& L) {
+    return reinterpret_cast<uint32_t*>(const_cast<uint16_t*>(L.bstart));
+}
+// Length of the match at i against i - 1 (>= 1 known equal bytes), capped at lim: the first
+// change at or after i - 1 ends it.
+__device__ __forceinline__ uint32_t run_len(const MatchLDS& L, uint32_t i, uint32_t lim) {
+    const uint32_t* C = chg_bits(L);
+    const uint32_t x = i - 1u, a = x >> 5;   // lim <= 258: a change at x + lim - 1 <= 32a + 288 decides
+    uint32_t r = 0xFFFFFFFFu;
+#pragma unroll
+    for (int t0 = 0; t0 < 10; t0 += 5) {   // 5 independent reads per round; most runs end in the first
+        if (r != 0xFFFFFFFFu) break;
+        uint32_t w[5];
+#pragma unroll
+        for (int t = 0; t < 5; t++) w[t] = C[min(a + (uint32_t)(t0 + t), (uint32_t)(DMX_BLK / 32 - 1))];
+        if (t0 == 0) w[0] &= ~0u << (x & 31);
+#pragma unroll
+        for (int t = 4; t >= 0; t--) r = w[t] ? ((a + (uint32_t)(t0 + t)) << 5) + (uint32_t)__builtin_ctz(w[t]) : r;
+    }
+    return r == 0xFFFFFFFFu ? lim : min(r - x, lim);
+}
+
+// Builds the change bitmap (bounded mode, K <= KE, after P0: bstart is free) and returns
+// whether the block is run-dominated: at least a quarter of its 32-byte segments hold fewer
+// than 8 byte changes.  Such blocks search with run_len (search_positions<.., true>).
+__device__ __forceinline__ bool build_chg(MatchLDS& L, uint32_t bn, uint32_t tid) {
+    const uint32_t lo = tid << 5;
+    const uint4 v0 = *reinterpret_cast<const uint4*>(&L.data[lo >> 2]);
+    const uint4 v1 = *reinterpret_cast<const uint4*>(&L.data[(lo >> 2) + 4]);
+    const uint32_t w[9] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, L.data[(lo >> 2) + 8]};
+    uint32_t m = 0;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {   // byte b of word t vs the byte after it
+        const uint32_t nx = __builtin_amdgcn_alignbyte(w[t + 1], w[t], 1);
+        const uint32_t x = w[t] ^ nx;
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) m |= (((x >> (8 * bb)) & 0xFFu) != 0u ? 1u : 0u) << (4 * t + bb);
+    }
+    const uint32_t last = bn ? bn - 1u : 0u;   // positions >= bn - 1 end every run
+    if (lo + 32 > last) m |= lo >= last ? 0xFFFFFFFFu : ~((1u << (last - lo)) - 1u);
+    chg_bits(L)[tid] = m;
+    return __syncthreads_count(lo < bn && __popc(m) < 8) * 4 >= (int)((bn + 31) >> 5);
+}
+
 // Could candidate q (known to match [0, 16)) be strictly longer than best (>= 16)? Only if
 // it also matches the byte at offset best.
 __device__ __forceinline__ bool may_beat(const MatchLDS& L, uint32_t i, uint32_t q, uint32_t best) {
@@ -278,7 +327,7 @@ __device__ __forceinline__ void cand_steps(uint32_t jmax, uint32_t i0, uint32_t 
 // wave's lanes through an LDS queue (one round for typical text instead of max-popcount
 // rounds) and merged with atomicMax on the key, which orders longest, then nearest.
 // kb = entry of lane 0 of the chunk (owner lane o has entry kb + o).
-template <bool SHORT>
+template <bool SHORT, bool RUNS>
 __device__ __forceinline__ uint32_t resolve_full(MatchLDS& L, uint32_t bn, uint32_t lane, uint32_t wave, uint32_t k,
                                                  uint32_t i, uint32_t lim_eff, uint32_t bestkey, uint32_t full,
                                                  uint32_t kb) {
@@ -287,7 +336,9 @@ __device__ __forceinline__ uint32_t resolve_full(MatchLDS& L, uint32_t bn, uint3
         const uint32_t j = (uint32_t)__builtin_ctz(full) + 1u;
         full &= full - 1u;
         const uint32_t q = L.sorted[k - j];
-        const uint32_t len = min(ext_len(L, i, q, CB, lim_eff), lim_eff);
+        // distance 1 (runs): the length is where the run ends, from the change bitmap
+        const uint32_t len = min(q + 1u == i && SHORT && RUNS ? run_len(L, i, lim_eff) : ext_len(L, i, q, CB, lim_eff),
+                                 lim_eff);
         bestkey = max(bestkey, (len << 15) | q);
     }
     if ((bestkey >> 15) >= lim_eff) full = 0;
@@ -351,10 +402,11 @@ __device__ __forceinline__ uint32_t resolve_full(MatchLDS& L, uint32_t bn, uint3
 // DMX_F_DICT: hbk = the history kernel's result of entry k (len << 16 | dist, 0 = none, in
 // the same bucket order); the history is older than the whole block, so it replaces the
 // block's own match only when strictly longer.
+template <bool DICT>
 __device__ __forceinline__ void store_result(MatchLDS& L, uint16_t* __restrict__ pg, uint32_t k, uint32_t i,
                                              uint32_t bestkey, const uint32_t* __restrict__ hbk) {
     uint32_t len = bestkey >> 15, dist = bestkey ? i - (bestkey & 0x7FFFu) : 0u;
-    if (hbk) {
+    if (DICT) {
         const uint32_t hw = hbk[k];
         if ((hw >> 16) > len) { len = hw >> 16; dist = hw & 0xFFFFu; }
     }
@@ -400,12 +452,14 @@ __device__ __forceinline__ void cand_steps_emb(uint32_t K, uint32_t i0, uint32_t
         cand_step_emb<GUARD, CLAMP>(j, sj, x0, x1, x2, i0, i1, i2, nc, lim_eff, jkey, full);
 }
 
+template <bool DICT, bool RUNS>
 __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint16_t* __restrict__ pg,
                                      uint32_t tid, bool stamp, uint64_t& tdef, const uint32_t* __restrict__ hbk) {
     const uint32_t lane = tid & 63, wave = tid >> 6;
     const uint32_t K = max_chain > 0 ? (uint32_t)max_chain : 0xFFFFFFFFu;
     const uint32_t nvalid = bn > 2 ? bn - 2 : 0;   // positions with a full trigram = entries of S
     uint32_t iters = 0;
+    if (RUNS) build_chg(L, bn, tid);
     if (K <= KE) {
         // bounded mode with a short chain: chunks of 64-K owned entries, halo embedded
         const uint32_t own = 64 - K;
@@ -442,9 +496,9 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
             uint32_t bestkey = 0;
             if (act && (jkey >> 8) >= 3) bestkey = ((jkey >> 8) << 15) | (uint32_t)L.sorted[k - (255u - (jkey & 255u))];
             const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
-            bestkey = resolve_full<true>(L, bn, lane, wave, k, i, lim_eff, bestkey, full, base - K);
+            bestkey = resolve_full<true, RUNS>(L, bn, lane, wave, k, i, lim_eff, bestkey, full, base - K);
             if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
-            if (act) store_result(L, pg, k, i, bestkey, hbk);
+            if (act) store_result<DICT>(L, pg, k, i, bestkey, hbk);
         }
     } else
     for (uint32_t k0 = wave << 6; k0 < nvalid; k0 += MT) {
@@ -498,7 +552,7 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
         uint32_t bestkey = 0;
         if (act && (jkey >> 8) >= 3) bestkey = ((jkey >> 8) << 15) | (uint32_t)L.sorted[k - (255u - (jkey & 255u))];
         const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
-        bestkey = resolve_full<false>(L, bn, lane, wave, k, i, lim_eff, bestkey, full, k0);
+        bestkey = resolve_full<false, false>(L, bn, lane, wave, k, i, lim_eff, bestkey, full, k0);
         if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
         // chains longer than KD (exhaustive mode): continue from LDS, CW candidates per iteration
         for (uint32_t c = KD;; c += CW) {
@@ -523,7 +577,7 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
                 }
             }
         }
-        if (act) store_result(L, pg, k, i, bestkey, hbk);
+        if (act) store_result<DICT>(L, pg, k, i, bestkey, hbk);
     }
     // the last two positions have no trigram: literals
     if (tid < 2 && bn >= 1 + tid) {
@@ -972,6 +1026,7 @@ __global__ __launch_bounds__(MT) void dmx_hist_kernel(const uint8_t* __restrict_
     }
 }
 
+template <bool DICT>
 __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
                                                        int32_t max_chain, uint32_t mflags, uint16_t* __restrict__ dist_g,
                                                        const uint16_t* __restrict__ chs, uint32_t* __restrict__ tok_g,
@@ -994,6 +1049,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
     for (uint32_t k = tid; k < DMX_HIST; k += MT) L.hist[k] = 0;
     for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) L.lit[k] = 0;
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
+    uint32_t runny = 0;   // 16-byte chunks with fewer than 4 byte changes (run-dominated blocks)
     for (uint32_t k = tid; k < DATA_WORDS / 4; k += MT) {   // 16-byte chunks
         const uint32_t p = k << 4;
         uint4 v;
@@ -1006,11 +1062,23 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
             v = make_uint4(w[0], w[1], w[2], w[3]);
         }
         *reinterpret_cast<uint4*>(&L.data[k << 2]) = v;
+        // run-dominated blocks take the run_len search (search_positions<.., true>): count the
+        // 16-byte chunks with fewer than 4 byte changes
+        const uint32_t c0 = v.x ^ __builtin_amdgcn_alignbyte(v.y, v.x, 1), c1 = v.y ^ __builtin_amdgcn_alignbyte(v.z, v.y, 1),
+                       c2 = v.z ^ __builtin_amdgcn_alignbyte(v.w, v.z, 1), c3 = v.w ^ (v.w >> 8);
+        uint32_t nch = 0;
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++)
+            nch += ((c0 >> (8 * bb)) & 0xFFu ? 1u : 0u) + ((c1 >> (8 * bb)) & 0xFFu ? 1u : 0u) +
+                   ((c2 >> (8 * bb)) & 0xFFu ? 1u : 0u) + (bb < 3 && ((c3 >> (8 * bb)) & 0xFFu) ? 1u : 0u);
+        runny += (p < bn && nch < 4) ? 1u : 0u;
     }
+    runny = wave_sum_u32(runny);
+    if (lane == 0) L.wexit[wave] = runny;   // free until the walk; published by the barriers below
     // DMX_F_DICT: the chain kernel already sorted this block; the history kernel's
     // results (bucket order) wait in the block's token slots until P3
-    const uint32_t* hbk = (mflags & 4u) ? tok_g + (uint64_t)b * DMX_BLK : nullptr;
-    if (hbk) {
+    const uint32_t* hbk = DICT ? tok_g + (uint64_t)b * DMX_BLK : nullptr;
+    if (DICT) {
         const uint32_t nv = bn > 2 ? bn - 2 : 0;
         const uint16_t* Sg = chs + (uint64_t)(b + 1) * DMX_BLK;
         for (uint32_t k = tid; k < (nv + 7) / 8; k += MT)
@@ -1049,8 +1117,16 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
     // ---- P1: longest match of every position ----
     const uint64_t t0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t tdef = 0;
-    for (uint32_t attempt = 0;; attempt++) {   // one call site keeps the search inlined
-        const uint32_t its = search_positions(L, bn, max_chain, pg, tid, dbg != nullptr, tdef, hbk);
+    for (uint32_t attempt = 0;; attempt++) {
+        // run-dominated blocks (zeros, long runs) search with the change bitmap; a separate
+        // instantiation keeps its registers out of the common path
+        // (counted per wave while staging; the sort's barriers published the counts)
+        uint32_t nrun = 0;
+#pragma unroll
+        for (int w = 0; w < MW; w++) nrun += L.wexit[w];
+        const bool runs = max_chain > 0 && max_chain <= KE && nrun * 4 >= ((bn + 15) >> 4);
+        const uint32_t its = runs ? search_positions<DICT, true>(L, bn, max_chain, pg, tid, dbg != nullptr, tdef, hbk)
+                                  : search_positions<DICT, false>(L, bn, max_chain, pg, tid, dbg != nullptr, tdef, hbk);
         if (dbg && lane == 0 && attempt == 0) {
             atomicAdd((unsigned long long*)&st_iters, (unsigned long long)its);
             atomicMax((unsigned long long*)&st_search, (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
@@ -1128,11 +1204,18 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
     // sequential path.  Typical text converges in a few rounds; a run of long matches moves
     // the true entry one segment per round, so after JR rounds the serial resolution below
     // finishes from the current (valid) segment paths.
-    bool conv = false;
+    bool conv = false, serial = false;
+    if (tid == 0) L.ntok = 0;
     {
         uint32_t entry = tid << 5;   // what W1 assumed
         uint32_t r = 0;
         for (; r < JR; r++) {
+            if (r == 3) {   // not converged yet: few tokens (runs of long matches) -> serial walk below
+                const uint32_t pc = wave_sum_u32((uint32_t)__popc(L.tsm[tid]));
+                if (lane == 0) atomicAdd(&L.ntok, pc);
+                __syncthreads();
+                if (L.ntok <= WALK_SERIAL) { serial = true; break; }
+            }
             const uint32_t e = tid == 0 ? 0u : L.exitp[tid - 1];
             __syncthreads();
             const bool ch = (tid << 5) < bn && e != entry;   // segments past the block end stay empty
@@ -1147,6 +1230,23 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
             if (!__syncthreads_or(ch)) { conv = true; break; }
         }
         if (dbg && tid == 0) st_rounds = r;
+    }
+    if (serial) {   // few tokens (runs of long matches): one lane walks the path token by token
+        {
+            conv = true;
+            L.tsm[tid] = 0;
+            __syncthreads();
+            if (tid == 0) {
+                uint32_t p = 0, wi = 0, cw = 0;
+                while (p < bn) {
+                    if ((p >> 5) != wi) { L.tsm[wi] = cw; cw = 0; wi = p >> 5; }
+                    cw |= 1u << (p & 31);
+                    p += adv_of(L, p);
+                }
+                L.tsm[wi] = cw;
+            }
+            __syncthreads();
+        }
     }
     if (!conv) {
         {   // W2: each wave resolves its 64 segments assuming it is entered at 2048*wave.
@@ -2397,9 +2497,13 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                                o.max_chain, (const uint8_t*)o.dict, dict_len, c->chs, c->che, c->tok, dbg);
         }
         if (ev) (void)hipEventRecord(ev[1], s);
-        hipLaunchKernelGGL(dmx_match_kernel, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw,
-                           o.max_chain, ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u) |
-                           ((o.flags & DMX_F_DICT) ? 4u : 0u), c->dist, c->chs, c->tok, c->hist, c->info, dbg);
+        const uint32_t mfl = ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u);
+        if (o.flags & DMX_F_DICT)
+            hipLaunchKernelGGL(dmx_match_kernel<true>, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n,
+                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg);
+        else
+            hipLaunchKernelGGL(dmx_match_kernel<false>, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n,
+                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg);
         if (ev) (void)hipEventRecord(ev[2], s);
         if (o.flags & DMX_F_SPLIT)
             hipLaunchKernelGGL(dmx_huff_split_kernel, dim3(nblk), dim3(64 * SPW), 0, s, c->tok, c->info, c->codes, c->hdr,

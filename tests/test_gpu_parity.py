@@ -251,3 +251,40 @@ def test_c3_scale_roundtrip(enc):
     for b in (0, 1526, 3051):
         blk = a[b * 32768:(b + 1) * 32768].tobytes()
         assert np.array_equal(enc.tokens(b), O.parse_block(blk))
+
+
+def _run_heavy(seed=7):
+    rng = np.random.default_rng(seed)
+    parts = []
+    while sum(map(len, parts)) < 200000:
+        r = rng.random()
+        if r < 0.6:   # a run, lengths around and beyond the 258 cap and the block edges
+            parts.append(bytes([int(rng.integers(0, 4))]) * int(rng.choice([1, 2, 3, 12, 13, 255, 258, 259, 300, 5000])))
+        elif r < 0.8:
+            parts.append(bytes(int(rng.integers(0, 256)) for _ in range(int(rng.integers(1, 20)))))
+        else:
+            parts.append((b"ab" * 400)[: int(rng.integers(2, 700))])
+    return b"".join(parts)
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 8])
+@pytest.mark.parametrize("lazy", [False, True])
+def test_run_dominated_blocks(enc, k, lazy):
+    """Run-dominated blocks search with the change bitmap (run_len, bounded mode K <= 8):
+    byte-identical to the oracle, also mixed with text blocks, with the dict, and on the
+    exact-sort fallback (which rebuilds the bitmap)."""
+    text = D.gen_text(100000, 3).tobytes()
+    for data in (_run_heavy(), bytes(100000), text[:40000] + _run_heavy(9)[:70000] + text[40000:],
+                 b"\x00" * 32767 + b"\x01" + b"\x00" * 40000):
+        f = D.DMX_ZLIB | (D.DMX_F_LAZY if lazy else 0)
+        z, _ = enc.compress_bytes(data, max_chain=k, flags=f)
+        assert z == O.compress(data, max_chain=k, lazy=lazy)
+        check_stream(z, data)
+        z2, _ = enc.compress_bytes(data, max_chain=k, flags=f | D.DMX_F_EXACT_SORT)
+        assert z2 == z
+        zd, _ = enc.compress_bytes(data, max_chain=k, flags=f | D.DMX_F_DICT)
+        assert zd == O.compress(data, max_chain=k, lazy=lazy, dict=True)
+    for sw in (16, 100, 1000, 4096):
+        data = _run_heavy(11)[:50000]
+        z, _ = enc.compress_bytes(data, sw=sw, max_chain=k, flags=D.DMX_ZLIB | (D.DMX_F_LAZY if lazy else 0))
+        assert z == O.compress(data, sw=sw, max_chain=k, lazy=lazy), sw
