@@ -1049,7 +1049,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
     for (uint32_t k = tid; k < DMX_HIST; k += MT) L.hist[k] = 0;
     for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) L.lit[k] = 0;
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
-    uint32_t runny = 0;   // 16-byte chunks with fewer than 4 byte changes (run-dominated blocks)
+    uint32_t runny = 0;   // 16-byte chunks of one repeated byte (run-dominated blocks)
     for (uint32_t k = tid; k < DATA_WORDS / 4; k += MT) {   // 16-byte chunks
         const uint32_t p = k << 4;
         uint4 v;
@@ -1063,15 +1063,8 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         }
         *reinterpret_cast<uint4*>(&L.data[k << 2]) = v;
         // run-dominated blocks take the run_len search (search_positions<.., true>): count the
-        // 16-byte chunks with fewer than 4 byte changes
-        const uint32_t c0 = v.x ^ __builtin_amdgcn_alignbyte(v.y, v.x, 1), c1 = v.y ^ __builtin_amdgcn_alignbyte(v.z, v.y, 1),
-                       c2 = v.z ^ __builtin_amdgcn_alignbyte(v.w, v.z, 1), c3 = v.w ^ (v.w >> 8);
-        uint32_t nch = 0;
-#pragma unroll
-        for (int bb = 0; bb < 4; bb++)
-            nch += ((c0 >> (8 * bb)) & 0xFFu ? 1u : 0u) + ((c1 >> (8 * bb)) & 0xFFu ? 1u : 0u) +
-                   ((c2 >> (8 * bb)) & 0xFFu ? 1u : 0u) + (bb < 3 && ((c3 >> (8 * bb)) & 0xFFu) ? 1u : 0u);
-        runny += (p < bn && nch < 4) ? 1u : 0u;
+        // 16-byte chunks that are one repeated byte
+        runny += (p < bn && v.x == v.y && v.y == v.z && v.z == v.w && v.x == (v.x & 0xFFu) * 0x01010101u) ? 1u : 0u;
     }
     runny = wave_sum_u32(runny);
     if (lane == 0) L.wexit[wave] = runny;   // free until the walk; published by the barriers below
