@@ -1802,25 +1802,33 @@ __global__ __launch_bounds__(64) void dmx_huff_kernel(const uint32_t* __restrict
     }
 }
 
-// K2s (DMX_F_SPLIT): adaptive block splitting.  Quarter k of a block holds
-// the tokens whose start lies in [(k*bn)>>2, ((k+1)*bn)>>2).  All 640 threads rebuild the
-// per-quarter histograms from the block's tokens (a prefix sum of token lengths gives the
-// starts); then wave g plans group g -- one of the 10 contiguous runs of quarters -- with
-// huff_block (fixed or dynamic; the whole block keeps the stored option); thread 0 picks
-// the cheapest of the 8 cut masks (ties: fewer blocks, then the smaller mask; no empty
-// group), and waves 0..nsub-1 write the chosen blocks' codes, headers and token ranges.
-// The rule is DESIGN.md §4.5.
+// K2s (DMX_F_SPLIT): adaptive block splitting, DESIGN.md §4.5.  Quarter k of
+// a block holds the tokens whose start lies in [(k*bn)>>2, ((k+1)*bn)>>2).  Three launches,
+// so that the ten latency-bound Huffman plans per block run as separate small workgroups
+// (up to 16 per CU) instead of ten waves of one 105 KB workgroup (one per CU):
+//   dmx_split_hist_kernel    per block: per-quarter histograms and quarter token bounds,
+//                            rebuilt from the tokens (a prefix sum of token lengths gives
+//                            their starts) -> HBM scratch;
+//   dmx_split_plan_kernel    per (block, group): group g is one of the 10 contiguous runs of
+//                            quarters, planned with huff_block (fixed or dynamic; only the
+//                            whole block keeps the stored option) -> cost, codes, header;
+//   dmx_split_choose_kernel  per block: the cheapest of the 8 cut masks (ties: fewer blocks,
+//                            then the smaller mask; no empty group); the chosen groups'
+//                            codes, headers and token ranges into the sub-block slots.
 #define SPW 10
 __constant__ uint8_t c_gi[SPW] = {0, 1, 2, 3, 0, 1, 2, 0, 1, 0};
 __constant__ uint8_t c_gj[SPW] = {0, 1, 2, 3, 1, 2, 3, 2, 3, 3};
 
-struct SplitLDS {
+struct SplitGroup {
+    uint32_t bt, hbits, empty, pad;
+    uint64_t body, cost;
+};
+struct SplitScratch {   // per block, in HBM (dmx_ctx.split)
     uint32_t qh[4][DMX_HIST];
-    uint32_t qt[5];
-    uint32_t wsum[SPW];
-    uint32_t gbt[SPW], ghb[SPW], gempty[SPW];
-    uint64_t gbody[SPW], gcost[SPW];
-    uint32_t nsub, sg[DMX_NSUB];
+    uint32_t qt[8];
+    SplitGroup g[SPW];
+    uint32_t code[SPW][DMX_HIST];
+    uint32_t hdr[SPW][DMX_HDR_WORDS];
 };
 
 __device__ __forceinline__ uint32_t grp_of(uint32_t i, uint32_t j) {   // inverse of c_gi / c_gj
@@ -1828,37 +1836,32 @@ __device__ __forceinline__ uint32_t grp_of(uint32_t i, uint32_t j) {   // invers
     return (len == 0 ? 0u : len == 1 ? 4u : len == 2 ? 7u : 9u) + i;
 }
 
-__global__ __launch_bounds__(64 * SPW) void dmx_huff_split_kernel(const uint32_t* __restrict__ tok_g,
-                                                                  dmx_blkinfo* __restrict__ info,
-                                                                  uint32_t* __restrict__ codes_g,
-                                                                  uint32_t* __restrict__ hdr_g,
-                                                                  dmx_subinfo* __restrict__ sub_g,
-                                                                  uint32_t nblk, uint32_t flags) {
-    __shared__ K2LDS K[SPW];
-    __shared__ SplitLDS Q;
+#define SHT 640
+__global__ __launch_bounds__(SHT) void dmx_split_hist_kernel(const uint32_t* __restrict__ tok_g,
+                                                             const dmx_blkinfo* __restrict__ info,
+                                                             SplitScratch* __restrict__ sp) {
+    __shared__ uint32_t qh[4][DMX_HIST];
+    __shared__ uint32_t qt[5], wsum[SHT / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t b = blockIdx.x;
     const uint32_t ntok = info[b].ntok, bn = info[b].n;
-    const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1) ? 1u : 0u;
-    for (uint32_t k = tid; k < 4 * DMX_HIST; k += 64 * SPW) (&Q.qh[0][0])[k] = 0;
-    if (tid < 5) Q.qt[tid] = tid == 4 ? ntok : 0u;
+    for (uint32_t k = tid; k < 4 * DMX_HIST; k += SHT) (&qh[0][0])[k] = 0;
+    if (tid < 5) qt[tid] = tid == 4 ? ntok : 0u;
     __syncthreads();
-
-    // per-quarter histograms and quarter token boundaries
     const uint32_t B1 = bn >> 2, B2 = (2 * bn) >> 2, B3 = (3 * bn) >> 2;
     const uint32_t* tb = tok_g + (uint64_t)b * DMX_BLK;
     uint32_t carry = 0, c1 = 0, c2 = 0, c3 = 0;
-    for (uint32_t base = 0; base < ntok; base += 64 * SPW) {
+    for (uint32_t base = 0; base < ntok; base += SHT) {
         const uint32_t t = base + tid;
         const uint32_t tk = t < ntok ? tb[t] : 0u;
         const uint32_t adv = t < ntok ? ((tk >> 9) == 0 ? 1u : (tk & 0x1FFu)) : 0u;
         const uint32_t incl = wave_incl_scan(adv);
-        if (lane == 63) Q.wsum[wave] = incl;
+        if (lane == 63) wsum[wave] = incl;
         __syncthreads();
         uint32_t wbase = 0, tot = 0;
 #pragma unroll
-        for (uint32_t w = 0; w < SPW; w++) {
-            const uint32_t x = Q.wsum[w];
+        for (uint32_t w = 0; w < SHT / 64; w++) {
+            const uint32_t x = wsum[w];
             if (w < wave) wbase += x;
             tot += x;
         }
@@ -1869,13 +1872,13 @@ __global__ __launch_bounds__(64 * SPW) void dmx_huff_split_kernel(const uint32_t
             c2 += st < B2;
             c3 += st < B3;
             if ((tk >> 9) == 0) {
-                atomicAdd(&Q.qh[q][tk], 1u);
+                atomicAdd(&qh[q][tk], 1u);
             } else {
                 uint32_t sy, eb, ev;
                 len_sym(tk & 0x1FFu, sy, eb, ev);
-                atomicAdd(&Q.qh[q][sy], 1u);
+                atomicAdd(&qh[q][sy], 1u);
                 dist_sym(tk >> 9, sy, eb, ev);
-                atomicAdd(&Q.qh[q][DMX_DIST0 + sy], 1u);
+                atomicAdd(&qh[q][DMX_DIST0 + sy], 1u);
             }
         }
         carry += tot;
@@ -1885,42 +1888,65 @@ __global__ __launch_bounds__(64 * SPW) void dmx_huff_split_kernel(const uint32_t
     c2 = wave_sum_u32(c2);
     c3 = wave_sum_u32(c3);
     if (lane == 0) {
-        atomicAdd(&Q.qt[1], c1);
-        atomicAdd(&Q.qt[2], c2);
-        atomicAdd(&Q.qt[3], c3);
+        atomicAdd(&qt[1], c1);
+        atomicAdd(&qt[2], c2);
+        atomicAdd(&qt[3], c3);
     }
     __syncthreads();
+    SplitScratch& o = sp[b];
+    for (uint32_t k = tid; k < 4 * DMX_HIST; k += SHT) (&o.qh[0][0])[k] = (&qh[0][0])[k];
+    if (tid < 5) o.qt[tid] = qt[tid];
+}
 
-    // one group per wave
-    {
-        K2LDS& S = K[wave];
-        const uint32_t i = c_gi[wave], j = c_gj[wave];
-        for (int s = (int)lane; s < 288; s += 64) {
-            uint32_t f = 0;
-            if (s == 256) f = 1;   // end of block
-            else if (s < 286)
-                for (uint32_t q = i; q <= j; q++) f += Q.qh[q][s];
-            S.fll[s] = f;
-        }
-        for (int s = (int)lane; s < 32; s += 64) {
-            uint32_t f = 0;
-            if (s < 30)
-                for (uint32_t q = i; q <= j; q++) f += Q.qh[q][DMX_DIST0 + s];
-            S.fd[s] = f;
-        }
-        wsync();
-        const HuffRes h = huff_block(S, bn, j == 3 ? final_bit : 0u, wave == SPW - 1, lane);
-        if (lane == 0) {
-            Q.gbt[wave] = h.bt;
-            Q.ghb[wave] = h.hbits;
-            Q.gbody[wave] = h.body;
-            Q.gcost[wave] = h.cost;
-            Q.gempty[wave] = Q.qt[j + 1] == Q.qt[i];
-        }
+__global__ __launch_bounds__(64) void dmx_split_plan_kernel(SplitScratch* __restrict__ sp,
+                                                            const dmx_blkinfo* __restrict__ info, uint32_t nblk,
+                                                            uint32_t flags) {
+    __shared__ K2LDS S;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t b = blockIdx.x / SPW, g = blockIdx.x % SPW;
+    SplitScratch& o = sp[b];
+    const uint32_t bn = info[b].n;
+    const uint32_t i = c_gi[g], j = c_gj[g];
+    const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1 && j == 3) ? 1u : 0u;
+    for (int s = (int)lane; s < 288; s += 64) {
+        uint32_t f = 0;
+        if (s == 256) f = 1;   // end of block
+        else if (s < 286)
+            for (uint32_t q = i; q <= j; q++) f += o.qh[q][s];
+        S.fll[s] = f;
     }
-    __syncthreads();
+    for (int s = (int)lane; s < 32; s += 64) {
+        uint32_t f = 0;
+        if (s < 30)
+            for (uint32_t q = i; q <= j; q++) f += o.qh[q][DMX_DIST0 + s];
+        S.fd[s] = f;
+    }
+    wsync();
+    const HuffRes h = huff_block(S, bn, final_bit, g == SPW - 1, lane);
+    for (int k = (int)lane; k < 316; k += 64) o.code[g][k] = S.code[k];
+    for (uint32_t k = lane; k < (h.hbits + 31) / 32; k += 64) o.hdr[g][k] = S.hdr[k];
+    if (lane == 0) {
+        SplitGroup r;
+        r.bt = h.bt;
+        r.hbits = h.hbits;
+        r.empty = o.qt[j + 1] == o.qt[i];
+        r.pad = 0;
+        r.body = h.body;
+        r.cost = h.cost;
+        o.g[g] = r;
+    }
+}
 
-    if (tid == 0) {   // cheapest cut mask: bit k = a cut after quarter k
+__global__ __launch_bounds__(64) void dmx_split_choose_kernel(const SplitScratch* __restrict__ sp,
+                                                              dmx_blkinfo* __restrict__ info,
+                                                              uint32_t* __restrict__ codes_g,
+                                                              uint32_t* __restrict__ hdr_g,
+                                                              dmx_subinfo* __restrict__ sub_g) {
+    __shared__ uint32_t sg[DMX_NSUB], nsub_s;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    const SplitScratch& o = sp[b];
+    if (lane == 0) {   // cheapest cut mask: bit k = a cut after quarter k
         int best = -1;
         uint64_t bestc = 0;
         for (uint32_t c = 0; c < 8; c++) {
@@ -1930,8 +1956,8 @@ __global__ __launch_bounds__(64 * SPW) void dmx_huff_split_kernel(const uint32_t
             for (uint32_t k = 0; k < 4; k++)
                 if (k == 3 || ((c >> k) & 1u)) {
                     const uint32_t g = grp_of(start, k);
-                    if (Q.gempty[g]) ok = false;
-                    tot += Q.gcost[g];
+                    if (o.g[g].empty) ok = false;
+                    tot += o.g[g].cost;
                     start = k + 1;
                 }
             if (!ok) continue;
@@ -1941,46 +1967,41 @@ __global__ __launch_bounds__(64 * SPW) void dmx_huff_split_kernel(const uint32_t
             }
         }
         uint32_t ns = 0, start = 0;
-        for (uint32_t k = 0; k < 4; k++)
-            if (k == 3 || (((uint32_t)best >> k) & 1u)) {
-                Q.sg[ns++] = grp_of(start, k);
-                start = k + 1;
-            }
-        Q.nsub = ns;
-    }
-    __syncthreads();
-
-    const uint32_t nsub = Q.nsub;
-    if (wave < nsub) {
-        const uint32_t s = wave, g = Q.sg[s];
-        const uint64_t slot = (uint64_t)b * DMX_NSUB + s;
-        uint32_t* cg = codes_g + slot * DMX_HIST;
-        for (int k = (int)lane; k < 316; k += 64) cg[k] = K[g].code[k];
-        uint32_t* hg = hdr_g + slot * DMX_HDR_WORDS;
-        for (uint32_t k = lane; k < (Q.ghb[g] + 31) / 32; k += 64) hg[k] = K[g].hdr[k];
-        if (lane == 0) {
-            dmx_subinfo si;
-            si.t0 = Q.qt[c_gi[g]];
-            si.t1 = Q.qt[c_gj[g] + 1];
-            si.btype = Q.gbt[g];
-            si.hdr_bits = Q.ghb[g];
-            si.body_bits = Q.gbody[g];
-            sub_g[slot] = si;
-        }
-    }
-    if (tid == 0) {
         uint32_t hb = 0, bt = 1;
         uint64_t body = 0;
-        for (uint32_t s = 0; s < nsub; s++) {
-            const uint32_t g = Q.sg[s];
-            hb += Q.ghb[g];
-            body += Q.gbody[g];
-            if (Q.gbt[g] == 2) bt = 2;
-        }
-        info[b].btype = nsub == 1 ? Q.gbt[Q.sg[0]] : bt;
+        for (uint32_t k = 0; k < 4; k++)
+            if (k == 3 || (((uint32_t)best >> k) & 1u)) {
+                const uint32_t g = grp_of(start, k);
+                sg[ns++] = g;
+                hb += o.g[g].hbits;
+                body += o.g[g].body;
+                if (o.g[g].bt == 2) bt = 2;
+                start = k + 1;
+            }
+        nsub_s = ns;
+        info[b].btype = ns == 1 ? o.g[sg[0]].bt : bt;
         info[b].hdr_bits = hb;
         info[b].body_bits = body;
-        info[b].nsub = nsub;
+        info[b].nsub = ns;
+    }
+    wsync();
+    const uint32_t nsub = nsub_s;
+    for (uint32_t s = 0; s < nsub; s++) {
+        const uint32_t g = sg[s];
+        const uint64_t slot = (uint64_t)b * DMX_NSUB + s;
+        uint32_t* cg = codes_g + slot * DMX_HIST;
+        for (int k = (int)lane; k < 316; k += 64) cg[k] = o.code[g][k];
+        uint32_t* hg = hdr_g + slot * DMX_HDR_WORDS;
+        for (uint32_t k = lane; k < (o.g[g].hbits + 31) / 32; k += 64) hg[k] = o.hdr[g][k];
+        if (lane == 0) {
+            dmx_subinfo si;
+            si.t0 = o.qt[c_gi[g]];
+            si.t1 = o.qt[c_gj[g] + 1];
+            si.btype = o.g[g].bt;
+            si.hdr_bits = o.g[g].hbits;
+            si.body_bits = o.g[g].body;
+            sub_g[slot] = si;
+        }
     }
 }
 
@@ -2315,6 +2336,8 @@ struct dmx_ctx {
     uint16_t* chs;        // DMX_F_DICT: (cap_chain) x DMX_BLK bucket-sorted positions per block (+ the dict)
     uint16_t* che;        // DMX_F_DICT: (cap_chain) x DMX_NBUCKET bucket ends
     uint64_t cap_chain;
+    void* split;          // DMX_F_SPLIT: cap_split x SplitScratch (per-block plans of the 10 groups)
+    uint64_t cap_split;
     // timing: a ring of event sets so timed encodes never block the host
     int timing;
     hipEvent_t ev[DMX_EV_RING][6];
@@ -2413,6 +2436,7 @@ extern "C" void dmx_ctx_destroy(dmx_ctx* c) {
     if (c->d_dict) (void)hipFree(c->d_dict);
     if (c->chs) (void)hipFree(c->chs);
     if (c->che) (void)hipFree(c->che);
+    if (c->split) (void)hipFree(c->split);
     for (int j = 0; j < DMX_EV_RING; j++)
         for (int k = 0; k < 6; k++) if (c->ev[j][k]) (void)hipEventDestroy(c->ev[j][k]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -2451,6 +2475,13 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
     if (nblk64 > c->cap_blocks || nblk64 > 0x7FFFFFFFull) return -(int)E_SZ;
     const uint32_t nblk = (uint32_t)nblk64;
     HIPCHK(hipSetDevice(c->device));
+    if ((o.flags & DMX_F_SPLIT) && c->cap_split < c->cap_blocks) {   // split plan scratch, on first use
+        if (c->split) (void)hipFree(c->split);
+        c->split = NULL;
+        c->cap_split = 0;
+        HIPCHK(hipMalloc(&c->split, c->cap_blocks * sizeof(SplitScratch)));
+        c->cap_split = c->cap_blocks;
+    }
     if ((o.flags & DMX_F_DICT) && c->cap_chain < c->cap_blocks + 1) {   // chain export buffers, on first use
         if (c->chs) (void)hipFree(c->chs);
         if (c->che) (void)hipFree(c->che);
@@ -2499,8 +2530,14 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                                (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg);
         if (ev) (void)hipEventRecord(ev[2], s);
         if (o.flags & DMX_F_SPLIT)
-            hipLaunchKernelGGL(dmx_huff_split_kernel, dim3(nblk), dim3(64 * SPW), 0, s, c->tok, c->info, c->codes, c->hdr,
-                               c->sub, nblk, o.flags);
+            {
+                hipLaunchKernelGGL(dmx_split_hist_kernel, dim3(nblk), dim3(SHT), 0, s, c->tok, c->info,
+                                   (SplitScratch*)c->split);
+                hipLaunchKernelGGL(dmx_split_plan_kernel, dim3(nblk * SPW), dim3(64), 0, s, (SplitScratch*)c->split,
+                                   c->info, nblk, o.flags);
+                hipLaunchKernelGGL(dmx_split_choose_kernel, dim3(nblk), dim3(64), 0, s, (const SplitScratch*)c->split,
+                                   c->info, c->codes, c->hdr, c->sub);
+            }
         else
             hipLaunchKernelGGL(dmx_huff_kernel, dim3(nblk), dim3(64), 0, s, c->hist, c->info, c->codes, c->hdr, c->sub,
                                nblk, o.flags);
