@@ -85,6 +85,12 @@ def cpu_baseline(data, budget_s: float):
 
 
 def main() -> int:
+    # The contract is ONE JSON line on stdout.  Libraries print there too (RCCL's version
+    # banner at communicator creation), so fd 1 points at stderr for the whole run and the
+    # JSON line is written to the saved original.
+    json_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -102,7 +108,12 @@ def main() -> int:
                          "the block before each shard inside the step")
     ap.add_argument("--exhaustive-steps", type=int, default=3,
                     help="also time this many exhaustive-parse steps (reported under 'exhaustive')")
-    ap.add_argument("--gather", default="root", choices=["root", "all", "none"])
+    ap.add_argument("--gather", default="root", choices=["root", "root-sync", "all", "none"],
+                    help="N > 1: root = chunks to rank 0 point-to-point, pipelined (the gather of step i-1 "
+                         "overlaps the encode of step i, double-buffered); root-sync = the same, step by step; "
+                         "all = max-padded all_gather; none = encode only")
+    ap.add_argument("--pipeline-test", type=int, default=0,
+                    help="run the pipelined gather loop at N = 1 too (single-rank process group; tests the path)")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds per CPU baseline leg (0 = skip)")
     ap.add_argument("--traffic-csv", default="",
                     help="comma-separated rocprofv3 counter CSVs / dirs (FETCH_SIZE and WRITE_SIZE passes)")
@@ -117,9 +128,12 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    use_pg = world > 1 or bool(args.pipeline_test)
+    if use_pg:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), rank=rank, world_size=world)
     else:
         torch.cuda.set_device(0)
     dev = torch.device(f"cuda:{local}")
@@ -153,18 +167,67 @@ def main() -> int:
     lens = S.shard_lengths(n, dev) if (world > 1 and args.dict) else None
     halo = [None]
 
-    def step():
+    def halo_exchange():
         if lens is not None:   # f1 across shards: the block before this shard, from the previous rank
             halo[0] = S.exchange_history(d_in, n, lens=lens, out=halo[0])
             enc.opts.dict, enc.opts.dict_len = (halo[0].data_ptr(), halo[0].numel()) if halo[0] is not None \
                 else (None, 0)
+
+    def step():
+        halo_exchange()
         enc.encode_async(d_in.data_ptr(), n, d_out.data_ptr(), cap, stream)
         if world > 1 and args.gather != "none":
             r = enc.result(stream)   # chunk length (device -> host) before the exchange
-            S.gather_chunks(d_out, int(r.out_len), root=0 if args.gather == "root" else None)
+            S.gather_chunks(d_out, int(r.out_len), root=None if args.gather == "all" else 0)
+
+    # Pipelined gather (N > 1, --gather root): step i encodes into buffer i % 2 on the compute
+    # stream while the chunk of step i - 1 goes to rank 0 on a comm stream.  The chunk length
+    # comes back through an asynchronous 64 B copy into pinned memory; the compute stream
+    # waits for the gather that last used a buffer before encoding into it again.
+    pipelined = use_pg and args.gather == "root"
+    if pipelined:
+        d_outs = [d_out, torch.empty_like(d_out)]
+        res_h = [torch.zeros(64, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+        enc_done = [torch.cuda.Event(), torch.cuda.Event()]
+        gat_done = [None, None]
+        comm = torch.cuda.Stream(device=dev)
+        cur = torch.cuda.current_stream(dev)
+
+        def p_encode(i):
+            k = i % 2
+            if gat_done[k] is not None:
+                cur.wait_event(gat_done[k])
+            halo_exchange()
+            enc.encode_async(d_in.data_ptr(), n, d_outs[k].data_ptr(), cap, stream)
+            enc.result_async(res_h[k].data_ptr(), stream)
+            enc_done[k].record(cur)
+
+        def p_gather(i):
+            k = i % 2
+            enc_done[k].synchronize()
+            ln = int(np.frombuffer(res_h[k].numpy()[:8].tobytes(), dtype=np.uint64)[0])
+            with torch.cuda.stream(comm):
+                comm.wait_event(enc_done[k])
+                S.gather_chunks(d_outs[k], ln, root=0)
+                ev = torch.cuda.Event()
+                ev.record(comm)
+                gat_done[k] = ev
+
+        def run(steps):
+            for i in range(steps):
+                p_encode(i)
+                if i >= 1:
+                    p_gather(i - 1)
+            if steps:
+                p_gather(steps - 1)
+    else:
+        def run(steps):
+            for _ in range(steps):
+                step()
 
     # correctness of the measured configuration (outside the timed region)
-    step()
+    run(1)
+    torch.cuda.synchronize(dev)
     res = enc.result(stream)
     out_len = int(res.out_len)
     ok = True
@@ -213,8 +276,7 @@ def main() -> int:
                                "stream: one wave decodes the whole zlib stream (dict blocks chain)",
                        "kernel": "dmx_inflate_index_kernel" if indexed else "dmx_inflate_stream_kernel"}
     del dec
-    for _ in range(args.warmup):
-        step()
+    run(args.warmup)
     torch.cuda.synchronize(dev)
 
     enc.set_timing(True)
@@ -222,8 +284,7 @@ def main() -> int:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    run(args.steps)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -303,7 +364,8 @@ def main() -> int:
                 "parse": ("exhaustive (reference semantics)" if args.max_chain == 0 else f"max_chain={args.max_chain}")
                          + (", lazy" if args.lazy else ", greedy") + (", split" if args.split else "")
                          + (", dict" if args.dict else ""),
-                "parallelism": f"blocks sharded over {world} GPU(s)" + (f", gather={args.gather}" if world > 1 else ""),
+                "parallelism": f"blocks sharded over {world} GPU(s)" + (f", gather={args.gather}" if world > 1 else "")
+                               + (", pipelined" if pipelined else ""),
             },
             "ratio": round(out_len / n, 5),
             "size_vs_ref_pct": size_pct,
@@ -332,9 +394,10 @@ def main() -> int:
         }
         if base:
             line["gpu_over_cpu"] = round(value / base["value"], 1) if base["value"] else None
-        print(json.dumps(line), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
     enc.close()
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
     return 0 if ok else 1
 

@@ -105,6 +105,7 @@ def lib() -> ctypes.CDLL:
         "dmx_max_compressed": ([u64, i32], u64),
         "dmx_encode_async": ([vp, vp, u64, vp, u64, ctypes.POINTER(Opts), vp], ctypes.c_int),
         "dmx_encode_result": ([vp, ctypes.POINTER(Result), vp], ctypes.c_int),
+        "dmx_encode_result_async": ([vp, vp, vp], ctypes.c_int),
         "dmx_encode_host": ([vp, u64, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(Opts)], ctypes.c_int),
         "dmx_last_blocks": ([vp, u32p, u8p, u32p, u32], ctypes.c_int),
         "dmx_last_tokens": ([vp, u32, u32p, u32], ctypes.c_int),
@@ -274,6 +275,12 @@ class Encoder:
         if r.status:
             raise DeflateError(r.status, "encode")
         return r
+
+    def result_async(self, host_ptr: int, stream: int | None = None) -> None:
+        """Enqueue the D2H copy of the last encode's 64 B dmx_result into host_ptr (pinned
+        memory, e.g. a pin_memory uint8 tensor); read it after the stream or an event."""
+        _check(self._L.dmx_encode_result_async(self._ctx, ctypes.c_void_p(host_ptr), ctypes.c_void_p(stream or 0)),
+               "dmx_encode_result_async")
 
     # -- introspection of the last encode (tests / stats) --
     def blocks(self, nblk: int):

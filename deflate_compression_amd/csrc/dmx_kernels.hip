@@ -2560,6 +2560,14 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
     return 0;
 }
 
+extern "C" int dmx_encode_result_async(dmx_ctx* c, dmx_result* r, void* stream) {
+    if (!c || !r) return -(int)E_INVAL;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(hipMemcpyAsync(r, c->res, sizeof(dmx_result), hipMemcpyDeviceToHost, s));
+    return 0;
+}
+
 extern "C" int dmx_encode_result(dmx_ctx* c, dmx_result* r, void* stream) {
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;

@@ -171,6 +171,11 @@ int dmx_encode_async(dmx_ctx* ctx, const void* d_in, uint64_t n, void* d_out, ui
                      const dmx_opts* opts, void* stream);
 /* Wait for the last encode on `stream` and copy its dmx_result to the host. */
 int dmx_encode_result(dmx_ctx* ctx, dmx_result* r, void* stream);
+/* Enqueue the copy of the last encode's dmx_result into r (pinned host memory for a truly
+ * asynchronous copy) on `stream`, without waiting: the caller waits on the stream or on an
+ * event recorded after this call.  Lets a pipeline (bench.py, N > 1) learn chunk i's length
+ * while encode i + 1 runs. */
+int dmx_encode_result_async(dmx_ctx* ctx, dmx_result* r, void* stream);
 
 /* Host-buffer convenience (H2D, encode, D2H) on a cached per-device context.
  * *out_len receives the stream length; out must hold dmx_max_compressed(n, sw). */
