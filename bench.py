@@ -84,6 +84,48 @@ def cpu_baseline(data, budget_s: float):
     return out
 
 
+def end_to_end(host, args):
+    """The drop-in fd API end to end (file-in/file-out): read(fd_in), H2D, encode,
+    D2H, write(fd_out), with the bench's parse settings; best of 3 (the first call also
+    creates the cached device context).  PCIe-inclusive, so never the headline value."""
+    import tempfile
+    import deflate_compression_amd as D
+    env = {"DMX_MAX_CHAIN": str(args.max_chain), "DMX_LAZY": str(args.lazy), "DMX_SPLIT": str(args.split),
+           "DMX_DICT": str(args.dict)}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    td = tempfile.mkdtemp(dir="/tmp")
+    fi, fo = os.path.join(td, "in"), os.path.join(td, "out")
+    try:
+        host.tofile(fi)
+        best, rc = None, 0
+        for _ in range(3):
+            a = os.open(fi, os.O_RDONLY)
+            b = os.open(fo, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+            t0 = time.perf_counter()
+            rc = D.deflate_compress(a, b, -1, 32768, 0)
+            t1 = time.perf_counter()
+            os.close(a)
+            os.close(b)
+            best = t1 - t0 if best is None else min(best, t1 - t0)
+        with open(fo, "rb") as f:
+            z = f.read()
+        ok = rc == 0 and zlib.decompress(z) == host.tobytes()
+        return {"value": round(host.size / best / 1e9, 3), "unit": "GB/s", "ms": round(best * 1e3, 2), "rc": rc,
+                "compressed_bytes": len(z), "inflates": ok,
+                "path": "deflate_compress(fd_in, fd_out): read + H2D + encode + D2H + write, best of 3"}
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        for x in (fi, fo):
+            if os.path.exists(x):
+                os.remove(x)
+        os.rmdir(td)
+
+
 def main() -> int:
     # The contract is ONE JSON line on stdout.  Libraries print there too (RCCL's version
     # banner at communicator creation), so fd 1 points at stderr for the whole run and the
@@ -337,8 +379,14 @@ def main() -> int:
             except Exception as e:  # pragma: no cover
                 log("traffic csv unreadable:", e)
         cpu = {}
+        e2e = zl6 = None
         if world == 1 and args.cpu_budget > 0:
             cpu = cpu_baseline(host, args.cpu_budget)
+            try:
+                e2e = end_to_end(host, args)
+            except Exception as e:  # pragma: no cover
+                log("end-to-end fd API leg failed:", e)
+            zl6 = len(zlib.compress(host.tobytes(), 6))   # context: zlib -6 on the same input
         base = cpu.get("reference") or cpu.get("port")
         size_pct = s_ref_bytes = None
         if "s_ref" in cpu and cpu["s_ref"][0] == n:
@@ -388,6 +436,9 @@ def main() -> int:
                 "launch_ms": round(dom_ms, 4),
                 "launches_timed": nstage,
             },
+            "end_to_end_fd_api": e2e,
+            "zlib6": None if zl6 is None else {"ratio": round(zl6 / n, 5), "compressed_bytes": zl6,
+                                                 "ours_vs_zlib6_pct": round((out_len / zl6 - 1) * 100, 3)},
             "cpu_baseline": base,
             "cpu_baseline_port": cpu.get("port") if base is not cpu.get("port") else None,
             "host": {"cpu": platform.processor() or platform.machine(), "nproc": os.cpu_count()},

@@ -2744,6 +2744,157 @@ extern "C" int dmx_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint
     return r;
 }
 
+// --- streaming file-in/file-out (the fd API without per-token stats) ---
+// The input is read in chunks of `chunk` bytes (a multiple of sw) straight into pinned
+// buffers; chunk i is copied to the device and encoded while the host writes chunk i-1's
+// stream and reads chunk i+1.  Every chunk is a shard of one zlib stream (DESIGN.md §6
+// framing): the header on the first, a sync flush after every chunk that is not known to
+// be the last (a one-byte lookahead tells), BFINAL on the last, and the Adler-32 combined
+// on the host.  With
+// DMX_F_DICT the previous chunk's last sw bytes are the history of each chunk's first block,
+// so the parse equals the one-shot parse.  One chunk: byte-identical to dmx_encode_host.
+#include <unistd.h>
+#include <errno.h>
+static int64_t read_full(int fd, uint8_t* b, uint64_t cap) {
+    uint64_t len = 0;
+    while (len < cap) {
+        const ssize_t r = read(fd, b + len, cap - len);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            return -(int64_t)E_NEXIST;
+        }
+        if (r == 0) break;
+        len += (uint64_t)r;
+    }
+    return (int64_t)len;
+}
+// One chunk with a one-byte lookahead, so a chunk that ends exactly at EOF is known to be
+// the last before it is encoded (then a stream of one chunk is byte-identical to the
+// one-shot stream).  *carry: the lookahead byte of the previous call (-1: none); *eof: no
+// byte follows this chunk.
+static int64_t read_chunk(int fd, uint8_t* b, uint64_t chunk, int* carry, bool* eof) {
+    uint64_t off = 0;
+    if (*carry >= 0) b[off++] = (uint8_t)*carry;
+    const int64_t r = read_full(fd, b + off, chunk - off);
+    if (r < 0) return r;
+    const uint64_t len = off + (uint64_t)r;
+    *carry = -1;
+    *eof = true;
+    if (len == chunk) {
+        uint8_t nb;
+        const int64_t q = read_full(fd, &nb, 1);
+        if (q < 0) return q;
+        if (q == 1) {
+            *carry = nb;
+            *eof = false;
+        }
+    }
+    return (int64_t)len;
+}
+static int write_full(int fd, const uint8_t* p, uint64_t n) {
+    while (n) {
+        const ssize_t w = write(fd, p, n);
+        if (w < 0) {
+            if (errno == EINTR) continue;
+            return -(int)E_PIPE;
+        }
+        p += w;
+        n -= (uint64_t)w;
+    }
+    return 0;
+}
+
+extern "C" int dmx_encode_fd(int fd_in, int fd_out, const dmx_opts* opts, uint64_t chunk) {
+    dmx_opts o = {0, 0, DMX_ZLIB, 0, NULL, 0};
+    if (opts) o = *opts;
+    if (o.sw == 0) o.sw = DMX_BLK;
+    if (o.sw < 1 || o.sw > DMX_BLK) return -(int)E_RANGE;
+    const uint64_t sw = (uint64_t)o.sw;
+    if (chunk < sw) chunk = sw;
+    chunk -= chunk % sw;
+    const uint32_t pflags = o.flags & (DMX_F_LAZY | DMX_F_SPLIT | DMX_F_DICT | DMX_F_EXACT_SORT);
+    const char* dev_s = getenv("DMX_DEVICE");
+    pthread_mutex_lock(&g_mu);
+    int err = 0;
+    dmx_ctx* c = dmx_cached_ctx(dev_s ? atoi(dev_s) : 0, chunk, &err);
+    int r = err;
+    uint8_t* hin[2] = {NULL, NULL};
+    uint8_t* hout = NULL;
+    dmx_result* hres = NULL;
+    void* din[2] = {NULL, NULL};
+    void* dout = NULL;
+    const uint64_t ocap = dmx_max_compressed(chunk, o.sw);
+    if (!r) r = ctx_reserve(c, chunk / sw);
+    if (!r && hip_fail(hipSetDevice(c->device), "hipSetDevice")) r = -(int)E_DEVICE;
+    for (int k = 0; !r && k < 2; k++) {
+        if (hip_fail(hipHostMalloc((void**)&hin[k], chunk + 16, 0), "hipHostMalloc")) r = -(int)E_MALLOC;
+        else if (hip_fail(hipMalloc(&din[k], chunk + 16), "hipMalloc")) r = -(int)E_DEVICE;
+    }
+    if (!r && hip_fail(hipHostMalloc((void**)&hout, ocap, 0), "hipHostMalloc")) r = -(int)E_MALLOC;
+    if (!r && hip_fail(hipHostMalloc((void**)&hres, sizeof(dmx_result), 0), "hipHostMalloc")) r = -(int)E_MALLOC;
+    if (!r && hip_fail(hipMalloc(&dout, ocap), "hipMalloc")) r = -(int)E_DEVICE;
+    hipStream_t s = c ? c->stream : NULL;
+    int64_t len = 0;
+    int carry = -1;
+    bool eof = true;
+    if (!r) {
+        len = read_chunk(fd_in, hin[0], chunk, &carry, &eof);
+        if (len < 0) r = (int)len;
+    }
+    uint32_t adler = 1;
+    uint64_t total = 0;
+    for (uint64_t i = 0; !r; i++) {
+        const int cur = (int)(i & 1);
+        const bool last = eof;
+        dmx_opts oc = o;
+        oc.flags = pflags | (i == 0 ? DMX_F_HEADER : 0u) | (last ? DMX_F_FINAL : 0u);
+        oc.dict = NULL;
+        oc.dict_len = 0;
+        if ((pflags & DMX_F_DICT) && i > 0) {      // the previous chunk's tail (still on the device)
+            oc.dict = (const uint8_t*)din[cur ^ 1] + (chunk - sw);
+            oc.dict_len = sw;
+        }
+        if (len && hip_fail(hipMemcpyAsync(din[cur], hin[cur], (size_t)len, hipMemcpyHostToDevice, s), "H2D"))
+            r = -(int)E_DEVICE;
+        if (!r) r = dmx_encode_async(c, din[cur], (uint64_t)len, dout, ocap, &oc, s);
+        if (!r) r = dmx_encode_result_async(c, hres, s);
+        int64_t nlen = 0;
+        if (!r && !last) {   // the next chunk, read while the device encodes this one
+            nlen = read_chunk(fd_in, hin[cur ^ 1], chunk, &carry, &eof);
+            if (nlen < 0) r = (int)nlen;
+        }
+        if (!r && hip_fail(hipStreamSynchronize(s), "hipStreamSynchronize")) r = -(int)E_DEVICE;
+        if (!r && hres->status) r = hres->status;
+        if (!r && hip_fail(hipMemcpy(hout, dout, hres->out_len, hipMemcpyDeviceToHost), "D2H")) r = -(int)E_DEVICE;
+        if (!r && fd_out >= 0) r = write_full(fd_out, hout, hres->out_len);
+        if (!r) {
+            adler = dmx_adler32_combine(adler, hres->adler, (uint64_t)len);
+            total += (uint64_t)len;
+        }
+        if (last) break;
+        len = nlen;
+    }
+    if (!r && fd_out >= 0) {
+        uint8_t tail[6];
+        int nt = 0;
+        tail[nt++] = (uint8_t)(adler >> 24);
+        tail[nt++] = (uint8_t)(adler >> 16);
+        tail[nt++] = (uint8_t)(adler >> 8);
+        tail[nt++] = (uint8_t)adler;
+        r = write_full(fd_out, tail, (uint64_t)nt);
+    }
+    (void)total;
+    for (int k = 0; k < 2; k++) {
+        if (hin[k]) (void)hipHostFree(hin[k]);
+        if (din[k]) (void)hipFree(din[k]);
+    }
+    if (hout) (void)hipHostFree(hout);
+    if (hres) (void)hipHostFree(hres);
+    if (dout) (void)hipFree(dout);
+    pthread_mutex_unlock(&g_mu);
+    return r;
+}
+
 // Per-block match-kernel phase stamps of the last encode (DMX_STAMPS=1): for each block
 // {cycles to build the chains (wave 0), cycles until the last wave finished searching,
 //  cycles of walk + compaction, tokens}.  Diagnostic only.

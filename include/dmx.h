@@ -182,6 +182,14 @@ int dmx_encode_result_async(dmx_ctx* ctx, dmx_result* r, void* stream);
 int dmx_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t out_cap,
                     uint64_t* out_len, const dmx_opts* opts);
 
+/* Streaming file-in/file-out encode (deflate_compress without fd_stats): reads fd_in in
+ * chunks of `chunk` bytes (rounded down to a multiple of sw; 0 = sw) into pinned memory,
+ * encodes chunk i on the device while reading chunk i+1, writes one zlib stream to fd_out
+ * (chunks joined by sync flushes, Adler-32 combined on the host; DMX_F_DICT carries the
+ * history across chunks).  opts->flags: the parse/block options (DMX_F_LAZY, _SPLIT, _DICT);
+ * the framing is its own.  Returns 0 or -E_*. */
+int dmx_encode_fd(int fd_in, int fd_out, const dmx_opts* opts, uint64_t chunk);
+
 /* ---- GPU inflate, csrc/dmx_inflate_dev.hip ---- */
 /* One entry per independently decodable DEFLATE block: start bit in the stream, output
  * offset and length.  Blocks of a dmx stream never reference earlier blocks. */

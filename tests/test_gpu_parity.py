@@ -288,3 +288,36 @@ def test_run_dominated_blocks(enc, k, lazy):
         data = _run_heavy(11)[:50000]
         z, _ = enc.compress_bytes(data, sw=sw, max_chain=k, flags=D.DMX_ZLIB | (D.DMX_F_LAZY if lazy else 0))
         assert z == O.compress(data, sw=sw, max_chain=k, lazy=lazy), sw
+
+
+@pytest.mark.parametrize("n", [0, 1, 100000, 1 << 20, (1 << 20) + 1, 3 << 20, (3 << 20) + 777])
+@pytest.mark.parametrize("mode", ["exhaustive", "k8_lazy", "k8_lazy_dict"])
+def test_fd_api_streaming_chunks(tmp_path, n, mode):
+    """deflate_compress without fd_stats streams the file in chunks (DMX_CHUNK_MB) through
+    pinned buffers: one chunk is byte-identical to the one-shot stream; several chunks form
+    one zlib stream (sync flushes, host Adler-32 combine; a one-byte lookahead makes an input
+    that ends on a chunk boundary one chunk); with DMX_F_DICT the parse equals the one-shot one."""
+    import os
+    text = D.gen_text(max(n, 1), 31).tobytes()[:n]
+    fi, fo = tmp_path / "in", tmp_path / "out"
+    fi.write_bytes(text)
+    env = {"DMX_CHUNK_MB": "1", "DMX_MAX_CHAIN": "0" if mode == "exhaustive" else "8",
+           "DMX_LAZY": "0" if mode == "exhaustive" else "1", "DMX_DICT": "1" if "dict" in mode else "0"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        with open(fi, "rb") as a, open(fo, "wb") as b:
+            assert D.deflate_compress(a.fileno(), b.fileno(), -1, 32768, 0) == 0
+    finally:
+        for k, v in old.items():
+            os.environ.pop(k, None) if v is None else os.environ.__setitem__(k, v)
+    z = fo.read_bytes()
+    assert zlib.decompress(z) == text
+    assert D.deflate_decompress(z) == text
+    kw = dict(max_chain=0 if mode == "exhaustive" else 8, lazy=mode != "exhaustive", dict="dict" in mode)
+    if n <= 1 << 20:
+        assert z == O.compress(text, **kw)
+    else:   # the parse is the one-shot parse: the chunks' tokens equal the oracle's blocks
+        one = O.compress(text, **kw)
+        nchunks = (n + (1 << 20) - 1) >> 20
+        assert abs(len(z) - len(one)) <= 8 * nchunks
