@@ -91,7 +91,7 @@ def end_to_end(host, args):
     import tempfile
     import deflate_compression_amd as D
     env = {"DMX_MAX_CHAIN": str(args.max_chain), "DMX_LAZY": str(args.lazy), "DMX_SPLIT": str(args.split),
-           "DMX_DICT": str(args.dict)}
+           "DMX_DICT": str(args.dict), "DMX_STORE_CHECK": str(args.store_check)}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     td = tempfile.mkdtemp(dir="/tmp")
@@ -145,6 +145,8 @@ def main() -> int:
                     help="1 = lazy evaluation parse (DMX_F_LAZY, SURVEY §8 f2)")
     ap.add_argument("--split", type=int, default=int(os.environ.get("DMX_SPLIT", "0")),
                     help="1 = adaptive block splitting (DMX_F_SPLIT, SURVEY §8 f3)")
+    ap.add_argument("--store-check", type=int, default=int(os.environ.get("DMX_STORE_CHECK", "1")),
+                    help="1 = noise blocks stored without a parse (DMX_F_STORE_CHECK, DESIGN.md §4.7)")
     ap.add_argument("--dict", type=int, default=int(os.environ.get("DMX_DICT", "0")),
                     help="1 = cross-block dictionary (DMX_F_DICT, SURVEY §8 f1); N > 1: halo exchange of "
                          "the block before each shard inside the step")
@@ -200,6 +202,8 @@ def main() -> int:
         flags |= D.DMX_F_SPLIT
     if args.dict:
         flags |= D.DMX_F_DICT
+    if args.store_check:
+        flags |= D.DMX_F_STORE_CHECK
     enc = D.Encoder(local, n, 32768, args.max_chain, flags)
     d_in = torch.from_numpy(host).to(dev)
     cap = D.max_compressed(n)
@@ -337,7 +341,7 @@ def main() -> int:
     exh = None
     if world == 1 and args.max_chain != 0 and args.exhaustive_steps > 0:
         # the reference's own parse (every earlier position of the bucket), same input
-        ex = D.Encoder(local, n, 32768, 0, flags & ~(D.DMX_F_LAZY | D.DMX_F_DICT | D.DMX_F_SPLIT))
+        ex = D.Encoder(local, n, 32768, 0, flags & ~(D.DMX_F_LAZY | D.DMX_F_DICT | D.DMX_F_SPLIT | D.DMX_F_STORE_CHECK))
         ex.encode_async(d_in.data_ptr(), n, d_out.data_ptr(), cap, stream)
         ex_len = int(ex.result(stream).out_len)
         torch.cuda.synchronize(dev)
@@ -363,7 +367,7 @@ def main() -> int:
         ms_step = dt / args.steps * 1e3
         value = tot_in * args.steps / dt / 1e9
         dom = max((k for k in stage_ms if k != "total"), key=stage_ms.get)
-        kname = {"dict": "dmx_hist_kernel", "huff": "dmx_split_plan_kernel" if args.split else "dmx_huff_kernel"}.get(
+        kname = {"pre": "dmx_hist_kernel" if args.dict else "dmx_store_check_kernel", "huff": "dmx_split_plan_kernel" if args.split else "dmx_huff_kernel"}.get(
             dom, f"dmx_{dom}_kernel")
         dom_ms = stage_ms[dom]
         algo_bytes = n + out_len   # per launch on this rank: input read + stream written
@@ -411,7 +415,7 @@ def main() -> int:
                 "block": 32768,
                 "parse": ("exhaustive (reference semantics)" if args.max_chain == 0 else f"max_chain={args.max_chain}")
                          + (", lazy" if args.lazy else ", greedy") + (", split" if args.split else "")
-                         + (", dict" if args.dict else ""),
+                         + (", dict" if args.dict else "") + (", store-check" if args.store_check else ""),
                 "parallelism": f"blocks sharded over {world} GPU(s)" + (f", gather={args.gather}" if world > 1 else "")
                                + (", pipelined" if pipelined else ""),
             },

@@ -23,7 +23,7 @@ import struct
 __all__ = [
     "DeflateError", "Opts", "Result", "Encoder", "lib", "compress", "deflate_compress",
     "deflate_decompress", "max_compressed", "adler32_combine", "gen_text", "gen_random",
-    "COMPRESS_STATS", "E", "DMX_F_HEADER", "DMX_F_TRAILER", "DMX_F_FINAL", "DMX_ZLIB", "DMX_F_LAZY", "DMX_F_EXACT_SORT", "DMX_F_SPLIT", "inflate_gpu",
+    "COMPRESS_STATS", "E", "DMX_F_HEADER", "DMX_F_TRAILER", "DMX_F_FINAL", "DMX_ZLIB", "DMX_F_LAZY", "DMX_F_EXACT_SORT", "DMX_F_SPLIT", "DMX_F_DICT", "DMX_F_STORE_CHECK", "inflate_gpu",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -37,6 +37,7 @@ DMX_F_LAZY = 8
 DMX_F_EXACT_SORT = 16
 DMX_F_SPLIT = 32
 DMX_F_DICT = 64
+DMX_F_STORE_CHECK = 128
 _M = 1 << 24
 # global_errors.h:64-75 and deflate_errors.h:134-147
 E = {
@@ -152,17 +153,18 @@ def max_compressed(n: int, sw: int = 32768) -> int:
 
 
 def compress(data, sw: int = 32768, max_chain: int = 0, flags: int = DMX_ZLIB, lazy: bool = False,
-             split: bool = False, dict: bool = False, pre=None) -> bytes:
+             split: bool = False, dict: bool = False, pre=None, store_check: bool = False) -> bytes:
     """Encode a host buffer on the GPU; returns the zlib stream (or raw DEFLATE with flags).
     lazy = f2 lazy parse (DMX_F_LAZY), split = f3 adaptive block splitting (DMX_F_SPLIT),
-    dict = f1 cross-block dictionary (DMX_F_DICT; pre = the bytes before `data`)."""
+    dict = f1 cross-block dictionary (DMX_F_DICT; pre = the bytes before `data`),
+    store_check = noise blocks stored without a parse (DMX_F_STORE_CHECK)."""
     L = lib()
     p, n, keep = _buf(data)
     cap = max_compressed(n, sw)
     out = ctypes.create_string_buffer(cap)
     olen = ctypes.c_uint64(0)
     o = Opts(sw, max_chain, flags | (DMX_F_LAZY if lazy else 0) | (DMX_F_SPLIT if split else 0) |
-             (DMX_F_DICT if dict else 0), 0)
+             (DMX_F_DICT if dict else 0) | (DMX_F_STORE_CHECK if store_check else 0), 0)
     pk = None
     if dict and pre is not None and len(pre):
         pk = ctypes.create_string_buffer(bytes(pre), len(pre))
@@ -362,7 +364,7 @@ class Encoder:
         ms = (ctypes.c_double * 6)()
         cnt = ctypes.c_uint32(0)
         self._L.dmx_ctx_stage_times(self._ctx, ms, ctypes.byref(cnt))
-        return {k: v for k, v in zip(["dict", "match", "huff", "scan", "pack", "total"], list(ms))}, cnt.value
+        return {k: v for k, v in zip(["pre", "match", "huff", "scan", "pack", "total"], list(ms))}, cnt.value
 
     # -- host convenience on this context via torch tensors --
     def compress_tensor(self, t_in, stream=None, opts: Opts | None = None):

@@ -169,6 +169,9 @@ int deflate_compress(int fd_in, int fd_out, int fd_stats, swi sw, int ops) {
     if (sp && atoi(sp) > 0) o.flags |= DMX_F_SPLIT;
     const char* dc = getenv("DMX_DICT");   /* 1 = cross-block dictionary (DMX_F_DICT) */
     if (dc && atoi(dc) > 0) o.flags |= DMX_F_DICT;
+    const char* sc = getenv("DMX_STORE_CHECK");   /* 1 = noise blocks stored unparsed (§4.7);
+                                                   * not with fd_stats: such blocks have no tokens */
+    if (sc && atoi(sc) > 0 && fd_stats < 0) o.flags |= DMX_F_STORE_CHECK;
     o.reserved = 0;
     o.dict = NULL;
     o.dict_len = 0;

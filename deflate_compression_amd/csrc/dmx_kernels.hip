@@ -1026,6 +1026,171 @@ __global__ __launch_bounds__(MT) void dmx_hist_kernel(const uint8_t* __restrict_
     }
 }
 
+// K0 (DMX_F_STORE_CHECK): the noise check of every block, so that noise
+// blocks skip the parse and go out stored.  One 256-thread workgroup per block.
+//   pass 1: stream the block from HBM once (16 B per thread and step): the 8 bit-plane
+//           counts (v_bcnt on masked words, registers only) and the Adler-32 partial sums.
+//           Text, runs and 7-bit data fail the bit-plane test here and leave.
+//   pass 2 (noise-like blocks only; the re-read hits L2): byte histogram and 18-bit
+//           4-gram presence bitmap in LDS (33 KB, several workgroups per CU).
+// A block that passes gets its whole record here (stored, no tokens); the match kernel then
+// skips it and the Huffman kernels leave it alone.  Same integer rule as
+// dmx_oracle_store_check.
+#define SCT 256
+__device__ __forceinline__ void sc_load(const uint8_t* d, uint32_t p, uint32_t bn, bool aligned16, uint32_t w[5]) {
+    if (aligned16 && p + 20 <= bn) {
+        const uint4 v = *reinterpret_cast<const uint4*>(d + p);
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        w[4] = *reinterpret_cast<const uint32_t*>(d + p + 16);
+    } else {   // block tail (or unaligned input): bytes past bn read as 0
+#pragma unroll
+        for (int j = 0; j < 5; j++) w[j] = 0;
+        for (uint32_t j = 0; j < 20; j++)
+            if (p + j < bn) w[j >> 2] |= (uint32_t)d[p + j] << (8 * (j & 3));
+    }
+}
+
+__global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
+                                                              dmx_blkinfo* __restrict__ info) {
+    __shared__ uint32_t bm[1u << 13];
+    __shared__ uint32_t hist[256];
+    __shared__ uint64_t red[10][SCT / 64];
+    __shared__ uint32_t pass_s;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t b = blockIdx.x;
+    const uint64_t off = (uint64_t)b * sw;
+    const uint32_t bn = (uint32_t)((n - off) < sw ? (n - off) : sw);
+    const uint8_t* d = in + off;
+    if (bn < 1024) {
+        if (tid == 0) info[b].prestored = 0;
+        return;
+    }
+    const bool aligned16 = ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
+    // ---- pass 1: bit planes + Adler sums ----
+    uint32_t ones[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t s = 0, t = 0;
+    auto chunk1 = [&](uint32_t p, const uint32_t* w) {   // 16 bytes at block offset p
+        uint32_t ts = 0, tt = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) ones[k] += __builtin_popcount(w[q] & (0x01010101u << k));
+            ts = __builtin_amdgcn_sad_u8(w[q], 0u, ts);                                  // sum of bytes
+            tt = __builtin_amdgcn_udot4(w[q], 0x03020100u + 0x04040404u * q, tt, false);  // sum of j * byte
+        }
+        s += ts;
+        t += (uint64_t)p * ts + tt;
+    };
+    if (aligned16 && bn == SCT * 16 * 8) {   // full 32 KiB block: all 8 loads in flight at once
+        uint4 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) v[i] = *reinterpret_cast<const uint4*>(d + ((tid + i * SCT) << 4));
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+            chunk1((tid + i * SCT) << 4, w);
+        }
+    } else {
+        for (uint32_t p = tid << 4; p < bn; p += SCT << 4) {
+            uint32_t w[5];
+            sc_load(d, p, bn, aligned16, w);
+            chunk1(p, w);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) ones[k] = wave_sum_u32(ones[k]);
+    s = wave_sum_u64(s);
+    t = wave_sum_u64(t);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) red[k][wave] = ones[k];
+        red[8][wave] = s;
+        red[9][wave] = t;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        bool ok = true;
+        for (int k = 0; k < 8; k++) {
+            int64_t o = 0;
+#pragma unroll
+            for (int w = 0; w < SCT / 64; w++) o += (int64_t)red[k][w];
+            const int64_t dv = 2 * o - (int64_t)bn;
+            ok = ok && 8 * (dv < 0 ? -dv : dv) <= (int64_t)bn;
+        }
+        pass_s = ok ? 1u : 0u;
+        if (!ok) info[b].prestored = 0;
+    }
+    __syncthreads();
+    if (!pass_s) return;
+    // ---- pass 2: byte histogram + 4-gram bitmap ----
+    for (uint32_t k = tid; k < (1u << 13) / 4; k += SCT) reinterpret_cast<uint4*>(bm)[k] = make_uint4(0, 0, 0, 0);
+    hist[tid] = 0;
+    __syncthreads();
+    auto chunk2 = [&](uint32_t p, const uint32_t* w) {   // 16 positions at block offset p (w[4]: next 4 bytes)
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            const uint32_t lo = w[j >> 2], hi = w[(j >> 2) + 1];
+            const uint32_t g4 = (j & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(j & 3)) : lo;
+            if (p + j < bn) atomicAdd(&hist[c], 1u);
+            if (p + j + 4 <= bn) {
+                const uint32_t g = (g4 * 0x9E3779B1u) >> 14;
+                atomicOr(&bm[g >> 5], 1u << (g & 31));
+            }
+        }
+    };
+    if (aligned16 && bn == SCT * 16 * 8) {
+        uint4 v[8];
+        uint32_t nx[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t p = (tid + i * SCT) << 4;
+            v[i] = *reinterpret_cast<const uint4*>(d + p);
+            nx[i] = p + 16 < bn ? *reinterpret_cast<const uint32_t*>(d + p + 16) : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t w[5] = {v[i].x, v[i].y, v[i].z, v[i].w, nx[i]};
+            chunk2((tid + i * SCT) << 4, w);
+        }
+    } else {
+        for (uint32_t p = tid << 4; p < bn; p += SCT << 4) {
+            uint32_t w[5];
+            sc_load(d, p, bn, aligned16, w);
+            chunk2(p, w);
+        }
+    }
+    __syncthreads();
+    uint64_t distinct = 0;
+    for (uint32_t k = tid; k < (1u << 13); k += SCT) distinct += __builtin_popcount(bm[k]);
+    const uint64_t hc = hist[tid];
+    uint64_t s2 = hc * hc;
+    distinct = wave_sum_u64(distinct);
+    s2 = wave_sum_u64(s2);
+    __syncthreads();   // red[] reused
+    if (lane == 0) { red[0][wave] = distinct; red[1][wave] = s2; }
+    __syncthreads();
+    if (tid == 0) {
+        uint64_t S = 0, T = 0, Dn = 0, S2 = 0;
+#pragma unroll
+        for (int w = 0; w < SCT / 64; w++) { S += red[8][w]; T += red[9][w]; Dn += red[0][w]; S2 += red[1][w]; }
+        const uint64_t n2 = (uint64_t)bn * bn;
+        const uint64_t coll = (uint64_t)(bn - 3) - Dn;
+        const bool sto = 256 * S2 <= n2 + (n2 >> 4) + 256 * (uint64_t)bn && 64 * coll <= 5 * (uint64_t)bn;
+        info[b].prestored = sto ? 1u : 0u;
+        if (sto) {
+            info[b].ntok = 0;
+            info[b].n = bn;
+            info[b].adl_s = S;
+            info[b].adl_w = (uint64_t)bn * S - T;
+            info[b].btype = 0;
+            info[b].hdr_bits = 3;
+            info[b].body_bits = 0;
+            info[b].nsub = 1;
+        }
+    }
+}
+
 template <bool DICT>
 __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
                                                        int32_t max_chain, uint32_t mflags, uint16_t* __restrict__ dist_g,
@@ -1036,6 +1201,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
     __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def, tp0[3], st_rounds;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t b = blockIdx.x;
+    if ((mflags & 4u) && info[b].prestored) return;   // stored by the noise check (K0)
     const uint64_t off = (uint64_t)b * sw;
     const uint32_t bn = (uint32_t)((n - off) < sw ? (n - off) : sw);
     const uint8_t* d = in + off;
@@ -1346,6 +1512,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         info[b].n = bn;
         info[b].adl_s = L.adl_s;
         info[b].adl_w = (uint64_t)bn * L.adl_s - L.adl_t;
+        info[b].prestored = 0;
     }
 }
 
@@ -1776,6 +1943,7 @@ __global__ __launch_bounds__(64) void dmx_huff_kernel(const uint32_t* __restrict
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x;
     const uint32_t* hg = hist_g + (uint64_t)b * DMX_HIST;
+    if (info[b].prestored) return;   // K0 wrote the stored record
     const uint32_t bn = info[b].n;
     const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1) ? 1u : 0u;
 
@@ -1844,6 +2012,7 @@ __global__ __launch_bounds__(SHT) void dmx_split_hist_kernel(const uint32_t* __r
     __shared__ uint32_t qt[5], wsum[SHT / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t b = blockIdx.x;
+    if (info[b].prestored) return;   // K0 wrote the stored record
     const uint32_t ntok = info[b].ntok, bn = info[b].n;
     for (uint32_t k = tid; k < 4 * DMX_HIST; k += SHT) (&qh[0][0])[k] = 0;
     if (tid < 5) qt[tid] = tid == 4 ? ntok : 0u;
@@ -1905,6 +2074,7 @@ __global__ __launch_bounds__(64) void dmx_split_plan_kernel(SplitScratch* __rest
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x / SPW, g = blockIdx.x % SPW;
     SplitScratch& o = sp[b];
+    if (info[b].prestored) return;
     const uint32_t bn = info[b].n;
     const uint32_t i = c_gi[g], j = c_gj[g];
     const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1 && j == 3) ? 1u : 0u;
@@ -1946,6 +2116,7 @@ __global__ __launch_bounds__(64) void dmx_split_choose_kernel(const SplitScratch
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x;
     const SplitScratch& o = sp[b];
+    if (info[b].prestored) return;
     if (lane == 0) {   // cheapest cut mask: bit k = a cut after quarter k
         int best = -1;
         uint64_t bestc = 0;
@@ -2039,62 +2210,156 @@ __device__ __forceinline__ void gor_bits(uint32_t* out32, uint64_t pos, uint32_t
     if (sh + nb > 32) atomicOr(&out32[w + 1], v >> (32 - sh));
 }
 
+// zlib header (bits 0..15), the sync flush after a non-final shard's last block, the
+// Adler-32 trailer; T = end of the last block, end = byte-aligned end of the DEFLATE data.
+__device__ __forceinline__ void stream_framing(uint32_t* out32, uint32_t flags, uint32_t nblk, uint64_t T,
+                                               uint64_t end, uint32_t adler) {
+    const uint64_t start = (flags & DMX_F_HEADER) ? 16 : 0;
+    if (flags & DMX_F_HEADER) gor_bits(out32, 0, 0x9C78u, 16);
+    if (nblk == 0 && (flags & DMX_F_FINAL)) gor_bits(out32, start, 3u, 3);  // BFINAL=1, BTYPE=01, EOB=0000000
+    if (!(flags & DMX_F_FINAL) && nblk > 0) gor_bits(out32, align8(T + 3) + 16, 0xFFFFu, 16);  // sync flush
+    if (flags & DMX_F_TRAILER) {
+        const uint32_t a = adler;
+        const uint32_t be = (a >> 24) | ((a >> 8) & 0xFF00u) | ((a << 8) & 0xFF0000u) | (a << 24);
+        gor_bits(out32, end, be, 32);
+    }
+}
+
 #define ST 1024
 #define ADL_MOD 65521u
+#define SCAN_TILE 256
 
-__global__ __launch_bounds__(ST) void dmx_scan_kernel(dmx_blkinfo* __restrict__ info, uint32_t nblk, uint64_t n,
-                                                      uint32_t sw, uint32_t flags, uint64_t out_cap,
+// K3, the stream layout, in three launches so that the per-block records are read by many
+// CUs (one workgroup reading 32 768 records of 64 B was 0.2 ms):
+//   dmx_scan_tile_kernel   per tile of 256 blocks: the blocks' layout elements (Mono: bits,
+//                          or "align then bits" for stored blocks) scanned in the tile; each
+//                          block's tile-local exclusive prefix parked in its off_bits/len_bits,
+//                          the tile aggregate and the Adler/token/type partial sums -> tiles[];
+//   dmx_scan_kernel        one workgroup: the tile aggregates -> tile prefixes, stream end,
+//                          Adler-32, out_len, status (dmx_result); zeroes the words past the
+//                          last block; an empty input gets its whole stream here;
+//   dmx_scan_apply_kernel  per tile: absolute offsets, and zero the words each block shares
+//                          with a neighbour (the pack kernel ORs those).
+// The zlib header, sync flush and trailer are ORed by the pack kernel (first/last block).
+struct ScanTile {
+    uint64_t a, c, s;                      // aggregate Mono (s: has a stored block)
+    uint64_t ps, pa, pc;                   // exclusive prefix over the tiles before
+    uint64_t adl_s1, adl_s2, ntok, nsto, nfix;
+    uint64_t pad_[5];
+};
+
+__device__ __forceinline__ Mono blk_elem(const dmx_blkinfo& bi) {
+    Mono e = {0, 0, 0};
+    if (bi.btype == 0) { e.s = 1; e.a = 3; e.c = 32 + 8 * (uint64_t)bi.n; }
+    else { e.c = bi.hdr_bits + bi.body_bits; }
+    return e;
+}
+
+__global__ __launch_bounds__(SCAN_TILE) void dmx_scan_tile_kernel(dmx_blkinfo* __restrict__ info, uint32_t nblk,
+                                                                 uint64_t n, uint32_t sw, ScanTile* __restrict__ tiles) {
+    __shared__ Mono wtot[SCAN_TILE / 64];
+    __shared__ uint64_t red[SCAN_TILE / 64][5];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t b = blockIdx.x * SCAN_TILE + tid;
+    Mono e = {0, 0, 0};
+    uint64_t s1 = 0, s2 = 0, nt = 0, ns = 0, nf = 0;
+    if (b < nblk) {
+        const dmx_blkinfo bi = info[b];
+        e = blk_elem(bi);
+        const uint64_t end_b = (uint64_t)b * sw + bi.n;
+        s1 = bi.adl_s % ADL_MOD;
+        s2 = (bi.adl_w % ADL_MOD + ((n - end_b) % ADL_MOD) * s1) % ADL_MOD;
+        nt = bi.ntok;
+        ns = bi.btype == 0;
+        nf = bi.btype == 1;
+    }
+    Mono x = e;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const Mono y = mshfl_up(x, o);
+        if (lane >= (uint32_t)o) x = mcompose(y, x);
+    }
+    const Mono before = mshfl_up(x, 1);
+    if (lane == 63) wtot[wave] = x;
+    s1 = wave_sum_u64(s1);
+    s2 = wave_sum_u64(s2);
+    nt = wave_sum_u64(nt);
+    ns = wave_sum_u64(ns);
+    nf = wave_sum_u64(nf);
+    if (lane == 0) { red[wave][0] = s1; red[wave][1] = s2; red[wave][2] = nt; red[wave][3] = ns; red[wave][4] = nf; }
+    __syncthreads();
+    Mono pre = {0, 0, 0};
+    for (uint32_t w = 0; w < wave; w++) pre = mcompose(pre, wtot[w]);
+    if (lane) pre = mcompose(pre, before);
+    if (b < nblk) {   // tile-local exclusive prefix, finished by dmx_scan_apply_kernel
+        info[b].off_bits = pre.c;
+        info[b].len_bits = ((uint64_t)pre.s << 32) | pre.a;
+    }
+    if (tid == 0) {
+        Mono agg = {0, 0, 0};
+        uint64_t a1 = 0, a2 = 0, t2 = 0, t3 = 0, t4 = 0;
+        for (int w = 0; w < SCAN_TILE / 64; w++) {
+            agg = mcompose(agg, wtot[w]);
+            a1 += red[w][0]; a2 += red[w][1]; t2 += red[w][2]; t3 += red[w][3]; t4 += red[w][4];
+        }
+        ScanTile& T = tiles[blockIdx.x];
+        T.a = agg.a; T.c = agg.c; T.s = agg.s;
+        T.adl_s1 = a1 % ADL_MOD; T.adl_s2 = a2 % ADL_MOD; T.ntok = t2; T.nsto = t3; T.nfix = t4;
+    }
+}
+
+__global__ __launch_bounds__(ST) void dmx_scan_kernel(ScanTile* __restrict__ tiles, uint32_t nblk, uint64_t n,
+                                                      uint32_t flags, uint64_t out_cap,
                                                       uint32_t* __restrict__ out32, dmx_result* __restrict__ res) {
     __shared__ Mono wtot[ST / 64];
     __shared__ Mono carry_s;
     __shared__ uint64_t red[ST / 64][5];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t start = (flags & DMX_F_HEADER) ? 16 : 0;
-    if (tid == 0) { carry_s.s = 0; carry_s.a = 0; carry_s.c = 0; }
+    const uint32_t ntile = (nblk + SCAN_TILE - 1) / SCAN_TILE;
     uint64_t adl_s1 = 0, adl_s2 = 0, ntok = 0, nsto = 0, nfix = 0;
-    __syncthreads();
-    for (uint32_t c0 = 0; c0 < nblk; c0 += ST) {
-        const uint32_t b = c0 + tid;
-        Mono e = {0, 0, 0};
-        dmx_blkinfo bi;
-        if (b < nblk) {
-            bi = info[b];
-            if (bi.btype == 0) { e.s = 1; e.a = 3; e.c = 32 + 8 * (uint64_t)bi.n; }
-            else { e.c = bi.hdr_bits + bi.body_bits; }
-            const uint64_t end_b = (uint64_t)b * sw + bi.n;
-            adl_s1 += bi.adl_s % ADL_MOD;
-            adl_s2 += (bi.adl_w % ADL_MOD + ((n - end_b) % ADL_MOD) * (bi.adl_s % ADL_MOD)) % ADL_MOD;
-            ntok += bi.ntok;
-            nsto += bi.btype == 0;
-            nfix += bi.btype == 1;
-        }
-        Mono x = e;  // inclusive scan in the wave
+    // thread t owns tiles [t C, t C + C)
+    const uint32_t C = (ntile + ST - 1) / ST;
+    const uint32_t t0 = tid * C < ntile ? tid * C : ntile, t1 = t0 + C < ntile ? t0 + C : ntile;
+    Mono agg = {0, 0, 0};
+    for (uint32_t t = t0; t < t1; t++) {
+        const ScanTile T = tiles[t];
+        Mono e;
+        e.s = (uint32_t)T.s; e.a = T.a; e.c = T.c;
+        agg = mcompose(agg, e);
+        adl_s1 = (adl_s1 + T.adl_s1) % ADL_MOD;
+        adl_s2 = (adl_s2 + T.adl_s2) % ADL_MOD;
+        ntok += T.ntok;
+        nsto += T.nsto;
+        nfix += T.nfix;
+    }
+    Mono x = agg;  // inclusive scan in the wave
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const Mono y = mshfl_up(x, o);
-            if (lane >= (uint32_t)o) x = mcompose(y, x);
+    for (int o = 1; o < 64; o <<= 1) {
+        const Mono y = mshfl_up(x, o);
+        if (lane >= (uint32_t)o) x = mcompose(y, x);
+    }
+    if (lane == 63) wtot[wave] = x;
+    __syncthreads();
+    if (tid == 0) {   // exclusive prefix over waves
+        Mono acc = {0, 0, 0};
+        for (int w = 0; w < ST / 64; w++) {
+            const Mono t = wtot[w];
+            wtot[w] = acc;
+            acc = mcompose(acc, t);
         }
-        if (lane == 63) wtot[wave] = x;
-        __syncthreads();
-        if (tid == 0) {   // exclusive prefix over waves, seeded with the carry
-            Mono acc = carry_s;
-            for (int w = 0; w < ST / 64; w++) {
-                const Mono t = wtot[w];
-                wtot[w] = acc;
-                acc = mcompose(acc, t);
-            }
-            carry_s = acc;
+        carry_s = acc;
+    }
+    __syncthreads();
+    {
+        const Mono before = mshfl_up(x, 1);
+        Mono pre = (lane == 0) ? wtot[wave] : mcompose(wtot[wave], before);
+        for (uint32_t t = t0; t < t1; t++) {
+            tiles[t].ps = pre.s; tiles[t].pa = pre.a; tiles[t].pc = pre.c;
+            Mono e;
+            e.s = (uint32_t)tiles[t].s; e.a = tiles[t].a; e.c = tiles[t].c;
+            pre = mcompose(pre, e);
         }
-        __syncthreads();
-        const Mono before = mshfl_up(x, 1);   // inclusive prefix of lane-1 (all lanes active)
-        if (b < nblk) {
-            const Mono excl_w = wtot[wave];
-            const Mono pre = (lane == 0) ? excl_w : mcompose(excl_w, before);
-            const uint64_t o = mapply(pre, start);
-            info[b].off_bits = o;
-            info[b].len_bits = mapply(e, o) - o;
-        }
-        __syncthreads();
     }
     // reductions
     adl_s1 = wave_sum_u64(adl_s1 % ADL_MOD);
@@ -2136,27 +2401,37 @@ __global__ __launch_bounds__(ST) void dmx_scan_kernel(dmx_blkinfo* __restrict__ 
     }
     __syncthreads();
     if (s_status) return;
-    // zero every word a block shares with a neighbour or with the framing
-    for (uint32_t b = tid; b < nblk; b += ST) {
-        const uint64_t o = info[b].off_bits, l = info[b].len_bits;
-        out32[o >> 5] = 0;
-        out32[(o + l - 1) >> 5] = 0;
-    }
+    // zero the words past the last block (the framing goes there)
     const uint64_t T = s_T, end = s_end;
     const uint64_t tail_end = end + ((flags & DMX_F_TRAILER) ? 32 : 0);
     for (uint64_t w = (T >> 5) + tid; w < ((tail_end + 31) >> 5); w += ST) out32[w] = 0;
-    if (tid == 0 && start) out32[0] = 0;
-    __syncthreads();
-    if (tid == 0) {
-        if (flags & DMX_F_HEADER) gor_bits(out32, 0, 0x9C78u, 16);
-        if (nblk == 0 && (flags & DMX_F_FINAL)) gor_bits(out32, start, 3u, 3);  // BFINAL=1, BTYPE=01, EOB=0000000
-        if (!(flags & DMX_F_FINAL) && nblk > 0) gor_bits(out32, align8(T + 3) + 16, 0xFFFFu, 16);  // sync flush
-        if (flags & DMX_F_TRAILER) {
-            const uint32_t a = s_adler;
-            const uint32_t be = (a >> 24) | ((a >> 8) & 0xFF00u) | ((a << 8) & 0xFF0000u) | (a << 24);
-            gor_bits(out32, end, be, 32);
-        }
+    if (nblk == 0) {   // no pack launch: the whole stream is written here
+        if (tid == 0 && start) out32[0] = 0;
+        __syncthreads();
+        if (tid == 0) stream_framing(out32, flags, 0, T, end, s_adler);
     }
+}
+
+__global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply_kernel(dmx_blkinfo* __restrict__ info, uint32_t nblk,
+                                                                  uint32_t flags, const ScanTile* __restrict__ tiles,
+                                                                  uint32_t* __restrict__ out32,
+                                                                  const dmx_result* __restrict__ res) {
+    if (res->status) return;
+    const uint32_t b = blockIdx.x * SCAN_TILE + threadIdx.x;
+    if (b >= nblk) return;
+    const uint64_t start = (flags & DMX_F_HEADER) ? 16 : 0;
+    const ScanTile& T = tiles[blockIdx.x];
+    Mono tp, lp;
+    tp.s = (uint32_t)T.ps; tp.a = T.pa; tp.c = T.pc;
+    const dmx_blkinfo bi = info[b];
+    lp.c = bi.off_bits; lp.s = (uint32_t)(bi.len_bits >> 32); lp.a = bi.len_bits & 0xFFFFFFFFu;
+    const Mono pre = mcompose(tp, lp);
+    const uint64_t o = mapply(pre, start);
+    const uint64_t l = mapply(blk_elem(bi), o) - o;
+    info[b].off_bits = o;
+    info[b].len_bits = l;
+    out32[o >> 5] = 0;            // shared with the block before (or the zlib header)
+    out32[(o + l - 1) >> 5] = 0;  // shared with the block after (or the framing)
 }
 
 // ------------------------------------------------------------------------------------
@@ -2173,6 +2448,18 @@ __device__ __forceinline__ void st_or64(uint32_t* st, uint32_t pos, uint64_t v, 
     atomicOr(&st[w], (uint32_t)a);
     if (sh + nb > 32) atomicOr(&st[w + 1], (uint32_t)(a >> 32));
     if (sh + nb > 64) atomicOr(&st[w + 2], (uint32_t)(v >> (64 - sh)));
+}
+
+// The first block ORs the zlib header, the last one the sync flush / trailer (the scan
+// zeroed those words; every write into them is an atomicOr).
+__device__ __forceinline__ void pack_framing(uint32_t* out32, uint32_t flags, uint32_t nblk, uint32_t b,
+                                             const dmx_result* res) {
+    if (b == 0 && (flags & DMX_F_HEADER)) gor_bits(out32, 0, 0x9C78u, 16);
+    if (b == nblk - 1) {
+        const uint64_t T = res->end_bits;
+        const uint64_t end = (flags & DMX_F_FINAL) ? align8(T) : align8(T + 3) + 32;
+        stream_framing(out32, flags & ~DMX_F_HEADER, nblk, T, end, res->adler);
+    }
 }
 
 __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict__ in, uint32_t sw,
@@ -2192,20 +2479,70 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
     const uint32_t s0 = (uint32_t)(O & 31);
     const uint32_t nwords = (uint32_t)((s0 + Lb + 31) >> 5);
     const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1) ? 1u : 0u;
+    if (bi.btype == 0) {
+        // stored block straight from the input to the output, no LDS: the 3 header bits at s0,
+        // LEN/NLEN at byte P/8, the data from byte B0 (bit offsets relative to word O >> 5).
+        // Whole output quads (16-byte aligned in the stream) come from one 20-byte read of
+        // the block and byte alignment in registers; the first word, the ragged ends and
+        // unaligned blocks take the bytewise path.  The first and last words are shared
+        // with the neighbouring blocks (zeroed by the scan kernel): atomicOr there.
+        const uint8_t* d = in + (uint64_t)b * sw;
+        const uint32_t bn = bi.n;
+        const uint32_t P = (s0 + 3 + 7) & ~7u, B0 = (P + 32) >> 3;
+        const uint32_t lenw = (bn & 0xFFFFu) | ((~bn & 0xFFFFu) << 16);
+        const uint64_t gw0 = O >> 5;
+        auto gen_word = [&](uint32_t k) -> uint32_t {
+            uint32_t v = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < 4; i++) {
+                const uint32_t q = 4 * k + i;
+                uint32_t by;
+                if (q >= B0) by = (q - B0) < bn ? d[q - B0] : 0u;
+                else if (q >= (P >> 3)) by = (lenw >> (8 * (q - (P >> 3)))) & 0xFFu;
+                else by = (uint32_t)((((uint64_t)final_bit << s0) >> (8 * q)) & 0xFFu);
+                v |= by << (8 * i);
+            }
+            return v;
+        };
+        auto put_word = [&](uint32_t k, uint32_t v) {
+            if ((k == 0 && s0 != 0) || (k == nwords - 1 && ((s0 + Lb) & 31) != 0)) atomicOr(&out32[gw0 + k], v);
+            else out32[gw0 + k] = v;
+        };
+        const bool dal = (reinterpret_cast<uintptr_t>(d) & 3) == 0;
+        const uint32_t ks = 4 - (uint32_t)(gw0 & 3);                      // first quad: (gw0 + ks) % 4 == 0, ks >= 1
+        const uint32_t nq = (dal && nwords > ks + 1) ? (nwords - 1 - ks) >> 2 : 0;   // quads short of the last word
+        for (uint32_t j = tid; j < nq; j += PT) {
+            const uint32_t k = ks + 4 * j;
+            const int64_t o0 = (int64_t)(4 * k) - (int64_t)B0;
+            if (o0 >= 0 && (uint64_t)((o0 & ~3ll) + 20) <= bn) {
+                const uint32_t* p32 = reinterpret_cast<const uint32_t*>(d + (o0 & ~3ll));
+                const uint32_t w0 = p32[0], w1 = p32[1], w2 = p32[2], w3 = p32[3], w4 = p32[4];
+                const uint32_t sh = (uint32_t)(o0 & 3);
+                uint4 v;
+                v.x = sh ? __builtin_amdgcn_alignbyte(w1, w0, sh) : w0;
+                v.y = sh ? __builtin_amdgcn_alignbyte(w2, w1, sh) : w1;
+                v.z = sh ? __builtin_amdgcn_alignbyte(w3, w2, sh) : w2;
+                v.w = sh ? __builtin_amdgcn_alignbyte(w4, w3, sh) : w3;
+                *reinterpret_cast<uint4*>(&out32[gw0 + k]) = v;   // never word 0 or the last word
+            } else {
+#pragma unroll
+                for (uint32_t i = 0; i < 4; i++) out32[gw0 + k + i] = gen_word(k + i);
+            }
+        }
+        // the words outside the quads: [0, ks) and [ks + 4 nq, nwords)
+        const uint32_t kq = nq ? ks + 4 * nq : 0;
+        const uint32_t nrest = nq ? ks + (nwords - kq) : nwords;
+        for (uint32_t r = tid; r < nrest; r += PT) {
+            const uint32_t k = nq ? (r < ks ? r : kq + (r - ks)) : r;
+            put_word(k, gen_word(k));
+        }
+        if (tid == 0 && (b == 0 || b == nblk - 1)) pack_framing(out32, flags, nblk, b, res);
+        return;
+    }
     for (uint32_t k = tid; k < nwords; k += PT) stage[k] = 0;
     for (uint32_t k = tid; k < 316; k += PT) code[k] = codes_g[(uint64_t)b * DMX_NSUB * DMX_HIST + k];
     __syncthreads();
-    if (bi.btype == 0) {
-        const uint8_t* d = in + (uint64_t)b * sw;
-        const uint32_t P = (s0 + 3 + 7) & ~7u;
-        if (tid == 0) {
-            st_or64(stage, s0, final_bit, 3);
-            st_or64(stage, P, (bi.n & 0xFFFFu) | ((~bi.n & 0xFFFFu) << 16), 32);
-        }
-        __syncthreads();
-        uint8_t* st8 = reinterpret_cast<uint8_t*>(stage) + ((P + 32) >> 3);
-        for (uint32_t k = tid; k < bi.n; k += PT) st8[k] = d[k];
-    } else {
+    {   // (stored blocks left above)
         // one or more DEFLATE blocks (f3 split): header, tokens [t0, t1), end of block
         const uint32_t* tb = tok_g + (uint64_t)b * DMX_BLK;
         uint32_t pos = s0;
@@ -2302,6 +2639,7 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
         if ((k == 0 && first_partial) || (k == nwords - 1 && last_partial)) atomicOr(&out32[gw0 + k], v);
         else out32[gw0 + k] = v;
     }
+    if (tid == 0 && (b == 0 || b == nblk - 1)) pack_framing(out32, flags, nblk, b, res);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2321,6 +2659,7 @@ struct dmx_ctx {
     uint32_t* hdr;    // cap_blocks * DMX_NSUB * DMX_HDR_WORDS
     dmx_subinfo* sub; // cap_blocks * DMX_NSUB
     dmx_blkinfo* info;
+    ScanTile* tiles;  // cap_blocks / SCAN_TILE + 1: per-tile aggregates and prefixes (scan)
     dmx_result* res;
     uint64_t* dbg;        // optional per-block phase stamps (DMX_STAMPS=1)
     uint64_t dbg_cap;
@@ -2370,7 +2709,9 @@ static void ctx_free_ws(dmx_ctx* c) {
     if (c->hdr) (void)hipFree(c->hdr);
     if (c->sub) (void)hipFree(c->sub);
     if (c->info) (void)hipFree(c->info);
+    if (c->tiles) (void)hipFree(c->tiles);
     c->dist = NULL; c->tok = NULL; c->hist = NULL; c->codes = NULL; c->hdr = NULL; c->sub = NULL; c->info = NULL;
+    c->tiles = NULL;
     c->cap_blocks = 0;
 }
 
@@ -2385,6 +2726,7 @@ static int ctx_reserve(dmx_ctx* c, uint64_t nblk) {
     HIPCHK(hipMalloc(&c->hdr, cb * DMX_NSUB * DMX_HDR_WORDS * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&c->sub, cb * DMX_NSUB * sizeof(dmx_subinfo)));
     HIPCHK(hipMalloc(&c->info, cb * sizeof(dmx_blkinfo)));
+    HIPCHK(hipMalloc(&c->tiles, (cb / SCAN_TILE + 1) * sizeof(ScanTile)));
     c->cap_blocks = cb;
     return 0;
 }
@@ -2520,8 +2862,13 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
             hipLaunchKernelGGL(dmx_hist_kernel, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw,
                                o.max_chain, (const uint8_t*)o.dict, dict_len, c->chs, c->che, c->tok, dbg);
         }
+        // stage 0 also holds K0, the noise check (DMX_F_STORE_CHECK)
+        if (o.flags & DMX_F_STORE_CHECK)
+            hipLaunchKernelGGL(dmx_store_check_kernel, dim3(nblk), dim3(SCT), 0, s, (const uint8_t*)d_in, n,
+                               (uint32_t)o.sw, c->info);
         if (ev) (void)hipEventRecord(ev[1], s);
-        const uint32_t mfl = ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u);
+        const uint32_t mfl = ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u) |
+                             ((o.flags & DMX_F_STORE_CHECK) ? 4u : 0u);
         if (o.flags & DMX_F_DICT)
             hipLaunchKernelGGL(dmx_match_kernel<true>, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n,
                                (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg);
@@ -2547,8 +2894,15 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         (void)hipEventRecord(ev[2], s);
         (void)hipEventRecord(ev[3], s);
     }
-    hipLaunchKernelGGL(dmx_scan_kernel, dim3(1), dim3(ST), 0, s, c->info, nblk, n, (uint32_t)o.sw, o.flags, out_cap,
+    const uint32_t ntile = (nblk + SCAN_TILE - 1) / SCAN_TILE;
+    if (nblk)
+        hipLaunchKernelGGL(dmx_scan_tile_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, n, (uint32_t)o.sw,
+                           c->tiles);
+    hipLaunchKernelGGL(dmx_scan_kernel, dim3(1), dim3(ST), 0, s, c->tiles, nblk, n, o.flags, out_cap,
                        (uint32_t*)d_out, c->res);
+    if (nblk)
+        hipLaunchKernelGGL(dmx_scan_apply_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, o.flags, c->tiles,
+                           (uint32_t*)d_out, (const dmx_result*)c->res);
     if (ev) (void)hipEventRecord(ev[4], s);
     if (nblk)
         hipLaunchKernelGGL(dmx_pack_kernel, dim3(nblk), dim3(PT), 0, s, (const uint8_t*)d_in, (uint32_t)o.sw, c->tok,
@@ -2812,7 +3166,7 @@ extern "C" int dmx_encode_fd(int fd_in, int fd_out, const dmx_opts* opts, uint64
     const uint64_t sw = (uint64_t)o.sw;
     if (chunk < sw) chunk = sw;
     chunk -= chunk % sw;
-    const uint32_t pflags = o.flags & (DMX_F_LAZY | DMX_F_SPLIT | DMX_F_DICT | DMX_F_EXACT_SORT);
+    const uint32_t pflags = o.flags & (DMX_F_LAZY | DMX_F_SPLIT | DMX_F_DICT | DMX_F_EXACT_SORT | DMX_F_STORE_CHECK);
     const char* dev_s = getenv("DMX_DEVICE");
     pthread_mutex_lock(&g_mu);
     int err = 0;

@@ -129,6 +129,13 @@ struct compress_stats {
                             strictly longer than the block's own.  Block 0
                             uses dmx_opts.dict when given.  Blocks then depend on their
                             predecessor: inflate with the stream mode, not the block index. */
+#define DMX_F_STORE_CHECK 128u  /* block option: a block whose bytes pass an
+                                 * integer noise check (flat byte histogram, few 4-byte
+                                 * repeats) is emitted stored without a parse -- the stored
+                                 * path runs at HBM speed instead of the match kernel's.  An
+                                 * encoder policy of our own (the reference always parses);
+                                 * the oracle applies the same rule.  Such blocks have no
+                                 * tokens (no compress_stats records). */
 
 typedef struct {
     int32_t sw;        /* block size 1..32768 (0 = 32768) */

@@ -631,17 +631,60 @@ static void orc_plan_split(const uint32_t* tok, int ntok, int bn, orc_split_plan
         }
 }
 
+/* ---- 7b. incompressible-block check (DMX_F_STORE_CHECK) --------------
+ *
+ * An encoder policy, not part of the reference (whose parse always runs): a block is
+ * emitted stored, without a parse, when its bytes look like noise by two integer
+ * statistics both sides compute exactly:
+ *   S2   = sum over byte values c of h[c]^2            (h = byte histogram of the block)
+ *   coll = (bn - 3) - |{ g(p) : 0 <= p <= bn - 4 }|    (g = 18-bit hash of the 4 bytes at p,
+ *          (d[p] | d[p+1] << 8 | d[p+2] << 16 | d[p+3] << 24) * 0x9E3779B1 >> 14)
+ *   ones_k = number of bytes with bit k set, k = 0..7
+ * stored iff bn >= 1024, 8 * |2 * ones_k - bn| <= bn for every k (a cheap first test: text,
+ * runs and anything 7-bit fail it without a histogram), 256 * S2 <= bn^2 + bn^2 / 16 + 256 * bn (noise gives about
+ * bn^2 + 255 * bn: the byte distribution is within 6 % of flat in collision entropy) and 64 * coll <= 5 * bn (4-byte repeats at most about
+ * what 2^18 buckets give noise: 1 962 expected at bn = 32 768, threshold 2 560).  A block
+ * of repeats with a flat byte histogram (0, 1, ..., 255 cycled) fails the second test.
+ */
+int dmx_oracle_store_check(const uint8_t* d, int bn) {
+    if (bn < 1024) return 0;
+    uint64_t h[256] = {0};
+    for (int k = 0; k < bn; k++) h[d[k]]++;
+    for (int bit = 0; bit < 8; bit++) {   /* bit planes: every bit set in about half the bytes */
+        int64_t ones = 0;
+        for (int c = 0; c < 256; c++)
+            if ((c >> bit) & 1) ones += (int64_t)h[c];
+        const int64_t dev = 2 * ones - bn;
+        if (8 * (dev < 0 ? -dev : dev) > bn) return 0;
+    }
+    uint64_t s2 = 0;
+    for (int c = 0; c < 256; c++) s2 += h[c] * h[c];
+    const uint64_t n2 = (uint64_t)bn * (uint64_t)bn;
+    if (256 * s2 > n2 + (n2 >> 4) + 256 * (uint64_t)bn) return 0;
+    uint32_t* bm = (uint32_t*)calloc(1u << 13, sizeof(uint32_t));
+    uint64_t distinct = 0;
+    for (int p = 0; p + 4 <= bn; p++) {
+        const uint32_t w = (uint32_t)d[p] | (uint32_t)d[p + 1] << 8 | (uint32_t)d[p + 2] << 16 | (uint32_t)d[p + 3] << 24;
+        const uint32_t g = (w * 0x9E3779B1u) >> 14;
+        if (!(bm[g >> 5] & (1u << (g & 31)))) { bm[g >> 5] |= 1u << (g & 31); distinct++; }
+    }
+    free(bm);
+    const uint64_t coll = (uint64_t)(bn - 3) - distinct;
+    return 64 * coll <= 5 * (uint64_t)bn;
+}
+
 /* ---- 8. whole stream ---------------------------------------------------------------- */
 
 /*
  * Compress `in` (n bytes) into a zlib stream.  Returns the stream length, or
  * -1 if `cap` is too small.  sw = block size (1..32768), max_chain as above,
- * lazy = f2 parse, split = f3 block splitting.  If btypes != NULL it receives the
+ * lazy = f2 parse, blkopt bit 0 = f3 block splitting, bit 1 = the §4.7 store check.  If btypes != NULL it receives the
  * chosen BTYPE of every block (split blocks: the type of their first sub-block).
  */
 long long dmx_oracle_compress_ex3(const uint8_t* in, size_t n, int sw, int max_chain, int hash_kind,
-                                  int lazy, int split, int dict, const uint8_t* pre, size_t npre,
+                                  int lazy, int blkopt, int dict, const uint8_t* pre, size_t npre,
                                   uint8_t* out, size_t cap, uint8_t* btypes) {
+    const int split = blkopt & 1, store_check = (blkopt >> 1) & 1;   /* f3; §4.7 */
     if (sw <= 0 || sw > 32768) return -2;
     if (cap < 8) return -1;
     memset(out, 0, cap);
@@ -665,6 +708,12 @@ long long dmx_oracle_compress_ex3(const uint8_t* in, size_t n, int sw, int max_c
         int hn = 0;
         if (dict && b > 0) { hist = in + off - (size_t)sw; hn = sw; }
         else if (dict && pre && npre > 0) { hn = npre < (size_t)sw ? (int)npre : sw; hist = pre + npre - (size_t)hn; }
+        if (store_check && dmx_oracle_store_check(in + off, bn)) {   /* stored without a parse */
+            P->btype = 0;
+            if (btypes) btypes[b] = 0;
+            orc_write_block(&w, in + off, bn, NULL, 0, P, b + 1 == nblk);
+            continue;
+        }
         int ntok = dmx_oracle_parse_block_hist(hist, hn, in + off, bn, max_chain, hash_kind, lazy, tok);
         if (split) {
             orc_plan_split(tok, ntok, bn, SP);

@@ -60,6 +60,8 @@ def lib():
         L.dmx_oracle_parse_block_hist.argtypes = [u8p, ctypes.c_int, u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                   ctypes.c_int, u32p]
         L.dmx_oracle_parse_block_hist.restype = ctypes.c_int
+        L.dmx_oracle_store_check.argtypes = [u8p, ctypes.c_int]
+        L.dmx_oracle_store_check.restype = ctypes.c_int
         L.dmx_oracle_plan.argtypes = [u32p, ctypes.c_int, ctypes.c_int, u64p, u8p, u8p]
         L.dmx_oracle_plan.restype = ctypes.c_int
         _lib = L
@@ -110,21 +112,28 @@ def adler32(data) -> int:
 
 def compress(data, sw: int = 32768, max_chain: int = 0, hash_kind: int = HASH_MUL,
              want_btypes: bool = False, lazy: bool = False, split: bool = False, dict: bool = False,
-             pre=None):
+             pre=None, store_check: bool = False):
     """zlib stream of `data`; lazy = f2 parse, split = f3 adaptive block splitting,
-    dict = f1 cross-block dictionary (pre: the bytes before `data`, history of block 0)."""
+    dict = f1 cross-block dictionary (pre: the bytes before `data`, history of block 0),
+    store_check = blocks that pass the DESIGN.md §4.7 noise check are stored unparsed."""
     a = _as_u8(data)
     nblk = (a.size + sw - 1) // sw
     cap = a.size + 5 * (nblk + 1) + 64
     out = np.zeros(cap, dtype=np.uint8)
     bt = np.zeros(max(nblk, 1), dtype=np.uint8)
     pa = _as_u8(pre if pre is not None else b"")
-    r = lib().dmx_oracle_compress_ex3(_u8(a), a.size, sw, max_chain, hash_kind, int(lazy), int(split),
-                                      int(dict), _u8(pa), pa.size, _u8(out), cap, _u8(bt))
+    r = lib().dmx_oracle_compress_ex3(_u8(a), a.size, sw, max_chain, hash_kind, int(lazy),
+                                      int(split) | (2 if store_check else 0), int(dict), _u8(pa), pa.size, _u8(out), cap, _u8(bt))
     if r < 0:
         raise RuntimeError(f"oracle compress failed: {r}")
     z = out[:r].tobytes()
     return (z, bt[:nblk].copy()) if want_btypes else z
+
+
+def store_check(block) -> bool:
+    """would DMX_F_STORE_CHECK emit this block stored without a parse?"""
+    a = _as_u8(block)
+    return bool(lib().dmx_oracle_store_check(_u8(a), a.size))
 
 
 def plan(tokens: np.ndarray, n: int):
