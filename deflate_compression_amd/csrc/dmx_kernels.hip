@@ -1081,10 +1081,18 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
         s += ts;
         t += (uint64_t)p * ts + tt;
     };
-    if (aligned16 && bn == SCT * 16 * 8) {   // full 32 KiB block: all 8 loads in flight at once
-        uint4 v[8];
+    // full 32 KiB block: all loads in flight at once, and the data stays in registers for
+    // pass 2 (w4: the 4 bytes after each chunk, for the 4-grams that straddle it)
+    const bool full = aligned16 && bn == SCT * 16 * 8;
+    uint4 v[8];
+    uint32_t nx[8];
+    if (full) {
 #pragma unroll
-        for (int i = 0; i < 8; i++) v[i] = *reinterpret_cast<const uint4*>(d + ((tid + i * SCT) << 4));
+        for (int i = 0; i < 8; i++) {
+            const uint32_t p = (tid + i * SCT) << 4;
+            v[i] = *reinterpret_cast<const uint4*>(d + p);
+            nx[i] = p + 16 < bn ? *reinterpret_cast<const uint32_t*>(d + p + 16) : 0u;
+        }
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
@@ -1139,15 +1147,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
             }
         }
     };
-    if (aligned16 && bn == SCT * 16 * 8) {
-        uint4 v[8];
-        uint32_t nx[8];
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const uint32_t p = (tid + i * SCT) << 4;
-            v[i] = *reinterpret_cast<const uint4*>(d + p);
-            nx[i] = p + 16 < bn ? *reinterpret_cast<const uint32_t*>(d + p + 16) : 0u;
-        }
+    if (full) {
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const uint32_t w[5] = {v[i].x, v[i].y, v[i].z, v[i].w, nx[i]};
