@@ -175,9 +175,9 @@ int deflate_compress(int fd_in, int fd_out, int fd_stats, swi sw, int ops) {
     o.reserved = 0;
     o.dict = NULL;
     o.dict_len = 0;
-    if (fd_stats < 0) {   /* streaming: chunks of DMX_CHUNK_MB MiB (default 32) through pinned buffers */
+    if (fd_stats < 0) {   /* streaming: chunks of DMX_CHUNK_MB MiB (default 16) through pinned buffers */
         const char* cm = getenv("DMX_CHUNK_MB");
-        const uint64_t mb = cm && atoi(cm) > 0 ? (uint64_t)atoi(cm) : 32u;
+        const uint64_t mb = cm && atoi(cm) > 0 ? (uint64_t)atoi(cm) : 16u;
         return dmx_encode_fd(fd_in, fd_out, &o, mb << 20);
     }
     uint8_t* in = NULL;

@@ -2672,6 +2672,13 @@ struct dmx_ctx {
     void* d_out;
     uint64_t d_out_cap;
     void* d_dict;         // DMX_F_DICT history of block 0 (DMX_BLK bytes)
+    // dmx_encode_fd streaming buffers, kept across calls (pinning ~100 MB costs ms)
+    uint8_t* fd_hin[2];   // pinned input chunks
+    uint8_t* fd_hout[2];  // pinned output chunks
+    void* fd_din[2];      // device input chunks (the previous one is the next chunk's history)
+    void* fd_dout;
+    dmx_result* fd_hres;  // pinned
+    uint64_t fd_chunk, fd_ocap;
     uint16_t* chs;        // DMX_F_DICT: (cap_chain) x DMX_BLK bucket-sorted positions per block (+ the dict)
     uint16_t* che;        // DMX_F_DICT: (cap_chain) x DMX_NBUCKET bucket ends
     uint64_t cap_chain;
@@ -2776,6 +2783,13 @@ extern "C" void dmx_ctx_destroy(dmx_ctx* c) {
     if (c->d_in) (void)hipFree(c->d_in);
     if (c->d_out) (void)hipFree(c->d_out);
     if (c->d_dict) (void)hipFree(c->d_dict);
+    for (int k = 0; k < 2; k++) {
+        if (c->fd_hin[k]) (void)hipHostFree(c->fd_hin[k]);
+        if (c->fd_hout[k]) (void)hipHostFree(c->fd_hout[k]);
+        if (c->fd_din[k]) (void)hipFree(c->fd_din[k]);
+    }
+    if (c->fd_dout) (void)hipFree(c->fd_dout);
+    if (c->fd_hres) (void)hipHostFree(c->fd_hres);
     if (c->chs) (void)hipFree(c->chs);
     if (c->che) (void)hipFree(c->che);
     if (c->split) (void)hipFree(c->split);
@@ -3100,15 +3114,18 @@ extern "C" int dmx_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint
 
 // --- streaming file-in/file-out (the fd API without per-token stats) ---
 // The input is read in chunks of `chunk` bytes (a multiple of sw) straight into pinned
-// buffers; chunk i is copied to the device and encoded while the host writes chunk i-1's
-// stream and reads chunk i+1.  Every chunk is a shard of one zlib stream (DESIGN.md §6
-// framing): the header on the first, a sync flush after every chunk that is not known to
-// be the last (a one-byte lookahead tells), BFINAL on the last, and the Adler-32 combined
-// on the host.  With
-// DMX_F_DICT the previous chunk's last sw bytes are the history of each chunk's first block,
-// so the parse equals the one-shot parse.  One chunk: byte-identical to dmx_encode_host.
+// buffers; chunk i is copied to the device and encoded while the host reads chunk i+1
+// (several pread threads when fd_in is a regular file) and a writer thread writes chunk
+// i-1's stream (writes stay in order: writer i starts after writer i-1 has ended).  Every
+// chunk is a shard of one zlib stream (DESIGN.md §6 framing): the header on the first, a
+// sync flush after every chunk that is not known to be the last (the file size, or a
+// one-byte lookahead on pipes, tells), BFINAL on the last, and the Adler-32 combined on the
+// host.  With DMX_F_DICT the previous chunk's last sw bytes (still in HBM) are the history
+// of each chunk's first block, so the parse equals the one-shot parse.  One chunk:
+// byte-identical to dmx_encode_host.  Pinned and device buffers live in the cached context.
 #include <unistd.h>
 #include <errno.h>
+#include <sys/stat.h>
 static int64_t read_full(int fd, uint8_t* b, uint64_t cap) {
     uint64_t len = 0;
     while (len < cap) {
@@ -3119,29 +3136,6 @@ static int64_t read_full(int fd, uint8_t* b, uint64_t cap) {
         }
         if (r == 0) break;
         len += (uint64_t)r;
-    }
-    return (int64_t)len;
-}
-// One chunk with a one-byte lookahead, so a chunk that ends exactly at EOF is known to be
-// the last before it is encoded (then a stream of one chunk is byte-identical to the
-// one-shot stream).  *carry: the lookahead byte of the previous call (-1: none); *eof: no
-// byte follows this chunk.
-static int64_t read_chunk(int fd, uint8_t* b, uint64_t chunk, int* carry, bool* eof) {
-    uint64_t off = 0;
-    if (*carry >= 0) b[off++] = (uint8_t)*carry;
-    const int64_t r = read_full(fd, b + off, chunk - off);
-    if (r < 0) return r;
-    const uint64_t len = off + (uint64_t)r;
-    *carry = -1;
-    *eof = true;
-    if (len == chunk) {
-        uint8_t nb;
-        const int64_t q = read_full(fd, &nb, 1);
-        if (q < 0) return q;
-        if (q == 1) {
-            *carry = nb;
-            *eof = false;
-        }
     }
     return (int64_t)len;
 }
@@ -3158,6 +3152,119 @@ static int write_full(int fd, const uint8_t* p, uint64_t n) {
     return 0;
 }
 
+// Reader: a regular file of known size is read with FD_READERS parallel preads per chunk;
+// anything else (pipes) with read() and a one-byte lookahead.
+#define FD_READERS 4
+struct FdReader {
+    int fd;
+    bool seekable;
+    uint64_t off, size;   // seekable: next file offset, file size
+    int carry;            // pipes: the lookahead byte (-1: none)
+    bool eof;             // no byte after the chunk just read
+};
+struct PreadJob {
+    int fd;
+    uint8_t* b;
+    uint64_t off, len;
+    int rc;
+};
+static void* pread_job(void* a) {
+    PreadJob* j = (PreadJob*)a;
+    uint64_t done = 0;
+    j->rc = 0;
+    while (done < j->len) {
+        const ssize_t r = pread(j->fd, j->b + done, j->len - done, (off_t)(j->off + done));
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            j->rc = -(int)E_NEXIST;
+            return NULL;
+        }
+        if (r == 0) break;
+        done += (uint64_t)r;
+    }
+    if (done < j->len) j->rc = -(int)E_NEXIST;   // the file shrank under us
+    return NULL;
+}
+static int64_t fd_read_chunk(FdReader* R, uint8_t* b, uint64_t chunk) {
+    if (R->seekable) {
+        const uint64_t left = R->size - R->off, len = left < chunk ? left : chunk;
+        const uint64_t piece = ((len + FD_READERS - 1) / FD_READERS + 4095) & ~4095ull;
+        PreadJob jobs[FD_READERS];
+        pthread_t th[FD_READERS];
+        bool started[FD_READERS] = {false, false, false, false};
+        int nj = 0;
+        for (uint64_t o = 0; o < len; o += piece, nj++) {
+            jobs[nj] = {R->fd, b + o, R->off + o, (len - o) < piece ? (len - o) : piece, 0};
+            if (nj > 0 && pthread_create(&th[nj], NULL, pread_job, &jobs[nj]) == 0) started[nj] = true;
+            else if (nj > 0) pread_job(&jobs[nj]);
+        }
+        if (nj > 0) pread_job(&jobs[0]);
+        int rc = 0;
+        for (int k = 0; k < nj; k++) {
+            if (started[k]) pthread_join(th[k], NULL);
+            if (jobs[k].rc) rc = jobs[k].rc;
+        }
+        if (rc) return rc;
+        R->off += len;
+        R->eof = R->off >= R->size;
+        return (int64_t)len;
+    }
+    uint64_t off = 0;
+    if (R->carry >= 0) b[off++] = (uint8_t)R->carry;
+    const int64_t r = read_full(R->fd, b + off, chunk - off);
+    if (r < 0) return r;
+    const uint64_t len = off + (uint64_t)r;
+    R->carry = -1;
+    R->eof = true;
+    if (len == chunk) {
+        uint8_t nb;
+        const int64_t q = read_full(R->fd, &nb, 1);
+        if (q < 0) return q;
+        if (q == 1) {
+            R->carry = nb;
+            R->eof = false;
+        }
+    }
+    return (int64_t)len;
+}
+
+struct WriteJob {
+    int fd;
+    const uint8_t* p;
+    uint64_t n;
+    int rc;
+};
+static void* write_job(void* a) {
+    WriteJob* j = (WriteJob*)a;
+    j->rc = write_full(j->fd, j->p, j->n);
+    return NULL;
+}
+
+static int fd_buffers(dmx_ctx* c, uint64_t chunk, uint64_t ocap) {
+    if (c->fd_chunk >= chunk && c->fd_ocap >= ocap) return 0;
+    for (int k = 0; k < 2; k++) {
+        if (c->fd_hin[k]) (void)hipHostFree(c->fd_hin[k]);
+        if (c->fd_hout[k]) (void)hipHostFree(c->fd_hout[k]);
+        if (c->fd_din[k]) (void)hipFree(c->fd_din[k]);
+        c->fd_hin[k] = c->fd_hout[k] = NULL;
+        c->fd_din[k] = NULL;
+    }
+    if (c->fd_dout) (void)hipFree(c->fd_dout);
+    c->fd_dout = NULL;
+    c->fd_chunk = c->fd_ocap = 0;
+    for (int k = 0; k < 2; k++) {
+        if (hip_fail(hipHostMalloc((void**)&c->fd_hin[k], chunk + 16, 0), "hipHostMalloc")) return -(int)E_MALLOC;
+        if (hip_fail(hipHostMalloc((void**)&c->fd_hout[k], ocap, 0), "hipHostMalloc")) return -(int)E_MALLOC;
+        if (hip_fail(hipMalloc(&c->fd_din[k], chunk + 16), "hipMalloc")) return -(int)E_DEVICE;
+    }
+    if (hip_fail(hipMalloc(&c->fd_dout, ocap), "hipMalloc")) return -(int)E_DEVICE;
+    if (!c->fd_hres && hip_fail(hipHostMalloc((void**)&c->fd_hres, sizeof(dmx_result), 0), "hipHostMalloc"))
+        return -(int)E_MALLOC;
+    c->fd_chunk = chunk;
+    c->fd_ocap = ocap;
+    return 0;
+}
+
 extern "C" int dmx_encode_fd(int fd_in, int fd_out, const dmx_opts* opts, uint64_t chunk) {
     dmx_opts o = {0, 0, DMX_ZLIB, 0, NULL, 0};
     if (opts) o = *opts;
@@ -3167,84 +3274,89 @@ extern "C" int dmx_encode_fd(int fd_in, int fd_out, const dmx_opts* opts, uint64
     if (chunk < sw) chunk = sw;
     chunk -= chunk % sw;
     const uint32_t pflags = o.flags & (DMX_F_LAZY | DMX_F_SPLIT | DMX_F_DICT | DMX_F_EXACT_SORT | DMX_F_STORE_CHECK);
+    FdReader R = {fd_in, false, 0, 0, -1, true};
+    {   // a regular file of known size from the current offset: parallel preads
+        struct stat st;
+        const off_t cur = lseek(fd_in, 0, SEEK_CUR);
+        if (cur >= 0 && fstat(fd_in, &st) == 0 && S_ISREG(st.st_mode) && (uint64_t)st.st_size >= (uint64_t)cur) {
+            R.seekable = true;
+            R.off = (uint64_t)cur;
+            R.size = (uint64_t)st.st_size;
+        }
+    }
     const char* dev_s = getenv("DMX_DEVICE");
     pthread_mutex_lock(&g_mu);
     int err = 0;
     dmx_ctx* c = dmx_cached_ctx(dev_s ? atoi(dev_s) : 0, chunk, &err);
     int r = err;
-    uint8_t* hin[2] = {NULL, NULL};
-    uint8_t* hout = NULL;
-    dmx_result* hres = NULL;
-    void* din[2] = {NULL, NULL};
-    void* dout = NULL;
     const uint64_t ocap = dmx_max_compressed(chunk, o.sw);
     if (!r) r = ctx_reserve(c, chunk / sw);
     if (!r && hip_fail(hipSetDevice(c->device), "hipSetDevice")) r = -(int)E_DEVICE;
-    for (int k = 0; !r && k < 2; k++) {
-        if (hip_fail(hipHostMalloc((void**)&hin[k], chunk + 16, 0), "hipHostMalloc")) r = -(int)E_MALLOC;
-        else if (hip_fail(hipMalloc(&din[k], chunk + 16), "hipMalloc")) r = -(int)E_DEVICE;
-    }
-    if (!r && hip_fail(hipHostMalloc((void**)&hout, ocap, 0), "hipHostMalloc")) r = -(int)E_MALLOC;
-    if (!r && hip_fail(hipHostMalloc((void**)&hres, sizeof(dmx_result), 0), "hipHostMalloc")) r = -(int)E_MALLOC;
-    if (!r && hip_fail(hipMalloc(&dout, ocap), "hipMalloc")) r = -(int)E_DEVICE;
+    if (!r) r = fd_buffers(c, chunk, ocap);
     hipStream_t s = c ? c->stream : NULL;
     int64_t len = 0;
-    int carry = -1;
-    bool eof = true;
     if (!r) {
-        len = read_chunk(fd_in, hin[0], chunk, &carry, &eof);
+        len = fd_read_chunk(&R, c->fd_hin[0], chunk);
         if (len < 0) r = (int)len;
     }
     uint32_t adler = 1;
-    uint64_t total = 0;
+    WriteJob wj[2];
+    pthread_t wt[2];
+    bool wact[2] = {false, false};
     for (uint64_t i = 0; !r; i++) {
         const int cur = (int)(i & 1);
-        const bool last = eof;
+        const bool last = R.eof;
         dmx_opts oc = o;
         oc.flags = pflags | (i == 0 ? DMX_F_HEADER : 0u) | (last ? DMX_F_FINAL : 0u);
         oc.dict = NULL;
         oc.dict_len = 0;
         if ((pflags & DMX_F_DICT) && i > 0) {      // the previous chunk's tail (still on the device)
-            oc.dict = (const uint8_t*)din[cur ^ 1] + (chunk - sw);
+            oc.dict = (const uint8_t*)c->fd_din[cur ^ 1] + (chunk - sw);
             oc.dict_len = sw;
         }
-        if (len && hip_fail(hipMemcpyAsync(din[cur], hin[cur], (size_t)len, hipMemcpyHostToDevice, s), "H2D"))
+        if (len && hip_fail(hipMemcpyAsync(c->fd_din[cur], c->fd_hin[cur], (size_t)len, hipMemcpyHostToDevice, s), "H2D"))
             r = -(int)E_DEVICE;
-        if (!r) r = dmx_encode_async(c, din[cur], (uint64_t)len, dout, ocap, &oc, s);
-        if (!r) r = dmx_encode_result_async(c, hres, s);
+        if (!r) r = dmx_encode_async(c, c->fd_din[cur], (uint64_t)len, c->fd_dout, ocap, &oc, s);
+        if (!r) r = dmx_encode_result_async(c, c->fd_hres, s);
         int64_t nlen = 0;
         if (!r && !last) {   // the next chunk, read while the device encodes this one
-            nlen = read_chunk(fd_in, hin[cur ^ 1], chunk, &carry, &eof);
+            nlen = fd_read_chunk(&R, c->fd_hin[cur ^ 1], chunk);
             if (nlen < 0) r = (int)nlen;
         }
         if (!r && hip_fail(hipStreamSynchronize(s), "hipStreamSynchronize")) r = -(int)E_DEVICE;
-        if (!r && hres->status) r = hres->status;
-        if (!r && hip_fail(hipMemcpy(hout, dout, hres->out_len, hipMemcpyDeviceToHost), "D2H")) r = -(int)E_DEVICE;
-        if (!r && fd_out >= 0) r = write_full(fd_out, hout, hres->out_len);
-        if (!r) {
-            adler = dmx_adler32_combine(adler, hres->adler, (uint64_t)len);
-            total += (uint64_t)len;
+        if (!r && c->fd_hres->status) r = c->fd_hres->status;
+        const uint64_t olen = r ? 0 : c->fd_hres->out_len;
+        const uint32_t cadl = r ? 0 : c->fd_hres->adler;
+        if (wact[cur]) {   // writer i-2 used this buffer (writer i-1 waited for it already)
+            pthread_join(wt[cur], NULL);
+            wact[cur] = false;
+            if (!r && wj[cur].rc) r = wj[cur].rc;
         }
+        if (!r && hip_fail(hipMemcpy(c->fd_hout[cur], c->fd_dout, olen, hipMemcpyDeviceToHost), "D2H")) r = -(int)E_DEVICE;
+        if (wact[cur ^ 1]) {   // in order: writer i starts after writer i-1
+            pthread_join(wt[cur ^ 1], NULL);
+            wact[cur ^ 1] = false;
+            if (!r && wj[cur ^ 1].rc) r = wj[cur ^ 1].rc;
+        }
+        if (!r && fd_out >= 0) {
+            wj[cur] = {fd_out, c->fd_hout[cur], olen, 0};
+            if (pthread_create(&wt[cur], NULL, write_job, &wj[cur]) == 0) wact[cur] = true;
+            else r = write_full(fd_out, c->fd_hout[cur], olen);
+        }
+        if (!r) adler = dmx_adler32_combine(adler, cadl, (uint64_t)len);
         if (last) break;
         len = nlen;
     }
+    for (int k = 0; k < 2; k++)
+        if (wact[k]) {
+            pthread_join(wt[k], NULL);
+            if (!r && wj[k].rc) r = wj[k].rc;
+        }
     if (!r && fd_out >= 0) {
-        uint8_t tail[6];
-        int nt = 0;
-        tail[nt++] = (uint8_t)(adler >> 24);
-        tail[nt++] = (uint8_t)(adler >> 16);
-        tail[nt++] = (uint8_t)(adler >> 8);
-        tail[nt++] = (uint8_t)adler;
-        r = write_full(fd_out, tail, (uint64_t)nt);
+        const uint8_t tail[4] = {(uint8_t)(adler >> 24), (uint8_t)(adler >> 16), (uint8_t)(adler >> 8), (uint8_t)adler};
+        r = write_full(fd_out, tail, 4);
     }
-    (void)total;
-    for (int k = 0; k < 2; k++) {
-        if (hin[k]) (void)hipHostFree(hin[k]);
-        if (din[k]) (void)hipFree(din[k]);
-    }
-    if (hout) (void)hipHostFree(hout);
-    if (hres) (void)hipHostFree(hres);
-    if (dout) (void)hipFree(dout);
+    if (R.seekable) (void)lseek(fd_in, (off_t)R.off, SEEK_SET);   // consumed, as read() would leave it
     pthread_mutex_unlock(&g_mu);
     return r;
 }

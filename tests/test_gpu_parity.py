@@ -321,3 +321,48 @@ def test_fd_api_streaming_chunks(tmp_path, n, mode):
         one = O.compress(text, **kw)
         nchunks = (n + (1 << 20) - 1) >> 20
         assert abs(len(z) - len(one)) <= 8 * nchunks
+
+
+@pytest.mark.parametrize("n", [0, 5000, 1 << 20, (5 << 19) + 3])
+def test_fd_api_streaming_pipes_and_offsets(tmp_path, n):
+    """The streaming fd path on pipes (read() + one-byte lookahead, output through a pipe)
+    and on a regular file read from a non-zero offset (parallel preads from there; the
+    offset is left at EOF, as read() would leave it)."""
+    import os
+    import threading
+    text = D.gen_text(max(n, 1), 77).tobytes()[:n]
+    env = {"DMX_CHUNK_MB": "1", "DMX_MAX_CHAIN": "8", "DMX_LAZY": "1"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        # pipes in and out
+        ri, wi = os.pipe()
+        ro, wo = os.pipe()
+        got = []
+        feeder = threading.Thread(target=lambda: (os.write(wi, text) if text else None, os.close(wi)))
+        reader = threading.Thread(target=lambda: got.append(b"".join(iter(lambda: os.read(ro, 1 << 16), b""))))
+        feeder.start()
+        reader.start()
+        rc = D.deflate_compress(ri, wo, -1, 32768, 0)
+        os.close(wo)
+        feeder.join()
+        reader.join()
+        os.close(ri)
+        os.close(ro)
+        assert rc == 0
+        assert zlib.decompress(got[0]) == text
+        # regular file from an offset
+        fi, fo = tmp_path / "in", tmp_path / "out"
+        fi.write_bytes(b"HEADER----" + text)
+        with open(fi, "rb") as a, open(fo, "wb") as b:
+            assert os.read(a.fileno(), 10) == b"HEADER----"
+            assert D.deflate_compress(a.fileno(), b.fileno(), -1, 32768, 0) == 0
+            assert os.lseek(a.fileno(), 0, os.SEEK_CUR) == 10 + n
+        z = fo.read_bytes()
+        assert zlib.decompress(z) == text
+        assert z == got[0]   # same framing whichever reader ran
+        if n <= 1 << 20:
+            assert z == O.compress(text, max_chain=8, lazy=True)
+    finally:
+        for k, v in old.items():
+            os.environ.pop(k, None) if v is None else os.environ.__setitem__(k, v)
