@@ -489,6 +489,22 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
                 const bool bad = act && ei >= 1 && pn > i && dmx_hash(dn & 0xFFFFFFu) == dmx_hash(i0 & 0xFFFFFFu);
                 if (__ballot(bad)) L.sortbad = 1;
             }
+            if (RUNS) {
+                // inside a run: when the distance-1 match already has the longest possible
+                // length, it is the answer (entry k-1 is position i-1 -- same trigram, so the
+                // same bucket, and no position lies between them -- and nearest wins ties).
+                // A chunk whose lanes all end here skips the candidate steps.
+                bool rdone = false;
+                uint32_t rkey = 0;
+                if (act && i >= 1 && run_len(L, i, lim_eff) >= lim_eff) {
+                    rkey = (lim_eff << 15) | (i - 1);
+                    rdone = true;
+                }
+                if (__ballot(act && !rdone) == 0) {
+                    if (act) store_result<DICT>(L, pg, k, i, rkey, hbk);
+                    continue;
+                }
+            }
             if (base == 0) cand_steps_emb<true, true>(K, i0, i1, i2, nc, lim_eff, jkey, full);
             else if (__ballot(act && lim_eff < CB)) cand_steps_emb<false, true>(K, i0, i1, i2, nc, lim_eff, jkey, full);
             else cand_steps_emb<false, false>(K, i0, i1, i2, nc, lim_eff, jkey, full);
