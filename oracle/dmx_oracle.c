@@ -634,43 +634,48 @@ static void orc_plan_split(const uint32_t* tok, int ntok, int bn, orc_split_plan
 /* ---- 7b. incompressible-block check (DMX_F_STORE_CHECK) --------------
  *
  * An encoder policy, not part of the reference (whose parse always runs): a block is
- * emitted stored, without a parse, when its bytes look like noise by two integer
+ * emitted stored, without a parse, when its bytes look like noise by three integer
  * statistics both sides compute exactly:
- *   S2   = sum over byte values c of h[c]^2            (h = byte histogram of the block)
- *   coll = (bn - 3) - |{ g(p) : 0 <= p <= bn - 4 }|    (g = 18-bit hash of the 4 bytes at p,
- *          (d[p] | d[p+1] << 8 | d[p+2] << 16 | d[p+3] << 24) * 0x9E3779B1 >> 14)
  *   ones_k = number of bytes with bit k set, k = 0..7
- * stored iff bn >= 1024, 8 * |2 * ones_k - bn| <= bn for every k (a cheap first test: text,
- * runs and anything 7-bit fail it without a histogram), 256 * S2 <= bn^2 + bn^2 / 16 + 256 * bn (noise gives about
- * bn^2 + 255 * bn: the byte distribution is within 6 % of flat in collision entropy) and 64 * coll <= 5 * bn (4-byte repeats at most about
- * what 2^18 buckets give noise: 1 962 expected at bn = 32 768, threshold 2 560).  A block
- * of repeats with a flat byte histogram (0, 1, ..., 255 cycled) fails the second test.
+ *   S2     = sum over byte values c of h[c]^2, h = histogram of the bytes at EVEN positions
+ *            (m = (bn + 1) / 2 of them)
+ *   x(p)   = (d[p] | d[p+1] << 8 | d[p+2] << 16 | d[p+3] << 24) * 0x9E3779B1 (32 bits),
+ *            p = 0 .. bn - 4; the 4-gram at p is SAMPLED when bit 13 of x(p) is clear (a
+ *            content-defined half: a repeated 4-gram is sampled at both places)
+ *   q      = number of sampled positions; coll = q - |{ x(p) >> 14 : p sampled }|
+ * stored iff bn >= 4096, 8 * |2 * ones_k - bn| <= bn for every k (a cheap first test: text,
+ * runs and anything 7-bit fail it), 256 * S2 <= m^2 + m^2 / 16 + 256 * m (noise gives about
+ * m^2 + 255 m), 4 * q >= bn, and 64 * coll <= 5 * q (noise: ~512 at bn = 32 768, threshold
+ * ~1 280).  A block of repeats with a flat byte histogram (0, 1, ..., 255 cycled) fails the
+ * last test.
  */
 int dmx_oracle_store_check(const uint8_t* d, int bn) {
-    if (bn < 1024) return 0;
-    uint64_t h[256] = {0};
-    for (int k = 0; k < bn; k++) h[d[k]]++;
+    if (bn < 4096) return 0;
     for (int bit = 0; bit < 8; bit++) {   /* bit planes: every bit set in about half the bytes */
         int64_t ones = 0;
-        for (int c = 0; c < 256; c++)
-            if ((c >> bit) & 1) ones += (int64_t)h[c];
+        for (int k = 0; k < bn; k++) ones += (d[k] >> bit) & 1;
         const int64_t dev = 2 * ones - bn;
         if (8 * (dev < 0 ? -dev : dev) > bn) return 0;
     }
+    uint64_t h[256] = {0};
+    for (int k = 0; k < bn; k += 2) h[d[k]]++;
     uint64_t s2 = 0;
     for (int c = 0; c < 256; c++) s2 += h[c] * h[c];
-    const uint64_t n2 = (uint64_t)bn * (uint64_t)bn;
-    if (256 * s2 > n2 + (n2 >> 4) + 256 * (uint64_t)bn) return 0;
+    const uint64_t m = (uint64_t)(bn + 1) / 2, m2 = m * m;
+    if (256 * s2 > m2 + (m2 >> 4) + 256 * m) return 0;
     uint32_t* bm = (uint32_t*)calloc(1u << 13, sizeof(uint32_t));
-    uint64_t distinct = 0;
+    uint64_t q = 0, distinct = 0;
     for (int p = 0; p + 4 <= bn; p++) {
         const uint32_t w = (uint32_t)d[p] | (uint32_t)d[p + 1] << 8 | (uint32_t)d[p + 2] << 16 | (uint32_t)d[p + 3] << 24;
-        const uint32_t g = (w * 0x9E3779B1u) >> 14;
+        const uint32_t x = w * 0x9E3779B1u;
+        if (x & (1u << 13)) continue;
+        q++;
+        const uint32_t g = x >> 14;
         if (!(bm[g >> 5] & (1u << (g & 31)))) { bm[g >> 5] |= 1u << (g & 31); distinct++; }
     }
     free(bm);
-    const uint64_t coll = (uint64_t)(bn - 3) - distinct;
-    return 64 * coll <= 5 * (uint64_t)bn;
+    const uint64_t coll = q - distinct;
+    return 4 * q >= (uint64_t)bn && 64 * coll <= 5 * q;
 }
 
 /* ---- 8. whole stream ---------------------------------------------------------------- */

@@ -21,20 +21,23 @@ def np_store_check(block) -> bool:
     """The §4.7 rule, restated in numpy (independent of the C oracle)."""
     b = np.frombuffer(bytes(block), dtype=np.uint8)
     n = b.size
-    if n < 1024:
+    if n < 4096:
         return False
     bits = np.unpackbits(b[:, None], axis=1)
     if np.any(8 * np.abs(2 * bits.sum(axis=0).astype(np.int64) - n) > n):
         return False
-    h = np.bincount(b, minlength=256).astype(np.uint64)
+    h = np.bincount(b[0::2], minlength=256).astype(np.uint64)
     s2 = int((h * h).sum())
-    if 256 * s2 > n * n + ((n * n) >> 4) + 256 * n:
+    m = (n + 1) // 2
+    if 256 * s2 > m * m + ((m * m) >> 4) + 256 * m:
         return False
     w = (b[:-3].astype(np.uint64) | b[1:-2].astype(np.uint64) << 8 | b[2:-1].astype(np.uint64) << 16
          | b[3:].astype(np.uint64) << 24)
-    g = ((w * 0x9E3779B1) & 0xFFFFFFFF) >> 14
-    coll = (n - 3) - np.unique(g).size
-    return 64 * coll <= 5 * n
+    x = (w * 0x9E3779B1) & 0xFFFFFFFF
+    g = x[(x & (1 << 13)) == 0] >> 14
+    q = g.size
+    coll = q - np.unique(g).size
+    return 4 * q >= n and 64 * coll <= 5 * q
 
 
 def _noise(n, seed, alphabet=256):
@@ -67,9 +70,9 @@ def cases():
         "noise_hi": bytes(x | 0x40 if i % 3 == 0 else x for i, x in enumerate(_noise(32768, 10))),
         "zeros": bytes(32768),
         "text": text[:32768],
-        "short_1023": _noise(1023, 6),
-        "short_1024": _noise(1024, 7),
-        "short_3000": _noise(3000, 8),
+        "short_4095": _noise(4095, 6),
+        "short_4096": _noise(4096, 7),
+        "short_9000": _noise(9000, 8),
     }
 
 
@@ -87,8 +90,8 @@ def test_rule_matches_numpy_statement():
 def test_expected_decisions():
     c = cases()
     want = {"noise": True, "noise_248": True, "noise_232": False, "noise_rep1": True, "noise_rep8": False,
-            "cycle": False, "noise_7bit": False, "noise_hi": False, "zeros": False, "text": False, "short_1023": False, "short_1024": True,
-            "short_3000": True}
+            "cycle": False, "noise_7bit": False, "noise_hi": False, "zeros": False, "text": False, "short_4095": False, "short_4096": True,
+            "short_9000": True}
     for k, v in want.items():
         assert O.store_check(c[k]) == v, k
 
@@ -96,7 +99,7 @@ def test_expected_decisions():
 def mixed_input():
     c = cases()
     order = ["noise", "text", "noise_248", "noise_232", "cycle", "noise_7bit", "noise_hi", "noise_rep1", "noise_rep8", "zeros", "noise"]
-    return b"".join(c[k] for k in order) + c["short_3000"]
+    return b"".join(c[k] for k in order) + c["short_9000"]
 
 
 @pytest.mark.parametrize("kw", [dict(), dict(max_chain=8, lazy=True), dict(max_chain=8, lazy=True, split=True),
@@ -144,10 +147,10 @@ def test_gpu_stream_equals_oracle(enc, k, lazy, split, dct):
 
 
 @gpu
-@pytest.mark.parametrize("sw", [1024, 1500, 4096, 32767])
+@pytest.mark.parametrize("sw", [1024, 4096, 5000, 32767])
 def test_gpu_windows_and_edges(enc, sw):
     data = mixed_input()[:200003]
-    for n in (0, 1, 1023, 1024, 1025, sw, sw + 1, 3 * sw + 999, len(data)):
+    for n in (0, 1, 4095, 4096, 4097, sw, sw + 1, 3 * sw + 999, len(data)):
         d = data[:n]
         z, _ = enc.compress_bytes(d, sw=sw, max_chain=8, flags=D.DMX_ZLIB | D.DMX_F_STORE_CHECK | D.DMX_F_LAZY)
         assert z == O.compress(d, sw=sw, max_chain=8, lazy=True, store_check=True), (sw, n)
