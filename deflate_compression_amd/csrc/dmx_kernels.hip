@@ -1614,23 +1614,43 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
         wsync();
         return;
     }
-    // rank among the used symbols: compare with every key, broadcast by readlane
-    uint32_t rk[NR];
+    // rank among the used symbols: the used keys are compacted first (S.code is free until
+    // canon_codes), so the broadcast loop runs over the m used keys only, not all n slots
+    const uint32_t nru = (m + 63) >> 6;   // registers holding used keys
+    {
+        uint32_t base = 0;
 #pragma unroll
-    for (int r = 0; r < NR; r++) rk[r] = 0;
+        for (int r = 0; r < NR; r++) {
+            const bool u = key[r] != 0xFFFFFFFFu;
+            const uint64_t um = __ballot(u);
+            if (u) S.code[base + (uint32_t)__popcll(um & ((1ull << lane) - 1ull))] = key[r];
+            base += (uint32_t)__popcll(um);
+        }
+    }
+    wsync();
+    uint32_t ck[NR], rk[NR];
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+        const uint32_t i = (uint32_t)r * 64 + lane;
+        ck[r] = i < m ? S.code[i] : 0xFFFFFFFFu;
+        rk[r] = 0;
+    }
 #pragma unroll
     for (int r2 = 0; r2 < NR; r2++) {
-        for (int l2 = 0; l2 < 64; l2++) {
-            const uint32_t k2 = __builtin_amdgcn_readlane(key[r2], l2);
+        if ((uint32_t)r2 >= nru) break;
+        const uint32_t cnt2 = min(m - 64u * (uint32_t)r2, 64u);
+        for (uint32_t l2 = 0; l2 < cnt2; l2++) {
+            const uint32_t k2 = __builtin_amdgcn_readlane(ck[r2], (int)l2);
 #pragma unroll
-            for (int r = 0; r < NR; r++) rk[r] += k2 < key[r] ? 1u : 0u;
+            for (int r = 0; r < NR; r++)
+                if ((uint32_t)r < nru) rk[r] += k2 < ck[r] ? 1u : 0u;
         }
     }
 #pragma unroll
     for (int r = 0; r < NR; r++)
-        if (key[r] != 0xFFFFFFFFu) {
-            S.fs[rk[r]] = key[r] >> 9;
-            S.sym[rk[r]] = (uint16_t)(key[r] & 511u);
+        if (ck[r] != 0xFFFFFFFFu) {
+            S.fs[rk[r]] = ck[r] >> 9;
+            S.sym[rk[r]] = (uint16_t)(ck[r] & 511u);
         }
     for (int k = (int)lane; k < 64; k += 64) S.blc[k] = 0;
     wsync();
