@@ -3399,6 +3399,7 @@ extern "C" int dmx_encode_fd(int fd_in, int fd_out, const dmx_opts* opts, uint64
         r = write_full(fd_out, tail, 4);
     }
     if (R.seekable) (void)lseek(fd_in, (off_t)R.off, SEEK_SET);   // consumed, as read() would leave it
+    if (r && c && s) (void)hipStreamSynchronize(s);   // an error left copies in flight from the cached buffers
     pthread_mutex_unlock(&g_mu);
     return r;
 }
