@@ -139,8 +139,9 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="text", choices=sorted(WORKLOADS))
     ap.add_argument("--bytes", type=int, default=0, help="override bytes per rank")
-    ap.add_argument("--max-chain", type=int, default=int(os.environ.get("DMX_MAX_CHAIN", "8")),
-                    help="0 = exhaustive (reference parse); K = K newest chain entries (default 8)")
+    ap.add_argument("--max-chain", type=int, default=int(os.environ.get("DMX_MAX_CHAIN", "6")),
+                    help="0 = exhaustive (reference parse); K = K newest chain entries (default 6: the "
+                         "fastest setting inside the <= 2 %% size budget on C3 text, +1.32 %% vs S_ref)")
     ap.add_argument("--lazy", type=int, default=int(os.environ.get("DMX_LAZY", "1")),
                     help="1 = lazy evaluation parse (DMX_F_LAZY, SURVEY §8 f2)")
     ap.add_argument("--split", type=int, default=int(os.environ.get("DMX_SPLIT", "0")),
@@ -150,6 +151,9 @@ def main() -> int:
     ap.add_argument("--dict", type=int, default=int(os.environ.get("DMX_DICT", "0")),
                     help="1 = cross-block dictionary (DMX_F_DICT, SURVEY §8 f1); N > 1: halo exchange of "
                          "the block before each shard inside the step")
+    ap.add_argument("--tradeoff", default="4,8,16",
+                    help="N = 1: also time these max_chain values (same flags) for the speed/size curve "
+                         "(reported under 'tradeoff'; '' = skip)")
     ap.add_argument("--exhaustive-steps", type=int, default=3,
                     help="also time this many exhaustive-parse steps (reported under 'exhaustive')")
     ap.add_argument("--gather", default="root", choices=["root", "root-sync", "all", "none"],
@@ -338,6 +342,24 @@ def main() -> int:
     stage_ms, nstage = enc.stage_times()
     enc.set_timing(False)
     dt = t1 - t0
+    # the speed / size curve over max_chain, same input and flags (outside the timed region)
+    tradeoff = []
+    if world == 1 and args.tradeoff and not pipelined:
+        for kc in [int(x) for x in args.tradeoff.split(",") if x.strip()]:
+            if kc == args.max_chain:
+                continue
+            te = D.Encoder(local, n, 32768, kc, flags)
+            te.encode_async(d_in.data_ptr(), n, d_out.data_ptr(), cap, stream)
+            t_len = int(te.result(stream).out_len)
+            torch.cuda.synchronize(dev)
+            q0 = time.perf_counter()
+            for _ in range(5):
+                te.encode_async(d_in.data_ptr(), n, d_out.data_ptr(), cap, stream)
+            torch.cuda.synchronize(dev)
+            q1 = time.perf_counter()
+            te.close()
+            tradeoff.append({"max_chain": kc, "value": round(n * 5 / (q1 - q0) / 1e9, 3), "unit": "GB/s",
+                             "ratio": round(t_len / n, 5), "compressed_bytes": t_len, "steps": 5})
     exh = None
     if world == 1 and args.max_chain != 0 and args.exhaustive_steps > 0:
         # the reference's own parse (every earlier position of the bucket), same input
@@ -396,6 +418,8 @@ def main() -> int:
         if "s_ref" in cpu and cpu["s_ref"][0] == n:
             s_ref_bytes = cpu["s_ref"][1]
             size_pct = round((out_len / s_ref_bytes - 1) * 100, 3)
+            for t in tradeoff:
+                t["size_vs_ref_pct"] = round((t["compressed_bytes"] / s_ref_bytes - 1) * 100, 3)
         line = {
             "metric": "encode GB/s (uncompressed in) + compression ratio vs CPU ref, 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -423,6 +447,7 @@ def main() -> int:
             "size_vs_ref_pct": size_pct,
             "s_ref_bytes": s_ref_bytes,
             "exhaustive": exh,
+            "tradeoff": tradeoff or None,
             "compressed_bytes_rank0": out_len,
             "inflate_ok": ok,
             "gpu_inflate": gpu_inflate,

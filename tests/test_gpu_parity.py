@@ -100,7 +100,7 @@ def test_config_c2_zeros(enc):
     assert len(z) <= 1.02 * 1466
 
 
-@pytest.mark.parametrize("k", [1, 2, 4, 16, 64])
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 6, 7, 16, 64])
 def test_bounded_chain_parity(enc, k):
     data = D.gen_text(300000, 11).tobytes()
     z, _ = enc.compress_bytes(data, max_chain=k)
@@ -108,7 +108,7 @@ def test_bounded_chain_parity(enc, k):
     check_stream(z, data)
 
 
-@pytest.mark.parametrize("k", [0, 1, 4, 8, 16])
+@pytest.mark.parametrize("k", [0, 1, 4, 6, 8, 16])
 def test_lazy_parity(enc, golden_cases, k):
     """DMX_F_LAZY: byte-identical to the oracle's sequential lazy parse."""
     data = (golden_cases["bee0"] + D.gen_text(200000, 12).tobytes() + bytes(5000)
@@ -118,7 +118,7 @@ def test_lazy_parity(enc, golden_cases, k):
     check_stream(z, data)
 
 
-@pytest.mark.parametrize("k", [0, 8, 16])
+@pytest.mark.parametrize("k", [0, 6, 8, 16])
 def test_exact_sort_fallback_parity(enc, golden_cases, k):
     """The match-any sort (the fallback if lane-ordered LDS atomics ever misorder) gives the
     same stream as the fast sort and the oracle."""
@@ -267,7 +267,7 @@ def _run_heavy(seed=7):
     return b"".join(parts)
 
 
-@pytest.mark.parametrize("k", [1, 2, 4, 8])
+@pytest.mark.parametrize("k", [1, 2, 4, 6, 8])
 @pytest.mark.parametrize("lazy", [False, True])
 def test_run_dominated_blocks(enc, k, lazy):
     """Run-dominated blocks search with the change bitmap (run_len, bounded mode K <= 8):
