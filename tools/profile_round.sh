@@ -10,7 +10,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-BA="--cpu-budget 0 --exhaustive-steps 0 $*"
+BA="--cpu-budget 0 --exhaustive-steps 0 --tradeoff= $*"
 echo "[1/5] pytest -m gpu"; timeout -k 10 900 python3 -u -m pytest "$R/tests" -m gpu -x -q -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
 tail -2 "$OUT/pytest_gpu.log"
 echo "[2/5] kernel trace"; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 $BA > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
