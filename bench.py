@@ -389,7 +389,7 @@ def main() -> int:
         ms_step = dt / args.steps * 1e3
         value = tot_in * args.steps / dt / 1e9
         dom = max((k for k in stage_ms if k != "total"), key=stage_ms.get)
-        kname = {"pre": "dmx_hist_kernel" if args.dict else "dmx_store_check_kernel", "huff": "dmx_split_plan_kernel" if args.split else "dmx_huff_kernel"}.get(
+        kname = {"pre": "dmx_hist_kernel_t" if args.dict else "dmx_store_check_kernel", "huff": "dmx_split_plan_kernel" if args.split else "dmx_huff_kernel"}.get(
             dom, f"dmx_{dom}_kernel")
         dom_ms = stage_ms[dom]
         algo_bytes = n + out_len   # per launch on this rank: input read + stream written

@@ -855,7 +855,6 @@ __device__ __forceinline__ void sort_positions(MatchLDS& L, uint32_t bn, int32_t
 //                         (store_result) and overwrites with tokens in P3.
 // Chain slots: slot 0 = the dict (block "-1"), slot b + 1 = block b.
 // ------------------------------------------------------------------------------------
-#define HG 8   // history candidates per group
 #define TB8(W, i) (reinterpret_cast<const uint8_t*>(W)[i])
 
 // Stage bytes src[0, len) at LDS word array W (16-byte chunks, zero padded to nwords).
@@ -942,7 +941,12 @@ struct __attribute__((aligned(16))) HistLDS {
     uint32_t cur[DMX_BLK / 4 + 80];   // the block (targets), zero padded
 };
 
-__global__ __launch_bounds__(MT) void dmx_hist_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
+// HG = history candidates per group.  HG = 6 (K <= 6, the bench default) fits 62 VGPRs: 8
+// waves per SIMD, two 16-wave workgroups per CU as the 66 KB of LDS allow (C3, K=6: history
+// stage 1.88 -> 1.53 ms); HG = 8 needs 78 VGPRs (one workgroup per CU) and serves K > 6 in
+// fewer groups.
+template <int HG>
+__global__ __launch_bounds__(MT) void dmx_hist_kernel_t(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
                                                       int32_t max_chain, const uint8_t* __restrict__ pre, uint32_t npre,
                                                       const uint16_t* __restrict__ chs, const uint16_t* __restrict__ che,
                                                       uint32_t* __restrict__ hb_g, uint64_t* __restrict__ dbg) {
@@ -2915,7 +2919,8 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         if (o.flags & DMX_F_DICT) {
             hipLaunchKernelGGL(dmx_chain_kernel, dim3(nblk + 1), dim3(MT), 0, s, (const uint8_t*)d_in, n,
                                (uint32_t)o.sw, (const uint8_t*)o.dict, dict_len, c->chs, c->che);
-            hipLaunchKernelGGL(dmx_hist_kernel, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw,
+            hipLaunchKernelGGL((o.max_chain >= 1 && o.max_chain <= 6) ? dmx_hist_kernel_t<6> : dmx_hist_kernel_t<8>,
+                               dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw,
                                o.max_chain, (const uint8_t*)o.dict, dict_len, c->chs, c->che, c->tok, dbg);
         }
         // stage 0 also holds K0, the noise check (DMX_F_STORE_CHECK)
