@@ -1048,9 +1048,11 @@ __global__ __launch_bounds__(MT) void dmx_hist_kernel_t(const uint8_t* __restric
 
 // K0 (DMX_F_STORE_CHECK): the noise check of every block, so that noise
 // blocks skip the parse and go out stored.  One 256-thread workgroup per block.
-//   pass 1: stream the block from HBM once (16 B per thread and step): the 8 bit-plane
-//           counts (v_bcnt on masked words, registers only) and the Adler-32 partial sums.
-//           Text, runs and 7-bit data fail the bit-plane test here and leave.
+//   pass 0: the 8 bit-plane counts of the first 4096 bytes (one 16-byte load per thread,
+//           v_bcnt on masked words).  Text, runs and 7-bit data fail here and leave, having
+//           read an eighth of the block.
+//   pass 1: the whole block into registers (8 loads per thread in flight), Adler-32
+//           partial sums (v_sad_u8, v_dot4_u32_u8).
 //   pass 2 (noise-like blocks only; full blocks from the registers of pass 1): byte
 //           histogram of the even positions and 18-bit presence bitmap of the 4-grams
 //           sampled by content (bit 13 of their hash clear), LDS atomics (33 KB, several
@@ -1059,6 +1061,7 @@ __global__ __launch_bounds__(MT) void dmx_hist_kernel_t(const uint8_t* __restric
 // skips it and the Huffman kernels leave it alone.  Same integer rule as
 // dmx_oracle_store_check.
 #define SCT 256
+#define SC_PLANE 4096   // bytes of the bit-plane test (SCT x 16: one load per thread)
 __device__ __forceinline__ void sc_load(const uint8_t* d, uint32_t p, uint32_t bn, bool aligned16, uint32_t w[5]) {
     if (aligned16 && p + 20 <= bn) {
         const uint4 v = *reinterpret_cast<const uint4*>(d + p);
@@ -1088,15 +1091,44 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
         return;
     }
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
-    // ---- pass 1: bit planes + Adler sums ----
-    uint32_t ones[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // ---- pass 0: bit planes of the first 4096 bytes, one 16-byte load per thread ----
+    {
+        uint32_t w[5];
+        sc_load(d, tid << 4, bn, aligned16, w);
+        uint32_t ones[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            ones[k] = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) ones[k] += __builtin_popcount(w[q] & (0x01010101u << k));
+            ones[k] = wave_sum_u32(ones[k]);
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) red[k][wave] = ones[k];
+        }
+        __syncthreads();
+        if (tid == 0) {
+            bool ok = true;
+            for (int k = 0; k < 8; k++) {
+                int64_t o = 0;
+#pragma unroll
+                for (int w2 = 0; w2 < SCT / 64; w2++) o += (int64_t)red[k][w2];
+                const int64_t dv = 2 * o - (int64_t)SC_PLANE;
+                ok = ok && 8 * (dv < 0 ? -dv : dv) <= (int64_t)SC_PLANE;
+            }
+            pass_s = ok ? 1u : 0u;
+            if (!ok) info[b].prestored = 0;
+        }
+        __syncthreads();
+        if (!pass_s) return;
+    }
+    // ---- pass 1: Adler sums (the block's data into registers for pass 2) ----
     uint64_t s = 0, t = 0;
     auto chunk1 = [&](uint32_t p, const uint32_t* w) {   // 16 bytes at block offset p
         uint32_t ts = 0, tt = 0;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-#pragma unroll
-            for (int k = 0; k < 8; k++) ones[k] += __builtin_popcount(w[q] & (0x01010101u << k));
             ts = __builtin_amdgcn_sad_u8(w[q], 0u, ts);                                  // sum of bytes
             tt = __builtin_amdgcn_udot4(w[q], 0x03020100u + 0x04040404u * q, tt, false);  // sum of j * byte
         }
@@ -1127,31 +1159,12 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
             chunk1(p, w);
         }
     }
-#pragma unroll
-    for (int k = 0; k < 8; k++) ones[k] = wave_sum_u32(ones[k]);
     s = wave_sum_u64(s);
     t = wave_sum_u64(t);
     if (lane == 0) {
-#pragma unroll
-        for (int k = 0; k < 8; k++) red[k][wave] = ones[k];
         red[8][wave] = s;
         red[9][wave] = t;
     }
-    __syncthreads();
-    if (tid == 0) {
-        bool ok = true;
-        for (int k = 0; k < 8; k++) {
-            int64_t o = 0;
-#pragma unroll
-            for (int w = 0; w < SCT / 64; w++) o += (int64_t)red[k][w];
-            const int64_t dv = 2 * o - (int64_t)bn;
-            ok = ok && 8 * (dv < 0 ? -dv : dv) <= (int64_t)bn;
-        }
-        pass_s = ok ? 1u : 0u;
-        if (!ok) info[b].prestored = 0;
-    }
-    __syncthreads();
-    if (!pass_s) return;
     // ---- pass 2: byte histogram + 4-gram bitmap ----
     for (uint32_t k = tid; k < (1u << 13) / 4; k += SCT) reinterpret_cast<uint4*>(bm)[k] = make_uint4(0, 0, 0, 0);
     hist[tid] = 0;   // (8 padded sub-histograms by lane & 7 measured slower: 0.59 -> 0.77 ms per GiB)

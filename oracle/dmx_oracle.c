@@ -636,26 +636,26 @@ static void orc_plan_split(const uint32_t* tok, int ntok, int bn, orc_split_plan
  * An encoder policy, not part of the reference (whose parse always runs): a block is
  * emitted stored, without a parse, when its bytes look like noise by three integer
  * statistics both sides compute exactly:
- *   ones_k = number of bytes with bit k set, k = 0..7
+ *   ones_k = number of bytes among the first 4096 with bit k set, k = 0..7
  *   S2     = sum over byte values c of h[c]^2, h = histogram of the bytes at EVEN positions
  *            (m = (bn + 1) / 2 of them)
  *   x(p)   = (d[p] | d[p+1] << 8 | d[p+2] << 16 | d[p+3] << 24) * 0x9E3779B1 (32 bits),
  *            p = 0 .. bn - 4; the 4-gram at p is SAMPLED when bit 13 of x(p) is clear (a
  *            content-defined half: a repeated 4-gram is sampled at both places)
  *   q      = number of sampled positions; coll = q - |{ x(p) >> 14 : p sampled }|
- * stored iff bn >= 4096, 8 * |2 * ones_k - bn| <= bn for every k (a cheap first test: text,
- * runs and anything 7-bit fail it), 256 * S2 <= m^2 + m^2 / 16 + 256 * m (noise gives about
+ * stored iff bn >= 4096, 8 * |2 * ones_k - 4096| <= 4096 for every k (a cheap first test on
+ * an eighth of a block: text, runs and anything 7-bit fail it), 256 * S2 <= m^2 + m^2 / 16 + 256 * m (noise gives about
  * m^2 + 255 m), 4 * q >= bn, and 64 * coll <= 5 * q (noise: ~512 at bn = 32 768, threshold
  * ~1 280).  A block of repeats with a flat byte histogram (0, 1, ..., 255 cycled) fails the
  * last test.
  */
 int dmx_oracle_store_check(const uint8_t* d, int bn) {
     if (bn < 4096) return 0;
-    for (int bit = 0; bit < 8; bit++) {   /* bit planes: every bit set in about half the bytes */
+    for (int bit = 0; bit < 8; bit++) {   /* bit planes of the first 4096 bytes: each bit set in about half */
         int64_t ones = 0;
-        for (int k = 0; k < bn; k++) ones += (d[k] >> bit) & 1;
-        const int64_t dev = 2 * ones - bn;
-        if (8 * (dev < 0 ? -dev : dev) > bn) return 0;
+        for (int k = 0; k < 4096; k++) ones += (d[k] >> bit) & 1;
+        const int64_t dev = 2 * ones - 4096;
+        if (8 * (dev < 0 ? -dev : dev) > 4096) return 0;
     }
     uint64_t h[256] = {0};
     for (int k = 0; k < bn; k += 2) h[d[k]]++;

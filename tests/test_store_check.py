@@ -23,8 +23,8 @@ def np_store_check(block) -> bool:
     n = b.size
     if n < 4096:
         return False
-    bits = np.unpackbits(b[:, None], axis=1)
-    if np.any(8 * np.abs(2 * bits.sum(axis=0).astype(np.int64) - n) > n):
+    bits = np.unpackbits(b[:4096, None], axis=1)
+    if np.any(8 * np.abs(2 * bits.sum(axis=0).astype(np.int64) - 4096) > 4096):
         return False
     h = np.bincount(b[0::2], minlength=256).astype(np.uint64)
     s2 = int((h * h).sum())
