@@ -2499,6 +2499,7 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply_kernel(dmx_blkinfo* 
 
 #define PT 256
 #define TPT 8   // tokens per thread per packing round
+#define PK_RING 4096   // pack ring words: > 1 + max(160 header words, 2048 tokens x 48 bits / 32) + 1
 
 __device__ __forceinline__ void st_or64(uint32_t* st, uint32_t pos, uint64_t v, uint32_t nb) {
     if (!nb) return;
@@ -2527,7 +2528,7 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
                                                       const dmx_subinfo* __restrict__ sub_g,
                                                       uint32_t nblk, uint32_t flags, uint32_t* __restrict__ out32,
                                                       dmx_result* __restrict__ res) {
-    __shared__ uint32_t stage[DMX_STAGE_WORDS];
+    __shared__ uint32_t stage[PK_RING];
     __shared__ uint32_t code[DMX_HIST];
     __shared__ uint32_t wsum[PT / 64];
     if (res->status) return;
@@ -2598,13 +2599,37 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
         if (tid == 0 && (b == 0 || b == nblk - 1)) pack_framing(out32, flags, nblk, b, res);
         return;
     }
-    for (uint32_t k = tid; k < nwords; k += PT) stage[k] = 0;
+    // coded blocks: the bits go through a 16 KB LDS ring (PK_RING words) that is flushed to
+    // the stream before every header and every round of PT x TPT tokens (<= 3 072 words per
+    // round, <= 160 header words), so the LDS per workgroup is ~18 KB (8 per CU) instead of
+    // one 33 KB buffer for the whole block (4 per CU).  `base` = block word held in stage[0];
+    // ring positions are block bit positions minus 32 * base.
+    const uint64_t gw0 = O >> 5;
+    const bool first_partial = s0 != 0;
+    const bool last_partial = ((s0 + Lb) & 31) != 0;
+    uint32_t base = 0;
+    auto out_word = [&](uint32_t k, uint32_t v) {   // block word k (shared edge words: atomicOr)
+        if ((k == 0 && first_partial) || (k == nwords - 1 && last_partial)) atomicOr(&out32[gw0 + k], v);
+        else out32[gw0 + k] = v;
+    };
+    // write the ring's complete words below block bit `pos`; the partial word moves to stage[0]
+    auto flush = [&](uint32_t pos) {
+        __syncthreads();
+        const uint32_t done = (pos >> 5) - base;
+        for (uint32_t k = tid; k < done; k += PT) out_word(base + k, stage[k]);
+        const uint32_t part = stage[done];
+        __syncthreads();
+        for (uint32_t k = tid; k <= done; k += PT) stage[k] = k == 0 ? part : 0u;
+        base += done;
+        __syncthreads();
+    };
+    for (uint32_t k = tid; k < PK_RING; k += PT) stage[k] = 0;
     for (uint32_t k = tid; k < 316; k += PT) code[k] = codes_g[(uint64_t)b * DMX_NSUB * DMX_HIST + k];
     __syncthreads();
     {   // (stored blocks left above)
         // one or more DEFLATE blocks (f3 split): header, tokens [t0, t1), end of block
         const uint32_t* tb = tok_g + (uint64_t)b * DMX_BLK;
-        uint32_t pos = s0;
+        uint32_t pos = s0;   // block bit position
         for (uint32_t sb = 0; sb < bi.nsub; sb++) {
             const uint64_t slot = (uint64_t)b * DMX_NSUB + sb;
             const dmx_subinfo si = sub_g[slot];
@@ -2613,17 +2638,19 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
                 for (uint32_t k = tid; k < 316; k += PT) code[k] = codes_g[slot * DMX_HIST + k];
                 __syncthreads();
             }
+            flush(pos);
             const uint32_t* hg = hdr_g + slot * DMX_HDR_WORDS;
             const uint32_t hb = si.hdr_bits;
             for (uint32_t k = tid; k < (hb + 31) / 32; k += PT) {
                 const uint32_t nb = (hb - 32 * k) < 32 ? (hb - 32 * k) : 32;
-                st_or64(stage, pos + 32 * k, hg[k], nb);
+                st_or64(stage, pos - 32 * base + 32 * k, hg[k], nb);
             }
             pos += hb;
             // tokens: TPT consecutive tokens per thread; a per-thread bit accumulator flushes
             // whole words -- plain stores inside the thread's own bit range, atomicOr only on
             // the first and last word, which it shares with its neighbours
             for (uint32_t c = si.t0; c < si.t1; c += PT * TPT) {
+                flush(pos);
                 const uint32_t j0 = c + tid * TPT;
                 uint32_t pv[2 * TPT], pb[2 * TPT];   // up to two pieces per token, <= 28 bits each
                 uint32_t mybits = 0;
@@ -2662,7 +2689,7 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
                     tot += t;
                 }
                 if (mybits) {
-                    const uint32_t p0 = pos + wbase + incl - mybits;
+                    const uint32_t p0 = pos - 32 * base + wbase + incl - mybits;
                     uint32_t w = p0 >> 5, ab = p0 & 31;
                     uint64_t acc = 0;
                     bool first = true;
@@ -2685,19 +2712,12 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
                 __syncthreads();
             }
             const uint32_t cw = code[256];
-            if (tid == 0) st_or64(stage, pos, cw & 0xFFFFu, cw >> 16);
+            if (tid == 0) st_or64(stage, pos - 32 * base, cw & 0xFFFFu, cw >> 16);
             pos += cw >> 16;
         }
     }
     __syncthreads();
-    const uint64_t gw0 = O >> 5;
-    const bool first_partial = s0 != 0;
-    const bool last_partial = ((s0 + Lb) & 31) != 0;
-    for (uint32_t k = tid; k < nwords; k += PT) {
-        const uint32_t v = stage[k];
-        if ((k == 0 && first_partial) || (k == nwords - 1 && last_partial)) atomicOr(&out32[gw0 + k], v);
-        else out32[gw0 + k] = v;
-    }
+    for (uint32_t k = tid; base + k < nwords; k += PT) out_word(base + k, stage[k]);
     if (tid == 0 && (b == 0 || b == nblk - 1)) pack_framing(out32, flags, nblk, b, res);
 }
 
