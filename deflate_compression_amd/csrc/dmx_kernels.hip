@@ -642,7 +642,15 @@ __device__ __forceinline__ uint64_t group_of(unsigned long long* G, uint32_t v, 
 
 // T[v] += 1 for every valid lane (pair16: T holds two u16 counters per word); a single
 // add when the valid lanes share v (runs), instead of a 64-way conflicting LDS atomic.
+template <bool RUNCHK = true>
 __device__ __forceinline__ void count_add(uint32_t* T, uint32_t v, bool valid, bool pair16) {
+    if (!RUNCHK) {   // blocks that are not run-dominated: lanes rarely share v
+        if (valid) {
+            if (pair16) atomicAdd(&T[v >> 1], 1u << (16 * (v & 1)));
+            else atomicAdd(&T[v], 1u);
+        }
+        return;
+    }
     const uint64_t vm = __ballot(valid);
     if (vm == 0) return;
     const uint32_t first = (uint32_t)__builtin_ctzll(vm);
@@ -663,7 +671,9 @@ __device__ __forceinline__ void count_add(uint32_t* T, uint32_t v, bool valid, b
 // same-address lanes of one instruction get in lane order on gfx950 (verified at run time
 // by the search, see sort_positions).  A step whose valid lanes share v (runs) takes one
 // add of the group size instead of a 64-way conflicting atomic.
+template <bool RUNCHK = true>
 __device__ __forceinline__ uint32_t atomic_rank(uint32_t* T, uint32_t v, bool valid, uint64_t lt) {
+    if (!RUNCHK) return valid ? atomicAdd(&T[v], 1u) : 0u;
     const uint64_t vm = __ballot(valid);
     if (vm == 0) return 0;
     const uint32_t first = (uint32_t)__builtin_ctzll(vm);
@@ -703,7 +713,10 @@ __device__ __forceinline__ uint32_t block_excl_scan(MatchLDS& L, uint32_t v, uin
 // same-address lanes of one instruction (tools/atomic_order.hip: 0 of ~5e9 pairs out of
 // order).  That order is not a documented guarantee, so the search verifies the result
 // (every entry against its predecessor, sortbad) and the block falls back to EXACT.
-template <bool EXACT>
+// RUNCHK: count_add / atomic_rank first test whether all lanes of a step share one digit
+// (runs), which turns a 64-way same-address atomic into one add; blocks that are not
+// run-dominated (counted while staging) skip that test (correct either way).
+template <bool EXACT, bool RUNCHK = true>
 __device__ __forceinline__ void sort_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint32_t tid, bool stamp,
                                                uint64_t* tp0) {
     const uint32_t lane = tid & 63, wave = tid >> 6;
@@ -741,7 +754,7 @@ __device__ __forceinline__ void sort_positions(MatchLDS& L, uint32_t bn, int32_t
     for (int st = 0; st < 32; st++) {
         const uint32_t x = x0l + ((uint32_t)st << 6);
         const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
-        count_add(C + (wave << 7), h & 127u, x < nvl, false);
+        count_add<RUNCHK>(C + (wave << 7), h & 127u, x < nvl, false);
     }
     __syncthreads();
     {   // destinations, digit-major: entry (dg, w) at order 16*dg + w; two per thread
@@ -767,13 +780,13 @@ __device__ __forceinline__ void sort_positions(MatchLDS& L, uint32_t bn, int32_t
             dst = c + (uint32_t)__popcll(eq & lt);
             if (valid && (eq >> lane) == 1ull) C[(wave << 7) + dg] = c + (uint32_t)__popcll(eq);
         } else {   // same-address LDS atomics return in lane order (checked, see above)
-            dst = atomic_rank(&C[wave << 7], dg, valid, lt);
+            dst = atomic_rank<RUNCHK>(&C[wave << 7], dg, valid, lt);
         }
         if (valid) {
             L.sorted[dst] = (uint16_t)x;
             D2[dst] = (uint8_t)(h >> 7);
         }
-        count_add(C2, ((dst >> 11) << 6) | (h >> 7), valid, false);   // pass 2: (wave, digit)
+        count_add<RUNCHK>(C2, ((dst >> 11) << 6) | (h >> 7), valid, false);   // pass 2: (wave, digit)
         __builtin_amdgcn_sched_barrier(0);   // keep the unrolled steps apart (register pressure)
     }
     __syncthreads();
@@ -815,7 +828,7 @@ __device__ __forceinline__ void sort_positions(MatchLDS& L, uint32_t bn, int32_t
                 if ((eq >> lane) == 1ull) C2[(wave << 6) + dg] = c + (uint32_t)__popcll(eq);
             }
         } else {
-            const uint32_t dst = atomic_rank(&C2[wave << 6], dg, valid, lt);
+            const uint32_t dst = atomic_rank<RUNCHK>(&C2[wave << 6], dg, valid, lt);
             if (valid) L.sorted[dst] = (uint16_t)p;
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -1292,7 +1305,12 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         }
         __syncthreads();
     } else {
-        sort_positions<false>(L, bn, max_chain, tid, dbg != nullptr, tp0);
+        __syncthreads();   // the waves' run counts (L.wexit) are published
+        uint32_t nrun0 = 0;
+#pragma unroll
+        for (int w = 0; w < MW; w++) nrun0 += L.wexit[w];
+        if (nrun0 * 4 >= ((bn + 15) >> 4)) sort_positions<false, true>(L, bn, max_chain, tid, dbg != nullptr, tp0);
+        else sort_positions<false, false>(L, bn, max_chain, tid, dbg != nullptr, tp0);
     }
 
     {   // Adler-32 partial sums of this block
