@@ -164,10 +164,32 @@ __device__ __forceinline__ uint32_t match_bytes(uint64_t x) {   // equal leading
 __device__ __forceinline__ uint32_t wshr(uint32_t v, uint32_t lane0) {   // lane l <- lane l-1; lane 0 <- lane0
     return (uint32_t)__builtin_amdgcn_update_dpp((int)lane0, (int)v, 0x138, 0xF, 0xF, false);
 }
-// Length of a candidate known to match bytes [0, kk): 32 more bytes per LDS round trip.
+// Length of a candidate known to match bytes [0, kk): 16 bytes in the first LDS round trip
+// (most extensions end there), then 32 per round trip.
 // Each side is read as 9 aligned words and realigned with v_alignbyte (one VALU per 4
 // bytes); the first differing word comes from a mask of non-zero xors.
 __device__ __forceinline__ uint32_t ext_len(const MatchLDS& L, uint32_t i, uint32_t q, uint32_t kk, uint32_t lim) {
+    {   // first round: 16 bytes (5 aligned words per side) -- most extensions end there
+        const uint32_t a = (i + kk) >> 2, sa = (i + kk) & 3, c = (q + kk) >> 2, sc = (q + kk) & 3;
+        uint32_t wa[5], wc[5];
+#pragma unroll
+        for (int t = 0; t < 5; t++) { wa[t] = L.data[a + t]; wc[t] = L.data[c + t]; }
+        uint32_t x[4], nz = 0;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            x[t] = __builtin_amdgcn_alignbyte(wa[t + 1], wa[t], sa) ^ __builtin_amdgcn_alignbyte(wc[t + 1], wc[t], sc);
+            nz |= (x[t] != 0 ? 1u : 0u) << t;
+        }
+        if (nz) {
+            const uint32_t t0 = (uint32_t)__builtin_ctz(nz);
+            uint32_t xv = x[0];
+#pragma unroll
+            for (int t = 1; t < 4; t++) xv = (t0 == (uint32_t)t) ? x[t] : xv;
+            return kk + 4 * t0 + ((uint32_t)__builtin_ctz(xv) >> 3);
+        }
+        kk += 16;
+        if (kk >= lim) return kk;
+    }
     for (;;) {
         const uint32_t a = (i + kk) >> 2, sa = (i + kk) & 3, c = (q + kk) >> 2, sc = (q + kk) & 3;
         uint32_t wa[9], wc[9];
