@@ -21,6 +21,8 @@
 
 /* from dmx_kernels.hip */
 dmx_ctx* dmx_cached_ctx(int device, uint64_t max_input, int* err);
+void dmx_cached_lock(void);
+void dmx_cached_unlock(void);
 
 struct deflate_compr {
     int fd_in, fd_out, fd_stats;
@@ -188,6 +190,7 @@ int deflate_compress(int fd_in, int fd_out, int fd_stats, swi sw, int ops) {
     uint8_t* out = (uint8_t*)malloc(cap);
     if (!out) { free(in); return -E_MALLOC; }
     uint64_t out_len = 0;
+    dmx_cached_lock();   /* the stats read this encode's tokens back from the cached context */
     r = dmx_encode_host(in, n, out, cap, &out_len, &o);
     if (!r && fd_out >= 0) r = write_all(fd_out, out, out_len);
     if (!r && fd_stats >= 0) {
@@ -196,6 +199,7 @@ int deflate_compress(int fd_in, int fd_out, int fd_stats, swi sw, int ops) {
         dmx_ctx* c = dmx_cached_ctx(dev_s ? atoi(dev_s) : 0, n, &err);
         r = c ? write_stats(c, fd_stats, n, swv) : err;
     }
+    dmx_cached_unlock();
     free(in);
     free(out);
     return r;

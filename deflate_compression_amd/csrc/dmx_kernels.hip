@@ -3169,7 +3169,13 @@ extern "C" int dmx_last_subblock(dmx_ctx* c, uint32_t blk, uint32_t sub, uint32_
 // --- host-buffer convenience on a cached context per device ---
 
 #include <pthread.h>
-static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
+// Guards the cached per-device contexts (dmx_encode_host, dmx_encode_fd, the fd API).
+// Recursive: deflate_compress with fd_stats holds it across the encode and the token
+// introspection that follows (dmx_cached_lock / dmx_cached_unlock), so no other caller's
+// encode lands in between.
+static pthread_mutex_t g_mu = PTHREAD_RECURSIVE_MUTEX_INITIALIZER_NP;
+extern "C" void dmx_cached_lock(void) { pthread_mutex_lock(&g_mu); }
+extern "C" void dmx_cached_unlock(void) { pthread_mutex_unlock(&g_mu); }
 static dmx_ctx* g_ctx[64];
 
 extern "C" dmx_ctx* dmx_cached_ctx(int device, uint64_t max_input, int* err) {

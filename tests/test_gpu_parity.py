@@ -229,6 +229,38 @@ def test_fd_api_and_stats(tmp_path, golden_cases):
     assert O.replay(rt[: O.parse_block(data[:32768]).size]) == data[:32768]
 
 
+def test_fd_api_stats_concurrent(tmp_path, golden_cases):
+    """Two threads calling deflate_compress with fd_stats at once: the cached context is
+    held across each call's encode and its token read-back, so every call's records are
+    its own input's tokens."""
+    import threading
+    inputs = [golden_cases["bee0"] + golden_cases["bee1"], D.gen_text(70000, 91).tobytes()]
+    res = [None, None]
+
+    def run(j):
+        fi, fo, fs = tmp_path / f"in{j}", tmp_path / f"out{j}", tmp_path / f"st{j}"
+        fi.write_bytes(inputs[j])
+        for _ in range(4):
+            with open(fi, "rb") as a, open(fo, "wb") as b, open(fs, "wb") as c:
+                rc = D.deflate_compress(a.fileno(), b.fileno(), c.fileno(), 32768, 0)
+            st = np.frombuffer(fs.read_bytes(), dtype="<i4").reshape(-1, 6)
+            ll, d = st[:, 4].astype(np.uint32), st[:, 5].astype(np.uint32)
+            rt = np.where(d == 0, ll, (d << 9) | ll).astype(np.uint32)
+            ok = rc == 0 and fo.read_bytes() == O.compress(inputs[j]) and \
+                np.array_equal(rt, np.concatenate(O.parse(inputs[j])))
+            if not ok:
+                res[j] = False
+                return
+        res[j] = True
+
+    th = [threading.Thread(target=run, args=(j,)) for j in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert res == [True, True]
+
+
 def test_fd_api_errors(tmp_path):
     fi = tmp_path / "in"
     fi.write_bytes(b"abc")
