@@ -1290,6 +1290,8 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
     for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) L.lit[k] = 0;
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
     uint32_t runny = 0;   // 16-byte chunks of one repeated byte (run-dominated blocks)
+    const uint32_t c4 = bn ? (uint32_t)d[0] * 0x01010101u : 0u;
+    bool uni = true;      // every byte of the block equals byte 0
     for (uint32_t k = tid; k < DATA_WORDS / 4; k += MT) {   // 16-byte chunks
         const uint32_t p = k << 4;
         uint4 v;
@@ -1305,6 +1307,12 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         // run-dominated blocks take the run_len search (search_positions<.., true>): count the
         // 16-byte chunks that are one repeated byte
         runny += (p < bn && v.x == v.y && v.y == v.z && v.z == v.w && v.x == (v.x & 0xFFu) * 0x01010101u) ? 1u : 0u;
+        if (p + 16 <= bn) {
+            uni = uni && v.x == c4 && v.y == c4 && v.z == c4 && v.w == c4;
+        } else if (p < bn) {   // the tail chunk: its bytes below bn
+            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+            for (uint32_t j = 0; j < bn - p; j++) uni = uni && ((w4[j >> 2] >> (8 * (j & 3))) & 0xFFu) == (c4 & 0xFFu);
+        }
     }
     runny = wave_sum_u32(runny);
     if (lane == 0) L.wexit[wave] = runny;   // free until the walk; published by the barriers below
@@ -1327,7 +1335,45 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         }
         __syncthreads();
     } else {
-        __syncthreads();   // the waves' run counts (L.wexit) are published
+        // a block of one repeated byte (no dictionary): the parse is known in closed form --
+        // a literal, then distance-1 matches of min(258, bytes left) while >= 3 bytes are
+        // left, then literals -- which is exactly what the search + walk would produce
+        // (position i's nearest candidate is i - 1, matching to the block's end; lazy
+        // evaluation never defers: i + 1 is never longer).  Tokens, histograms and the
+        // block record are written directly.
+        if (__syncthreads_and(uni)) {   // (also publishes the waves' run counts)
+            const uint32_t c = c4 & 0xFFu;
+            if (tid == 0) {
+                uint32_t* tb = tok_g + (uint64_t)b * DMX_BLK;
+                uint32_t nt = 0;
+                for (uint32_t p = 0; p < bn;) {
+                    const uint32_t r = bn - p;
+                    if (p >= 1 && r >= 3) {
+                        const uint32_t len = r < MAXLEN ? r : MAXLEN;
+                        tb[nt++] = (1u << 9) | len;
+                        uint32_t sy, eb, ev;
+                        len_sym(len, sy, eb, ev);
+                        L.hist[sy]++;
+                        dist_sym(1u, sy, eb, ev);
+                        L.hist[DMX_DIST0 + sy]++;
+                        p += len;
+                    } else {
+                        tb[nt++] = c;
+                        L.hist[c]++;
+                        p++;
+                    }
+                }
+                const uint64_t S = (uint64_t)c * bn, T = (uint64_t)c * ((uint64_t)bn * (bn - 1) / 2);
+                info[b].ntok = nt;
+                info[b].n = bn;
+                info[b].adl_s = S;
+                info[b].adl_w = (uint64_t)bn * S - T;
+                info[b].prestored = 0;
+            }
+            __syncthreads();
+            for (uint32_t k = tid; k < DMX_HIST; k += MT) hist_g[(uint64_t)b * DMX_HIST + k] = L.hist[k];
+            return;
+        }
         uint32_t nrun0 = 0;
 #pragma unroll
         for (int w = 0; w < MW; w++) nrun0 += L.wexit[w];
