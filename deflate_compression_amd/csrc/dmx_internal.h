@@ -26,7 +26,8 @@ typedef struct {
     uint64_t off_bits;  /* scan kernel: absolute bit offset of the block in the output */
     uint64_t len_bits;  /* scan kernel: bits the block occupies (stored: incl. padding) */
     uint32_t nsub;      /* huff kernel: DEFLATE blocks emitted for this block (1..4, f3 split) */
-    uint32_t prestored; /* store-check kernel: 1 = stored without a parse (DMX_F_STORE_CHECK) */
+    uint32_t prestored; /* store-check kernel (DMX_F_STORE_CHECK): 1 = stored without a parse,
+                         * 2 = one repeated byte, parsed in closed form; 0 = parsed by K1 */
 } dmx_blkinfo;
 
 /* One emitted DEFLATE block inside an sw block (DMX_NSUB per block; f3 split). */

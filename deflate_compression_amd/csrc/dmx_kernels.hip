@@ -1110,8 +1110,45 @@ __device__ __forceinline__ void sc_load(const uint8_t* d, uint32_t p, uint32_t b
     }
 }
 
+// The parse of a block of bn copies of byte c in closed form (what the search + walk give
+// for it, greedy or lazy, any chain bound, no dictionary): a literal, then q = (bn - 1) / 258
+// distance-1 matches of 258, then the rest r = (bn - 1) % 258 as one distance-1 match when
+// r >= 3, else r literals.  Tokens are written by the threads in parallel; thread 0 adds the
+// histogram counts to H (zeroed, DMX_HIST entries).  Returns the token count.
+__device__ __forceinline__ uint32_t uniform_parse(uint32_t bn, uint32_t c, uint32_t* __restrict__ tb, uint32_t* H,
+                                                  uint32_t tid, uint32_t nthr) {
+    const uint32_t R = bn ? bn - 1 : 0, q = R / MAXLEN, r = R % MAXLEN;
+    const uint32_t ntok = bn ? 1 + q + (r >= 3 ? 1 : r) : 0;
+    for (uint32_t k = tid; k < ntok; k += nthr) {
+        uint32_t t = c;
+        if (k >= 1 && k <= q) t = (1u << 9) | MAXLEN;
+        else if (k == q + 1 && r >= 3) t = (1u << 9) | r;
+        tb[k] = t;
+    }
+    if (tid == 0 && bn) {
+        uint32_t sy, eb, ev;
+        H[c] += 1 + (r >= 3 ? 0 : r);
+        if (q) {
+            len_sym(MAXLEN, sy, eb, ev);
+            H[sy] += q;
+        }
+        if (r >= 3) {
+            len_sym(r, sy, eb, ev);
+            H[sy] += 1;
+        }
+        if (q + (r >= 3 ? 1 : 0)) {
+            dist_sym(1u, sy, eb, ev);
+            H[DMX_DIST0 + sy] += q + (r >= 3 ? 1 : 0);
+        }
+    }
+    return ntok;
+}
+
+// prestored: 0 = parse in K1; 1 = stored by the noise check; 2 = a block of one repeated
+// byte, parsed here in closed form (K1 skips it, the Huffman kernels code it).
 __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
-                                                              dmx_blkinfo* __restrict__ info) {
+                                                              dmx_blkinfo* __restrict__ info, uint32_t* __restrict__ tok_g,
+                                                              uint32_t* __restrict__ hist_g, uint32_t uni_ok) {
     __shared__ uint32_t bm[1u << 13];
     __shared__ uint32_t hist[256];
     __shared__ uint64_t red[10][SCT / 64];
@@ -1142,7 +1179,9 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
 #pragma unroll
             for (int k = 0; k < 8; k++) red[k][wave] = ones[k];
         }
-        __syncthreads();
+        const uint32_t c4 = (uint32_t)d[0] * 0x01010101u;
+        const bool u0 = w[0] == c4 && w[1] == c4 && w[2] == c4 && w[3] == c4;
+        const bool uni4k = __syncthreads_and(u0) != 0;   // (also publishes red[])
         if (tid == 0) {
             bool ok = true;
             for (int k = 0; k < 8; k++) {
@@ -1156,7 +1195,40 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
             if (!ok) info[b].prestored = 0;
         }
         __syncthreads();
-        if (!pass_s) return;
+        if (!pass_s) {
+            if (!uni_ok || !uni4k) return;
+            // the first 4 KiB are one repeated byte: is the whole block?  Then its parse has
+            // a closed form (as in K1's uniform path; no dictionary): a literal, distance-1
+            // matches of min(258, bytes left) while >= 3 bytes are left, then literals.
+            bool u = true;
+            for (uint32_t p = (tid + SCT) << 4; p < bn; p += SCT << 4) {
+                uint32_t x[5];
+                sc_load(d, p, bn, aligned16, x);
+                const uint32_t nb = bn - p < 16 ? bn - p : 16;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t m = 4 * q + 4 <= (int)nb ? 0xFFFFFFFFu : (4 * q >= nb ? 0u : (1u << (8 * (nb - 4 * q))) - 1u);
+                    u = u && ((x[q] ^ c4) & m) == 0;
+                }
+            }
+            if (!__syncthreads_and(u)) return;
+            uint32_t* H = bm;   // the 320-entry histogram (bm is free here)
+            for (uint32_t k = tid; k < DMX_HIST; k += SCT) H[k] = 0;
+            __syncthreads();
+            const uint32_t c = c4 & 0xFFu;
+            const uint32_t nt = uniform_parse(bn, c, tok_g + (uint64_t)b * DMX_BLK, H, tid, SCT);
+            if (tid == 0) {
+                const uint64_t S = (uint64_t)c * bn, T = (uint64_t)c * ((uint64_t)bn * (bn - 1) / 2);
+                info[b].ntok = nt;
+                info[b].n = bn;
+                info[b].adl_s = S;
+                info[b].adl_w = (uint64_t)bn * S - T;
+                info[b].prestored = 2;
+            }
+            __syncthreads();
+            for (uint32_t k = tid; k < DMX_HIST; k += SCT) hist_g[(uint64_t)b * DMX_HIST + k] = H[k];
+            return;
+        }
     }
     // ---- pass 1: Adler sums (the block's data into registers for pass 2) ----
     uint64_t s = 0, t = 0;
@@ -1343,26 +1415,8 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         // block record are written directly.
         if (__syncthreads_and(uni)) {   // (also publishes the waves' run counts)
             const uint32_t c = c4 & 0xFFu;
+            const uint32_t nt = uniform_parse(bn, c, tok_g + (uint64_t)b * DMX_BLK, L.hist, tid, MT);
             if (tid == 0) {
-                uint32_t* tb = tok_g + (uint64_t)b * DMX_BLK;
-                uint32_t nt = 0;
-                for (uint32_t p = 0; p < bn;) {
-                    const uint32_t r = bn - p;
-                    if (p >= 1 && r >= 3) {
-                        const uint32_t len = r < MAXLEN ? r : MAXLEN;
-                        tb[nt++] = (1u << 9) | len;
-                        uint32_t sy, eb, ev;
-                        len_sym(len, sy, eb, ev);
-                        L.hist[sy]++;
-                        dist_sym(1u, sy, eb, ev);
-                        L.hist[DMX_DIST0 + sy]++;
-                        p += len;
-                    } else {
-                        tb[nt++] = c;
-                        L.hist[c]++;
-                        p++;
-                    }
-                }
                 const uint64_t S = (uint64_t)c * bn, T = (uint64_t)c * ((uint64_t)bn * (bn - 1) / 2);
                 info[b].ntok = nt;
                 info[b].n = bn;
@@ -2088,7 +2142,7 @@ __global__ __launch_bounds__(64) void dmx_huff_kernel(const uint32_t* __restrict
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x;
     const uint32_t* hg = hist_g + (uint64_t)b * DMX_HIST;
-    if (info[b].prestored) return;   // K0 wrote the stored record
+    if (info[b].prestored == 1) return;   // K0 wrote the stored record
     const uint32_t bn = info[b].n;
     const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1) ? 1u : 0u;
 
@@ -2157,7 +2211,7 @@ __global__ __launch_bounds__(SHT) void dmx_split_hist_kernel(const uint32_t* __r
     __shared__ uint32_t qt[5], wsum[SHT / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t b = blockIdx.x;
-    if (info[b].prestored) return;   // K0 wrote the stored record
+    if (info[b].prestored == 1) return;   // K0 wrote the stored record
     const uint32_t ntok = info[b].ntok, bn = info[b].n;
     for (uint32_t k = tid; k < 4 * DMX_HIST; k += SHT) (&qh[0][0])[k] = 0;
     if (tid < 5) qt[tid] = tid == 4 ? ntok : 0u;
@@ -2219,7 +2273,7 @@ __global__ __launch_bounds__(64) void dmx_split_plan_kernel(SplitScratch* __rest
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x / SPW, g = blockIdx.x % SPW;
     SplitScratch& o = sp[b];
-    if (info[b].prestored) return;
+    if (info[b].prestored == 1) return;
     const uint32_t bn = info[b].n;
     const uint32_t i = c_gi[g], j = c_gj[g];
     const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1 && j == 3) ? 1u : 0u;
@@ -2261,7 +2315,7 @@ __global__ __launch_bounds__(64) void dmx_split_choose_kernel(const SplitScratch
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x;
     const SplitScratch& o = sp[b];
-    if (info[b].prestored) return;
+    if (info[b].prestored == 1) return;
     if (lane == 0) {   // cheapest cut mask: bit k = a cut after quarter k
         int best = -1;
         uint64_t bestc = 0;
@@ -3045,7 +3099,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         // stage 0 also holds K0, the noise check (DMX_F_STORE_CHECK)
         if (o.flags & DMX_F_STORE_CHECK)
             hipLaunchKernelGGL(dmx_store_check_kernel, dim3(nblk), dim3(SCT), 0, s, (const uint8_t*)d_in, n,
-                               (uint32_t)o.sw, c->info);
+                               (uint32_t)o.sw, c->info, c->tok, c->hist, (o.flags & DMX_F_DICT) ? 0u : 1u);
         if (ev) (void)hipEventRecord(ev[1], s);
         const uint32_t mfl = ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u) |
                              ((o.flags & DMX_F_STORE_CHECK) ? 4u : 0u);
