@@ -398,3 +398,24 @@ def test_fd_api_streaming_pipes_and_offsets(tmp_path, n):
     finally:
         for k, v in old.items():
             os.environ.pop(k, None) if v is None else os.environ.__setitem__(k, v)
+
+
+@pytest.mark.parametrize("check", [False, True])
+@pytest.mark.parametrize("k,lazy", [(0, False), (6, True), (8, False), (16, True)])
+def test_uniform_blocks_closed_form(enc, check, k, lazy):
+    """Blocks of one repeated byte take a closed-form parse (K1's uniform path, or K0's with
+    DMX_F_STORE_CHECK): byte-identical to the oracle's search for every remainder of
+    (n - 1) mod 258 around the 3-byte threshold, several byte values, short and full blocks,
+    uniform blocks next to text and runs that are almost uniform."""
+    fl = D.DMX_ZLIB | (D.DMX_F_LAZY if lazy else 0) | (D.DMX_F_STORE_CHECK if check else 0)
+    for c in (0x00, 0x41, 0xFF):
+        for n in (1, 2, 3, 4, 5, 258, 259, 260, 261, 262, 516, 517, 518, 4095, 4096, 4097, 32767, 32768):
+            data = bytes([c]) * n
+            z, _ = enc.compress_bytes(data, max_chain=k, flags=fl)
+            assert z == O.compress(data, max_chain=k, lazy=lazy, store_check=check), (c, n)
+    almost = bytearray(32768)
+    almost[20000] = 1   # one odd byte: not uniform
+    data = bytes(32768) + D.gen_text(40000, 3).tobytes() + bytes([7]) * 32768 + bytes(almost) + bytes([9]) * 1000
+    z, _ = enc.compress_bytes(data, max_chain=k, flags=fl)
+    assert z == O.compress(data, max_chain=k, lazy=lazy, store_check=check)
+    assert zlib.decompress(z) == data
