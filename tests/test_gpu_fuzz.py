@@ -56,3 +56,26 @@ def test_fuzz_parity(enc, seed):
     zo = O.compress(data, sw=sw, max_chain=k, lazy=lazy, split=split, dict=dct, store_check=chk)
     assert z == zo, dict(n=len(data), sw=sw, k=k, lazy=lazy, split=split, dict=dct, check=chk)
     assert zlib.decompress(z) == data
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("DMX_FUZZ_N", "40")) // 2))
+def test_fuzz_inflate(enc, seed):
+    """GPU inflate on the same mixtures: zlib's own streams (levels, strategies, window
+    sizes) through the whole-stream decoder, and our streams through the block index."""
+    rng = np.random.default_rng(5000 + seed)
+    data = b"".join(piece(rng) for _ in range(int(rng.integers(1, 8))))[: 1 << 20]
+    lvl = int(rng.integers(0, 10))
+    strat = int(rng.choice([zlib.Z_DEFAULT_STRATEGY, zlib.Z_FILTERED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE, zlib.Z_FIXED]))
+    wbits = int(rng.integers(9, 16))
+    co = zlib.compressobj(lvl, zlib.DEFLATED, wbits, 8, strat)
+    zz = co.compress(data) + co.flush()
+    if wbits == 15:   # the stream decoder reads zlib headers of window 32 KiB
+        t = torch.frombuffer(bytearray(zz), dtype=torch.uint8).cuda()
+        out, st = D.inflate_gpu(t, len(data) + 16)
+        assert st == 0 and out.cpu().numpy().tobytes() == data
+    fl = D.DMX_ZLIB | (D.DMX_F_LAZY if seed & 1 else 0) | (D.DMX_F_SPLIT if seed & 2 else 0) | D.DMX_F_STORE_CHECK
+    zt, r = enc.compress_tensor(torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda(),
+                                opts=D.Opts(32768, 6, fl, 0))
+    ix, nb = enc.block_index()
+    out, st = D.inflate_gpu(zt, len(data), index=ix, nblk=nb)
+    assert st == 0 and out.cpu().numpy().tobytes() == data
