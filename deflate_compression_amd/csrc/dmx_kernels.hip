@@ -212,13 +212,18 @@ __device__ __forceinline__ uint32_t ext_len(const MatchLDS& L, uint32_t i, uint3
         if (kk >= lim) return kk;
     }
 }
-// Change bitmap (bounded mode, K <= KD: bucket starts are not needed, so it lives in
-// bstart): bit p = data[p] != data[p+1] (set for p >= bn - 1).  Built at the start of the
-// search (search_positions); gives a distance-1 candidate's exact length in a few word reads.
-__device__ __forceinline__ uint32_t* chg_bits(MatchLDS& L) { return reinterpret_cast<uint32_t*>(L.bstart); }
-__device__ __forceinline__ uint32_t* chg_bits(const MatchLDS& L) {
-    return reinterpret_cast<uint32_t*>(const_cast<uint16_t*>(L.bstart));
-}
+// Change bitmap (bounded mode with a short chain, K <= KE: the walk's exit array is free
+// during the search): bit p = data[p] != data[p+1] (set for p >= bn - 1).  Built at the
+// start of the search (search_positions); gives a distance-1 candidate's exact length in a
+// few word reads.
+__device__ __forceinline__ uint32_t* chg_bits(MatchLDS& L) { return L.exitp; }
+__device__ __forceinline__ uint32_t* chg_bits(const MatchLDS& L) { return const_cast<uint32_t*>(L.exitp); }
+// Winner of every entry of S in the short-chain mode (K <= KE), 4 bits per entry in bucket
+// order, in bstart (bucket starts are not needed there): 0 = no match, j = 1..KE = chain
+// candidate j (entry k - j of S), 15 = the history match (DMX_F_DICT).  After the search
+// the distance of entry k is S[k] - S[k - j]: no distance staging buffer in HBM.
+#define NIB_HIST 15u
+__device__ __forceinline__ uint32_t* nib_words(MatchLDS& L) { return reinterpret_cast<uint32_t*>(L.bstart); }
 // Length of the match at i against i - 1 (>= 1 known equal bytes), capped at lim: the first
 // change at or after i - 1 ends it.
 __device__ __forceinline__ uint32_t run_len(const MatchLDS& L, uint32_t i, uint32_t lim) {
@@ -474,6 +479,60 @@ __device__ __forceinline__ void cand_steps_emb(uint32_t K, uint32_t i0, uint32_t
         cand_step_emb<GUARD, CLAMP>(j, sj, x0, x1, x2, i0, i1, i2, nc, lim_eff, jkey, full);
 }
 
+// Result of entry k (position i) in the short-chain mode: length (0 = none) and winner j
+// (chain candidate, 1..KE).  The length goes to len8 / lit in position order, the winner to
+// the entry's nibble; the distance is recovered after the search (nibble_dists).
+// DMX_F_DICT: the history kernel's result of entry k (len << 16 | dist, 0 = none, bucket
+// order) replaces the block's own match only when strictly longer.
+template <bool DICT>
+__device__ __forceinline__ void store_short(MatchLDS& L, uint32_t k, uint32_t i, uint32_t len, uint32_t j,
+                                            const uint32_t* __restrict__ hbk) {
+    if (DICT) {
+        const uint32_t hw = hbk[k];
+        if ((hw >> 16) > len) { len = hw >> 16; j = NIB_HIST; }
+    }
+    if (len == 0) {
+        atomicOr(&L.lit[i >> 5], 1u << (i & 31));
+        L.len8[i] = 0;
+    } else {
+        L.len8[i] = (uint8_t)(len - 3);
+        atomicOr(&nib_words(L)[k >> 3], j << ((k & 7u) << 2));
+    }
+}
+
+// The queued entries of one wave (qn <= 64, items k | full << 15): lane l takes item l and
+// extends its full candidates from LDS, nearest first (a farther one must be strictly
+// longer, so it is extended only if it also matches the byte at the best length), then
+// stores the entry's result.
+template <bool DICT, bool RUNS>
+__device__ __forceinline__ void ext_queue(MatchLDS& L, uint32_t bn, uint32_t* Qw, uint32_t qn, uint32_t lane,
+                                       const uint32_t* __restrict__ hbk) {
+    __builtin_amdgcn_wave_barrier();
+    if (lane < qn) {
+        const uint32_t it = lds_ld(&Qw[lane]);
+        const uint32_t k = it & 0x7FFFu;
+        uint32_t full = it >> 15;
+        const uint32_t i = L.sorted[k];
+        const uint32_t lim = min(bn - i, (uint32_t)MAXLEN);
+        const uint8_t* D8 = reinterpret_cast<const uint8_t*>(L.data);
+        uint32_t bj = (uint32_t)__builtin_ctz(full) + 1u;
+        full &= full - 1u;
+        uint32_t q = L.sorted[k - bj];
+        // distance 1 (runs): the length is where the run ends, from the change bitmap
+        uint32_t bl = min(q + 1u == i && RUNS ? run_len(L, i, lim) : ext_len(L, i, q, CB, lim), lim);
+        while (full && bl < lim) {
+            const uint32_t j = (uint32_t)__builtin_ctz(full) + 1u;
+            full &= full - 1u;
+            q = L.sorted[k - j];
+            if (D8[q + bl] != D8[i + bl]) continue;
+            const uint32_t len = min(ext_len(L, i, q, CB, lim), lim);
+            if (len > bl) { bl = len; bj = j; }
+        }
+        store_short<DICT>(L, k, i, bl, bj, hbk);
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 template <bool DICT, bool RUNS>
 __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint16_t* __restrict__ pg,
                                      uint32_t tid, bool stamp, uint64_t& tdef, const uint32_t* __restrict__ hbk) {
@@ -483,60 +542,83 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
     uint32_t iters = 0;
     if (RUNS) build_chg(L, bn, tid);
     if (K <= KE) {
-        // bounded mode with a short chain: chunks of 64-K owned entries, halo embedded
+        // bounded mode with a short chain: chunks of 64-K owned entries, halo embedded.
+        // Entries with a candidate equal in all CB register bytes need the LDS extension; they
+        // go to a per-wave queue (up to 64, in tsm) that is extended with all 64 lanes at once
+        // when the next chunk would overflow it, instead of a few lanes of every chunk.
+        uint32_t* Qw = L.tsm + (wave << 6);
+        const uint64_t lt = (1ull << lane) - 1ull;
+        uint32_t qn = 0;   // queued entries (wave-uniform)
         const uint32_t own = 64 - K;
-        for (uint32_t base = wave * own; base < nvalid; base += MW * own) {
+        // one call site of ext_queue (code size, registers): the pass after the last chunk
+        // only flushes the queue
+        for (uint32_t base = wave * own;; base += MW * own) {
+            const bool more = base < nvalid;   // wave-uniform
             const int ei = (int)(base + lane) - (int)K;   // entry of this lane
             const uint32_t k = (uint32_t)ei;
-            const bool load = ei >= 0 && k < nvalid;
-            const bool act = lane >= K && k < nvalid;
-            uint32_t i = 0, nc = 0, lim_eff = 0;
-            uint64_t iv0 = 0;
-            uint32_t i2 = 0;
-            if (load) {
-                i = L.sorted[k];
-                iv0 = ld8(L.data, i);
-                i2 = ld4(L.data, i + 8);
-            }
-            if (act) {
-                nc = min(k, K);
-                lim_eff = (bn - i) < MAXLEN ? (bn - i) : MAXLEN;
-            }
-            iters += K;
-            uint32_t jkey = 0, full = 0;
-            const uint32_t i0 = (uint32_t)iv0, i1 = (uint32_t)(iv0 >> 32);
-            {   // sort check: the predecessor entry (lane - 1) must be earlier if same bucket
-                const uint32_t pn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)i, 0x138, 0xF, 0xF, true);
-                const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)i0, 0x138, 0xF, 0xF, true);
-                const bool bad = act && ei >= 1 && pn > i && dmx_hash(dn & 0xFFFFFFu) == dmx_hash(i0 & 0xFFFFFFu);
-                if (__ballot(bad)) L.sortbad = 1;
-            }
-            if (RUNS) {
-                // inside a run: when the distance-1 match already has the longest possible
-                // length, it is the answer (entry k-1 is position i-1 -- same trigram, so the
-                // same bucket, and no position lies between them -- and nearest wins ties).
-                // A chunk whose lanes all end here skips the candidate steps.
-                bool rdone = false;
-                uint32_t rkey = 0;
-                if (act && i >= 1 && run_len(L, i, lim_eff) >= lim_eff) {
-                    rkey = (lim_eff << 15) | (i - 1);
-                    rdone = true;
+            const bool act = more && lane >= K && k < nvalid;
+            uint32_t i = 0, lim_eff = 0, jkey = 0, full = 0;
+            bool done = false;   // result already stored (runs)
+            if (more) {
+                const bool load = ei >= 0 && k < nvalid;
+                uint32_t nc = 0;
+                uint64_t iv0 = 0;
+                uint32_t i2 = 0;
+                if (load) {
+                    i = L.sorted[k];
+                    iv0 = ld8(L.data, i);
+                    i2 = ld4(L.data, i + 8);
                 }
-                if (__ballot(act && !rdone) == 0) {
-                    if (act) store_result<DICT>(L, pg, k, i, rkey, hbk);
-                    continue;
+                if (act) {
+                    nc = min(k, K);
+                    lim_eff = (bn - i) < MAXLEN ? (bn - i) : MAXLEN;
+                }
+                iters += K;
+                const uint32_t i0 = (uint32_t)iv0, i1 = (uint32_t)(iv0 >> 32);
+                {   // sort check: the predecessor entry (lane - 1) must be earlier if same bucket
+                    const uint32_t pn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)i, 0x138, 0xF, 0xF, true);
+                    const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)i0, 0x138, 0xF, 0xF, true);
+                    const bool bad = act && ei >= 1 && pn > i && dmx_hash(dn & 0xFFFFFFu) == dmx_hash(i0 & 0xFFFFFFu);
+                    if (__ballot(bad)) L.sortbad = 1;
+                }
+                bool skip = false;
+                if (RUNS) {
+                    // inside a run: when the distance-1 match already has the longest possible
+                    // length, it is the answer (entry k-1 is position i-1 -- same trigram, so the
+                    // same bucket, and no position lies between them -- and nearest wins ties).
+                    // A chunk whose lanes all end here skips the candidate steps.
+                    const bool rdone = act && i >= 1 && run_len(L, i, lim_eff) >= lim_eff;
+                    if (__ballot(act && !rdone) == 0) {
+                        if (act) store_short<DICT>(L, k, i, lim_eff, 1u, hbk);
+                        done = true;
+                        skip = true;
+                    }
+                }
+                if (!skip) {
+                    if (base == 0) cand_steps_emb<true, true>(K, i0, i1, i2, nc, lim_eff, jkey, full);
+                    else if (__ballot(act && lim_eff < CB)) cand_steps_emb<false, true>(K, i0, i1, i2, nc, lim_eff, jkey, full);
+                    else cand_steps_emb<false, false>(K, i0, i1, i2, nc, lim_eff, jkey, full);
+                    if (lim_eff <= CB) full = 0;
                 }
             }
-            if (base == 0) cand_steps_emb<true, true>(K, i0, i1, i2, nc, lim_eff, jkey, full);
-            else if (__ballot(act && lim_eff < CB)) cand_steps_emb<false, true>(K, i0, i1, i2, nc, lim_eff, jkey, full);
-            else cand_steps_emb<false, false>(K, i0, i1, i2, nc, lim_eff, jkey, full);
-            if (lim_eff <= CB) full = 0;
-            uint32_t bestkey = 0;
-            if (act && (jkey >> 8) >= 3) bestkey = ((jkey >> 8) << 15) | (uint32_t)L.sorted[k - (255u - (jkey & 255u))];
-            const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
-            bestkey = resolve_full<true, RUNS>(L, bn, lane, wave, k, i, lim_eff, bestkey, full, base - K);
-            if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
-            if (act) store_result<DICT>(L, pg, k, i, bestkey, hbk);
+            // a full candidate is the register best (CB bytes, the nearest such): the queue
+            // item is the entry and its full mask
+            const bool push = act && !done && full != 0;
+            const uint64_t pm = __ballot(push);
+            const uint32_t np = (uint32_t)__popcll(pm);
+            if (qn + np > 64 || (!more && qn)) {
+                const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
+                ext_queue<DICT, RUNS>(L, bn, Qw, qn, lane, hbk);
+                if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
+                qn = 0;
+            }
+            if (!more) break;
+            if (push) lds_st(&Qw[qn + (uint32_t)__popcll(pm & lt)], k | (full << 15));
+            qn += np;
+            if (act && !push && !done) {
+                const uint32_t m = jkey >> 8;
+                store_short<DICT>(L, k, i, m >= 3 ? m : 0u, m >= 3 ? 255u - (jkey & 255u) : 0u, hbk);
+            }
         }
     } else
     for (uint32_t k0 = wave << 6; k0 < nvalid; k0 += MT) {
@@ -1337,6 +1419,24 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
     }
 }
 
+// Diagnostic (DMX_DEBUG_STOP=1|2|3, never in a product run): end the block after P0 (sort),
+// P1 (search) or P2 (walk), recording it as an empty block, so that SQ counters of the
+// truncated kernel give the instruction count of each phase by difference.  The stream
+// of such an encode is not the input's.
+__device__ __forceinline__ bool dbg_stop(uint32_t mflags, uint32_t phase, dmx_blkinfo* info, uint32_t* hist_g,
+                                         uint32_t b, uint32_t bn, uint32_t tid) {
+    if (((mflags >> 8) & 3u) != phase) return false;
+    for (uint32_t k = tid; k < DMX_HIST; k += MT) hist_g[(uint64_t)b * DMX_HIST + k] = 0;
+    if (tid == 0) {
+        info[b].ntok = 0;
+        info[b].n = bn;
+        info[b].adl_s = 0;
+        info[b].adl_w = 0;
+        info[b].prestored = 0;
+    }
+    return true;
+}
+
 template <bool DICT>
 __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
                                                        int32_t max_chain, uint32_t mflags, uint16_t* __restrict__ dist_g,
@@ -1435,6 +1535,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         else sort_positions<false, false>(L, bn, max_chain, tid, dbg != nullptr, tp0);
     }
 
+    if (dbg_stop(mflags, 1, info, hist_g, b, bn, tid)) return;
     {   // Adler-32 partial sums of this block
         uint64_t s = 0, t = 0;
         const uint32_t lo = tid << 5;   // 32 bytes per thread, read as two 16-byte vectors
@@ -1463,6 +1564,10 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
 #pragma unroll
         for (int w = 0; w < MW; w++) nrun += L.wexit[w];
         const bool runs = max_chain > 0 && max_chain <= KE && nrun * 4 >= ((bn + 15) >> 4);
+        if (max_chain > 0 && max_chain <= KE) {   // the winners' nibbles (bstart is free after P0)
+            reinterpret_cast<uint4*>(nib_words(L))[tid] = make_uint4(0, 0, 0, 0);
+            __syncthreads();
+        }
         const uint32_t its = runs ? search_positions<DICT, true>(L, bn, max_chain, pg, tid, dbg != nullptr, tdef, hbk)
                                   : search_positions<DICT, false>(L, bn, max_chain, pg, tid, dbg != nullptr, tdef, hbk);
         if (dbg && lane == 0 && attempt == 0) {
@@ -1476,6 +1581,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         sort_positions<true>(L, bn, max_chain, tid, dbg != nullptr, tp0);
     }
     const uint64_t t1 = dbg ? __builtin_amdgcn_s_memtime() : 0;
+    if (dbg_stop(mflags, 2, info, hist_g, b, bn, tid)) return;
 
     // ---- P1b (DMX_F_LAZY): lazy evaluation as a per-position rule on the search results.
     // Position p (a match) becomes a literal when p+1 holds a strictly longer match; the
@@ -1510,17 +1616,41 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         L.tsm[tid] = m;
         L.exitp[tid] = p;
     }
-    {   // the sorted positions are dead: permute the best distances (bucket order in pg)
-        // into position order in the same LDS slots, through registers (32 per thread)
+    {   // the sorted positions are dead: permute the best distances (bucket order) into
+        // position order in the same LDS slots, through registers (32 per thread).  Short
+        // chains (K <= KE): distance = S[k] - S[k - j] from the winner nibble j of entry k (the
+        // history's from its result); longer chains staged the distances in pg (HBM).
         __syncthreads();
         const uint32_t nvalid = bn > 2 ? bn - 2 : 0;
         uint4 dv[4], pv[4];
+        if (max_chain > 0 && max_chain <= KE) {
+            const uint32_t* NW = nib_words(L);
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t c = tid + (uint32_t)j * MT;   // 8 entries per 16-byte chunk
-            const bool in = c * 8 < nvalid;
-            dv[j] = in ? reinterpret_cast<const uint4*>(pg)[c] : make_uint4(0, 0, 0, 0);
-            pv[j] = in ? reinterpret_cast<const uint4*>(L.sorted)[c] : make_uint4(0, 0, 0, 0);
+            for (int j = 0; j < 4; j++) {
+                const uint32_t c = tid + (uint32_t)j * MT;   // 8 entries per 16-byte chunk
+                const bool in = c * 8 < nvalid;
+                pv[j] = in ? reinterpret_cast<const uint4*>(L.sorted)[c] : make_uint4(0, 0, 0, 0);
+                const uint32_t nw = in ? NW[c] : 0u;
+                const uint32_t pw[4] = {pv[j].x, pv[j].y, pv[j].z, pv[j].w};
+                uint32_t dw[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int e = 0; e < 8; e++) {
+                    const uint32_t jj = (nw >> (4 * e)) & 15u, kk = c * 8 + (uint32_t)e;
+                    uint32_t dist = 0;
+                    if (jj == NIB_HIST) dist = DICT ? (hbk[kk] & 0xFFFFu) : 0u;
+                    else if (jj) dist = ((pw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu) - (uint32_t)L.sorted[kk - jj];
+                    dw[e >> 1] |= dist << (16 * (e & 1));
+                }
+                dv[j] = make_uint4(dw[0], dw[1], dw[2], dw[3]);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t c = tid + (uint32_t)j * MT;   // 8 entries per 16-byte chunk
+                const bool in = c * 8 < nvalid;
+                dv[j] = in ? reinterpret_cast<const uint4*>(pg)[c] : make_uint4(0, 0, 0, 0);
+                pv[j] = in ? reinterpret_cast<const uint4*>(L.sorted)[c] : make_uint4(0, 0, 0, 0);
+            }
         }
         __syncthreads();
 #pragma unroll
@@ -1622,6 +1752,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         __syncthreads();
     }
     if (dbg && tid == 0) st_w23 = __builtin_amdgcn_s_memtime() - t1;
+    if (dbg_stop(mflags, 3, info, hist_g, b, bn, tid)) return;
 
     // ---- P3: compaction + histograms ----
     {
@@ -3101,8 +3232,9 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
             hipLaunchKernelGGL(dmx_store_check_kernel, dim3(nblk), dim3(SCT), 0, s, (const uint8_t*)d_in, n,
                                (uint32_t)o.sw, c->info, c->tok, c->hist, (o.flags & DMX_F_DICT) ? 0u : 1u);
         if (ev) (void)hipEventRecord(ev[1], s);
+        const char* dstop = getenv("DMX_DEBUG_STOP");   // diagnostic only (dbg_stop)
         const uint32_t mfl = ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u) |
-                             ((o.flags & DMX_F_STORE_CHECK) ? 4u : 0u);
+                             ((o.flags & DMX_F_STORE_CHECK) ? 4u : 0u) | (dstop ? ((uint32_t)atoi(dstop) & 3u) << 8 : 0u);
         if (o.flags & DMX_F_DICT)
             hipLaunchKernelGGL(dmx_match_kernel<true>, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n,
                                (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg);

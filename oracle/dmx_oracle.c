@@ -681,71 +681,179 @@ int dmx_oracle_store_check(const uint8_t* d, int bn) {
 /* ---- 8. whole stream ---------------------------------------------------------------- */
 
 /*
- * Compress `in` (n bytes) into a zlib stream.  Returns the stream length, or
- * -1 if `cap` is too small.  sw = block size (1..32768), max_chain as above,
- * lazy = f2 parse, blkopt bit 0 = f3 block splitting, bit 1 = the §4.7 store check.  If btypes != NULL it receives the
- * chosen BTYPE of every block (split blocks: the type of their first sub-block).
+ * Compress `in` (n bytes) into a DEFLATE stream framed by `flags` (the DMX_F_* framing bits
+ * of include/dmx.h, restated here): 1 = zlib header 78 9C, 2 = Adler-32 trailer, 4 = the
+ * last block carries BFINAL.  Without 4 the stream ends with an empty stored block (a sync
+ * flush: 3 zero bits, byte alignment, 00 00 FF FF) so that another shard can follow
+ * (DESIGN.md §6); a shard with no blocks then writes nothing, with 4 it writes one fixed
+ * block holding only EOB.  flags = 7 is a complete zlib stream.  Returns the stream length,
+ * or -1 if `cap` is too small.  sw = block size (1..32768), max_chain as above, lazy = f2
+ * parse, blkopt bit 0 = f3 block splitting, bit 1 = the §4.7 store check.  If btypes != NULL
+ * it receives the chosen BTYPE of every block (split blocks: the type of their first
+ * sub-block).
  */
-long long dmx_oracle_compress_ex3(const uint8_t* in, size_t n, int sw, int max_chain, int hash_kind,
-                                  int lazy, int blkopt, int dict, const uint8_t* pre, size_t npre,
-                                  uint8_t* out, size_t cap, uint8_t* btypes) {
+#define ORC_F_HEADER 1
+#define ORC_F_TRAILER 2
+#define ORC_F_FINAL 4
+
+/* One sw block: parse (with its history), plan, and write it into w. */
+static void orc_block(orc_bw* w, const uint8_t* in, size_t n, size_t b, size_t nblk, int sw, int max_chain,
+                      int hash_kind, int lazy, int blkopt, int dict, const uint8_t* pre, size_t npre, int final,
+                      uint32_t* tok, orc_plan* P, orc_split_plan* SP, uint8_t* btypes) {
     const int split = blkopt & 1, store_check = (blkopt >> 1) & 1;   /* f3; §4.7 */
-    if (sw <= 0 || sw > 32768) return -2;
-    if (cap < 8) return -1;
+    size_t off = b * (size_t)sw;
+    int bn = (int)((n - off) < (size_t)sw ? (n - off) : (size_t)sw);
+    /* f1: the previous sw block is the history (block 0: the last sw bytes of pre) */
+    const uint8_t* hist = NULL;
+    int hn = 0;
+    if (dict && b > 0) { hist = in + off - (size_t)sw; hn = sw; }
+    else if (dict && pre && npre > 0) { hn = npre < (size_t)sw ? (int)npre : sw; hist = pre + npre - (size_t)hn; }
+    const int last = final && b + 1 == nblk;
+    if (store_check && dmx_oracle_store_check(in + off, bn)) {   /* stored without a parse */
+        P->btype = 0;
+        if (btypes) btypes[b] = 0;
+        orc_write_block(w, in + off, bn, NULL, 0, P, last);
+        return;
+    }
+    int ntok = dmx_oracle_parse_block_hist(hist, hn, in + off, bn, max_chain, hash_kind, lazy, tok);
+    if (split) {
+        orc_plan_split(tok, ntok, bn, SP);
+        if (btypes) btypes[b] = (uint8_t)SP->P[SP->g[0]].btype;
+        for (int s = 0; s < SP->nsub; s++)
+            orc_write_block(w, in + off, bn, tok + SP->t0[s], SP->t1[s] - SP->t0[s], &SP->P[SP->g[s]],
+                            last && s + 1 == SP->nsub);
+    } else {
+        orc_plan_block(tok, ntok, bn, P);
+        if (btypes) btypes[b] = (uint8_t)P->btype;
+        orc_write_block(w, in + off, bn, tok, ntok, P, last);
+    }
+    (void)nblk;
+}
+
+/* The framing after the last block, then the trailer; returns the stream length or -1. */
+static long long orc_finish(orc_bw* w, uint8_t* out, size_t cap, size_t nblk, int flags, uint32_t adler) {
+    const size_t hdr = (flags & ORC_F_HEADER) ? 2 : 0;
+    if (!(flags & ORC_F_FINAL) && nblk) {   /* sync flush: an empty stored block */
+        orc_put(w, 0, 3);
+        orc_align(w);
+        orc_put(w, 0x0000, 16);
+        orc_put(w, 0xFFFF, 16);
+    }
+    orc_align(w);
+    if (w->overflow) return -1;
+    size_t nbytes = (size_t)(orc_bitpos(w) >> 3);
+    const size_t tl = (flags & ORC_F_TRAILER) ? 4 : 0;
+    if (hdr + nbytes + tl > cap) return -1;
+    if (tl) {
+        uint8_t* tail = out + hdr + nbytes;
+        tail[0] = (uint8_t)(adler >> 24);
+        tail[1] = (uint8_t)(adler >> 16);
+        tail[2] = (uint8_t)(adler >> 8);
+        tail[3] = (uint8_t)adler;
+    }
+    return (long long)(hdr + nbytes + tl);
+}
+
+static orc_bw orc_start(uint8_t* out, size_t cap, size_t nblk, int flags) {
     memset(out, 0, cap);
-    out[0] = 0x78;
-    out[1] = 0x9C;
-    orc_bw w = {out + 2, cap - 6, 0, 0, 0, 0};
-    size_t nblk = n == 0 ? 0 : (n + (size_t)sw - 1) / (size_t)sw;
-    if (nblk == 0) {
+    const size_t hdr = (flags & ORC_F_HEADER) ? 2 : 0;
+    if (hdr) { out[0] = 0x78; out[1] = 0x9C; }
+    orc_bw w = {out + hdr, cap - hdr - 4, 0, 0, 0, 0};
+    if (nblk == 0 && (flags & ORC_F_FINAL)) {
         orc_put(&w, 1, 1);  /* BFINAL, fixed, EOB only */
         orc_put(&w, 1, 2);
         orc_put(&w, 0, 7);
     }
+    return w;
+}
+
+long long dmx_oracle_compress_framed(const uint8_t* in, size_t n, int sw, int max_chain, int hash_kind,
+                                     int lazy, int blkopt, int dict, const uint8_t* pre, size_t npre, int flags,
+                                     uint8_t* out, size_t cap, uint8_t* btypes) {
+    if (sw <= 0 || sw > 32768) return -2;
+    if (cap < 8) return -1;
+    size_t nblk = n == 0 ? 0 : (n + (size_t)sw - 1) / (size_t)sw;
+    orc_bw w = orc_start(out, cap, nblk, flags);
     uint32_t* tok = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)sw);
     orc_plan* P = (orc_plan*)malloc(sizeof(orc_plan));
-    orc_split_plan* SP = split ? (orc_split_plan*)malloc(sizeof(orc_split_plan)) : NULL;
-    for (size_t b = 0; b < nblk; b++) {
-        size_t off = b * (size_t)sw;
-        int bn = (int)((n - off) < (size_t)sw ? (n - off) : (size_t)sw);
-        /* f1: the previous sw block is the history (block 0: the last sw bytes of pre) */
-        const uint8_t* hist = NULL;
-        int hn = 0;
-        if (dict && b > 0) { hist = in + off - (size_t)sw; hn = sw; }
-        else if (dict && pre && npre > 0) { hn = npre < (size_t)sw ? (int)npre : sw; hist = pre + npre - (size_t)hn; }
-        if (store_check && dmx_oracle_store_check(in + off, bn)) {   /* stored without a parse */
-            P->btype = 0;
-            if (btypes) btypes[b] = 0;
-            orc_write_block(&w, in + off, bn, NULL, 0, P, b + 1 == nblk);
-            continue;
-        }
-        int ntok = dmx_oracle_parse_block_hist(hist, hn, in + off, bn, max_chain, hash_kind, lazy, tok);
-        if (split) {
-            orc_plan_split(tok, ntok, bn, SP);
-            if (btypes) btypes[b] = (uint8_t)SP->P[SP->g[0]].btype;
-            for (int s = 0; s < SP->nsub; s++)
-                orc_write_block(&w, in + off, bn, tok + SP->t0[s], SP->t1[s] - SP->t0[s], &SP->P[SP->g[s]],
-                                b + 1 == nblk && s + 1 == SP->nsub);
-        } else {
-            orc_plan_block(tok, ntok, bn, P);
-            if (btypes) btypes[b] = (uint8_t)P->btype;
-            orc_write_block(&w, in + off, bn, tok, ntok, P, b + 1 == nblk);
-        }
-    }
+    orc_split_plan* SP = (blkopt & 1) ? (orc_split_plan*)malloc(sizeof(orc_split_plan)) : NULL;
+    for (size_t b = 0; b < nblk; b++)
+        orc_block(&w, in, n, b, nblk, sw, max_chain, hash_kind, lazy, blkopt, dict, pre, npre, flags & ORC_F_FINAL,
+                  tok, P, SP, btypes);
     free(tok);
     free(P);
     free(SP);
-    orc_align(&w);
-    if (w.overflow) return -1;
-    size_t nbytes = (size_t)(orc_bitpos(&w) >> 3);
-    if (2 + nbytes + 4 > cap) return -1;
-    uint32_t ad = dmx_oracle_adler32(in, n);
-    uint8_t* tail = out + 2 + nbytes;
-    tail[0] = (uint8_t)(ad >> 24);
-    tail[1] = (uint8_t)(ad >> 16);
-    tail[2] = (uint8_t)(ad >> 8);
-    tail[3] = (uint8_t)ad;
-    return (long long)(2 + nbytes + 4);
+    return orc_finish(&w, out, cap, nblk, flags, (flags & ORC_F_TRAILER) ? dmx_oracle_adler32(in, n) : 0u);
+}
+
+long long dmx_oracle_compress_ex3(const uint8_t* in, size_t n, int sw, int max_chain, int hash_kind,
+                                  int lazy, int blkopt, int dict, const uint8_t* pre, size_t npre,
+                                  uint8_t* out, size_t cap, uint8_t* btypes) {
+    return dmx_oracle_compress_framed(in, n, sw, max_chain, hash_kind, lazy, blkopt, dict, pre, npre,
+                                      ORC_F_HEADER | ORC_F_TRAILER | ORC_F_FINAL, out, cap, btypes);
+}
+
+/* Append the first nbits bits of buf (LSB-first) to w, 32 bits per put. */
+static void orc_put_bits(orc_bw* w, const uint8_t* buf, uint64_t nbits) {
+    uint64_t k = 0;
+    for (; k + 32 <= nbits; k += 32) {
+        const uint8_t* p = buf + (k >> 3);
+        orc_put(w, (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24, 32);
+    }
+    for (; k < nbits; k += 8) {
+        const int nb = nbits - k < 8 ? (int)(nbits - k) : 8;
+        orc_put(w, buf[k >> 3], nb);
+    }
+}
+
+/*
+ * The same stream as dmx_oracle_compress_framed, with the blocks parsed, planned and written
+ * in parallel (OpenMP over blocks, nthreads threads; 0 = the OpenMP default): every block
+ * into a bit buffer of its own, then the buffers joined in order.  Blocks are independent
+ * (each parses its own window; with dict the history is input bytes, not parse state), so
+ * the stream is byte-identical to the serial one.  This is the all-cores CPU baseline of
+ * bench.py (SURVEY.md §8d ii).
+ */
+long long dmx_oracle_compress_par(const uint8_t* in, size_t n, int sw, int max_chain, int hash_kind, int lazy,
+                                  int blkopt, int dict, int flags, int nthreads, uint8_t* out, size_t cap) {
+    if (sw <= 0 || sw > 32768) return -2;
+    if (cap < 8) return -1;
+    size_t nblk = n == 0 ? 0 : (n + (size_t)sw - 1) / (size_t)sw;
+    const size_t bcap = (size_t)sw + (size_t)sw / 2 + 1024;   /* stored, or up to 4 sub-blocks + headers */
+    uint8_t* bb = (uint8_t*)malloc(nblk ? nblk * bcap : 1);
+    uint64_t* bits = (uint64_t*)calloc(nblk ? nblk : 1, sizeof(uint64_t));
+    int bad = 0;
+    if (!bb || !bits) { free(bb); free(bits); return -3; }
+#pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1) if (nthreads != 1)
+    {
+        uint32_t* tok = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)sw);
+        orc_plan* P = (orc_plan*)malloc(sizeof(orc_plan));
+        orc_split_plan* SP = (blkopt & 1) ? (orc_split_plan*)malloc(sizeof(orc_split_plan)) : NULL;
+#pragma omp for schedule(dynamic, 4)
+        for (size_t b = 0; b < nblk; b++) {
+            uint8_t* buf = bb + b * bcap;
+            memset(buf, 0, bcap);
+            orc_bw w = {buf, bcap, 0, 0, 0, 0};
+            orc_block(&w, in, n, b, nblk, sw, max_chain, hash_kind, lazy, blkopt, dict, NULL, 0,
+                      flags & ORC_F_FINAL, tok, P, SP, NULL);
+            const uint64_t nb = orc_bitpos(&w);
+            orc_align(&w);   /* flush the partial byte into buf */
+            if (w.overflow) bad = 1;
+            bits[b] = nb;
+        }
+        free(tok);
+        free(P);
+        free(SP);
+    }
+    long long r = -1;
+    if (!bad) {
+        orc_bw w = orc_start(out, cap, nblk, flags);
+        for (size_t b = 0; b < nblk; b++) orc_put_bits(&w, bb + b * bcap, bits[b]);
+        r = orc_finish(&w, out, cap, nblk, flags, (flags & ORC_F_TRAILER) ? dmx_oracle_adler32(in, n) : 0u);
+    }
+    free(bb);
+    free(bits);
+    return r;
 }
 
 long long dmx_oracle_compress_ex2(const uint8_t* in, size_t n, int sw, int max_chain, int hash_kind,

@@ -57,6 +57,14 @@ def lib():
                                               ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p, ctypes.c_size_t,
                                               u8p, ctypes.c_size_t, u8p]
         L.dmx_oracle_compress_ex3.restype = ctypes.c_longlong
+        L.dmx_oracle_compress_framed.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p, ctypes.c_size_t,
+                                                 ctypes.c_int, u8p, ctypes.c_size_t, u8p]
+        L.dmx_oracle_compress_framed.restype = ctypes.c_longlong
+        L.dmx_oracle_compress_par.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                              u8p, ctypes.c_size_t]
+        L.dmx_oracle_compress_par.restype = ctypes.c_longlong
         L.dmx_oracle_parse_block_hist.argtypes = [u8p, ctypes.c_int, u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                   ctypes.c_int, u32p]
         L.dmx_oracle_parse_block_hist.restype = ctypes.c_int
@@ -110,24 +118,45 @@ def adler32(data) -> int:
     return int(lib().dmx_oracle_adler32(_u8(a), a.size))
 
 
+F_HEADER, F_TRAILER, F_FINAL = 1, 2, 4   # include/dmx.h framing bits (DMX_ZLIB = 7)
+
+
 def compress(data, sw: int = 32768, max_chain: int = 0, hash_kind: int = HASH_MUL,
              want_btypes: bool = False, lazy: bool = False, split: bool = False, dict: bool = False,
-             pre=None, store_check: bool = False):
+             pre=None, store_check: bool = False, flags: int = 7):
     """zlib stream of `data`; lazy = f2 parse, split = f3 adaptive block splitting,
     dict = f1 cross-block dictionary (pre: the bytes before `data`, history of block 0),
-    store_check = blocks that pass the DESIGN.md §4.7 noise check are stored unparsed."""
+    store_check = blocks that pass the DESIGN.md §4.7 noise check are stored unparsed.
+    flags = the framing (F_HEADER | F_TRAILER | F_FINAL = a zlib stream; a shard of one
+    otherwise, DESIGN.md §6: no BFINAL -> ends with a sync flush)."""
     a = _as_u8(data)
     nblk = (a.size + sw - 1) // sw
     cap = a.size + 5 * (nblk + 1) + 64
     out = np.zeros(cap, dtype=np.uint8)
     bt = np.zeros(max(nblk, 1), dtype=np.uint8)
     pa = _as_u8(pre if pre is not None else b"")
-    r = lib().dmx_oracle_compress_ex3(_u8(a), a.size, sw, max_chain, hash_kind, int(lazy),
-                                      int(split) | (2 if store_check else 0), int(dict), _u8(pa), pa.size, _u8(out), cap, _u8(bt))
+    r = lib().dmx_oracle_compress_framed(_u8(a), a.size, sw, max_chain, hash_kind, int(lazy),
+                                         int(split) | (2 if store_check else 0), int(dict), _u8(pa), pa.size,
+                                         flags, _u8(out), cap, _u8(bt))
     if r < 0:
         raise RuntimeError(f"oracle compress failed: {r}")
     z = out[:r].tobytes()
     return (z, bt[:nblk].copy()) if want_btypes else z
+
+
+def compress_par(data, sw: int = 32768, max_chain: int = 0, lazy: bool = False, split: bool = False,
+                 dict: bool = False, store_check: bool = False, flags: int = 7, threads: int = 0) -> bytes:
+    """The same stream as compress(), blocks encoded in parallel by `threads` OpenMP threads
+    (dmx_oracle_compress_par; the all-cores CPU baseline)."""
+    a = _as_u8(data)
+    nblk = (a.size + sw - 1) // sw
+    cap = a.size + 5 * (nblk + 1) + 64
+    out = np.zeros(cap, dtype=np.uint8)
+    r = lib().dmx_oracle_compress_par(_u8(a), a.size, sw, max_chain, HASH_MUL, int(lazy),
+                                      int(split) | (2 if store_check else 0), int(dict), flags, threads, _u8(out), cap)
+    if r < 0:
+        raise RuntimeError(f"oracle compress_par failed: {r}")
+    return out[:r].tobytes()
 
 
 def store_check(block) -> bool:
