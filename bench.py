@@ -2,11 +2,17 @@
 """bench.py -- DEFLATE encode throughput on MI355X (BASELINE.json metric).
 
 One "step" = one full encode of the rank's resident input (HBM -> HBM zlib stream),
-i.e. all five kernels of the hot path.  N = 1 workload: config C3 (enwik8-sized
-enwik-style text, 100 000 000 B, 3 052 blocks of 32 KiB).  N > 1 (one process per GPU
-under torch.distributed.run): weak scaling, every rank encodes its own 100 MB shard
-(per-rank seed) framed as a shard of one stream, and the compressed chunks are
-gathered to rank 0 over RCCL (point-to-point over xGMI) inside the timed region.
+i.e. every kernel of the hot path.  N = 1 workload: config C3 (enwik8-sized enwik-style
+text, 100 000 000 B, 3 052 blocks of 32 KiB).  N > 1 (one process per GPU): weak
+scaling, every rank encodes its own 100 MB shard (per-rank seed) framed as a shard of one
+stream, and the compressed chunks are gathered to rank 0 over RCCL (point-to-point over
+xGMI) inside the timed region.
+
+`python bench.py --gpus N` with WORLD_SIZE unset starts the N rank processes itself
+(torch.distributed.run, before anything touches the GPU) and exits with their status;
+a rank whose world differs from --gpus exits non-zero.  Before timing, rank 0 inflates the
+stitched N-rank stream (header + chunks + combined Adler-32) and compares it with every
+rank's input: a wrong stream makes the run fail.
 
 Prints ONE JSON line on rank 0 (see DESIGN.md §5 for the roofline accounting).
 """
@@ -15,7 +21,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import platform
+import socket
+import subprocess
 import sys
 import time
 import zlib
@@ -24,6 +31,10 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
+# VALU issue ceiling: 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 32-bit integer
+# instruction (tools/valu_peak.hip measured 3.7-4.2 cycles, 526-630 G/s; profiles/r02_a)
+VALU_PEAK_GIPS = 256 * 4 * 2.4 / 4.0
+COUNTERS = os.path.join(REPO, "tools", "roofline_counters.json")
 
 WORKLOADS = {
     # name: (bytes per rank, generator, seed, description)
@@ -38,6 +49,86 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="text", choices=sorted(WORKLOADS))
+    ap.add_argument("--bytes", type=int, default=0, help="override bytes per rank")
+    ap.add_argument("--max-chain", type=int, default=int(os.environ.get("DMX_MAX_CHAIN", "6")),
+                    help="0 = exhaustive (reference parse); K = K newest chain entries (default 6: the "
+                         "fastest setting inside the <= 2 %% size budget on C3 text, +1.32 %% vs S_ref)")
+    ap.add_argument("--lazy", type=int, default=int(os.environ.get("DMX_LAZY", "1")),
+                    help="1 = lazy evaluation parse (DMX_F_LAZY, SURVEY §8 f2)")
+    ap.add_argument("--split", type=int, default=int(os.environ.get("DMX_SPLIT", "0")),
+                    help="1 = adaptive block splitting (DMX_F_SPLIT, SURVEY §8 f3)")
+    ap.add_argument("--store-check", type=int, default=int(os.environ.get("DMX_STORE_CHECK", "1")),
+                    help="1 = noise blocks stored without a parse (DMX_F_STORE_CHECK, DESIGN.md §4.7)")
+    ap.add_argument("--dict", type=int, default=int(os.environ.get("DMX_DICT", "0")),
+                    help="1 = cross-block dictionary (DMX_F_DICT, SURVEY §8 f1); N > 1: halo exchange of "
+                         "the block before each shard inside the step")
+    ap.add_argument("--tradeoff", default="4,8,16",
+                    help="N = 1: also time these max_chain values (same flags) for the speed/size curve "
+                         "(reported under 'tradeoff'; '' = skip)")
+    ap.add_argument("--exhaustive-steps", type=int, default=3,
+                    help="also time this many exhaustive-parse steps (reported under 'exhaustive')")
+    ap.add_argument("--gather", default="root", choices=["root", "root-sync", "all", "none"],
+                    help="N > 1: root = chunks to rank 0 point-to-point, pipelined (the gather of step i-1 "
+                         "overlaps the encode of step i, double-buffered); root-sync = the same, step by step; "
+                         "all = max-padded all_gather; none = encode only")
+    ap.add_argument("--pipeline-test", type=int, default=0,
+                    help="run the pipelined gather loop at N = 1 too (single-rank process group; tests the path)")
+    ap.add_argument("--cpu-budget", type=float, default=8.0,
+                    help="seconds per CPU baseline leg (0 = skip the CPU legs)")
+    ap.add_argument("--long-run", type=float, default=1.0,
+                    help="N = 1: after the timed steps, time further steps for about this many seconds "
+                         "(reported under 'long_run'; 0 = skip)")
+    ap.add_argument("--traffic-csv", default="",
+                    help="comma-separated rocprofv3 counter CSVs / dirs (FETCH_SIZE and WRITE_SIZE passes); "
+                         "default: the committed tools/roofline_counters.json")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="test hook: start the ranks and check the world over gloo, no GPU work")
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args, argv) -> int:
+    """--gpus N > 1 without a launcher: start N ranks with torch.distributed.run (nothing in
+    this process has touched a GPU) and return their exit status.  Rank 0 prints the line."""
+    port = int(os.environ.get("MASTER_PORT") or _free_port())
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    log("bench: starting", args.gpus, "ranks:", " ".join(cmd))
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def launch_check(args, json_fd: int) -> int:
+    """--launch-check: the launcher and the world size, over gloo, without a GPU."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = torch.tensor([rank + 1], dtype=torch.int64)
+    dist.all_reduce(t)
+    ok = int(t.item()) == world * (world + 1) // 2
+    dist.barrier()
+    if rank == 0:
+        os.write(json_fd, (json.dumps({"launch_check": True, "n_gpus": world, "ranks_ok": ok}) + "\n").encode())
+    dist.destroy_process_group()
+    return 0 if ok else 1
+
+
 def make_input(kind: str, n: int, seed: int):
     import numpy as np
     import deflate_compression_amd as D
@@ -48,40 +139,98 @@ def make_input(kind: str, n: int, seed: int):
     return np.zeros(n, dtype=np.uint8)
 
 
-def cpu_baseline(data, budget_s: float):
-    """Time the CPU side on rank 0: the reference encoder itself (oracle/_ref, built
-    from /root/reference's own sources; one process per 32 KiB block, as it is only
-    correct for one window) if that binary is present, plus our C port of the
-    reference parse + emitter (oracle/dmx_oracle.c).  Bounded samples, 1 core each.
-    The port runs the reference's exhaustive parse, so its output size over the
-    sample is the reference-semantics size S_ref the GPU's size is compared with."""
+def parse_str(args) -> str:
+    return (("exhaustive" if args.max_chain == 0 else f"max_chain={args.max_chain}")
+            + (", lazy" if args.lazy else ", greedy") + (", split" if args.split else "")
+            + (", dict" if args.dict else "") + (", store-check" if args.store_check else ""))
+
+
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        aff = os.cpu_count()
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or aff
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity": aff, "threads": threads}
+
+
+def cpu_baselines(data, args, budget_s: float):
+    """CPU legs on rank 0 (SURVEY §8d ii), on the GPU box's host cores, in the same run:
+      same_parse  -- oracle/dmx_oracle.c (C port of the reference parse + our Huffman/emitter)
+                     with the GPU line's parse flags, blocks in parallel on all the threads the
+                     box gives this job (OpenMP; OMP_NUM_THREADS), over the workload in pieces
+                     until the budget is spent;
+      exhaustive  -- the same port with the reference's own exhaustive parse, all threads: its
+                     size over the whole input is S_ref, the size the GPU stream is compared with;
+      reference   -- the reference encoder itself (oracle/_ref, built from /root/reference's own
+                     sources), one process per 32 KiB block, 1 core, with its per-token estimator
+                     (only where it was built).
+    """
     from oracle import oracle as O
+    info = cpu_info()
+    thr = info["threads"]
     out = {}
-    # port: whole 1 MiB pieces (32 blocks each) until the budget is used
-    t0 = time.perf_counter()
-    done = 0
-    zbytes = 0
-    blk = 1 << 20
-    while done < data.size and time.perf_counter() - t0 < budget_s:
-        zbytes += len(O.compress(data[done:done + blk], max_chain=0)) - 6   # minus zlib framing
-        done += min(blk, data.size - done)
-    dt = time.perf_counter() - t0
-    out["port"] = {"value": done / dt / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
-                   "sample": f"first {done} B of the workload, oracle/dmx_oracle.c compress "
-                             f"(reference exhaustive parse + Huffman/emitter), 1 thread"}
-    out["s_ref"] = (done, zbytes + 6)
+    n = int(data.size)
+    sw = 32768
+
+    def leg(max_chain, lazy, split, dct, store, budget, name):
+        kw = dict(lazy=lazy, split=split, dict=dct, store_check=store, threads=thr)
+        piece = min(n, sw * max(4 * thr, 32))
+        t0 = time.perf_counter()
+        O.compress_par(data[:piece], sw, max_chain, flags=5, **kw)   # probe: the first piece
+        tp = time.perf_counter() - t0
+        if piece and tp / piece * n <= 2 * budget:
+            # the whole workload in one call: one stream, its exact size
+            t0 = time.perf_counter()
+            z = O.compress_par(data, sw, max_chain, flags=7, **kw)
+            dt = time.perf_counter() - t0
+            done, zb, how = n, len(z), "all"
+        else:   # a bounded sample: pieces until the budget is spent (first piece included)
+            done, zb, dt = piece, None, tp
+            while done < n and dt < budget:
+                hi = min(n, done + piece)
+                q0 = time.perf_counter()
+                O.compress_par(data[done:hi], sw, max_chain, flags=4, **kw)
+                dt += time.perf_counter() - q0
+                done = hi
+            how = "first"
+        return {"value": round(done / dt / 1e9, 6), "unit": "GB/s", "cores": thr, "kind": "port",
+                "sample": f"{how} {done} B of the workload, oracle/dmx_oracle.c {name}, blocks in parallel on "
+                          f"{thr} OpenMP threads (dmx_oracle_compress_par)",
+                "cpu_model": info["cpu_model"], "nproc": info["nproc"]}, done, zb
+
+    parse = parse_str(args)
+    r, _, _ = leg(args.max_chain, bool(args.lazy), bool(args.split), bool(args.dict), bool(args.store_check),
+                  budget_s, f"compress ({parse}: the GPU line's parse)")
+    r["parse"] = parse
+    out["same_parse"] = r
+    r, done, zb = leg(0, False, False, False, False, budget_s,
+                      "compress (the reference's exhaustive greedy parse + Huffman/emitter)")
+    r["parse"] = "exhaustive, greedy (reference semantics)"
+    out["exhaustive"] = r
+    out["s_ref"] = (done, zb)   # the reference parse's stream over the whole input (None: sampled)
     if O.ref_available():
         t0 = time.perf_counter()
         done = 0
-        while done < data.size and time.perf_counter() - t0 < budget_s:
-            O.ref_stats(data[done:done + 32768].tobytes())
-            done += min(32768, data.size - done)
+        while done < n and time.perf_counter() - t0 < budget_s:
+            O.ref_stats(data[done:done + sw].tobytes())
+            done += min(sw, n - done)
         dt = time.perf_counter() - t0
-        out["reference"] = {"value": done / dt / 1e9, "unit": "GB/s", "cores": 1, "kind": "reference",
+        out["reference"] = {"value": round(done / dt / 1e9, 9), "unit": "GB/s", "cores": 1, "kind": "reference",
                             "sample": f"first {done} B of the workload in 32 KiB blocks through the reference "
                                       "encoder (src/deflate_compress.c + aht.c + h_tree.c, oracle/_ref), "
-                                      "1 process at a time, incl. its per-token estimator"}
-    return out
+                                      "1 process at a time, incl. its per-token estimator",
+                            "cpu_model": info["cpu_model"]}
+    return out, info
 
 
 def end_to_end(host, args):
@@ -126,46 +275,66 @@ def end_to_end(host, args):
         os.rmdir(td)
 
 
+def verify_stitched(chunks, adlers, lens, expected_pieces) -> bool:
+    """Rank 0: the N shard chunks + the combined Adler-32 trailer must inflate (zlib) to the
+    concatenation of every rank's input (expected_pieces: callables returning rank r's bytes)."""
+    from deflate_compression_amd import shard as S
+    adler = S.combine_adler(adlers, lens)
+    d = zlib.decompressobj()
+    pend = b""
+    r = 0
+    want = expected_pieces[0]() if expected_pieces else b""
+    try:
+        for part in list(chunks) + [S.trailer(adler)]:
+            pend += d.decompress(part)
+            while r < len(expected_pieces) and len(pend) >= len(want):
+                if pend[:len(want)] != want:
+                    return False
+                pend = pend[len(want):]
+                r += 1
+                want = expected_pieces[r]() if r < len(expected_pieces) else b""
+        pend += d.flush()
+    except zlib.error:   # corrupt stream or Adler-32 mismatch
+        return False
+    return d.eof and r == len(expected_pieces) and pend == b"" and not d.unused_data
+
+
+def roofline_counters(kname: str, parse: str, workload: str):
+    """Per-block SQ / PMC figures of `kname` from the committed profile (tools/roofline_counters.json,
+    written by tools/pmc.py from profiles/<tag>), if it was taken on this configuration."""
+    try:
+        with open(COUNTERS) as f:
+            c = json.load(f)
+    except (OSError, ValueError):
+        return None, "tools/roofline_counters.json missing"
+    if c.get("parse") != parse or c.get("workload") != workload:
+        return None, f"counters were taken on {c.get('workload')!r} / {c.get('parse')!r}"
+    k = c.get("kernels", {}).get(kname)
+    if not k:
+        return None, f"no counters for {kname}"
+    return {**k, "source": c.get("source")}, None
+
+
 def main() -> int:
     # The contract is ONE JSON line on stdout.  Libraries print there too (RCCL's version
     # banner at communicator creation), so fd 1 points at stderr for the whole run and the
     # JSON line is written to the saved original.
+    argv = sys.argv[1:]
+    args = parse_args(argv)
+    if args.gpus < 1:
+        log("bench: --gpus must be >= 1")
+        return 2
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args, argv)   # before any GPU call in this process
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        log(f"bench: --gpus {args.gpus} but the launcher started {world} rank(s)")
+        return 2
     json_fd = os.dup(1)
     sys.stdout.flush()
     os.dup2(2, 1)
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="text", choices=sorted(WORKLOADS))
-    ap.add_argument("--bytes", type=int, default=0, help="override bytes per rank")
-    ap.add_argument("--max-chain", type=int, default=int(os.environ.get("DMX_MAX_CHAIN", "6")),
-                    help="0 = exhaustive (reference parse); K = K newest chain entries (default 6: the "
-                         "fastest setting inside the <= 2 %% size budget on C3 text, +1.32 %% vs S_ref)")
-    ap.add_argument("--lazy", type=int, default=int(os.environ.get("DMX_LAZY", "1")),
-                    help="1 = lazy evaluation parse (DMX_F_LAZY, SURVEY §8 f2)")
-    ap.add_argument("--split", type=int, default=int(os.environ.get("DMX_SPLIT", "0")),
-                    help="1 = adaptive block splitting (DMX_F_SPLIT, SURVEY §8 f3)")
-    ap.add_argument("--store-check", type=int, default=int(os.environ.get("DMX_STORE_CHECK", "1")),
-                    help="1 = noise blocks stored without a parse (DMX_F_STORE_CHECK, DESIGN.md §4.7)")
-    ap.add_argument("--dict", type=int, default=int(os.environ.get("DMX_DICT", "0")),
-                    help="1 = cross-block dictionary (DMX_F_DICT, SURVEY §8 f1); N > 1: halo exchange of "
-                         "the block before each shard inside the step")
-    ap.add_argument("--tradeoff", default="4,8,16",
-                    help="N = 1: also time these max_chain values (same flags) for the speed/size curve "
-                         "(reported under 'tradeoff'; '' = skip)")
-    ap.add_argument("--exhaustive-steps", type=int, default=3,
-                    help="also time this many exhaustive-parse steps (reported under 'exhaustive')")
-    ap.add_argument("--gather", default="root", choices=["root", "root-sync", "all", "none"],
-                    help="N > 1: root = chunks to rank 0 point-to-point, pipelined (the gather of step i-1 "
-                         "overlaps the encode of step i, double-buffered); root-sync = the same, step by step; "
-                         "all = max-padded all_gather; none = encode only")
-    ap.add_argument("--pipeline-test", type=int, default=0,
-                    help="run the pipelined gather loop at N = 1 too (single-rank process group; tests the path)")
-    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds per CPU baseline leg (0 = skip)")
-    ap.add_argument("--traffic-csv", default="",
-                    help="comma-separated rocprofv3 counter CSVs / dirs (FETCH_SIZE and WRITE_SIZE passes)")
-    args = ap.parse_args()
+    if args.launch_check:
+        return launch_check(args, json_fd)
 
     import numpy as np
     import torch
@@ -173,7 +342,6 @@ def main() -> int:
     import deflate_compression_amd as D
     from deflate_compression_amd import shard as S
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_pg = world > 1 or bool(args.pipeline_test)
@@ -190,12 +358,14 @@ def main() -> int:
     strong = args.workload == "enwik9"
     if args.bytes:
         per_rank = args.bytes
+    full = None
     if strong:
         total = per_rank
         full = make_input(gen, total, seed)
         lo, hi = S.shard_range(total, rank, world)
         host = np.ascontiguousarray(full[lo:hi])
-        del full
+        if rank != 0:
+            full = None
     else:
         host = make_input(gen, per_rank, seed + rank)
     n = int(host.size)
@@ -235,6 +405,7 @@ def main() -> int:
     # comes back through an asynchronous 64 B copy into pinned memory; the compute stream
     # waits for the gather that last used a buffer before encoding into it again.
     pipelined = use_pg and args.gather == "root"
+    last_buf = [d_out]
     if pipelined:
         d_outs = [d_out, torch.empty_like(d_out)]
         res_h = [torch.zeros(64, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
@@ -251,6 +422,7 @@ def main() -> int:
             enc.encode_async(d_in.data_ptr(), n, d_outs[k].data_ptr(), cap, stream)
             enc.result_async(res_h[k].data_ptr(), stream)
             enc_done[k].record(cur)
+            last_buf[0] = d_outs[k]
 
         def p_gather(i):
             k = i % 2
@@ -281,11 +453,44 @@ def main() -> int:
     res = enc.result(stream)
     out_len = int(res.out_len)
     ok = True
+    stitched = None
     if world == 1:
         z = d_out[:out_len].cpu().numpy().tobytes()
         ok = zlib.decompress(z) == host.tobytes()
         if not ok:
             log("ERROR: stream does not inflate to the input")
+    else:
+        # rank 0 stitches every rank's chunk (header on rank 0's, sync flushes between, BFINAL
+        # on the last) with the combined Adler-32 and inflates it against every rank's input
+        comm_s = torch.cuda.current_stream(dev)
+        torch.cuda.synchronize(dev)
+        outs, glens = S.gather_chunks(last_buf[0], out_len, root=0)
+        meta = torch.tensor([n, int(res.adler)], dtype=torch.int64, device=dev)
+        metas = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(world)]
+        dist.all_gather(metas, meta)
+        comm_s.synchronize()
+        flag = torch.zeros(1, dtype=torch.int64, device=dev)
+        if rank == 0:
+            ns = [int(m[0].item()) for m in metas]
+            ads = [int(m[1].item()) for m in metas]
+            chunks = [o.cpu().numpy().tobytes() for o in outs]
+            if strong:
+                bounds = [S.shard_range(per_rank, r, world) for r in range(world)]
+                pieces = [(lambda lo=lo, hi=hi: full[lo:hi].tobytes()) for lo, hi in bounds]
+            else:
+                pieces = [(lambda r=r: make_input(gen, per_rank, seed + r).tobytes()) for r in range(world)]
+            t0 = time.perf_counter()
+            ok = verify_stitched(chunks, ads, ns, pieces)
+            stitched = {"inflates": ok, "bytes": sum(len(c) for c in chunks) + 4, "input_bytes": sum(ns),
+                        "check_s": round(time.perf_counter() - t0, 2),
+                        "how": "rank 0: chunks gathered over RCCL + combined Adler-32 trailer, zlib inflate, "
+                               "compared with every rank's input"}
+            if not ok:
+                log("ERROR: the stitched multi-rank stream does not inflate to the ranks' inputs")
+            flag[0] = 1 if ok else 0
+        dist.broadcast(flag, 0)
+        ok = bool(flag.item())
+        del full
     # GPU inflate of the same stream: every block decoded in parallel from the
     # encoder's block index, compared bit for bit with the input; timed with events
     # (dict streams reference the previous block: the whole-stream decoder, one timed run)
@@ -294,9 +499,10 @@ def main() -> int:
     dec = torch.empty(n, dtype=torch.uint8, device=dev)
     ist = torch.zeros(16, dtype=torch.uint8, device=dev)
     Lib = D.lib()
+    inf_src = last_buf[0]
 
     def inflate():
-        rc = Lib.dmx_inflate_async(d_out.data_ptr(), out_len, ix.data_ptr() if indexed else None, nblk,
+        rc = Lib.dmx_inflate_async(inf_src.data_ptr(), out_len, ix.data_ptr() if indexed else None, nblk,
                                    dec.data_ptr(), n, ist.data_ptr(), stream)
         if rc != 0:
             raise RuntimeError(f"dmx_inflate_async: {rc}")
@@ -342,6 +548,18 @@ def main() -> int:
     stage_ms, nstage = enc.stage_times()
     enc.set_timing(False)
     dt = t1 - t0
+    # a longer run of the same step (outside the timed region): the timed region above is what
+    # the driver asked for; this shows the rate holds over about a second of back-to-back steps
+    long_run = None
+    if world == 1 and args.long_run > 0 and not pipelined:
+        reps = max(args.steps, int(args.long_run / max(dt / max(args.steps, 1), 1e-4)))
+        torch.cuda.synchronize(dev)
+        q0 = time.perf_counter()
+        run(reps)
+        torch.cuda.synchronize(dev)
+        q1 = time.perf_counter()
+        long_run = {"steps": reps, "s": round(q1 - q0, 3), "value": round(n * reps / (q1 - q0) / 1e9, 3),
+                    "ms_per_step": round((q1 - q0) / reps * 1e3, 4)}
     # the speed / size curve over max_chain, same input and flags (outside the timed region)
     tradeoff = []
     if world == 1 and args.tradeoff and not pipelined:
@@ -389,12 +607,13 @@ def main() -> int:
         ms_step = dt / args.steps * 1e3
         value = tot_in * args.steps / dt / 1e9
         dom = max((k for k in stage_ms if k != "total"), key=stage_ms.get)
-        kname = {"pre": "dmx_hist_kernel_t" if args.dict else "dmx_store_check_kernel", "huff": "dmx_split_plan_kernel" if args.split else "dmx_huff_kernel"}.get(
-            dom, f"dmx_{dom}_kernel")
+        kname = {"pre": "dmx_hist_kernel_t" if args.dict else "dmx_store_check_kernel",
+                 "huff": "dmx_split_plan_kernel" if args.split else "dmx_huff_kernel"}.get(dom, f"dmx_{dom}_kernel")
         dom_ms = stage_ms[dom]
         algo_bytes = n + out_len   # per launch on this rank: input read + stream written
         achieved = algo_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
-        traffic = None
+        parse = parse_str(args)
+        traffic, valu, why = None, None, None
         if args.traffic_csv:
             try:
                 import importlib.util
@@ -402,20 +621,42 @@ def main() -> int:
                 pmc = importlib.util.module_from_spec(spec)
                 spec.loader.exec_module(pmc)
                 traffic = pmc.traffic_per_launch(args.traffic_csv, kname)
+                if traffic:
+                    traffic["source"] = "this run's --traffic-csv"
             except Exception as e:  # pragma: no cover
                 log("traffic csv unreadable:", e)
-        cpu = {}
+        ctr, why = roofline_counters(kname, parse, args.workload)
+        nblk_all = int(res.nblocks)
+        if ctr:
+            parsed_blocks = nblk_all - int(res.nstored)   # K0-stored blocks skip the match kernel
+            if traffic is None and ctr.get("fetch_bytes_per_block") is not None:
+                traffic = {"bytes": round((ctr["fetch_bytes_per_block"] + ctr["write_bytes_per_block"]) * nblk_all),
+                           "fetch_bytes": round(ctr["fetch_bytes_per_block"] * nblk_all),
+                           "write_bytes": round(ctr["write_bytes_per_block"] * nblk_all),
+                           "correction": "FETCH_SIZE KiB x2 (gfx950 half-count), WRITE_SIZE KiB x1",
+                           "source": f"profile-run counters, {ctr['source']} (per block x this launch's blocks)"}
+            if ctr.get("valu_per_block") and dom_ms > 0:
+                vpl = ctr["valu_per_block"] * parsed_blocks
+                va = vpl / (dom_ms * 1e-3) / 1e9
+                valu = {"achieved": round(va, 1), "peak": round(VALU_PEAK_GIPS, 1), "unit": "G VALU wave-instr/s",
+                        "frac": round(va / VALU_PEAK_GIPS, 4), "instr_per_launch": round(vpl),
+                        "instr_per_block": round(ctr["valu_per_block"]),
+                        "peak_basis": "256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 integer VALU instruction "
+                                      "(tools/valu_peak.hip: 526-630 G/s measured)",
+                        "source": f"SQ_INSTS_VALU per block from {ctr['source']} x this launch's parsed blocks, "
+                                  "divided by this run's HIP-event launch time"}
+        cpu, info = ({}, cpu_info())
         e2e = zl6 = None
         if world == 1 and args.cpu_budget > 0:
-            cpu = cpu_baseline(host, args.cpu_budget)
+            cpu, info = cpu_baselines(host, args, args.cpu_budget)
             try:
                 e2e = end_to_end(host, args)
             except Exception as e:  # pragma: no cover
                 log("end-to-end fd API leg failed:", e)
             zl6 = len(zlib.compress(host.tobytes(), 6))   # context: zlib -6 on the same input
-        base = cpu.get("reference") or cpu.get("port")
+        base = cpu.get("same_parse")
         size_pct = s_ref_bytes = None
-        if "s_ref" in cpu and cpu["s_ref"][0] == n:
+        if "s_ref" in cpu and cpu["s_ref"][0] == n and cpu["s_ref"][1]:
             s_ref_bytes = cpu["s_ref"][1]
             size_pct = round((out_len / s_ref_bytes - 1) * 100, 3)
             for t in tradeoff:
@@ -435,11 +676,10 @@ def main() -> int:
             "data": "synthetic",
             "config": {
                 "workload": desc,
+                "name": args.workload,
                 "bytes_per_rank": n,
                 "block": 32768,
-                "parse": ("exhaustive (reference semantics)" if args.max_chain == 0 else f"max_chain={args.max_chain}")
-                         + (", lazy" if args.lazy else ", greedy") + (", split" if args.split else "")
-                         + (", dict" if args.dict else "") + (", store-check" if args.store_check else ""),
+                "parse": parse,
                 "parallelism": f"blocks sharded over {world} GPU(s)" + (f", gather={args.gather}" if world > 1 else "")
                                + (", pipelined" if pipelined else ""),
             },
@@ -448,32 +688,40 @@ def main() -> int:
             "s_ref_bytes": s_ref_bytes,
             "exhaustive": exh,
             "tradeoff": tradeoff or None,
+            "long_run": long_run,
             "compressed_bytes_rank0": out_len,
+            "compressed_bytes_all": tot_out,
             "inflate_ok": ok,
+            "stitched": stitched,
             "gpu_inflate": gpu_inflate,
             "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
             "roofline": {
-                "bound": "hbm",
+                "bound": "valu",
                 "kernel": kname,
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "frac_basis": "HBM: algorithmic bytes (input + stream) per launch / launch time / 8 TB/s; "
+                              "the binding roofline is roofline.valu (integer VALU issue)",
                 "traffic": traffic["bytes"] if traffic else None,
                 "traffic_detail": traffic,
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "launch_ms": round(dom_ms, 4),
                 "launches_timed": nstage,
+                "valu": valu,
+                "counters_note": why,
             },
             "end_to_end_fd_api": e2e,
             "zlib6": None if zl6 is None else {"ratio": round(zl6 / n, 5), "compressed_bytes": zl6,
                                                  "ours_vs_zlib6_pct": round((out_len / zl6 - 1) * 100, 3)},
             "cpu_baseline": base,
-            "cpu_baseline_port": cpu.get("port") if base is not cpu.get("port") else None,
-            "host": {"cpu": platform.processor() or platform.machine(), "nproc": os.cpu_count()},
+            "cpu_baseline_exhaustive": cpu.get("exhaustive"),
+            "cpu_baseline_reference": cpu.get("reference"),
+            "host": info,
         }
-        if base:
-            line["gpu_over_cpu"] = round(value / base["value"], 1) if base["value"] else None
+        if base and base["value"]:
+            line["gpu_over_cpu"] = round(value / base["value"], 1)
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(line) + "\n").encode())
     enc.close()

@@ -153,3 +153,32 @@ def test_dict_c3_scale_roundtrip(enc):
     finally:
         big.close()
     assert zlib.decompress(zd) == t.cpu().numpy().tobytes()
+
+
+def test_dict_regression_text_k4_greedy_repeated():
+    """The input of the one unexplained round-1 mismatch (test_dict_streams_match_oracle[False-4],
+    text, one byte off at ~15.9 KB of the stream: block 1, the first block with a history),
+    encoded 12 times in one process -- on one context, on fresh contexts, and after encodes of
+    other inputs and settings that leave different data in the chain / token buffers -- each
+    byte-equal to the oracle, and every block's tokens equal.  DESIGN.md §10 gives the analysis."""
+    data = _inputs()["text"]
+    flags = D.DMX_ZLIB | D.DMX_F_DICT
+    zo = O.compress(data, max_chain=4, lazy=False, dict=True)
+    ref = O.parse(data, max_chain=4, lazy=False, dict=True)
+    other = D.gen_text(400000, 77).tobytes()
+    shared = D.Encoder(0, 1 << 20)
+    try:
+        for rep in range(12):
+            e = shared if rep % 3 else D.Encoder(0, 1 << 20)
+            try:
+                if rep % 4 == 1:   # different data and settings in the buffers first
+                    e.compress_bytes(other, max_chain=8, flags=D.DMX_ZLIB | D.DMX_F_DICT | D.DMX_F_LAZY)
+                z, r = e.compress_bytes(data, max_chain=4, flags=flags)
+                assert z == zo, rep
+                for b, t in enumerate(ref):
+                    assert np.array_equal(e.tokens(b), t), (rep, b)
+            finally:
+                if e is not shared:
+                    e.close()
+    finally:
+        shared.close()

@@ -74,7 +74,36 @@ def traffic_per_launch(spec: str, kernel: str):
     }
 
 
+def counters_json(pmc_spec: str, sq_spec: str, nblk: int, parsed: int, source: str, parse: str, workload: str,
+                  kernel: str = "dmx_match_kernel") -> dict:
+    """tools/roofline_counters.json for bench.py: per-block FETCH / WRITE bytes (corrected)
+    and SQ instruction counts of `kernel`, from a profile of the bench configuration itself
+    (nblk blocks per launch, `parsed` of them through the kernel)."""
+    out = {"source": source, "parse": parse, "workload": workload, "blocks_per_launch": nblk, "kernels": {}}
+    t = traffic_per_launch(pmc_spec, kernel) if pmc_spec else None
+    sq = {k: v for k, v in per_kernel(sq_spec).items() if kernel in k} if sq_spec else {}
+    k = {}
+    if t:
+        k["fetch_bytes_per_block"] = t["fetch_bytes"] / nblk
+        k["write_bytes_per_block"] = t["write_bytes"] / nblk
+    if sq:
+        m = next(iter(sq.values()))
+        for c, name in (("SQ_INSTS_VALU", "valu_per_block"), ("SQ_INSTS_SALU", "salu_per_block"),
+                        ("SQ_INSTS_LDS", "lds_per_block"), ("SQ_LDS_BANK_CONFLICT", "lds_conflict_cycles_per_block"),
+                        ("SQ_LDS_IDX_ACTIVE", "lds_active_cycles_per_block")):
+            if c in m:
+                k[name] = m[c] / parsed
+    out["kernels"][kernel] = k
+    return out
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "--counters-json":
+        # --counters-json PMC_DIRS SQ_DIRS NBLK PARSED SOURCE PARSE WORKLOAD > tools/roofline_counters.json
+        import json
+        a = sys.argv[2:]
+        print(json.dumps(counters_json(a[0], a[1], int(a[2]), int(a[3]), a[4], a[5], a[6]), indent=1))
+        sys.exit(0)
     spec = sys.argv[1]
     for k, v in sorted(per_kernel(spec).items()):
         short = k.split("(")[0]
