@@ -73,15 +73,40 @@ __device__ __forceinline__ uint32_t len_eb_of_sym(uint32_t s) {  // s in 257..28
 __device__ __forceinline__ uint32_t dist_eb_of_sym(uint32_t s) { return s < 4 ? 0 : s / 2 - 1; }
 __device__ __forceinline__ uint32_t fixed_len(uint32_t s) { return s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8; }
 
+// Wave sums by DPP row shifts (lane 15 of each row of 16 ends with the row's sum) and four
+// readlanes; the result is uniform.  All 64 lanes must be active.  (__shfl_xor lowers to
+// ds_bpermute with per-lane index registers that the compiler keeps live, and spills, across
+// the match kernel.)
+#define DMX_DPP_SHR(x, n) ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)(x), 0x110 + (n), 0xF, 0xF, true))
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+    v += DMX_DPP_SHR(v, 1);
+    v += DMX_DPP_SHR(v, 2);
+    v += DMX_DPP_SHR(v, 4);
+    v += DMX_DPP_SHR(v, 8);
+    return __builtin_amdgcn_readlane(v, 15) + __builtin_amdgcn_readlane(v, 31) + __builtin_amdgcn_readlane(v, 47) +
+           __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ uint64_t dpp_shr64(uint64_t v, int n) {
+    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    uint32_t a, b;
+    switch (n) {
+        case 1: a = DMX_DPP_SHR(lo, 1); b = DMX_DPP_SHR(hi, 1); break;
+        case 2: a = DMX_DPP_SHR(lo, 2); b = DMX_DPP_SHR(hi, 2); break;
+        case 4: a = DMX_DPP_SHR(lo, 4); b = DMX_DPP_SHR(hi, 4); break;
+        default: a = DMX_DPP_SHR(lo, 8); b = DMX_DPP_SHR(hi, 8); break;
+    }
+    return (uint64_t)a | ((uint64_t)b << 32);
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32);
 }
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+    v += dpp_shr64(v, 1);
+    v += dpp_shr64(v, 2);
+    v += dpp_shr64(v, 4);
+    v += dpp_shr64(v, 8);
+    return readlane64(v, 15) + readlane64(v, 31) + readlane64(v, 47) + readlane64(v, 63);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1758,21 +1783,11 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
     {
         const uint32_t m = L.tsm[tid];
         const uint32_t cnt = __popc(m);
-        uint32_t x = cnt;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o);
-            if (lane >= (uint32_t)o) x += y;
-        }
+        const uint32_t x = wave_incl_scan(cnt);
         if (lane == 63) L.wsum[wave] = x;
         __syncthreads();
         if (wave == 0) {
-            uint32_t v = lane < MW ? L.wsum[lane] : 0, z = v;
-#pragma unroll
-            for (int o = 1; o < MW; o <<= 1) {
-                const uint32_t y = __shfl_up(z, o);
-                if (lane >= (uint32_t)o) z += y;
-            }
+            const uint32_t v = lane < MW ? L.wsum[lane] : 0, z = wave_incl_scan(v);
             if (lane < MW) L.wsum[lane] = z - v;
             if (lane == MW - 1) L.ntok = z;
         }
