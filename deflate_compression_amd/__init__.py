@@ -39,7 +39,7 @@ DMX_F_SPLIT = 32
 DMX_F_DICT = 64
 DMX_F_STORE_CHECK = 128
 _M = 1 << 24
-# global_errors.h:64-75 and deflate_errors.h:134-147
+# src/include/global_errors.h:24-35 and src/include/deflate_errors.h:9-22
 E = {
     "E_LEN": 1, "E_MALLOC": 2, "E_FORK": 3, "E_PIPE": 4, "E_CRC": 5, "E_SZ": 6, "E_EXIST": 7,
     "E_NEXIST": 8, "E_NONULL": 9, "E_RANGE": 10, "E_INVAL": 11, "E_RESERV": 12,
@@ -103,6 +103,10 @@ def lib() -> ctypes.CDLL:
         "dmx_ctx_create": ([ctypes.c_int, u64, ctypes.POINTER(vp)], ctypes.c_int),
         "dmx_ctx_destroy": ([vp], None),
         "dmx_ctx_reserve": ([vp, u64, i32], ctypes.c_int),
+        "dmx_ctx_reserve_flags": ([vp, u64, i32, u32], ctypes.c_int),
+        "dmx_fault_set": ([ctypes.c_char_p], ctypes.c_int),
+        "dmx_encode_fd_multi": ([ctypes.c_int, ctypes.c_int, ctypes.POINTER(Opts), u64,
+                                 ctypes.POINTER(ctypes.c_int), ctypes.c_int], ctypes.c_int),
         "dmx_max_compressed": ([u64, i32], u64),
         "dmx_encode_async": ([vp, vp, u64, vp, u64, ctypes.POINTER(Opts), vp], ctypes.c_int),
         "dmx_encode_result": ([vp, ctypes.POINTER(Result), vp], ctypes.c_int),
@@ -217,6 +221,11 @@ def inflate_gpu(z, out_cap: int, index=None, nblk: int = 0, stream=None):
     return out[:olen], status
 
 
+def fault_set(spec: str | None) -> int:
+    """Fault injection (tests): "malloc:N" / "launch:N" / None (dmx_fault_set)."""
+    return int(lib().dmx_fault_set(spec.encode() if spec else None))
+
+
 def adler32_combine(a: int, b: int, len_b: int) -> int:
     return int(lib().dmx_adler32_combine(a, b, len_b))
 
@@ -249,6 +258,12 @@ class Encoder:
         self.opts = Opts(sw, max_chain, flags, 0)
         self._ctx = ctypes.c_void_p()
         _check(self._L.dmx_ctx_create(device, max_input, ctypes.byref(self._ctx)), "dmx_ctx_create")
+        if flags & (DMX_F_SPLIT | DMX_F_DICT):   # the block options' scratch (no allocation per encode)
+            try:
+                self.reserve(max_input, sw, flags)
+            except DeflateError:
+                self.close()
+                raise
 
     def close(self) -> None:
         if self._ctx:
@@ -261,8 +276,10 @@ class Encoder:
         except Exception:
             pass
 
-    def reserve(self, n: int, sw: int = 32768) -> None:
-        _check(self._L.dmx_ctx_reserve(self._ctx, n, sw), "dmx_ctx_reserve")
+    def reserve(self, n: int, sw: int = 32768, flags: int = 0) -> None:
+        """Workspace for n bytes of sw-byte blocks, plus the scratch of DMX_F_SPLIT / DMX_F_DICT
+        (dmx_ctx_reserve_flags; synchronises only when it allocates)."""
+        _check(self._L.dmx_ctx_reserve_flags(self._ctx, n, sw, flags), "dmx_ctx_reserve_flags")
 
     def encode_async(self, d_in: int, n: int, d_out: int, cap: int, stream: int | None = None,
                      opts: Opts | None = None) -> None:
@@ -372,6 +389,7 @@ class Encoder:
         import torch
         o = opts or self.opts
         n = t_in.numel()
+        self.reserve(n, o.sw, o.flags)
         cap = max_compressed(n, o.sw)
         out = torch.empty(cap, dtype=torch.uint8, device=t_in.device)
         s = stream if stream is not None else torch.cuda.current_stream(t_in.device).cuda_stream
@@ -387,7 +405,7 @@ class Encoder:
         dev = f"cuda:{self.device}"
         a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
         t = torch.from_numpy(a.copy()).to(dev) if a.size else torch.empty(0, dtype=torch.uint8, device=dev)
-        self.reserve(a.size, sw)
+        self.reserve(a.size, sw, flags)
         o = Opts(sw, max_chain, flags, 0)
         if pre is not None and len(pre):
             tp = torch.from_numpy(np.frombuffer(bytes(pre), dtype=np.uint8).copy()).to(dev)

@@ -100,16 +100,26 @@ static void h_dist_sym(int dist, int* sym, int* eb) {
     *eb = e - 1;
 }
 
-/* One compress_stats record per token (deflate_compress.c:290-309) with exact costs:
- * tree_bits = header bits of the token's DEFLATE block, ll_bits/d_bits = running lit/len
- * and distance bits inside that block.  With DMX_F_SPLIT an sw block holds up to four
- * DEFLATE blocks, each with its own codes; the running sums restart at each. */
+/* One compress_stats record per token (deflate_compress.c:290-309), with the reference's
+ * accumulation: in the reference ll_bits / d_bits are the adaptive-Huffman scores of every
+ * token so far (ll_aht.score / d_aht.score, :297-298, aht.c:239-277) and tree_bits the cost
+ * of describing the current codes (h_tree_d_lens + the code-length tree, :292-295), so
+ * (tree_bits + ll_bits + d_bits) / bytes is the stream's rate so far.  Here the same sums
+ * are exact instead of estimated, over the whole stream:
+ *   tree_bits = header bits of every DEFLATE block begun so far (its own included: BFINAL /
+ *               BTYPE, and for dynamic blocks the code-length and code descriptions);
+ *   ll_bits   = lit/len code bits + length extra bits of every token so far (stored blocks:
+ *               8 per byte);
+ *   d_bits    = distance code bits + distance extra bits of every match so far.
+ * With DMX_F_SPLIT an sw block holds up to four DEFLATE blocks, each with its own codes.
+ * (Round 1 restarted the sums at every block) */
 static int write_stats(dmx_ctx* c, int fd, uint64_t n, int sw) {
     const uint32_t nblk = (uint32_t)((n + (uint64_t)sw - 1) / (uint64_t)sw);
     if (!nblk) return 0;
     uint32_t* tok = (uint32_t*)malloc(sizeof(uint32_t) * DMX_BLK);
     struct compress_stats* rec = (struct compress_stats*)malloc(sizeof(struct compress_stats) * DMX_BLK);
     int r = 0;
+    long long tree_bits = 0, ll_bits = 0, d_bits = 0;   /* over the whole stream */
     if (!tok || !rec) r = -E_MALLOC;
     for (uint32_t b = 0; !r && b < nblk; b++) {
         int nt = dmx_last_tokens(c, b, tok, DMX_BLK);
@@ -121,16 +131,16 @@ static int write_stats(dmx_ctx* c, int fd, uint64_t n, int sw) {
             uint32_t range[2], bt = 0, hb = 0;
             nsub = dmx_last_subblock(c, b, (uint32_t)sb, range, &bt, &hb, lens);
             if (nsub < 0) { r = nsub; break; }
-            int ll_bits = 0, d_bits = 0;
+            tree_bits += bt == 2 ? (long long)hb : 3;
             for (uint32_t k = range[0]; k < range[1]; k++) {
                 uint32_t t = tok[k];
                 struct compress_stats* cs = rec + k;
                 cs->bytes = (int)(pos + 1);
-                cs->tree_bits = bt == 2 ? (int)hb : 3;
+                cs->tree_bits = (int)tree_bits;
                 if ((t >> 9) == 0) {
                     cs->ll = (int)(t & 0xFF);
                     cs->d = 0;
-                    ll_bits += bt == 0 ? 8 : lens[t & 0xFF];
+                    ll_bits += bt == 0 ? 8 : (long long)lens[t & 0xFF];
                     pos += 1;
                 } else {
                     int len = (int)(t & 0x1FF), dist = (int)(t >> 9), sy, eb;
@@ -146,8 +156,8 @@ static int write_stats(dmx_ctx* c, int fd, uint64_t n, int sw) {
                     }
                     pos += (uint64_t)len;
                 }
-                cs->ll_bits = ll_bits;
-                cs->d_bits = d_bits;
+                cs->ll_bits = (int)ll_bits;
+                cs->d_bits = (int)d_bits;
             }
         }
         if (!r) r = write_all(fd, rec, sizeof(struct compress_stats) * (uint64_t)nt);
@@ -180,6 +190,10 @@ int deflate_compress(int fd_in, int fd_out, int fd_stats, swi sw, int ops) {
     if (fd_stats < 0) {   /* streaming: chunks of DMX_CHUNK_MB MiB (default 16) through pinned buffers */
         const char* cm = getenv("DMX_CHUNK_MB");
         const uint64_t mb = cm && atoi(cm) > 0 ? (uint64_t)atoi(cm) : 16u;
+        int devs[64];
+        const int nd = dmx_devices_from_env(devs, 64);   /* DMX_DEVICES: one host thread per GPU */
+        if (nd < 0) return nd;
+        if (nd > 0) return dmx_encode_fd_multi(fd_in, fd_out, &o, mb << 20, devs, nd);
         return dmx_encode_fd(fd_in, fd_out, &o, mb << 20);
     }
     uint8_t* in = NULL;

@@ -16,6 +16,7 @@
  * Returns 0 or -E_*.  Decoding is canonical-Huffman by code-length counts (one bit
  * per step), with a 9-bit first-level lookup table for the common short codes.
  */
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -102,6 +103,9 @@ static int build(huff* h, const uint8_t* len, int n) {
     return left;
 }
 
+/* Slow path: the canonical-code walk by per-length counts (first code / count / index per
+ * length, one bit at a time) is the well-known loop of Mark Adler's puff.c (zlib
+ * contrib/puff, zlib licence); restated here, it is not from the reference. */
 static int decode(ist* s, const huff* h) {
     need(s, FAST);  /* may be short at the very end; the slow path copes */
     if (s->bitcnt >= FAST) {
@@ -177,18 +181,22 @@ static int stored(ist* s) {
     return 0;
 }
 
+/* The fixed-code tables (RFC 1951 §3.2.6), built once: pthread_once makes concurrent
+ * callers of deflate_decompress wait for the complete tables instead of reading a table
+ * another thread is still writing. */
+static huff fixed_lh, fixed_dh;
+static pthread_once_t fixed_once = PTHREAD_ONCE_INIT;
+static void fixed_build(void) {
+    uint8_t l[288];
+    for (int k = 0; k < 288; k++) l[k] = k < 144 ? 8 : k < 256 ? 9 : k < 280 ? 7 : 8;
+    build(&fixed_lh, l, 288);
+    for (int k = 0; k < 30; k++) l[k] = 5;
+    build(&fixed_dh, l, 30);
+}
+
 static int fixed(ist* s) {
-    static huff lh, dh;
-    static int ready = 0;
-    if (!ready) {
-        uint8_t l[288];
-        for (int k = 0; k < 288; k++) l[k] = k < 144 ? 8 : k < 256 ? 9 : k < 280 ? 7 : 8;
-        build(&lh, l, 288);
-        for (int k = 0; k < 30; k++) l[k] = 5;
-        build(&dh, l, 30);
-        ready = 1;
-    }
-    return codes(s, &lh, &dh);
+    pthread_once(&fixed_once, fixed_build);
+    return codes(s, &fixed_lh, &fixed_dh);
 }
 
 static int dynamic(ist* s) {

@@ -39,4 +39,13 @@ typedef struct {
     uint64_t body_bits; /* coded tokens + extra bits + EOB */
 } dmx_subinfo;
 
+/* DMX_DEVICES parsed ("0,1,2,3" or "all"): entries written to devs, 0 if unset, -E_INVAL. */
+#ifdef __cplusplus
+extern "C" {
+#endif
+int dmx_devices_from_env(int* devs, int cap);
+#ifdef __cplusplus
+}
+#endif
+
 #endif

@@ -3049,6 +3049,7 @@ struct dmx_ctx {
     uint64_t cap_chain;
     void* split;          // DMX_F_SPLIT: cap_split x SplitScratch (per-block plans of the 10 groups)
     uint64_t cap_split;
+    uint32_t want;        // DMX_F_SPLIT / DMX_F_DICT: scratch kept reserved with the workspace
     // timing: a ring of event sets so timed encodes never block the host
     int timing;
     hipEvent_t ev[DMX_EV_RING][6];
@@ -3057,6 +3058,52 @@ struct dmx_ctx {
     double stage_ms[6];
     uint32_t stage_n;
 };
+
+// ---- fault injection (tests): DMX_FAULT="malloc:N" makes the N-th device / pinned allocation
+// from now fail, "launch:N" the N-th encode launch check; dmx_fault_set() sets it at run time.
+// Every error path must then return -E_* and leave nothing allocated that the context does
+// not own (global_errors.h:60-81 is the reference's checkpoint mechanism).
+#include <pthread.h>
+static pthread_mutex_t g_fault_mu = PTHREAD_MUTEX_INITIALIZER;
+static int g_fault_kind = 0;   // 1 = allocation, 2 = launch
+static long g_fault_left = 0;
+extern "C" int dmx_fault_set(const char* spec) {
+    int kind = 0;
+    long n = 0;
+    if (spec && *spec) {
+        if (!strncmp(spec, "malloc:", 7)) { kind = 1; n = atol(spec + 7); }
+        else if (!strncmp(spec, "launch:", 7)) { kind = 2; n = atol(spec + 7); }
+        else return -(int)E_INVAL;
+        if (n <= 0) return -(int)E_RANGE;
+    }
+    pthread_mutex_lock(&g_fault_mu);
+    g_fault_kind = kind;
+    g_fault_left = n;
+    pthread_mutex_unlock(&g_fault_mu);
+    return 0;
+}
+__attribute__((constructor)) static void dmx_fault_env(void) { (void)dmx_fault_set(getenv("DMX_FAULT")); }
+static bool fault_hit(int kind) {
+    if (!g_fault_kind) return false;
+    pthread_mutex_lock(&g_fault_mu);
+    bool hit = false;
+    if (g_fault_kind == kind && g_fault_left > 0 && --g_fault_left == 0) {
+        hit = true;
+        g_fault_kind = 0;
+    }
+    pthread_mutex_unlock(&g_fault_mu);
+    return hit;
+}
+static hipError_t dmx_malloc(void** p, size_t n) {
+    if (fault_hit(1)) { *p = NULL; return hipErrorOutOfMemory; }
+    return hipMalloc(p, n);
+}
+static hipError_t dmx_host_malloc(void** p, size_t n) {
+    if (fault_hit(1)) { *p = NULL; return hipErrorOutOfMemory; }
+    return hipHostMalloc(p, n, 0);
+}
+template <typename T>
+static hipError_t dmx_malloc(T** p, size_t n) { return dmx_malloc(reinterpret_cast<void**>(p), n); }
 
 static int hip_fail(hipError_t e, const char* what) {
     if (e != hipSuccess) {
@@ -3087,20 +3134,51 @@ static void ctx_free_ws(dmx_ctx* c) {
     c->cap_blocks = 0;
 }
 
+// Scratch of the block options, sized to the block capacity: split plans (DMX_F_SPLIT), the
+// exported chains of every block + the dict (DMX_F_DICT), and the diagnostic stamps.
+static int ctx_reserve_scratch(dmx_ctx* c) {
+    const uint64_t cb = c->cap_blocks;
+    if ((c->want & DMX_F_SPLIT) && c->cap_split < cb) {
+        if (c->split) (void)hipFree(c->split);
+        c->split = NULL;
+        c->cap_split = 0;
+        HIPCHK(dmx_malloc(&c->split, cb * sizeof(SplitScratch)));
+        c->cap_split = cb;
+    }
+    if ((c->want & DMX_F_DICT) && c->cap_chain < cb + 1) {
+        if (c->chs) (void)hipFree(c->chs);
+        if (c->che) (void)hipFree(c->che);
+        c->chs = NULL;
+        c->che = NULL;
+        c->cap_chain = 0;
+        HIPCHK(dmx_malloc(&c->chs, (cb + 1) * DMX_BLK * sizeof(uint16_t)));
+        HIPCHK(dmx_malloc(&c->che, (cb + 1) * DMX_NBUCKET * sizeof(uint16_t)));
+        c->cap_chain = cb + 1;
+    }
+    if (getenv("DMX_STAMPS") && c->dbg_cap < cb) {
+        if (c->dbg) (void)hipFree(c->dbg);
+        c->dbg = NULL;
+        c->dbg_cap = 0;
+        HIPCHK(dmx_malloc(&c->dbg, cb * DMX_STAMPS * sizeof(uint64_t)));
+        c->dbg_cap = cb;
+    }
+    return 0;
+}
+
 static int ctx_reserve(dmx_ctx* c, uint64_t nblk) {
-    if (nblk <= c->cap_blocks) return 0;
+    if (nblk <= c->cap_blocks) return ctx_reserve_scratch(c);
     ctx_free_ws(c);
     const uint64_t cb = nblk < 1 ? 1 : nblk;
-    HIPCHK(hipMalloc(&c->dist, cb * DMX_BLK * sizeof(uint16_t)));
-    HIPCHK(hipMalloc(&c->tok, cb * DMX_BLK * sizeof(uint32_t)));
-    HIPCHK(hipMalloc(&c->hist, cb * DMX_HIST * sizeof(uint32_t)));
-    HIPCHK(hipMalloc(&c->codes, cb * DMX_NSUB * DMX_HIST * sizeof(uint32_t)));
-    HIPCHK(hipMalloc(&c->hdr, cb * DMX_NSUB * DMX_HDR_WORDS * sizeof(uint32_t)));
-    HIPCHK(hipMalloc(&c->sub, cb * DMX_NSUB * sizeof(dmx_subinfo)));
-    HIPCHK(hipMalloc(&c->info, cb * sizeof(dmx_blkinfo)));
-    HIPCHK(hipMalloc(&c->tiles, (cb / SCAN_TILE + 1) * sizeof(ScanTile)));
+    HIPCHK(dmx_malloc(&c->dist, cb * DMX_BLK * sizeof(uint16_t)));
+    HIPCHK(dmx_malloc(&c->tok, cb * DMX_BLK * sizeof(uint32_t)));
+    HIPCHK(dmx_malloc(&c->hist, cb * DMX_HIST * sizeof(uint32_t)));
+    HIPCHK(dmx_malloc(&c->codes, cb * DMX_NSUB * DMX_HIST * sizeof(uint32_t)));
+    HIPCHK(dmx_malloc(&c->hdr, cb * DMX_NSUB * DMX_HDR_WORDS * sizeof(uint32_t)));
+    HIPCHK(dmx_malloc(&c->sub, cb * DMX_NSUB * sizeof(dmx_subinfo)));
+    HIPCHK(dmx_malloc(&c->info, cb * sizeof(dmx_blkinfo)));
+    HIPCHK(dmx_malloc(&c->tiles, (cb / SCAN_TILE + 1) * sizeof(ScanTile)));
     c->cap_blocks = cb;
-    return 0;
+    return ctx_reserve_scratch(c);
 }
 
 extern "C" int dmx_ctx_create(int device, uint64_t max_input, dmx_ctx** out) {
@@ -3115,8 +3193,8 @@ extern "C" int dmx_ctx_create(int device, uint64_t max_input, dmx_ctx** out) {
     dmx_ctx* c = (dmx_ctx*)calloc(1, sizeof(dmx_ctx));
     if (!c) return -(int)E_MALLOC;
     c->device = device;
-    if (hip_fail(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate")) { free(c); return -(int)E_DEVICE; }
-    if (hip_fail(hipMalloc(&c->res, sizeof(dmx_result)), "hipMalloc(res)")) { free(c); return -(int)E_DEVICE; }
+    if (hip_fail(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate")) { c->stream = NULL; dmx_ctx_destroy(c); return -(int)E_DEVICE; }
+    if (hip_fail(dmx_malloc(&c->res, sizeof(dmx_result)), "hipMalloc(res)")) { dmx_ctx_destroy(c); return -(int)E_DEVICE; }
     for (int j = 0; j < DMX_EV_RING; j++)
         for (int k = 0; k < 6; k++) (void)hipEventCreate(&c->ev[j][k]);
     const uint64_t nb = (max_input + DMX_BLK - 1) / DMX_BLK;
@@ -3126,17 +3204,25 @@ extern "C" int dmx_ctx_create(int device, uint64_t max_input, dmx_ctx** out) {
     return 0;
 }
 
-extern "C" int dmx_ctx_reserve(dmx_ctx* c, uint64_t n, int32_t sw) {
+extern "C" int dmx_ctx_reserve_flags(dmx_ctx* c, uint64_t n, int32_t sw, uint32_t flags) {
     if (!c) return -(int)E_INVAL;
     if (sw == 0) sw = DMX_BLK;
     if (sw < 1 || sw > DMX_BLK) return -(int)E_RANGE;
-    HIPCHK(hipSetDevice(c->device));
     const uint64_t nblk = (n + (uint64_t)sw - 1) / (uint64_t)sw;
-    if (nblk <= c->cap_blocks) return 0;
+    const uint32_t want = c->want | (flags & (DMX_F_SPLIT | DMX_F_DICT));
+    const bool stamps = getenv("DMX_STAMPS") != NULL;
+    const uint64_t cb = nblk > c->cap_blocks ? nblk : c->cap_blocks;
+    if (nblk <= c->cap_blocks && want == c->want && (!(want & DMX_F_SPLIT) || c->cap_split >= cb) &&
+        (!(want & DMX_F_DICT) || c->cap_chain >= cb + 1) && (!stamps || c->dbg_cap >= cb))
+        return 0;   // nothing to do: no synchronisation
+    HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipDeviceSynchronize());
+    c->want = want;
     return ctx_reserve(c, nblk);
 }
+
+extern "C" int dmx_ctx_reserve(dmx_ctx* c, uint64_t n, int32_t sw) { return dmx_ctx_reserve_flags(c, n, sw, 0); }
 
 extern "C" void dmx_ctx_destroy(dmx_ctx* c) {
     if (!c) return;
@@ -3196,23 +3282,10 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
     if (nblk64 > c->cap_blocks || nblk64 > 0x7FFFFFFFull) return -(int)E_SZ;
     const uint32_t nblk = (uint32_t)nblk64;
     HIPCHK(hipSetDevice(c->device));
-    if ((o.flags & DMX_F_SPLIT) && c->cap_split < c->cap_blocks) {   // split plan scratch, on first use
-        if (c->split) (void)hipFree(c->split);
-        c->split = NULL;
-        c->cap_split = 0;
-        HIPCHK(hipMalloc(&c->split, c->cap_blocks * sizeof(SplitScratch)));
-        c->cap_split = c->cap_blocks;
-    }
-    if ((o.flags & DMX_F_DICT) && c->cap_chain < c->cap_blocks + 1) {   // chain export buffers, on first use
-        if (c->chs) (void)hipFree(c->chs);
-        if (c->che) (void)hipFree(c->che);
-        c->chs = NULL;
-        c->che = NULL;
-        c->cap_chain = 0;
-        HIPCHK(hipMalloc(&c->chs, (c->cap_blocks + 1) * DMX_BLK * sizeof(uint16_t)));
-        HIPCHK(hipMalloc(&c->che, (c->cap_blocks + 1) * DMX_NBUCKET * sizeof(uint16_t)));
-        c->cap_chain = c->cap_blocks + 1;
-    }
+    // no allocation here (graph-capturable, no device-wide sync): the split / dictionary
+    // scratch comes from dmx_ctx_reserve_flags
+    if ((o.flags & DMX_F_SPLIT) && c->cap_split < nblk) return -(int)E_SZ;
+    if ((o.flags & DMX_F_DICT) && c->cap_chain < (uint64_t)nblk + 1) return -(int)E_SZ;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     hipEvent_t* ev = NULL;
     if (c->timing) {
@@ -3223,16 +3296,8 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         (void)hipEventRecord(ev[0], s);
     }
     if (nblk) {
-        uint64_t* dbg = NULL;
-        if (getenv("DMX_STAMPS")) {
-            if (c->dbg_cap < nblk) {
-                if (c->dbg) (void)hipFree(c->dbg);
-                c->dbg = NULL;
-                c->dbg_cap = 0;
-                if (hipMalloc(&c->dbg, (uint64_t)nblk * DMX_STAMPS * sizeof(uint64_t)) == hipSuccess) c->dbg_cap = nblk;
-            }
-            dbg = c->dbg;
-        }
+        // diagnostic phase stamps (DMX_STAMPS=1 when the context was reserved)
+        uint64_t* dbg = c->dbg_cap >= nblk ? c->dbg : NULL;
         // stage 0 "dict" (DMX_F_DICT only): the chain kernel (every block's sorted chains, and
         // the dict's) and the history search; otherwise the match kernel sorts its own block
         if (o.flags & DMX_F_DICT) {
@@ -3289,7 +3354,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         hipLaunchKernelGGL(dmx_pack_kernel, dim3(nblk), dim3(PT), 0, s, (const uint8_t*)d_in, (uint32_t)o.sw, c->tok,
                            c->codes, c->hdr, c->info, c->sub, nblk, o.flags, (uint32_t*)d_out, c->res);
     if (ev) (void)hipEventRecord(ev[5], s);
-    HIPCHK(hipGetLastError());
+    HIPCHK(fault_hit(2) ? hipErrorLaunchFailure : hipGetLastError());
     c->last_nblk = nblk;
     c->last_sw = (uint32_t)o.sw;
     return 0;
@@ -3440,7 +3505,7 @@ static int ensure_buf(void** p, uint64_t* cap, uint64_t need) {
     if (*p) (void)hipFree(*p);
     *p = NULL;
     *cap = 0;
-    HIPCHK(hipMalloc(p, need ? need : 16));
+    HIPCHK(dmx_malloc(p, need ? need : 16));
     *cap = need;
     return 0;
 }
@@ -3458,8 +3523,7 @@ extern "C" int dmx_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint
     dmx_ctx* c = dmx_cached_ctx(dev, n, &err);
     int r = err;
     if (!r) {
-        const uint64_t nblk = (n + (uint64_t)o.sw - 1) / (uint64_t)o.sw;
-        r = ctx_reserve(c, nblk);
+        r = dmx_ctx_reserve_flags(c, n, o.sw, o.flags);
     }
     const uint64_t dcap = dmx_max_compressed(n, o.sw);
     if (!r) r = ensure_buf(&c->d_in, &c->d_in_cap, n + 16);
@@ -3468,7 +3532,7 @@ extern "C" int dmx_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint
     if (!r && n && hip_fail(hipMemcpyAsync(c->d_in, in, n, hipMemcpyHostToDevice, c->stream), "H2D")) r = -(int)E_DEVICE;
     if (!r && (o.flags & DMX_F_DICT) && o.dict && o.dict_len) {   // host dictionary -> device
         const uint64_t dl = o.dict_len < (uint64_t)o.sw ? o.dict_len : (uint64_t)o.sw;
-        if (!c->d_dict && hip_fail(hipMalloc(&c->d_dict, DMX_BLK), "hipMalloc(dict)")) r = -(int)E_DEVICE;
+        if (!c->d_dict && hip_fail(dmx_malloc(&c->d_dict, DMX_BLK), "hipMalloc(dict)")) r = -(int)E_DEVICE;
         if (!r && hip_fail(hipMemcpyAsync(c->d_dict, (const uint8_t*)o.dict + (o.dict_len - dl), dl,
                                           hipMemcpyHostToDevice, c->stream), "H2D(dict)")) r = -(int)E_DEVICE;
         o.dict = c->d_dict;
@@ -3626,19 +3690,26 @@ static int fd_buffers(dmx_ctx* c, uint64_t chunk, uint64_t ocap) {
     c->fd_dout = NULL;
     c->fd_chunk = c->fd_ocap = 0;
     for (int k = 0; k < 2; k++) {
-        if (hip_fail(hipHostMalloc((void**)&c->fd_hin[k], chunk + 16, 0), "hipHostMalloc")) return -(int)E_MALLOC;
-        if (hip_fail(hipHostMalloc((void**)&c->fd_hout[k], ocap, 0), "hipHostMalloc")) return -(int)E_MALLOC;
-        if (hip_fail(hipMalloc(&c->fd_din[k], chunk + 16), "hipMalloc")) return -(int)E_DEVICE;
+        if (hip_fail(dmx_host_malloc((void**)&c->fd_hin[k], chunk + 16), "hipHostMalloc")) return -(int)E_MALLOC;
+        if (hip_fail(dmx_host_malloc((void**)&c->fd_hout[k], ocap), "hipHostMalloc")) return -(int)E_MALLOC;
+        if (hip_fail(dmx_malloc(&c->fd_din[k], chunk + 16), "hipMalloc")) return -(int)E_DEVICE;
     }
-    if (hip_fail(hipMalloc(&c->fd_dout, ocap), "hipMalloc")) return -(int)E_DEVICE;
-    if (!c->fd_hres && hip_fail(hipHostMalloc((void**)&c->fd_hres, sizeof(dmx_result), 0), "hipHostMalloc"))
+    if (hip_fail(dmx_malloc(&c->fd_dout, ocap), "hipMalloc")) return -(int)E_DEVICE;
+    if (!c->fd_hres && hip_fail(dmx_host_malloc((void**)&c->fd_hres, sizeof(dmx_result)), "hipHostMalloc"))
         return -(int)E_MALLOC;
     c->fd_chunk = chunk;
     c->fd_ocap = ocap;
     return 0;
 }
 
+static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts, uint64_t chunk);
+
 extern "C" int dmx_encode_fd(int fd_in, int fd_out, const dmx_opts* opts, uint64_t chunk) {
+    const char* dev_s = getenv("DMX_DEVICE");
+    return encode_fd_on(dev_s ? atoi(dev_s) : 0, fd_in, fd_out, opts, chunk);
+}
+
+static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts, uint64_t chunk) {
     dmx_opts o = {0, 0, DMX_ZLIB, 0, NULL, 0};
     if (opts) o = *opts;
     if (o.sw == 0) o.sw = DMX_BLK;
@@ -3657,13 +3728,12 @@ extern "C" int dmx_encode_fd(int fd_in, int fd_out, const dmx_opts* opts, uint64
             R.size = (uint64_t)st.st_size;
         }
     }
-    const char* dev_s = getenv("DMX_DEVICE");
     pthread_mutex_lock(&g_mu);
     int err = 0;
-    dmx_ctx* c = dmx_cached_ctx(dev_s ? atoi(dev_s) : 0, chunk, &err);
+    dmx_ctx* c = dmx_cached_ctx(device, chunk, &err);
     int r = err;
     const uint64_t ocap = dmx_max_compressed(chunk, o.sw);
-    if (!r) r = ctx_reserve(c, chunk / sw);
+    if (!r) r = dmx_ctx_reserve_flags(c, chunk, (int32_t)sw, pflags);
     if (!r && hip_fail(hipSetDevice(c->device), "hipSetDevice")) r = -(int)E_DEVICE;
     if (!r) r = fd_buffers(c, chunk, ocap);
     hipStream_t s = c ? c->stream : NULL;
@@ -3732,6 +3802,196 @@ extern "C" int dmx_encode_fd(int fd_in, int fd_out, const dmx_opts* opts, uint64
     if (R.seekable) (void)lseek(fd_in, (off_t)R.off, SEEK_SET);   // consumed, as read() would leave it
     if (r && c && s) (void)hipStreamSynchronize(s);   // an error left copies in flight from the cached buffers
     pthread_mutex_unlock(&g_mu);
+    return r;
+}
+
+// --- the fd path over several GPUs (dmx_encode_fd_multi, DMX_DEVICES) ---
+// One host thread per listed device, each with its own context and pinned buffers (cached per
+// list position).  Worker w takes chunks w, w + ndev, ...: pread from the file, H2D, encode,
+// D2H, then waits for its turn and writes the chunk in file order; the Adler-32 values are
+// combined in the same order.  The framing and the parse are dmx_encode_fd's, so the stream
+// is byte-identical to it with the same chunk size.
+static dmx_ctx* g_wctx[64];
+
+struct MultiJob {
+    int fd_in, fd_out;
+    uint64_t off0, size, chunk, nchunks, sw;
+    dmx_opts o;
+    uint32_t pflags;
+    int ndev;
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    uint64_t next;   // next chunk to write
+    uint32_t adler;
+    int err;
+};
+struct MultiWorker {
+    MultiJob* J;
+    dmx_ctx* c;
+    int w;
+};
+
+static int pread_full(int fd, uint8_t* b, uint64_t len, uint64_t off) {
+    uint64_t done = 0;
+    while (done < len) {
+        const ssize_t r = pread(fd, b + done, len - done, (off_t)(off + done));
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            return -(int)E_NEXIST;
+        }
+        if (r == 0) return -(int)E_NEXIST;   // the file shrank under us
+        done += (uint64_t)r;
+    }
+    return 0;
+}
+
+static void multi_fail(MultiJob* J, int r) {
+    pthread_mutex_lock(&J->mu);
+    if (!J->err) J->err = r;
+    pthread_cond_broadcast(&J->cv);
+    pthread_mutex_unlock(&J->mu);
+}
+
+static void* multi_worker(void* a) {
+    MultiWorker* W = (MultiWorker*)a;
+    MultiJob* J = W->J;
+    dmx_ctx* c = W->c;
+    if (hip_fail(hipSetDevice(c->device), "hipSetDevice")) { multi_fail(J, -(int)E_DEVICE); return NULL; }
+    const uint64_t ocap = dmx_max_compressed(J->chunk, (int32_t)J->sw);
+    hipStream_t s = c->stream;
+    for (uint64_t i = (uint64_t)W->w; i < J->nchunks; i += (uint64_t)J->ndev) {
+        if (__atomic_load_n(&J->err, __ATOMIC_RELAXED)) break;
+        const uint64_t lo = i * J->chunk, len = (J->size - J->off0 - lo) < J->chunk ? (J->size - J->off0 - lo) : J->chunk;
+        dmx_opts oc = J->o;
+        oc.flags = J->pflags | (i == 0 ? DMX_F_HEADER : 0u) | (i + 1 == J->nchunks ? DMX_F_FINAL : 0u);
+        oc.dict = NULL;
+        oc.dict_len = 0;
+        int r = len ? pread_full(J->fd_in, c->fd_hin[0], len, J->off0 + lo) : 0;
+        if (!r && (J->pflags & DMX_F_DICT) && i > 0) {   // the previous chunk's last sw bytes
+            r = pread_full(J->fd_in, c->fd_hin[1], J->sw, J->off0 + lo - J->sw);
+            if (!r && hip_fail(hipMemcpyAsync(c->fd_din[1], c->fd_hin[1], J->sw, hipMemcpyHostToDevice, s), "H2D"))
+                r = -(int)E_DEVICE;
+            oc.dict = c->fd_din[1];
+            oc.dict_len = J->sw;
+        }
+        if (!r && len && hip_fail(hipMemcpyAsync(c->fd_din[0], c->fd_hin[0], len, hipMemcpyHostToDevice, s), "H2D"))
+            r = -(int)E_DEVICE;
+        if (!r) r = dmx_encode_async(c, c->fd_din[0], len, c->fd_dout, ocap, &oc, s);
+        if (!r) r = dmx_encode_result_async(c, c->fd_hres, s);
+        if (!r && hip_fail(hipStreamSynchronize(s), "hipStreamSynchronize")) r = -(int)E_DEVICE;
+        if (!r && c->fd_hres->status) r = c->fd_hres->status;
+        const uint64_t olen = r ? 0 : c->fd_hres->out_len;
+        const uint32_t cadl = r ? 0 : c->fd_hres->adler;
+        if (!r && hip_fail(hipMemcpy(c->fd_hout[0], c->fd_dout, olen, hipMemcpyDeviceToHost), "D2H")) r = -(int)E_DEVICE;
+        if (r) { multi_fail(J, r); break; }
+        pthread_mutex_lock(&J->mu);   // in order: chunk i after chunk i - 1
+        while (J->next != i && !J->err) pthread_cond_wait(&J->cv, &J->mu);
+        if (!J->err) {
+            if (J->fd_out >= 0) r = write_full(J->fd_out, c->fd_hout[0], olen);
+            J->adler = dmx_adler32_combine(J->adler, cadl, len);
+            if (r) J->err = r;
+            J->next = i + 1;
+        }
+        pthread_cond_broadcast(&J->cv);
+        pthread_mutex_unlock(&J->mu);
+        if (r) break;
+    }
+    return NULL;
+}
+
+// DMX_DEVICES: "0,1,2,3" (a device may repeat: one context each) or "all"; the number of
+// entries written to devs, 0 when unset or empty.
+extern "C" int dmx_devices_from_env(int* devs, int cap) {
+    const char* e = getenv("DMX_DEVICES");
+    if (!e || !*e) return 0;
+    if (!strcmp(e, "all")) {
+        int nd = 0;
+        if (hipGetDeviceCount(&nd) != hipSuccess || nd <= 0) return 0;
+        for (int k = 0; k < nd && k < cap; k++) devs[k] = k;
+        return nd < cap ? nd : cap;
+    }
+    int n = 0;
+    for (const char* p = e; *p && n < cap;) {
+        char* end = NULL;
+        const long v = strtol(p, &end, 10);
+        if (end == p) return -(int)E_INVAL;
+        devs[n++] = (int)v;
+        p = *end == ',' ? end + 1 : end;
+        if (*end && *end != ',') return -(int)E_INVAL;
+    }
+    return n;
+}
+
+extern "C" int dmx_encode_fd_multi(int fd_in, int fd_out, const dmx_opts* opts, uint64_t chunk, const int* devices,
+                                   int ndev) {
+    if (!devices || ndev < 1 || ndev > 64) return -(int)E_RANGE;
+    int nd = 0;   // every listed device must exist, whether or not the input reaches it
+    if (hipGetDeviceCount(&nd) != hipSuccess || nd <= 0) return -(int)E_NEXIST;
+    for (int w = 0; w < ndev; w++)
+        if (devices[w] < 0 || devices[w] >= nd) return -(int)E_RANGE;
+    dmx_opts o = {0, 0, DMX_ZLIB, 0, NULL, 0};
+    if (opts) o = *opts;
+    if (o.sw == 0) o.sw = DMX_BLK;
+    if (o.sw < 1 || o.sw > DMX_BLK) return -(int)E_RANGE;
+    const uint64_t sw = (uint64_t)o.sw;
+    if (chunk < sw) chunk = sw;
+    chunk -= chunk % sw;
+    struct stat st;
+    const off_t cur = lseek(fd_in, 0, SEEK_CUR);
+    if (cur < 0 || fstat(fd_in, &st) != 0 || !S_ISREG(st.st_mode) || (uint64_t)st.st_size < (uint64_t)cur)
+        return encode_fd_on(devices[0], fd_in, fd_out, opts, chunk);   // a pipe: one device, one reader
+    MultiJob J;
+    J.fd_in = fd_in;
+    J.fd_out = fd_out;
+    J.off0 = (uint64_t)cur;
+    J.size = (uint64_t)st.st_size;
+    J.chunk = chunk;
+    J.sw = sw;
+    J.nchunks = (J.size - J.off0 + chunk - 1) / chunk;
+    if (J.nchunks == 0) J.nchunks = 1;   // an empty input is one empty chunk (header, EOB block, trailer)
+    J.o = o;
+    J.pflags = o.flags & (DMX_F_LAZY | DMX_F_SPLIT | DMX_F_DICT | DMX_F_EXACT_SORT | DMX_F_STORE_CHECK);
+    J.ndev = ndev < (int)J.nchunks ? ndev : (int)J.nchunks;
+    pthread_mutex_init(&J.mu, NULL);
+    pthread_cond_init(&J.cv, NULL);
+    J.next = 0;
+    J.adler = 1;
+    J.err = 0;
+    pthread_mutex_lock(&g_mu);
+    int r = 0;
+    MultiWorker W[64];
+    const uint64_t ocap = dmx_max_compressed(chunk, o.sw);
+    for (int w = 0; w < J.ndev && !r; w++) {   // the workers' contexts (cached per list position)
+        if (g_wctx[w] && g_wctx[w]->device != devices[w]) {
+            dmx_ctx_destroy(g_wctx[w]);
+            g_wctx[w] = NULL;
+        }
+        if (!g_wctx[w]) r = dmx_ctx_create(devices[w], chunk, &g_wctx[w]);
+        if (!r) r = dmx_ctx_reserve_flags(g_wctx[w], chunk, o.sw, J.pflags);
+        if (!r && hip_fail(hipSetDevice(g_wctx[w]->device), "hipSetDevice")) r = -(int)E_DEVICE;
+        if (!r) r = fd_buffers(g_wctx[w], chunk, ocap);
+        W[w] = {&J, g_wctx[w], w};
+    }
+    pthread_t th[64];
+    bool started[64] = {false};
+    for (int w = 0; w < J.ndev && !r; w++) {
+        if (pthread_create(&th[w], NULL, multi_worker, &W[w]) == 0) started[w] = true;
+        else { multi_fail(&J, -(int)E_FORK); r = -(int)E_FORK; }
+    }
+    for (int w = 0; w < J.ndev; w++)
+        if (started[w]) pthread_join(th[w], NULL);
+    if (!r) r = J.err;
+    if (!r && fd_out >= 0) {
+        const uint32_t ad = J.adler;
+        const uint8_t tail[4] = {(uint8_t)(ad >> 24), (uint8_t)(ad >> 16), (uint8_t)(ad >> 8), (uint8_t)ad};
+        r = write_full(fd_out, tail, 4);
+    }
+    if (!r) (void)lseek(fd_in, (off_t)J.size, SEEK_SET);   // consumed, as read() would leave it
+    for (int w = 0; w < J.ndev; w++)   // an error may have left copies in flight from the cached buffers
+        if (r && g_wctx[w]) { (void)hipSetDevice(g_wctx[w]->device); (void)hipStreamSynchronize(g_wctx[w]->stream); }
+    pthread_mutex_unlock(&g_mu);
+    pthread_mutex_destroy(&J.mu);
+    pthread_cond_destroy(&J.cv);
     return r;
 }
 

@@ -74,7 +74,7 @@ struct compress_stats {
     int d;
 };
 
-/* Error codes: global_errors.h:64-75 and deflate_errors.h:132-147 (returned negated). */
+/* Error codes: src/include/global_errors.h:24-35 and src/include/deflate_errors.h:9-22 (returned negated). */
 #define E_LEN 1
 #define E_MALLOC 2
 #define E_FORK 3
@@ -168,12 +168,19 @@ int dmx_ctx_create(int device, uint64_t max_input, dmx_ctx** out);
 void dmx_ctx_destroy(dmx_ctx* ctx);
 /* Grow the workspace (synchronising) so that n bytes with block size sw fit. */
 int dmx_ctx_reserve(dmx_ctx* ctx, uint64_t n, int32_t sw);
+/* The same, plus the scratch the block options need from then on: DMX_F_SPLIT (split plans)
+ * and DMX_F_DICT (every block's exported chains).  dmx_encode_async never allocates: with
+ * those flags on a context not reserved for them it returns -E_SZ.  Synchronises only when
+ * it allocates. */
+int dmx_ctx_reserve_flags(dmx_ctx* ctx, uint64_t n, int32_t sw, uint32_t flags);
 /* Worst-case output bytes for n input bytes with block size sw. */
 uint64_t dmx_max_compressed(uint64_t n, int32_t sw);
 
 /* Enqueue the whole encode of device buffer d_in[0..n) into d_out (capacity
  * out_cap) on `stream` (hipStream_t; NULL = the context's stream).  No host
- * synchronisation, no allocation.  Returns 0 or -E_* for argument errors. */
+ * synchronisation, no allocation (graph-capturable).  Returns 0 or -E_* for argument
+ * errors: -E_SZ when n needs more blocks than the context holds, or DMX_F_SPLIT /
+ * DMX_F_DICT on a context not reserved for them (dmx_ctx_reserve_flags). */
 int dmx_encode_async(dmx_ctx* ctx, const void* d_in, uint64_t n, void* d_out, uint64_t out_cap,
                      const dmx_opts* opts, void* stream);
 /* Wait for the last encode on `stream` and copy its dmx_result to the host. */
@@ -196,6 +203,21 @@ int dmx_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t out_ca
  * history across chunks).  opts->flags: the parse/block options (DMX_F_LAZY, _SPLIT, _DICT);
  * the framing is its own.  Returns 0 or -E_*. */
 int dmx_encode_fd(int fd_in, int fd_out, const dmx_opts* opts, uint64_t chunk);
+
+/* The same stream as dmx_encode_fd with the chunks spread over several GPUs: chunk i is
+ * read (pread), encoded and copied back by the host thread of devices[i % ndev], and the
+ * chunks are written to fd_out in order (one host thread per GPU).  Needs a
+ * regular file as fd_in (a pipe falls back to dmx_encode_fd on devices[0]).  A device may
+ * be listed more than once (one context per entry).  deflate_compress uses it when
+ * DMX_DEVICES lists more than one device ("0,1,2,3" or "all").  Returns 0 or -E_*. */
+int dmx_encode_fd_multi(int fd_in, int fd_out, const dmx_opts* opts, uint64_t chunk, const int* devices, int ndev);
+
+/* Test hook (fault injection): "malloc:N" makes the N-th device or pinned
+ * allocation of the library from now fail, "launch:N" the N-th encode's launch check;
+ * NULL or "" turns it off.  Also read from DMX_FAULT when the library loads.  The failing
+ * call returns -E_DEVICE (or -E_MALLOC for pinned memory) and leaves no allocation behind
+ * that its context does not own.  Returns 0, or -E_INVAL / -E_RANGE for a bad spec. */
+int dmx_fault_set(const char* spec);
 
 /* ---- GPU inflate, csrc/dmx_inflate_dev.hip ---- */
 /* One entry per independently decodable DEFLATE block: start bit in the stream, output

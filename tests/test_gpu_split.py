@@ -121,7 +121,8 @@ def test_split_gpu_inflate(enc, golden_cases):
 
 def test_split_stats(tmp_path, enc, monkeypatch):
     """fd API with DMX_SPLIT=1: the stream equals the oracle's split stream and the
-    compress_stats records follow each DEFLATE block's own codes and header."""
+    compress_stats records follow each DEFLATE block's own codes and header, in running sums
+    over the whole stream (dmx_host.c write_stats)."""
     data = _het(10, 7)
     fi, fo, fs = tmp_path / "in", tmp_path / "out", tmp_path / "st"
     fi.write_bytes(data)
@@ -135,10 +136,11 @@ def test_split_stats(tmp_path, enc, monkeypatch):
     enc.compress_bytes(data, max_chain=8, flags=D.DMX_ZLIB | D.DMX_F_SPLIT)
     nblk = (len(data) + 32767) // 32768
     row = 0
+    tree = ll = dd = 0
     for b in range(nblk):
         toks = enc.tokens(b)
         for (t0, t1, bt, hb, ln) in enc.subblocks(b):
-            ll = dd = 0
+            tree += hb if bt == 2 else 3
             for k in range(t0, t1):
                 t = int(toks[k])
                 if t >> 9 == 0:
@@ -152,7 +154,7 @@ def test_split_stats(tmp_path, enc, monkeypatch):
                         ll += int(ln[s]) + eb
                         s, eb = _dist_sym(dist)
                         dd += int(ln[286 + s]) + eb
-                assert st[row, 1] == (hb if bt == 2 else 3)
+                assert st[row, 1] == tree
                 assert st[row, 2] == ll and st[row, 3] == dd, (b, k)
                 row += 1
     assert row == st.shape[0]
