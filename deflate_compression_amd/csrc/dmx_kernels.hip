@@ -473,35 +473,37 @@ __device__ __forceinline__ void store_result(MatchLDS& L, uint16_t* __restrict__
 
 // Candidate steps with the halo embedded in the chunk (K <= KE): lanes 0..K-1 hold the K
 // entries before the chunk's owned entries, so a plain wave_shr feeds every owned lane.
+// The short-chain search compares CBS = 8 bytes in registers (two streams, 13 VALU per
+// step): only 8 % of text entries have a candidate equal in all 8 (4.6 % in 12), and those
+// go to the extension queue, which extends 64 of them at a time.
+#define CBS 8
 template <bool GUARD, bool CLAMP>
-__device__ __forceinline__ void cand_step_emb(uint32_t j, uint32_t sj, uint32_t& x0, uint32_t& x1, uint32_t& x2,
-                                              uint32_t i0, uint32_t i1, uint32_t i2, uint32_t nc, uint32_t lim_eff,
-                                              uint32_t& jkey, uint32_t& full) {
+__device__ __forceinline__ void cand_step_emb(uint32_t j, uint32_t sj, uint32_t& x0, uint32_t& x1, uint32_t i0,
+                                              uint32_t i1, uint32_t nc, uint32_t lim_eff, uint32_t& jkey,
+                                              uint32_t& full) {
     x0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x0, 0x138, 0xF, 0xF, true);
     x1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x1, 0x138, 0xF, 0xF, true);
-    x2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x2, 0x138, 0xF, 0xF, true);
-    // equal leading bits, 96 = all CB bytes: ffbl(0) = ~0 and the saturating adds keep it
-    // there, so one min3 picks the first differing word (v_add_u32 clamp + v_min3_u32)
-    const uint32_t mb = min(min(ffbl_hw(i0 ^ x0), __builtin_elementwise_add_sat(ffbl_hw(i1 ^ x1), 32u)),
-                            min(ffbl_hw(i2 ^ x2), 32u) + 64u);
-    uint32_t m;   // bytes (mb <= 96); opaque, else it is folded into a 3-op shift/mask/or
+    // equal leading bits, 64 = all CBS bytes: ffbl(0) = ~0 and the saturating add keeps it
+    // there; one min3 caps at 64 (v_add_u32 clamp + v_min3_u32)
+    const uint32_t mb = min(min(ffbl_hw(i0 ^ x0), __builtin_elementwise_add_sat(ffbl_hw(i1 ^ x1), 32u)), 64u);
+    uint32_t m;   // bytes (mb <= 64); opaque, else it is folded into a 3-op shift/mask/or
     asm("v_bfe_u32 %0, %1, 3, 4" : "=v"(m) : "v"(mb));
-    if (CLAMP) m = min(m, lim_eff);   // only chunks holding one of the last CB-1 positions
+    if (CLAMP) m = min(m, lim_eff);   // only chunks holding one of the last CBS-1 positions
     if (GUARD) {
         m = j <= nc ? m : 0u;
-        full |= (mb == 96u && j <= nc) ? (1u << (j - 1)) : 0u;
+        full |= (mb == 64u && j <= nc) ? (1u << (j - 1)) : 0u;
     } else {
-        full |= ((mb + 32u) >> 7) << (j - 1);   // 1 iff mb == 96
+        full |= (mb >> 6) << (j - 1);   // 1 iff mb == 64
     }
     jkey = max(jkey, (m << 8) | sj);
 }
 template <bool GUARD, bool CLAMP>
-__device__ __forceinline__ void cand_steps_emb(uint32_t K, uint32_t i0, uint32_t i1, uint32_t i2, uint32_t nc,
-                                               uint32_t lim_eff, uint32_t& jkey, uint32_t& full) {
-    uint32_t x0 = i0, x1 = i1, x2 = i2;
+__device__ __forceinline__ void cand_steps_emb(uint32_t K, uint32_t i0, uint32_t i1, uint32_t nc, uint32_t lim_eff,
+                                               uint32_t& jkey, uint32_t& full) {
+    uint32_t x0 = i0, x1 = i1;
     uint32_t sj = 254u;   // 255 - j, kept as its own uniform counter
     for (uint32_t j = 1; j <= K; j++, sj--)
-        cand_step_emb<GUARD, CLAMP>(j, sj, x0, x1, x2, i0, i1, i2, nc, lim_eff, jkey, full);
+        cand_step_emb<GUARD, CLAMP>(j, sj, x0, x1, i0, i1, nc, lim_eff, jkey, full);
 }
 
 // Result of entry k (position i) in the short-chain mode: length (0 = none) and winner j
@@ -544,13 +546,13 @@ __device__ __forceinline__ void ext_queue(MatchLDS& L, uint32_t bn, uint32_t* Qw
         full &= full - 1u;
         uint32_t q = L.sorted[k - bj];
         // distance 1 (runs): the length is where the run ends, from the change bitmap
-        uint32_t bl = min(q + 1u == i && RUNS ? run_len(L, i, lim) : ext_len(L, i, q, CB, lim), lim);
+        uint32_t bl = min(q + 1u == i && RUNS ? run_len(L, i, lim) : ext_len(L, i, q, CBS, lim), lim);
         while (full && bl < lim) {
             const uint32_t j = (uint32_t)__builtin_ctz(full) + 1u;
             full &= full - 1u;
             q = L.sorted[k - j];
             if (D8[q + bl] != D8[i + bl]) continue;
-            const uint32_t len = min(ext_len(L, i, q, CB, lim), lim);
+            const uint32_t len = min(ext_len(L, i, q, CBS, lim), lim);
             if (len > bl) { bl = len; bj = j; }
         }
         store_short<DICT>(L, k, i, bl, bj, hbk);
@@ -568,7 +570,7 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
     if (RUNS) build_chg(L, bn, tid);
     if (K <= KE) {
         // bounded mode with a short chain: chunks of 64-K owned entries, halo embedded.
-        // Entries with a candidate equal in all CB register bytes need the LDS extension; they
+        // Entries with a candidate equal in all CBS register bytes need the LDS extension; they
         // go to a per-wave queue (up to 64, in tsm) that is extended with all 64 lanes at once
         // when the next chunk would overflow it, instead of a few lanes of every chunk.
         uint32_t* Qw = L.tsm + (wave << 6);
@@ -588,11 +590,9 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
                 const bool load = ei >= 0 && k < nvalid;
                 uint32_t nc = 0;
                 uint64_t iv0 = 0;
-                uint32_t i2 = 0;
                 if (load) {
                     i = L.sorted[k];
                     iv0 = ld8(L.data, i);
-                    i2 = ld4(L.data, i + 8);
                 }
                 if (act) {
                     nc = min(k, K);
@@ -620,13 +620,13 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
                     }
                 }
                 if (!skip) {
-                    if (base == 0) cand_steps_emb<true, true>(K, i0, i1, i2, nc, lim_eff, jkey, full);
-                    else if (__ballot(act && lim_eff < CB)) cand_steps_emb<false, true>(K, i0, i1, i2, nc, lim_eff, jkey, full);
-                    else cand_steps_emb<false, false>(K, i0, i1, i2, nc, lim_eff, jkey, full);
-                    if (lim_eff <= CB) full = 0;
+                    if (base == 0) cand_steps_emb<true, true>(K, i0, i1, nc, lim_eff, jkey, full);
+                    else if (__ballot(act && lim_eff < CBS)) cand_steps_emb<false, true>(K, i0, i1, nc, lim_eff, jkey, full);
+                    else cand_steps_emb<false, false>(K, i0, i1, nc, lim_eff, jkey, full);
+                    if (lim_eff <= CBS) full = 0;
                 }
             }
-            // a full candidate is the register best (CB bytes, the nearest such): the queue
+            // a full candidate is the register best (CBS bytes, the nearest such): the queue
             // item is the entry and its full mask
             const bool push = act && !done && full != 0;
             const uint64_t pm = __ballot(push);
