@@ -41,6 +41,12 @@
 // ------------------------------------------------------------------------------------
 
 __device__ __forceinline__ uint32_t dmx_hash(uint32_t tri) { return (tri * 0x9E3779B1u) >> DMX_HASH_SHIFT; }
+// The order of the bucket-sorted array S: (bucket of the trigram in the low 3 bytes of w,
+// position p < 32768) as one integer, so that adjacent entries are checked with one compare.
+// Wave index as a scalar (wave-uniform: the SGPR keeps wave-derived LDS offsets out of
+// the vector registers of the match kernel, which otherwise spills them).
+__device__ __forceinline__ uint32_t wave_of(uint32_t tid) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6)); }
+__device__ __forceinline__ uint32_t sort_key(uint32_t w, uint32_t p) { return (dmx_hash(w & 0xFFFFFFu) << 15) | p; }
 
 // RFC 1951 §3.2.5 length -> symbol 257..285, extra-bit count, extra value
 __device__ __forceinline__ void len_sym(uint32_t len, uint32_t& sym, uint32_t& eb, uint32_t& ev) {
@@ -473,37 +479,63 @@ __device__ __forceinline__ void store_result(MatchLDS& L, uint16_t* __restrict__
 
 // Candidate steps with the halo embedded in the chunk (K <= KE): lanes 0..K-1 hold the K
 // entries before the chunk's owned entries, so a plain wave_shr feeds every owned lane.
-// The short-chain search compares CBS = 8 bytes in registers (two streams, 13 VALU per
+// The short-chain search compares CBS = 8 bytes in registers (two streams, 10 VALU per
 // step): only 8 % of text entries have a candidate equal in all 8 (4.6 % in 12), and those
 // go to the extension queue, which extends 64 of them at a time.
+// Key = (equal bits rounded down to bytes) | (8 - j): one v_and_or, 8 * bytes in the high
+// part, then the nearest (smallest j) -- K <= 8, so 8 - j fits the 3 low bits.  A key >= 64
+// means some candidate equals all CBS bytes; the queue finds which ones from LDS.
 #define CBS 8
 template <bool GUARD, bool CLAMP>
-__device__ __forceinline__ void cand_step_emb(uint32_t j, uint32_t sj, uint32_t& x0, uint32_t& x1, uint32_t i0,
-                                              uint32_t i1, uint32_t nc, uint32_t lim_eff, uint32_t& jkey,
-                                              uint32_t& full) {
+__device__ __forceinline__ void cand_step_emb(uint32_t j, uint32_t& x0, uint32_t& x1, uint32_t i0, uint32_t i1,
+                                              uint32_t nc, uint32_t lim_eff, uint32_t& jkey) {
     x0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x0, 0x138, 0xF, 0xF, true);
     x1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x1, 0x138, 0xF, 0xF, true);
     // equal leading bits, 64 = all CBS bytes: ffbl(0) = ~0 and the saturating add keeps it
     // there; one min3 caps at 64 (v_add_u32 clamp + v_min3_u32)
     const uint32_t mb = min(min(ffbl_hw(i0 ^ x0), __builtin_elementwise_add_sat(ffbl_hw(i1 ^ x1), 32u)), 64u);
-    uint32_t m;   // bytes (mb <= 64); opaque, else it is folded into a 3-op shift/mask/or
-    asm("v_bfe_u32 %0, %1, 3, 4" : "=v"(m) : "v"(mb));
-    if (CLAMP) m = min(m, lim_eff);   // only chunks holding one of the last CBS-1 positions
-    if (GUARD) {
-        m = j <= nc ? m : 0u;
-        full |= (mb == 64u && j <= nc) ? (1u << (j - 1)) : 0u;
-    } else {
-        full |= (mb >> 6) << (j - 1);   // 1 iff mb == 64
-    }
-    jkey = max(jkey, (m << 8) | sj);
+    uint32_t key;
+    if (CLAMP) key = (min(mb >> 3, lim_eff) << 3) | (8u - j);   // only chunks holding one of the last CBS-1 positions
+    else key = (mb & ~7u) | (8u - j);
+    if (GUARD) key = j <= nc ? key : 0u;
+    jkey = max(jkey, key);
 }
 template <bool GUARD, bool CLAMP>
 __device__ __forceinline__ void cand_steps_emb(uint32_t K, uint32_t i0, uint32_t i1, uint32_t nc, uint32_t lim_eff,
-                                               uint32_t& jkey, uint32_t& full) {
+                                               uint32_t& jkey) {
     uint32_t x0 = i0, x1 = i1;
-    uint32_t sj = 254u;   // 255 - j, kept as its own uniform counter
-    for (uint32_t j = 1; j <= K; j++, sj--)
-        cand_step_emb<GUARD, CLAMP>(j, sj, x0, x1, i0, i1, nc, lim_eff, jkey, full);
+    for (uint32_t j = 1; j <= K; j++) cand_step_emb<GUARD, CLAMP>(j, x0, x1, i0, i1, nc, lim_eff, jkey);
+}
+// The common chunk (no guard, no clamp) with K known at compile time: fully unrolled, so the
+// step's 8 - j is an inline constant and the key is one v_and_or_b32 (the compiler would
+// narrow the -8 mask to a non-inline 0x78 and split it); keys of two steps fold into one
+// v_max3.  10 VALU per step, no loop SALU.
+template <int SJ>
+__device__ __forceinline__ uint32_t step_key_c(uint32_t i0, uint32_t i1, uint32_t& x0, uint32_t& x1) {
+    x0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x0, 0x138, 0xF, 0xF, true);
+    x1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x1, 0x138, 0xF, 0xF, true);
+    const uint32_t mb = min(min(ffbl_hw(i0 ^ x0), __builtin_elementwise_add_sat(ffbl_hw(i1 ^ x1), 32u)), 64u);
+    uint32_t key;
+    asm("v_and_or_b32 %0, %1, -8, %2" : "=v"(key) : "v"(mb), "n"(SJ));
+    return key;
+}
+template <int J, int KK>
+__device__ __forceinline__ void steps_from(uint32_t i0, uint32_t i1, uint32_t& x0, uint32_t& x1, uint32_t& jkey) {
+    if constexpr (J <= KK) {
+        const uint32_t ka = step_key_c<8 - J>(i0, i1, x0, x1);
+        if constexpr (J + 1 <= KK) {
+            const uint32_t kb = step_key_c<7 - J>(i0, i1, x0, x1);
+            jkey = max(jkey, max(ka, kb));
+        } else {
+            jkey = max(jkey, ka);
+        }
+        steps_from<J + 2, KK>(i0, i1, x0, x1, jkey);
+    }
+}
+template <int KK>
+__device__ __forceinline__ void cand_steps_fixed(uint32_t i0, uint32_t i1, uint32_t& jkey) {
+    uint32_t x0 = i0, x1 = i1;
+    steps_from<1, KK>(i0, i1, x0, x1, jkey);
 }
 
 // Result of entry k (position i) in the short-chain mode: length (0 = none) and winner j
@@ -527,33 +559,43 @@ __device__ __forceinline__ void store_short(MatchLDS& L, uint32_t k, uint32_t i,
     }
 }
 
-// The queued entries of one wave (qn <= 64, items k | full << 15): lane l takes item l and
-// extends its full candidates from LDS, nearest first (a farther one must be strictly
-// longer, so it is extended only if it also matches the byte at the best length), then
-// stores the entry's result.
+// The queued entries of one wave (qn <= 64, items k | jw << 15: entry k, whose nearest
+// candidate equal in all CBS register bytes is chain candidate jw): lane l takes item l and
+// extends jw from LDS.  A farther candidate must be strictly longer, so it must equal the
+// CBS bytes and the byte at the best length: that byte is tested first (one read), the
+// CBS bytes only for the rare survivors.  Then the entry's result is stored.
 template <bool DICT, bool RUNS>
-__device__ __forceinline__ void ext_queue(MatchLDS& L, uint32_t bn, uint32_t* Qw, uint32_t qn, uint32_t lane,
-                                       const uint32_t* __restrict__ hbk) {
+__device__ __forceinline__ void ext_queue(MatchLDS& L, uint32_t bn, uint32_t K, uint32_t* Qw, uint32_t qn,
+                                          uint32_t lane, const uint32_t* __restrict__ hbk) {
     __builtin_amdgcn_wave_barrier();
     if (lane < qn) {
         const uint32_t it = lds_ld(&Qw[lane]);
-        const uint32_t k = it & 0x7FFFu;
-        uint32_t full = it >> 15;
+        const uint32_t k = it & 0x7FFFu, nc = min(k, K);
+        uint32_t bj = it >> 15;
         const uint32_t i = L.sorted[k];
         const uint32_t lim = min(bn - i, (uint32_t)MAXLEN);
         const uint8_t* D8 = reinterpret_cast<const uint8_t*>(L.data);
-        uint32_t bj = (uint32_t)__builtin_ctz(full) + 1u;
-        full &= full - 1u;
-        uint32_t q = L.sorted[k - bj];
+        const uint32_t q = L.sorted[k - bj];
         // distance 1 (runs): the length is where the run ends, from the change bitmap
         uint32_t bl = min(q + 1u == i && RUNS ? run_len(L, i, lim) : ext_len(L, i, q, CBS, lim), lim);
-        while (full && bl < lim) {
-            const uint32_t j = (uint32_t)__builtin_ctz(full) + 1u;
-            full &= full - 1u;
-            q = L.sorted[k - j];
-            if (D8[q + bl] != D8[i + bl]) continue;
-            const uint32_t len = min(ext_len(L, i, q, CBS, lim), lim);
-            if (len > bl) { bl = len; bj = j; }
+        if (bl < lim) {
+            // the byte test of every farther candidate at once (independent LDS reads)
+            const uint32_t ib = D8[i + bl], j0 = bj + 1u;
+            uint32_t surv = 0;
+#pragma unroll
+            for (uint32_t t = 0; t < KE - 1; t++) {
+                const uint32_t j = j0 + t;
+                const uint32_t qj = L.sorted[k - min(j, nc)];
+                surv |= (j <= nc && D8[qj + bl] == ib) ? 1u << t : 0u;
+            }
+            while (surv && bl < lim) {   // rare: test the CBS bytes, then extend
+                const uint32_t j = j0 + (uint32_t)__builtin_ctz(surv);
+                surv &= surv - 1u;
+                const uint32_t qj = L.sorted[k - j];
+                if (D8[qj + bl] != D8[i + bl] || ld8(L.data, qj) != ld8(L.data, i)) continue;
+                const uint32_t len = min(ext_len(L, i, qj, CBS, lim), lim);
+                if (len > bl) { bl = len; bj = j; }
+            }
         }
         store_short<DICT>(L, k, i, bl, bj, hbk);
     }
@@ -563,7 +605,7 @@ __device__ __forceinline__ void ext_queue(MatchLDS& L, uint32_t bn, uint32_t* Qw
 template <bool DICT, bool RUNS>
 __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint16_t* __restrict__ pg,
                                      uint32_t tid, bool stamp, uint64_t& tdef, const uint32_t* __restrict__ hbk) {
-    const uint32_t lane = tid & 63, wave = tid >> 6;
+    const uint32_t lane = tid & 63, wave = wave_of(tid);
     const uint32_t K = max_chain > 0 ? (uint32_t)max_chain : 0xFFFFFFFFu;
     const uint32_t nvalid = bn > 2 ? bn - 2 : 0;   // positions with a full trigram = entries of S
     uint32_t iters = 0;
@@ -584,7 +626,7 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
             const int ei = (int)(base + lane) - (int)K;   // entry of this lane
             const uint32_t k = (uint32_t)ei;
             const bool act = more && lane >= K && k < nvalid;
-            uint32_t i = 0, lim_eff = 0, jkey = 0, full = 0;
+            uint32_t i = 0, lim_eff = 0, jkey = 0;
             bool done = false;   // result already stored (runs)
             if (more) {
                 const bool load = ei >= 0 && k < nvalid;
@@ -600,11 +642,10 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
                 }
                 iters += K;
                 const uint32_t i0 = (uint32_t)iv0, i1 = (uint32_t)(iv0 >> 32);
-                {   // sort check: the predecessor entry (lane - 1) must be earlier if same bucket
-                    const uint32_t pn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)i, 0x138, 0xF, 0xF, true);
-                    const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)i0, 0x138, 0xF, 0xF, true);
-                    const bool bad = act && ei >= 1 && pn > i && dmx_hash(dn & 0xFFFFFFu) == dmx_hash(i0 & 0xFFFFFFu);
-                    if (__ballot(bad)) L.sortbad = 1;
+                {   // sort check: the predecessor entry (lane - 1) has a smaller (bucket, position)
+                    const uint32_t sk = sort_key(i0, i);
+                    const uint32_t pk = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sk, 0x138, 0xF, 0xF, true);
+                    if (__ballot(act && ei >= 1 && pk > sk)) L.sortbad = 1;
                 }
                 bool skip = false;
                 if (RUNS) {
@@ -620,29 +661,31 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
                     }
                 }
                 if (!skip) {
-                    if (base == 0) cand_steps_emb<true, true>(K, i0, i1, nc, lim_eff, jkey, full);
-                    else if (__ballot(act && lim_eff < CBS)) cand_steps_emb<false, true>(K, i0, i1, nc, lim_eff, jkey, full);
-                    else cand_steps_emb<false, false>(K, i0, i1, nc, lim_eff, jkey, full);
-                    if (lim_eff <= CBS) full = 0;
+                    if (base == 0) cand_steps_emb<true, true>(K, i0, i1, nc, lim_eff, jkey);
+                    else if (__ballot(act && lim_eff < CBS)) cand_steps_emb<false, true>(K, i0, i1, nc, lim_eff, jkey);
+                    else if (K == 6) cand_steps_fixed<6>(i0, i1, jkey);
+                    else if (K == 8) cand_steps_fixed<8>(i0, i1, jkey);
+                    else if (K == 4) cand_steps_fixed<4>(i0, i1, jkey);
+                    else cand_steps_emb<false, false>(K, i0, i1, nc, lim_eff, jkey);
                 }
             }
-            // a full candidate is the register best (CBS bytes, the nearest such): the queue
-            // item is the entry and its full mask
-            const bool push = act && !done && full != 0;
+            // a candidate equal in all CBS bytes (key >= 64) is the register best: the entry
+            // is queued for the LDS extension (unless the block end caps it there)
+            const bool push = act && !done && jkey >= (CBS << 3) && lim_eff > CBS;
             const uint64_t pm = __ballot(push);
             const uint32_t np = (uint32_t)__popcll(pm);
             if (qn + np > 64 || (!more && qn)) {
                 const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
-                ext_queue<DICT, RUNS>(L, bn, Qw, qn, lane, hbk);
+                ext_queue<DICT, RUNS>(L, bn, K, Qw, qn, lane, hbk);
                 if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
                 qn = 0;
             }
             if (!more) break;
-            if (push) lds_st(&Qw[qn + (uint32_t)__popcll(pm & lt)], k | (full << 15));
+            if (push) lds_st(&Qw[qn + (uint32_t)__popcll(pm & lt)], k | ((8u - (jkey & 7u)) << 15));
             qn += np;
             if (act && !push && !done) {
-                const uint32_t m = jkey >> 8;
-                store_short<DICT>(L, k, i, m >= 3 ? m : 0u, m >= 3 ? 255u - (jkey & 255u) : 0u, hbk);
+                const uint32_t m = jkey >> 3;
+                store_short<DICT>(L, k, i, m >= 3 ? m : 0u, m >= 3 ? 8u - (jkey & 7u) : 0u, hbk);
             }
         }
     } else
@@ -673,11 +716,10 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
         }
         const uint32_t i0 = (uint32_t)iv0, i1 = (uint32_t)(iv0 >> 32);
         const uint32_t h0 = (uint32_t)hv0, h1 = (uint32_t)(hv0 >> 32);
-        {   // sort check: the predecessor entry (lane - 1, lane 0: halo 0) earlier if same bucket
-            const uint32_t pn = wshr(i, __builtin_amdgcn_readlane(hq, 0));
-            const uint32_t dn = wshr(i0, __builtin_amdgcn_readlane(h0, 0));
-            const bool bad = act && k >= 1 && pn > i && dmx_hash(dn & 0xFFFFFFu) == dmx_hash(i0 & 0xFFFFFFu);
-            if (__ballot(bad)) L.sortbad = 1;
+        {   // sort check: the predecessor entry (lane - 1, lane 0: halo 0) has a smaller (bucket, position)
+            const uint32_t sk = sort_key(i0, i);
+            const uint32_t pk = wshr(sk, __builtin_amdgcn_readlane(sort_key(h0, hq), 0));
+            if (__ballot(act && k >= 1 && pk > sk)) L.sortbad = 1;
         }
         // wave-uniform bound: the largest chain length of the chunk, capped at KD
         uint32_t jmax = act ? min(nc, (uint32_t)KD) : 0;
@@ -848,7 +890,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(MatchLDS& L, uint32_t v, uin
 template <bool EXACT, bool RUNCHK = true>
 __device__ __forceinline__ void sort_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint32_t tid, bool stamp,
                                                uint64_t* tp0) {
-    const uint32_t lane = tid & 63, wave = tid >> 6;
+    const uint32_t lane = tid & 63, wave = wave_of(tid);
     const uint32_t nvalid = bn > 2 ? bn - 2 : 0;   // positions with a full trigram
     const bool need_starts = max_chain <= 0 || max_chain > KD;
     uint32_t* C = L.tsm;                                   // 16 x 128 pass-1 counters (tsm + exitp)
@@ -1056,7 +1098,8 @@ __global__ __launch_bounds__(MT) void dmx_chain_kernel(const uint8_t* __restrict
         else sort_positions<true>(L, len, 1, tid, false, tp0);
         for (uint32_t k = tid; k < DMX_NBUCKET; k += MT) L.bstart[k] = 0;
         __syncthreads();
-        bool bad = false;   // the lane-ordered atomic ranks are verified here, as in the search
+        bool bad = false;   // the lane-ordered atomic ranks are verified here, as in the search:
+                            // every adjacent pair ascends by (bucket, position), so S is sorted
         for (uint32_t k = tid; k < nv; k += MT) {
             const uint32_t q = L.sorted[k];
             const uint32_t h = dmx_hash(ld4(L.data, q) & 0xFFFFFFu);
@@ -1064,7 +1107,7 @@ __global__ __launch_bounds__(MT) void dmx_chain_kernel(const uint8_t* __restrict
                 const uint32_t q1 = L.sorted[k + 1];
                 const uint32_t h1 = dmx_hash(ld4(L.data, q1) & 0xFFFFFFu);
                 if (h1 != h) L.bstart[h] = (uint16_t)(k + 1);
-                else if (q1 < q) bad = true;
+                if (((h1 << 15) | q1) < ((h << 15) | q)) bad = true;
             } else {
                 L.bstart[h] = (uint16_t)(k + 1);
             }
@@ -1470,7 +1513,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
                                                        dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg) {
     __shared__ MatchLDS L;
     __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def, tp0[3], st_rounds;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = wave_of(tid);
     const uint32_t b = blockIdx.x;
     if ((mflags & 4u) && info[b].prestored) return;   // stored by the noise check (K0)
     const uint64_t off = (uint64_t)b * sw;
