@@ -148,9 +148,11 @@ __device__ __forceinline__ uint64_t fsh64(uint64_t lo, uint64_t hi, uint32_t sh)
     return sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
 }
 __device__ __forceinline__ uint64_t ld8(const uint32_t* W, uint32_t p) {   // bytes p..p+7
-    const uint64_t* Q = reinterpret_cast<const uint64_t*>(W);
-    const uint32_t a = p >> 3;
-    return fsh64(Q[a], Q[a + 1], (p & 7) << 3);
+    // three aligned dwords + two v_alignbyte (ds_read2_b32 + ds_read_b32: 6 LDS cycles and 2
+    // VALU; two 8-byte words + 64-bit shifts took ds_read2_b64, 8 cycles, and 6 VALU)
+    const uint32_t a = p >> 2, sh = p & 3;
+    const uint32_t w0 = W[a], w1 = W[a + 1], w2 = W[a + 2];
+    return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
 }
 __device__ __forceinline__ uint32_t ld4(const uint32_t* W, uint32_t p) {   // bytes p..p+3
     return __builtin_amdgcn_alignbyte(W[(p >> 2) + 1], W[p >> 2], p & 3);
@@ -1678,9 +1680,12 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
 
     // ---- P2: greedy path ----
     {   // W1: speculative walk of every 32-position segment from its start
-        const uint32_t lo = tid << 5;
+        const uint32_t lo = tid << 5, lw = L.lit[tid];   // the segment's literal bits: one read
         uint32_t m = 0, p = lo;
-        while (p < lo + 32 && p < bn) { m |= 1u << (p - lo); p += adv_of(L, p); }
+        while (p < lo + 32 && p < bn) {
+            m |= 1u << (p - lo);
+            p += ((lw >> (p - lo)) & 1u) ? 1u : (uint32_t)L.len8[p] + 3u;
+        }
         L.tsm[tid] = m;
         L.exitp[tid] = p;
     }
