@@ -201,12 +201,13 @@ __device__ __forceinline__ uint32_t wshr(uint32_t v, uint32_t lane0) {   // lane
 // (most extensions end there), then 32 per round trip.
 // Each side is read as 9 aligned words and realigned with v_alignbyte (one VALU per 4
 // bytes); the first differing word comes from a mask of non-zero xors.
-__device__ __forceinline__ uint32_t ext_len(const MatchLDS& L, uint32_t i, uint32_t q, uint32_t kk, uint32_t lim) {
+__device__ __forceinline__ uint32_t ext_len2(const uint32_t* A, uint32_t i, const uint32_t* B, uint32_t q, uint32_t kk,
+                                             uint32_t lim) {
     {   // first round: 16 bytes (5 aligned words per side) -- most extensions end there
         const uint32_t a = (i + kk) >> 2, sa = (i + kk) & 3, c = (q + kk) >> 2, sc = (q + kk) & 3;
         uint32_t wa[5], wc[5];
 #pragma unroll
-        for (int t = 0; t < 5; t++) { wa[t] = L.data[a + t]; wc[t] = L.data[c + t]; }
+        for (int t = 0; t < 5; t++) { wa[t] = A[a + t]; wc[t] = B[c + t]; }
         uint32_t x[4], nz = 0;
 #pragma unroll
         for (int t = 0; t < 4; t++) {
@@ -227,7 +228,7 @@ __device__ __forceinline__ uint32_t ext_len(const MatchLDS& L, uint32_t i, uint3
         const uint32_t a = (i + kk) >> 2, sa = (i + kk) & 3, c = (q + kk) >> 2, sc = (q + kk) & 3;
         uint32_t wa[9], wc[9];
 #pragma unroll
-        for (int t = 0; t < 9; t++) { wa[t] = L.data[a + t]; wc[t] = L.data[c + t]; }
+        for (int t = 0; t < 9; t++) { wa[t] = A[a + t]; wc[t] = B[c + t]; }
         uint32_t x[8], nz = 0;
 #pragma unroll
         for (int t = 0; t < 8; t++) {
@@ -244,6 +245,10 @@ __device__ __forceinline__ uint32_t ext_len(const MatchLDS& L, uint32_t i, uint3
         kk += 32;
         if (kk >= lim) return kk;
     }
+}
+// (both sides in the block)
+__device__ __forceinline__ uint32_t ext_len(const MatchLDS& L, uint32_t i, uint32_t q, uint32_t kk, uint32_t lim) {
+    return ext_len2(L.data, i, L.data, q, kk, lim);
 }
 // Change bitmap (bounded mode with a short chain, K <= KE: the walk's exit array is free
 // during the search): bit p = data[p] != data[p+1] (set for p >= bn - 1).  Built at the
@@ -1122,16 +1127,104 @@ __global__ __launch_bounds__(MT) void dmx_chain_kernel(const uint8_t* __restrict
         reinterpret_cast<uint4*>(E)[k] = reinterpret_cast<const uint4*>(L.bstart)[k];
 }
 
-// 66 KB: two workgroups per CU; the chains (S, bucket ends) are read through the caches
+// 146 KB, one workgroup per CU: the history, the block and the history's chains (S and the
+// bucket ends) all in LDS, so the candidate loop has no global-memory latency (with S and
+// the bucket ends read through the caches, two 66 KB workgroups per CU spent ~340 K cycles
+// per block waiting on three dependent L2 reads per entry)
 struct __attribute__((aligned(16))) HistLDS {
     uint32_t data[DATA_WORDS];        // the history, then the block's first bytes (sources crossing over)
     uint32_t cur[DMX_BLK / 4 + 80];   // the block (targets), zero padded
+    uint16_t sp[DMX_BLK];             // the history's entries in bucket order (its S)
+    uint16_t ep[DMX_NBUCKET];         // the history's bucket ends
+    uint32_t qd[MW][64][2];           // per wave: entries waiting for the LDS extension
 };
 
-// HG = history candidates per group.  HG = 6 (K <= 6, the bench default) fits 62 VGPRs: 8
-// waves per SIMD, two 16-wave workgroups per CU as the 66 KB of LDS allow (C3, K=6: history
-// stage 1.88 -> 1.53 ms); HG = 8 needs 78 VGPRs (one workgroup per CU) and serves K > 6 in
-// fewer groups.
+// One group of HG history candidates of entry i (target bytes t0..t2, bucket h): entries
+// x, x - 1, ... of the history's S, the cnt-th candidate onwards.  Updates the best (longest,
+// then nearest); returns whether the walk may stop (an entry past the distance limit or, in
+// the exhaustive walk, of another bucket).  ONE: K <= HG, the only group (no walk state).
+template <int HG, bool ONE, bool DEFER = false>
+__device__ __forceinline__ bool hist_group(const HistLDS& L, int32_t x, uint32_t cnt, uint32_t K, uint32_t h,
+                                           uint32_t t0, uint32_t t1, uint32_t t2, uint32_t i, uint32_t lim,
+                                           int32_t minq, uint32_t& best, uint32_t& bq, uint32_t* fullp = nullptr) {
+    const uint16_t* Sp = L.sp;
+    uint32_t q[HG], s0[HG], s1[HG], s2[HG];
+#pragma unroll
+    for (int g = 0; g < HG; g++) q[g] = (x - g >= 0 && (!ONE || (uint32_t)g < K)) ? (uint32_t)Sp[x - g] : 0u;
+#pragma unroll
+    for (int g = 0; g < HG; g++) {
+        const uint64_t v = ld8(L.data, q[g]);
+        s0[g] = (uint32_t)v;
+        s1[g] = (uint32_t)(v >> 32);
+        s2[g] = ld4(L.data, q[g] + 8);
+    }
+    uint32_t key = 0, full = 0;
+    bool left = false;
+#pragma unroll
+    for (int g = 0; g < HG; g++) {
+        if (ONE && (uint32_t)g >= K) break;   // uniform
+        const bool ok = x - g >= 0 && (ONE || cnt + (uint32_t)g < K) && (int32_t)q[g] >= minq;
+        const uint32_t mb = min(min(ffbl_hw(t0 ^ s0[g]), __builtin_elementwise_add_sat(ffbl_hw(t1 ^ s1[g]), 32u)),
+                                min(ffbl_hw(t2 ^ s2[g]), 32u) + 64u);
+        const uint32_t m = ok ? min(mb >> 3, lim) : 0u;
+        key = max(key, (m << 8) | (255u - (uint32_t)g));
+        full |= (ok && mb == 96u && lim > CB) ? (1u << g) : 0u;
+        if (!ONE) {
+            left = left || (x - g >= 0 && (int32_t)q[g] < minq);
+            if (K == 0xFFFFFFFFu)   // exhaustive: the walk ends at the bucket's start
+                left = left || (x - g >= 0 && dmx_hash(s0[g] & 0xFFFFFFu) != h);
+        }
+    }
+    if ((key >> 8) > best) { best = key >> 8; bq = q[255u - (key & 255u)]; }
+    if (DEFER) {   // the extension waits in the wave's queue (hist_flush)
+        *fullp = full;
+        return false;
+    }
+    while (full) {   // nearest first; a farther one must be strictly longer
+        const uint32_t g = (uint32_t)__builtin_ctz(full);
+        full &= full - 1u;
+        if (best >= lim) break;
+        uint32_t qg = q[0];
+#pragma unroll
+        for (int gg = 1; gg < HG; gg++) qg = (uint32_t)gg == g ? q[gg] : qg;
+        if (best > CB && TB8(L.data, qg + best) != TB8(L.cur, i + best)) continue;
+        const uint32_t kk = min(ext_len2(L.cur, i, L.data, qg, CB, lim), lim);   // 16, then 32 B per round
+        if (kk > best) { best = kk; bq = qg; }
+    }
+    return left;
+}
+
+// The queued entries of one wave (qn <= 64; items k | full << 16 and x | i << 16: entry k at
+// position i, its group of candidates from entry x of the history's S, full = those equal in
+// all CB register bytes): lane l extends item l's full candidates from LDS, nearest first,
+// a farther one only if it also matches the byte at the best length, and stores the result.
+// Extensions spread over all 64 lanes instead of the few lanes of each entry round that need one.
+__device__ __forceinline__ void hist_flush(const HistLDS& L, uint32_t wave, uint32_t qn, uint32_t lane, uint32_t hn,
+                                           uint32_t bn, uint32_t* __restrict__ hb) {
+    __builtin_amdgcn_wave_barrier();
+    if (lane < qn) {
+        const uint32_t w0 = lds_ld(const_cast<uint32_t*>(&L.qd[wave][lane][0]));
+        const uint32_t w1 = lds_ld(const_cast<uint32_t*>(&L.qd[wave][lane][1]));
+        const uint32_t k = w0 & 0xFFFFu, i = w1 >> 16;
+        const int32_t x = (int32_t)(w1 & 0xFFFFu);
+        uint32_t full = w0 >> 16;
+        const uint32_t lim = min(bn - i, (uint32_t)MAXLEN);
+        uint32_t best = CB, bq = L.sp[x - (int32_t)__builtin_ctz(full)];   // the nearest full one
+        while (full && best < lim) {
+            const uint32_t g = (uint32_t)__builtin_ctz(full);
+            full &= full - 1u;
+            const uint32_t qg = L.sp[x - (int32_t)g];
+            if (best > CB && TB8(L.data, qg + best) != TB8(L.cur, i + best)) continue;
+            const uint32_t kk = min(ext_len2(L.cur, i, L.data, qg, CB, lim), lim);
+            if (kk > best) { best = kk; bq = qg; }
+        }
+        hb[k] = (best << 16) | (hn - bq + i);
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// HG = history candidates per group: 6 for K <= 6 (the bench default), 8 otherwise (K > 6 in
+// fewer groups).
 template <int HG>
 __global__ __launch_bounds__(MT) void dmx_hist_kernel_t(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
                                                       int32_t max_chain, const uint8_t* __restrict__ pre, uint32_t npre,
@@ -1154,76 +1247,68 @@ __global__ __launch_bounds__(MT) void dmx_hist_kernel_t(const uint8_t* __restric
     const uint64_t tbeg = dbg ? __builtin_amdgcn_s_memtime() : 0;
     stage_bytes(L.data, DATA_WORDS, hs, hn, cur, bn, tid);
     stage_bytes(L.cur, DMX_BLK / 4 + 80, cur, bn, nullptr, 0, tid);
+    {   // the history's chains: S (hn - 2 entries, 8 per 16-byte load) and the bucket ends
+        const uint4* Sg = reinterpret_cast<const uint4*>(chs + (uint64_t)b * DMX_BLK);
+        const uint4* Eg = reinterpret_cast<const uint4*>(che + (uint64_t)b * DMX_NBUCKET);
+        for (uint32_t k = tid; k < (hn - 2 + 7) / 8; k += MT) reinterpret_cast<uint4*>(L.sp)[k] = Sg[k];
+        for (uint32_t k = tid; k < DMX_NBUCKET / 8; k += MT) reinterpret_cast<uint4*>(L.ep)[k] = Eg[k];
+    }
     __syncthreads();
     const uint64_t ts0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
     const uint16_t* Sc = chs + (uint64_t)(b + 1) * DMX_BLK;   // the block's entries in bucket order
-    const uint16_t* Sp = chs + (uint64_t)b * DMX_BLK;         // the history's
-    const uint16_t* Ep = che + (uint64_t)b * DMX_NBUCKET;     // the history's bucket ends
+    const uint16_t* Ep = L.ep;                                // the history's bucket ends (LDS)
     const uint32_t K = max_chain > 0 ? (uint32_t)max_chain : 0xFFFFFFFFu;
+    const uint32_t lane = tid & 63, wave = wave_of(tid);
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t qn = 0;   // queued entries of this wave (K <= HG)
     uint32_t inext = tid < nvalid ? (uint32_t)Sc[tid] : 0u;
-    for (uint32_t k = tid; k < nvalid; k += MT) {
+    // wave-uniform trip count (every lane runs the queue code); lanes past nvalid idle
+    for (uint32_t k0 = tid - lane; k0 < nvalid; k0 += MT) {
+        const uint32_t k = k0 + lane;
+        const bool act = k < nvalid;
         const uint32_t i = inext;
         if (k + MT < nvalid) inext = Sc[k + MT];   // next entry in flight during this one
-        const uint64_t tv = ld8(L.cur, i);
-        const uint32_t t0 = (uint32_t)tv, t1 = (uint32_t)(tv >> 32), t2 = ld4(L.cur, i + 8);
-        const uint32_t h = dmx_hash(t0 & 0xFFFFFFu);
-        const uint32_t lim = min(bn - i, (uint32_t)MAXLEN);
-        const int32_t minq = (int32_t)(hn + i) - 32768;   // distance <= 32768
-        uint32_t best = 0, bq = 0, cnt = 0;
-        // Candidates newest first in groups of HG, loaded together and compared branch-free
-        // in registers on 12 bytes (longest, then nearest); only candidates equal in all 12
-        // are extended, those farther than the best so far only if they match its last byte.  An entry older than the distance limit, or of another bucket, can
-        // never win (a bucket's older entries are farther still; another bucket is another
-        // trigram), so it is masked, and the walk ends after its group; the exhaustive walk
-        // also ends where the bucket does.
-        for (int32_t x = (int32_t)Ep[h] - 1; x >= 0 && cnt < K && best < lim; x -= HG, cnt += HG) {
-            uint32_t q[HG], s0[HG], s1[HG], s2[HG];
-#pragma unroll
-            for (int g = 0; g < HG; g++) q[g] = (x - g >= 0) ? (uint32_t)Sp[x - g] : 0u;
-#pragma unroll
-            for (int g = 0; g < HG; g++) {
-                const uint64_t v = ld8(L.data, q[g]);
-                s0[g] = (uint32_t)v;
-                s1[g] = (uint32_t)(v >> 32);
-                s2[g] = ld4(L.data, q[g] + 8);
+        uint32_t best = 0, bq = 0, full = 0;
+        int32_t x0 = -1;
+        if (act) {
+            const uint64_t tv = ld8(L.cur, i);
+            const uint32_t t0 = (uint32_t)tv, t1 = (uint32_t)(tv >> 32), t2 = ld4(L.cur, i + 8);
+            const uint32_t h = dmx_hash(t0 & 0xFFFFFFu);
+            const uint32_t lim = min(bn - i, (uint32_t)MAXLEN);
+            const int32_t minq = (int32_t)(hn + i) - 32768;   // distance <= 32768
+            // Candidates newest first in groups of HG, loaded together and compared
+            // branch-free in registers on 12 bytes (longest, then nearest); only candidates
+            // equal in all 12 are extended, those farther than the best so far only if they
+            // match its last byte.  An entry older than the distance limit, or of another
+            // bucket, can never win (a bucket's older entries are farther still; another bucket
+            // is another trigram), so it is masked, and the walk ends after its group; the
+            // exhaustive walk also ends where the bucket does.
+            x0 = (int32_t)Ep[h] - 1;
+            if (K <= (uint32_t)HG) {   // bounded (the bench's K = 6): one group, extensions queued
+                hist_group<HG, true, true>(L, x0, 0, K, h, t0, t1, t2, i, lim, minq, best, bq, &full);
+            } else {
+                uint32_t cnt = 0;
+                for (int32_t x = x0; x >= 0 && cnt < K && best < lim; x -= HG, cnt += HG)
+                    if (hist_group<HG, false>(L, x, cnt, K, h, t0, t1, t2, i, lim, minq, best, bq)) break;
             }
-            uint32_t key = 0, full = 0;
-            bool left = false;
-#pragma unroll
-            for (int g = 0; g < HG; g++) {
-                const bool ok = x - g >= 0 && cnt + (uint32_t)g < K && (int32_t)q[g] >= minq;
-                const uint32_t mb = min(min(ffbl_hw(t0 ^ s0[g]), __builtin_elementwise_add_sat(ffbl_hw(t1 ^ s1[g]), 32u)),
-                                        min(ffbl_hw(t2 ^ s2[g]), 32u) + 64u);
-                const uint32_t m = ok ? min(mb >> 3, lim) : 0u;
-                key = max(key, (m << 8) | (255u - (uint32_t)g));
-                full |= (ok && mb == 96u && lim > CB) ? (1u << g) : 0u;
-                left = left || (x - g >= 0 && (int32_t)q[g] < minq);
-                if (K == 0xFFFFFFFFu)   // exhaustive: the walk ends at the bucket's start
-                    left = left || (x - g >= 0 && dmx_hash(s0[g] & 0xFFFFFFu) != h);
-            }
-            if ((key >> 8) > best) { best = key >> 8; bq = q[255u - (key & 255u)]; }
-            while (full) {   // nearest first; a farther one must be strictly longer
-                const uint32_t g = (uint32_t)__builtin_ctz(full);
-                full &= full - 1u;
-                if (best >= lim) break;
-                uint32_t qg = q[0];
-#pragma unroll
-                for (int gg = 1; gg < HG; gg++) qg = (uint32_t)gg == g ? q[gg] : qg;
-                if (best > CB && TB8(L.data, qg + best) != TB8(L.cur, i + best)) continue;
-                uint32_t kk = CB;
-                for (;;) {
-                    const uint64_t xr = ld8(L.data, qg + kk) ^ ld8(L.cur, i + kk);
-                    if (xr) { kk += (uint32_t)__builtin_ctzll(xr) >> 3; break; }
-                    kk += 8;
-                    if (kk >= lim) break;
-                }
-                kk = min(kk, lim);
-                if (kk > best) { best = kk; bq = qg; }
-            }
-            if (left) break;
         }
-        hb[k] = best >= 3 ? (best << 16) | (hn - bq + i) : 0u;
+        const bool push = full != 0;
+        const uint64_t pm = __ballot(push);
+        const uint32_t np = (uint32_t)__popcll(pm);
+        if (qn + np > 64) {
+            hist_flush(L, wave, qn, lane, hn, bn, hb);
+            qn = 0;
+        }
+        if (push) {
+            const uint32_t slot = qn + (uint32_t)__popcll(pm & lt);
+            lds_st(&L.qd[wave][slot][0], k | (full << 16));
+            lds_st(&L.qd[wave][slot][1], (uint32_t)x0 | (i << 16));
+        } else if (act) {
+            hb[k] = best >= 3 ? (best << 16) | (hn - bq + i) : 0u;
+        }
+        qn += np;
     }
+    if (qn) hist_flush(L, wave, qn, lane, hn, bn, hb);
     if (dbg) {   // stamps 12..15: staged, searched
         __syncthreads();
         if (tid == 0) {
