@@ -171,8 +171,8 @@ __device__ __forceinline__ uint32_t adv_of(const MatchLDS& L, uint32_t p) {
 // down one lane per step with DPP wave_shr:1; lane 0 is fed from a halo of the KD
 // entries below the chunk.  Each step compares 64 candidates with ~20 VALU instructions
 // and no LDS traffic: 16 bytes give the exact length of any match < 16 (the usual case);
-// longer candidates extend from LDS 8 bytes per step.  Chains longer than KD (exhaustive
-// mode) continue from LDS, CW candidates per iteration.  The kept key is len << 15 | q:
+// longer candidates extend from LDS.  Chains longer than KD (exhaustive mode) run on in
+// further windows of KD register steps.  The kept key is len << 15 | q:
 // longest, then nearest (largest q) -- the reference's newest-first walk with strict >
 // (:249-263).  A lane stops comparing once its best is the longest possible length.
 #define KD 32
@@ -180,7 +180,6 @@ __device__ __forceinline__ uint32_t adv_of(const MatchLDS& L, uint32_t p) {
 #define KE 8    // chains up to KE candidates use chunks with the halo embedded (64-K owned entries)
 #define JR 8    // Jacobi rounds of the walk before the serial fallback
 #define WALK_SERIAL 1024   // fallback: at most this many tokens (approximate path) -> one-lane token walk
-#define CW 4
 __device__ __forceinline__ uint32_t ffbl(uint32_t x) {   // lowest set bit, ~0 for 0 (v_ffbl_b32)
     return x ? (uint32_t)__builtin_ctz(x) : 0xFFFFFFFFu;
 }
@@ -359,9 +358,11 @@ __device__ __forceinline__ void cand_step(uint32_t j, uint32_t& x0, uint32_t& x1
     x0 = wshr(x0, __builtin_amdgcn_readlane(h0, src));
     x1 = wshr(x1, __builtin_amdgcn_readlane(h1, src));
     x2 = wshr(x2, __builtin_amdgcn_readlane(h2, src));
-    // equal leading bits of the 12-byte window, 96 = all (ffbl(0) = ~0)
-    const uint32_t t = min(ffbl(i1 ^ x1), min(ffbl(i2 ^ x2), 32u) + 32u) + 32u;
-    const uint32_t mb = min(ffbl(i0 ^ x0), t);
+    // equal leading bits of the 12-byte window, 96 = all: opaque v_ffbl (~0 for 0), two
+    // saturating adds, v_min3, and the cap
+    const uint32_t mb = min(min(min(ffbl_hw(i0 ^ x0), __builtin_elementwise_add_sat(ffbl_hw(i1 ^ x1), 32u)),
+                                __builtin_elementwise_add_sat(ffbl_hw(i2 ^ x2), 64u)),
+                            96u);
     uint32_t m = min(mb >> 3, lim_eff);
     bool fl = mb == 96u;
     if (GUARD) {
@@ -372,10 +373,10 @@ __device__ __forceinline__ void cand_step(uint32_t j, uint32_t& x0, uint32_t& x1
     full |= fl ? (1u << src) : 0u;
 }
 template <bool GUARD>
-__device__ __forceinline__ void cand_steps(uint32_t jmax, uint32_t i0, uint32_t i1, uint32_t i2, uint32_t h0,
-                                           uint32_t h1, uint32_t h2, uint32_t nc, uint32_t lim_eff, uint32_t& jkey,
-                                           uint32_t& full) {
-    uint32_t x0 = i0, x1 = i1, x2 = i2, y0, y1, y2;
+__device__ __forceinline__ void cand_steps(uint32_t jmax, uint32_t& x0, uint32_t& x1, uint32_t& x2, uint32_t i0,
+                                           uint32_t i1, uint32_t i2, uint32_t h0, uint32_t h1, uint32_t h2, uint32_t nc,
+                                           uint32_t lim_eff, uint32_t& jkey, uint32_t& full) {
+    uint32_t y0, y1, y2;
     uint32_t j = 1;
     for (; j + 1 <= jmax; j += 2) {   // two steps per trip, alternating registers (no copies)
         y0 = x0; y1 = x1; y2 = x2;
@@ -696,6 +697,13 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
             }
         }
     } else
+    // Longer chains (K > KE, exhaustive mode): chunks of 64 entries, candidates in windows of
+    // KD = 32 steps.  The register streams (12 bytes) run on across windows; lane 0 is fed
+    // from a halo of the 32 entries below the window (lane l holds entry k0 - 1 - 32w - l),
+    // reloaded per window.  After each window: the window's best into the position-form key
+    // (len << 15 | q: longest, then nearest), and its candidates equal in all 12 register
+    // bytes extended from LDS (resolve_full).  A lane needs more windows while its chain goes
+    // on and its best is short of min(258, bn - i); the wave stops when no lane does.
     for (uint32_t k0 = wave << 6; k0 < nvalid; k0 += MT) {
         const uint32_t k = k0 + lane;
         const bool act = k < nvalid;
@@ -712,64 +720,51 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
             nc = K <= KD ? min(k, K) : min(k - (uint32_t)L.bstart[dmx_hash((uint32_t)iv0 & 0xFFFFFFu)], K);
             lim = (bn - i) < MAXLEN ? (bn - i) : MAXLEN;
         }
-        // halo: lane l < KD holds entry k0-1-l
-        uint32_t hq = 0;
-        uint64_t hv0 = 0;
-        uint32_t h2 = 0;
-        if (lane < KD && k0 >= lane + 1) {
-            hq = L.sorted[k0 - 1 - lane];
-            hv0 = ld8(L.data, hq);
-            h2 = ld4(L.data, hq + 8);
-        }
         const uint32_t i0 = (uint32_t)iv0, i1 = (uint32_t)(iv0 >> 32);
-        const uint32_t h0 = (uint32_t)hv0, h1 = (uint32_t)(hv0 >> 32);
-        {   // sort check: the predecessor entry (lane - 1, lane 0: halo 0) has a smaller (bucket, position)
-            const uint32_t sk = sort_key(i0, i);
-            const uint32_t pk = wshr(sk, __builtin_amdgcn_readlane(sort_key(h0, hq), 0));
-            if (__ballot(act && k >= 1 && pk > sk)) L.sortbad = 1;
-        }
-        // wave-uniform bound: the largest chain length of the chunk, capped at KD
-        uint32_t jmax = act ? min(nc, (uint32_t)KD) : 0;
-        jmax = max(jmax, dpp_shr(jmax, 1));
-        jmax = max(jmax, dpp_shr(jmax, 2));
-        jmax = max(jmax, dpp_shr(jmax, 4));
-        jmax = max(jmax, dpp_shr(jmax, 8));
-        jmax = max(max(__builtin_amdgcn_readlane(jmax, 15), __builtin_amdgcn_readlane(jmax, 31)),
-                   max(__builtin_amdgcn_readlane(jmax, 47), __builtin_amdgcn_readlane(jmax, 63)));
-        iters += jmax;
         const uint32_t lim_eff = act ? lim : 0;
-        uint32_t jkey = 0, full = 0;   // full: bit j-1 = candidate j matches all CB bytes
-        if (k0 == 0) cand_steps<true>(jmax, i0, i1, i2, h0, h1, h2, nc, lim_eff, jkey, full);
-        else cand_steps<false>(jmax, i0, i1, i2, h0, h1, h2, nc, lim_eff, jkey, full);
-        if (lim_eff <= CB) full = 0;
-        // position form of the best key: (len << 15) | source position
+        uint32_t x0 = i0, x1 = i1, x2 = i2;   // the candidate streams
         uint32_t bestkey = 0;
-        if (act && (jkey >> 8) >= 3) bestkey = ((jkey >> 8) << 15) | (uint32_t)L.sorted[k - (255u - (jkey & 255u))];
-        const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
-        bestkey = resolve_full<false, false>(L, bn, lane, wave, k, i, lim_eff, bestkey, full, k0);
-        if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
-        // chains longer than KD (exhaustive mode): continue from LDS, CW candidates per iteration
-        for (uint32_t c = KD;; c += CW) {
-            const bool more = act && c < nc && (bestkey >> 15) < lim;
-            if (__ballot(more) == 0) break;
-            iters++;
-            if (more) {
-                uint32_t q[CW];
-                uint64_t w[CW];
-#pragma unroll
-                for (int j = 0; j < CW; j++) q[j] = (c + j < nc) ? (uint32_t)L.sorted[k - 1 - c - j] : DMX_NONE16;
-#pragma unroll
-                for (int j = 0; j < CW; j++) w[j] = q[j] != DMX_NONE16 ? ld8(L.data, q[j]) : ~iv0;
-#pragma unroll
-                for (int j = 0; j < CW; j++) {
-                    uint32_t len = match_bytes(iv0 ^ w[j]);
-                    const uint32_t bl = bestkey >> 15;
-                    if (len == 8 && lim > 8 && bl < lim && (bl < 8 || may_beat(L, i, q[j], bl)))
-                        len = ext_len(L, i, q[j], 8, lim);
-                    if (len > lim) len = lim;
-                    if (len >= 3) bestkey = max(bestkey, (len << 15) | q[j]);
-                }
+        for (uint32_t jb = 0;; jb += KD) {
+            // lanes that still need candidates jb + 1 ...: wave-uniform window length
+            uint32_t need = (act && nc > jb && (bestkey >> 15) < lim) ? min(nc - jb, (uint32_t)KD) : 0u;
+            need = max(need, dpp_shr(need, 1));
+            need = max(need, dpp_shr(need, 2));
+            need = max(need, dpp_shr(need, 4));
+            need = max(need, dpp_shr(need, 8));
+            const uint32_t jmax = max(max(__builtin_amdgcn_readlane(need, 15), __builtin_amdgcn_readlane(need, 31)),
+                                      max(__builtin_amdgcn_readlane(need, 47), __builtin_amdgcn_readlane(need, 63)));
+            if (jmax == 0) break;
+            iters += jmax;
+            // halo of this window: lane l < KD holds entry k0 - 1 - jb - l
+            uint32_t hq = 0;
+            uint64_t hv0 = 0;
+            uint32_t h2 = 0;
+            if (lane < KD && k0 >= jb + lane + 1) {
+                hq = L.sorted[k0 - 1 - jb - lane];
+                hv0 = ld8(L.data, hq);
+                h2 = ld4(L.data, hq + 8);
             }
+            const uint32_t h0 = (uint32_t)hv0, h1 = (uint32_t)(hv0 >> 32);
+            if (jb == 0) {   // sort check: the predecessor (lane - 1, lane 0: halo 0) has a smaller (bucket, position)
+                const uint32_t sk = sort_key(i0, i);
+                const uint32_t pk = wshr(sk, __builtin_amdgcn_readlane(sort_key(h0, hq), 0));
+                if (__ballot(act && k >= 1 && pk > sk)) L.sortbad = 1;
+            }
+            // lanes without a candidate j of this window: halo lanes before the block start
+            // (k0 < jb + KD), or a bounded chain longer than KD ending inside the window
+            // (K <= KD needs no mask: the window is at most K steps long)
+            const uint32_t ncw = nc > jb ? nc - jb : 0u;
+            uint32_t jkey = 0, full = 0;   // full: bit j-1 = candidate jb + j matches all CB bytes
+            if (k0 < jb + KD || (K > KD && K < jb + KD)) cand_steps<true>(jmax, x0, x1, x2, i0, i1, i2, h0, h1, h2, ncw, lim_eff, jkey, full);
+            else cand_steps<false>(jmax, x0, x1, x2, i0, i1, i2, h0, h1, h2, ncw, lim_eff, jkey, full);
+            if (lim_eff <= CB || (bestkey >> 15) >= lim_eff) full = 0;
+            // the window's register best in position form; candidates of this window are
+            // farther than those of earlier windows, so a tie keeps the earlier (nearer) one
+            if (act && (jkey >> 8) >= 3)
+                bestkey = max(bestkey, ((jkey >> 8) << 15) | (uint32_t)L.sorted[k - jb - (255u - (jkey & 255u))]);
+            const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
+            bestkey = resolve_full<false, false>(L, bn, lane, wave, k - jb, i, lim_eff, bestkey, full, k0);
+            if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
         }
         if (act) store_result<DICT>(L, pg, k, i, bestkey, hbk);
     }
