@@ -180,6 +180,8 @@ __device__ __forceinline__ uint32_t adv_of(const MatchLDS& L, uint32_t p) {
 #define KE 8    // chains up to KE candidates use chunks with the halo embedded (64-K owned entries)
 #define JR 8    // Jacobi rounds of the walk before the serial fallback
 #define WALK_SERIAL 1024   // fallback: at most this many tokens (approximate path) -> one-lane token walk
+#define TPMAX (DMX_NBUCKET)   // token positions listed in bstart (u16) for the token-major compaction
+#define HSTR (DMX_HIST + 1)   // stride of the 4 histogram copies of the compaction
 __device__ __forceinline__ uint32_t ffbl(uint32_t x) {   // lowest set bit, ~0 for 0 (v_ffbl_b32)
     return x ? (uint32_t)__builtin_ctz(x) : 0xFFFFFFFFu;
 }
@@ -1594,7 +1596,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
                                                        uint32_t* __restrict__ hist_g,
                                                        dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg) {
     __shared__ MatchLDS L;
-    __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def, tp0[3], st_rounds;
+    __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def, tp0[3], st_rounds, st_p3a;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = wave_of(tid);
     const uint32_t b = blockIdx.x;
     if ((mflags & 4u) && info[b].prestored) return;   // stored by the noise check (K0)
@@ -1607,7 +1609,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
     // ---- P0: stage the block, the bucket starts and the bucket-sorted positions in LDS ----
     const uint64_t tbeg = dbg ? __builtin_amdgcn_s_memtime() : 0;
     if (tid == 0) { L.adl_s = 0; L.adl_t = 0; L.sortbad = (mflags & 2u) ? 1u : 0u; }   // 2: test hook
-    if (dbg && tid == 0) { st_search = 0; st_iters = 0; st_def = 0; }
+    if (dbg && tid == 0) { st_search = 0; st_iters = 0; st_def = 0; st_p3a = 0; }
     for (uint32_t k = tid; k < DMX_HIST; k += MT) L.hist[k] = 0;
     for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) L.lit[k] = 0;
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
@@ -1922,29 +1924,49 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         __syncthreads();
         uint32_t k = L.wsum[wave] + x - cnt;
         uint32_t* tb = tok_g + (uint64_t)b * DMX_BLK;
-        const uint32_t lw = L.lit[tid];
-        uint32_t mm = m;
-        while (mm) {
-            const uint32_t bit = __builtin_ctz(mm);
-            mm &= mm - 1;
-            const uint32_t p = (tid << 5) + bit;
-            uint32_t t;
-            if ((lw >> bit) & 1u) {
-                t = D8[p];
-                atomicAdd(&L.hist[t], 1u);
-            } else {
-                const uint32_t len = (uint32_t)L.len8[p] + 3u, dist = L.sorted[p];
-                t = (dist << 9) | len;
-                uint32_t s, eb, ev;
-                len_sym(len, s, eb, ev);
-                atomicAdd(&L.hist[s], 1u);
-                dist_sym(dist, s, eb, ev);
-                atomicAdd(&L.hist[DMX_DIST0 + s], 1u);
+        const uint32_t ntok = L.ntok;   // uniform (published by the barrier above)
+        // Token-major: every thread lists its segment's token positions in token order (a
+        // cheap serial loop), then each thread builds tokens t = tid, tid + 1024, ...: the work
+        // is balanced over the lanes (segments hold 0..32 tokens) and the token stores are
+        // coalesced.  The list lives in bstart (free after the permute), TPMAX tokens per round.
+        uint16_t* TP = reinterpret_cast<uint16_t*>(L.bstart);
+        // histograms in 4 copies (lane & 3; stride 321 words, so a symbol's copies sit in
+        // different banks): a quarter of the same-address atomics of popular symbols.  tsm +
+        // exitp (free now: the token words are in registers) hold them; summed into hist at the end.
+        uint32_t* HS = L.tsm;
+        for (uint32_t q = tid; q < 4 * HSTR; q += MT) HS[q] = 0;
+        uint32_t* hl = HS + (lane & 3u) * HSTR;
+        for (uint32_t r0 = 0; r0 < ntok; r0 += TPMAX) {
+            const uint32_t r1 = min(r0 + TPMAX, ntok);
+            if (r0) __syncthreads();   // the previous round's readers are done with the list
+            uint32_t kk = k;
+            for (uint32_t mm = m; mm && kk < r1; mm &= mm - 1u, kk++)
+                if (kk >= r0) TP[kk - r0] = (uint16_t)((tid << 5) + (uint32_t)__builtin_ctz(mm));
+            __syncthreads();
+            if (dbg && tid == 0 && r0 == 0) st_p3a = __builtin_amdgcn_s_memtime() - t1;   // first list built
+            for (uint32_t t = r0 + tid; t < r1; t += MT) {
+                const uint32_t p = TP[t - r0];
+                uint32_t tk;
+                if ((L.lit[p >> 5] >> (p & 31)) & 1u) {
+                    tk = D8[p];
+                    atomicAdd(&hl[tk], 1u);
+                } else {
+                    const uint32_t len = (uint32_t)L.len8[p] + 3u, dist = L.sorted[p];
+                    tk = (dist << 9) | len;
+                    uint32_t sy, eb, ev;
+                    len_sym(len, sy, eb, ev);
+                    atomicAdd(&hl[sy], 1u);
+                    dist_sym(dist, sy, eb, ev);
+                    atomicAdd(&hl[DMX_DIST0 + sy], 1u);
+                }
+                tb[t] = tk;
             }
-            tb[k++] = t;
         }
+        __syncthreads();
+        for (uint32_t q = tid; q < DMX_HIST; q += MT) L.hist[q] += HS[q] + HS[HSTR + q] + HS[2 * HSTR + q] + HS[3 * HSTR + q];
     }
     __syncthreads();
+    const uint64_t p3b = dbg ? __builtin_amdgcn_s_memtime() - t1 : 0;
     for (uint32_t k = tid; k < DMX_HIST; k += MT) hist_g[(uint64_t)b * DMX_HIST + k] = L.hist[k];
     if (dbg && tid == 0) {
         dbg[(uint64_t)b * DMX_STAMPS + 0] = t0 - tbeg;
@@ -1959,6 +1981,10 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         dbg[(uint64_t)b * DMX_STAMPS + 9] = tp0[1] - tbeg;   //   pass 1 done
         dbg[(uint64_t)b * DMX_STAMPS + 10] = tp0[2] - tbeg;  //   pass 2 done
         dbg[(uint64_t)b * DMX_STAMPS + 11] = st_rounds;      // walk: Jacobi rounds (JR = not converged)
+        if (!DICT) {   // (12, 13 are the history kernel's with DMX_F_DICT)
+            dbg[(uint64_t)b * DMX_STAMPS + 12] = st_p3a;     // P3: token list built (token-major path)
+            dbg[(uint64_t)b * DMX_STAMPS + 13] = p3b;        // P3: tokens and histograms done
+        }
     }
     if (tid == 0) {
         info[b].ntok = L.ntok;
