@@ -2017,7 +2017,6 @@ struct K2LDS {
     int32_t lstart[16];   // first sorted index that gets length d
     int32_t cnt[16];      // canonical codes: codes handed out per length so far
     uint32_t next[16];    // canonical codes: first code of each length
-    uint32_t code[320];   // canonical codes (bit-reversed) | len << 16
     uint32_t ccode[20];   // code-length codes, same packing
     // run-length coding of the code lengths (RFC 1951 §3.2.7)
     uint8_t rle_sym[320];
@@ -2071,7 +2070,7 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
         wsync();
         return;
     }
-    // rank among the used symbols: the used keys are compacted first (S.code is free until
+    // rank among the used symbols: the used keys are compacted first (S.nodew is free until
     // canon_codes), so the broadcast loop runs over the m used keys only, not all n slots
     const uint32_t nru = (m + 63) >> 6;   // registers holding used keys
     {
@@ -2080,7 +2079,7 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
         for (int r = 0; r < NR; r++) {
             const bool u = key[r] != 0xFFFFFFFFu;
             const uint64_t um = __ballot(u);
-            if (u) S.code[base + (uint32_t)__popcll(um & ((1ull << lane) - 1ull))] = key[r];
+            if (u) S.nodew[base + (uint32_t)__popcll(um & ((1ull << lane) - 1ull))] = key[r];
             base += (uint32_t)__popcll(um);
         }
     }
@@ -2089,7 +2088,7 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
 #pragma unroll
     for (int r = 0; r < NR; r++) {
         const uint32_t i = (uint32_t)r * 64 + lane;
-        ck[r] = i < m ? S.code[i] : 0xFFFFFFFFu;
+        ck[r] = i < m ? S.nodew[i] : 0xFFFFFFFFu;
         rk[r] = 0;
     }
 #pragma unroll
@@ -2318,9 +2317,10 @@ struct HuffRes {
 
 // Plan one DEFLATE block from the frequencies in S.fll / S.fd (EOB included): code
 // lengths, exact stored / fixed / dynamic costs, the type (the cheapest; stored only if
-// allow_stored), canonical codes in S.code and the header bits (BFINAL/BTYPE + trees)
+// allow_stored), canonical codes into codes_out (global) and the header bits (BFINAL/BTYPE + trees)
 // in S.hdr.  One wave.
-__device__ HuffRes huff_block(K2LDS& S, uint32_t bn, uint32_t final_bit, bool allow_stored, uint32_t lane) {
+__device__ HuffRes huff_block(K2LDS& S, uint32_t bn, uint32_t final_bit, bool allow_stored, uint32_t lane,
+                              uint32_t* __restrict__ codes_out) {
     for (int k = (int)lane; k < DMX_HDR_WORDS; k += 64) S.hdr[k] = 0;
     wsync();
     // lit/len and distance code lengths
@@ -2390,8 +2390,8 @@ __device__ HuffRes huff_block(K2LDS& S, uint32_t bn, uint32_t final_bit, bool al
     // fixed codes: the canonical assignment counts all 288 lit/len lengths (RFC 1951
     // 3.2.6: 280..287 are 8-bit codes, so the 9-bit codes of 144..255 start after them);
     // slots 286/287 are overwritten by the distance codes next (never emitted)
-    canon_codes<5>(S, S.lll, bt == 1 ? 288 : 286, S.code, lane);
-    canon_codes<1>(S, S.ld, 30, S.code + DMX_DIST0, lane);
+    canon_codes<5>(S, S.lll, bt == 1 ? 288 : 286, codes_out, lane);
+    canon_codes<1>(S, S.ld, 30, codes_out + DMX_DIST0, lane);
     wsync();
 
     // header bits: items (value, bits) placed by a prefix sum over their bit counts
@@ -2449,9 +2449,8 @@ __global__ __launch_bounds__(64) void dmx_huff_kernel(const uint32_t* __restrict
     for (int s = (int)lane; s < 288; s += 64) S.fll[s] = s < 286 ? (s == 256 ? 1u : hg[s]) : 0u;   // + end of block
     for (int s = (int)lane; s < 32; s += 64) S.fd[s] = s < 30 ? hg[DMX_DIST0 + s] : 0u;
     wsync();
-    const HuffRes h = huff_block(S, bn, final_bit, true, lane);
     uint32_t* cg = codes_g + (uint64_t)b * DMX_NSUB * DMX_HIST;
-    for (int s = (int)lane; s < 316; s += 64) cg[s] = S.code[s];
+    const HuffRes h = huff_block(S, bn, final_bit, true, lane, cg);
     uint32_t* hgout = hdr_g + (uint64_t)b * DMX_NSUB * DMX_HDR_WORDS;
     for (uint32_t k = lane; k < (h.hbits + 31) / 32; k += 64) hgout[k] = S.hdr[k];
     if (lane == 0) {
@@ -2591,8 +2590,7 @@ __global__ __launch_bounds__(64) void dmx_split_plan_kernel(SplitScratch* __rest
         S.fd[s] = f;
     }
     wsync();
-    const HuffRes h = huff_block(S, bn, final_bit, g == SPW - 1, lane);
-    for (int k = (int)lane; k < 316; k += 64) o.code[g][k] = S.code[k];
+    const HuffRes h = huff_block(S, bn, final_bit, g == SPW - 1, lane, o.code[g]);
     for (uint32_t k = lane; k < (h.hbits + 31) / 32; k += 64) o.hdr[g][k] = S.hdr[k];
     if (lane == 0) {
         SplitGroup r;
