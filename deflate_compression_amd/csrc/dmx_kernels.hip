@@ -700,11 +700,11 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
         }
     } else
     // Longer chains (K > KE, exhaustive mode): chunks of 64 entries, candidates in windows of
-    // KD = 32 steps.  The register streams (12 bytes) run on across windows; lane 0 is fed
-    // from a halo of the 32 entries below the window (lane l holds entry k0 - 1 - 32w - l),
-    // reloaded per window.  After each window: the window's best into the position-form key
-    // (len << 15 | q: longest, then nearest), and its candidates equal in all 12 register
-    // bytes extended from LDS (resolve_full).  A lane needs more windows while its chain goes
+    // KD = 32 steps; lane 0 is fed from a halo of the 32 entries below the window (lane l holds
+    // entry k0 - 1 - 32w - l), reloaded per window.  Window 0: 12-byte register streams, the
+    // window's best into the position-form key (len << 15 | q: longest, then nearest), and its
+    // candidates equal in all 12 register bytes extended from LDS (resolve_full).  Later
+    // windows: the byte-at-best filter below.  A lane needs more windows while its chain goes
     // on and its best is short of min(258, bn - i); the wave stops when no lane does.
     for (uint32_t k0 = wave << 6; k0 < nvalid; k0 += MT) {
         const uint32_t k = k0 + lane;
@@ -724,7 +724,7 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
         }
         const uint32_t i0 = (uint32_t)iv0, i1 = (uint32_t)(iv0 >> 32);
         const uint32_t lim_eff = act ? lim : 0;
-        uint32_t x0 = i0, x1 = i1, x2 = i2;   // the candidate streams
+        const uint8_t* D8 = reinterpret_cast<const uint8_t*>(L.data);
         uint32_t bestkey = 0;
         for (uint32_t jb = 0;; jb += KD) {
             // lanes that still need candidates jb + 1 ...: wave-uniform window length
@@ -743,30 +743,74 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
             uint32_t h2 = 0;
             if (lane < KD && k0 >= jb + lane + 1) {
                 hq = L.sorted[k0 - 1 - jb - lane];
-                hv0 = ld8(L.data, hq);
-                h2 = ld4(L.data, hq + 8);
-            }
-            const uint32_t h0 = (uint32_t)hv0, h1 = (uint32_t)(hv0 >> 32);
-            if (jb == 0) {   // sort check: the predecessor (lane - 1, lane 0: halo 0) has a smaller (bucket, position)
-                const uint32_t sk = sort_key(i0, i);
-                const uint32_t pk = wshr(sk, __builtin_amdgcn_readlane(sort_key(h0, hq), 0));
-                if (__ballot(act && k >= 1 && pk > sk)) L.sortbad = 1;
+                if (jb == 0) {
+                    hv0 = ld8(L.data, hq);
+                    h2 = ld4(L.data, hq + 8);
+                }
             }
             // lanes without a candidate j of this window: halo lanes before the block start
             // (k0 < jb + KD), or a bounded chain longer than KD ending inside the window
             // (K <= KD needs no mask: the window is at most K steps long)
             const uint32_t ncw = nc > jb ? nc - jb : 0u;
-            uint32_t jkey = 0, full = 0;   // full: bit j-1 = candidate jb + j matches all CB bytes
-            if (k0 < jb + KD || (K > KD && K < jb + KD)) cand_steps<true>(jmax, x0, x1, x2, i0, i1, i2, h0, h1, h2, ncw, lim_eff, jkey, full);
-            else cand_steps<false>(jmax, x0, x1, x2, i0, i1, i2, h0, h1, h2, ncw, lim_eff, jkey, full);
-            if (lim_eff <= CB || (bestkey >> 15) >= lim_eff) full = 0;
-            // the window's register best in position form; candidates of this window are
-            // farther than those of earlier windows, so a tie keeps the earlier (nearer) one
-            if (act && (jkey >> 8) >= 3)
-                bestkey = max(bestkey, ((jkey >> 8) << 15) | (uint32_t)L.sorted[k - jb - (255u - (jkey & 255u))]);
-            const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
-            bestkey = resolve_full<false, false>(L, bn, lane, wave, k - jb, i, lim_eff, bestkey, full, k0);
-            if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
+            const bool guard = k0 < jb + KD || (K > KD && K < jb + KD);
+            if (jb == 0) {
+                const uint32_t h0 = (uint32_t)hv0, h1 = (uint32_t)(hv0 >> 32);
+                {   // sort check: the predecessor (lane - 1, lane 0: halo 0) has a smaller (bucket, position)
+                    const uint32_t sk = sort_key(i0, i);
+                    const uint32_t pk = wshr(sk, __builtin_amdgcn_readlane(sort_key(h0, hq), 0));
+                    if (__ballot(act && k >= 1 && pk > sk)) L.sortbad = 1;
+                }
+                uint32_t x0 = i0, x1 = i1, x2 = i2;   // the candidate streams
+                uint32_t jkey = 0, full = 0;   // full: bit j-1 = candidate j matches all CB bytes
+                if (guard) cand_steps<true>(jmax, x0, x1, x2, i0, i1, i2, h0, h1, h2, ncw, lim_eff, jkey, full);
+                else cand_steps<false>(jmax, x0, x1, x2, i0, i1, i2, h0, h1, h2, ncw, lim_eff, jkey, full);
+                if (lim_eff <= CB) full = 0;
+                // the window's register best in position form
+                if (act && (jkey >> 8) >= 3)
+                    bestkey = ((jkey >> 8) << 15) | (uint32_t)L.sorted[k - (255u - (jkey & 255u))];
+                const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
+                bestkey = resolve_full<false, false>(L, bn, lane, wave, k, i, lim_eff, bestkey, full, k0);
+                if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
+            } else {
+                // Later windows: a candidate farther than all those seen can only win if it is
+                // strictly longer than the current best b, so it must equal the bytes at offsets
+                // t - 1 and t, t = max(b, 2).  Only the candidates' positions stream through the
+                // lanes (the halo holds positions only); each step reads those two bytes of
+                // every lane's candidate from LDS, and the survivors (about 1 % on text; 5 %
+                // with one byte) are kept in a mask and get their exact length from LDS after
+                // the window, nearest first.
+                const uint32_t bl0 = bestkey >> 15;
+                const bool live = act && nc > jb && bl0 < lim;
+                const uint32_t t = max(bl0, 2u);   // bytes t - 1 and t must both match
+                const uint32_t ob = live ? (uint32_t)D8[i + t - 1] | ((uint32_t)D8[i + t] << 8) : 0x10000u;
+                uint32_t xp = (uint32_t)L.sorted[k - min(jb, k)];          // lane l: entry k - jb
+                uint32_t surv = 0;
+                if (guard) {
+                    for (uint32_t j = 1; j <= jmax; j++) {
+                        xp = wshr(xp, __builtin_amdgcn_readlane(hq, (int)j - 1));
+                        const uint32_t cb = (uint32_t)D8[xp + t - 1] | ((uint32_t)D8[xp + t] << 8);
+                        surv |= (cb == ob && j <= ncw) ? 1u << (j - 1) : 0u;
+                    }
+                } else {
+                    for (uint32_t j = 1; j <= jmax; j++) {
+                        xp = wshr(xp, __builtin_amdgcn_readlane(hq, (int)j - 1));
+                        const uint32_t cb = (uint32_t)D8[xp + t - 1] | ((uint32_t)D8[xp + t] << 8);
+                        surv |= (cb == ob) ? 1u << (j - 1) : 0u;
+                    }
+                }
+                const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
+                while (surv) {   // nearest first; a candidate of another bucket cannot reach 3 bytes
+                    const uint32_t j = (uint32_t)__builtin_ctz(surv) + 1u;
+                    surv &= surv - 1u;
+                    const uint32_t bl = bestkey >> 15;
+                    if (bl >= lim) break;
+                    const uint32_t q = L.sorted[k - jb - j], tt = max(bl, 2u);
+                    if (D8[q + tt] != D8[i + tt]) continue;
+                    const uint32_t len = min(ext_len(L, i, q, 0, lim), lim);
+                    if (len >= 3) bestkey = max(bestkey, (len << 15) | q);
+                }
+                if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
+            }
         }
         if (act) store_result<DICT>(L, pg, k, i, bestkey, hbk);
     }
