@@ -773,29 +773,30 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
                 if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
             } else {
                 // Later windows: a candidate farther than all those seen can only win if it is
-                // strictly longer than the current best b, so it must equal the bytes at offsets
-                // t - 1 and t, t = max(b, 2).  Only the candidates' positions stream through the
-                // lanes (the halo holds positions only); each step reads those two bytes of
-                // every lane's candidate from LDS, and the survivors (about 1 % on text; 5 %
-                // with one byte) are kept in a mask and get their exact length from LDS after
-                // the window, nearest first.
+                // strictly longer than the current best b, so it must equal bytes [0, b] -- in
+                // particular the four ending at offset b (the first three while b < 3).  Only
+                // the candidates' positions stream through the lanes (the halo holds positions
+                // only); each step reads those four bytes of every lane's candidate from LDS
+                // (two aligned dwords), and the rare survivors (1 % on text with two bytes, 5 %
+                // with one) are kept in a mask and get their exact length from LDS after the
+                // window, nearest first.
                 const uint32_t bl0 = bestkey >> 15;
                 const bool live = act && nc > jb && bl0 < lim;
-                const uint32_t t = max(bl0, 2u);   // bytes t - 1 and t must both match
-                const uint32_t ob = live ? (uint32_t)D8[i + t - 1] | ((uint32_t)D8[i + t] << 8) : 0x10000u;
+                // bytes [s, s + 4), s = max(b, 3) - 3, must match (byte s + 3 only when b >= 3)
+                const uint32_t s0 = max(bl0, 3u) - 3u, msk = bl0 >= 3 ? 0xFFFFFFFFu : 0x00FFFFFFu;
+                const uint32_t ob = live ? ld4(L.data, i + s0) & msk : 0xFFFFFFFFu;
+                const uint32_t omsk = live ? msk : 0u;   // lanes without work never survive
                 uint32_t xp = (uint32_t)L.sorted[k - min(jb, k)];          // lane l: entry k - jb
                 uint32_t surv = 0;
                 if (guard) {
                     for (uint32_t j = 1; j <= jmax; j++) {
                         xp = wshr(xp, __builtin_amdgcn_readlane(hq, (int)j - 1));
-                        const uint32_t cb = (uint32_t)D8[xp + t - 1] | ((uint32_t)D8[xp + t] << 8);
-                        surv |= (cb == ob && j <= ncw) ? 1u << (j - 1) : 0u;
+                        surv |= ((ld4(L.data, xp + s0) & omsk) == ob && j <= ncw) ? 1u << (j - 1) : 0u;
                     }
                 } else {
                     for (uint32_t j = 1; j <= jmax; j++) {
                         xp = wshr(xp, __builtin_amdgcn_readlane(hq, (int)j - 1));
-                        const uint32_t cb = (uint32_t)D8[xp + t - 1] | ((uint32_t)D8[xp + t] << 8);
-                        surv |= (cb == ob) ? 1u << (j - 1) : 0u;
+                        surv |= ((ld4(L.data, xp + s0) & omsk) == ob) ? 1u << (j - 1) : 0u;
                     }
                 }
                 const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
