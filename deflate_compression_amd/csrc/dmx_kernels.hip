@@ -171,11 +171,13 @@ __device__ __forceinline__ uint32_t adv_of(const MatchLDS& L, uint32_t p) {
 // down one lane per step with DPP wave_shr:1; lane 0 is fed from a halo of the KD
 // entries below the chunk.  Each step compares 64 candidates with ~20 VALU instructions
 // and no LDS traffic: 16 bytes give the exact length of any match < 16 (the usual case);
-// longer candidates extend from LDS.  Chains longer than KD (exhaustive mode) run on in
-// further windows of KD register steps.  The kept key is len << 15 | q:
+// longer candidates extend from LDS.  Chains longer than KD (exhaustive mode): the W0
+// nearest candidates in registers, then windows of KD steps that stream only positions and
+// test the bytes a longer match needs (the byte-at-best filter).  The kept key is len << 15 | q:
 // longest, then nearest (largest q) -- the reference's newest-first walk with strict >
 // (:249-263).  A lane stops comparing once its best is the longest possible length.
 #define KD 32
+#define W0 8    // long chains: candidates of the first window, compared in registers (the rest filtered)
 #define CB 12   // bytes compared in registers per candidate step; longer matches extend from LDS
 #define KE 8    // chains up to KE candidates use chunks with the halo embedded (64-K owned entries)
 #define JR 8    // Jacobi rounds of the walk before the serial fallback
@@ -699,13 +701,14 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
             }
         }
     } else
-    // Longer chains (K > KE, exhaustive mode): chunks of 64 entries, candidates in windows of
-    // KD = 32 steps; lane 0 is fed from a halo of the 32 entries below the window (lane l holds
-    // entry k0 - 1 - 32w - l), reloaded per window.  Window 0: 12-byte register streams, the
-    // window's best into the position-form key (len << 15 | q: longest, then nearest), and its
-    // candidates equal in all 12 register bytes extended from LDS (resolve_full).  Later
-    // windows: the byte-at-best filter below.  A lane needs more windows while its chain goes
-    // on and its best is short of min(258, bn - i); the wave stops when no lane does.
+    // Longer chains (K > KE, exhaustive mode): chunks of 64 entries; lane 0 is fed from a halo
+    // of the entries below the window (lane l holds entry k0 - 1 - jb - l), reloaded per
+    // window.  Window 0 (the W0 = 8 nearest candidates; all of them for a bounded K <= KD):
+    // 12-byte register streams, the window's best into the position-form key (len << 15 | q:
+    // longest, then nearest), and its candidates equal in all 12 register bytes extended from
+    // LDS (resolve_full).  Later windows of KD = 32 candidates: the byte-at-best filter below.
+    // A lane needs more windows while its chain goes on and its best is short of
+    // min(258, bn - i); the wave stops when no lane does.
     for (uint32_t k0 = wave << 6; k0 < nvalid; k0 += MT) {
         const uint32_t k = k0 + lane;
         const bool act = k < nvalid;
@@ -726,9 +729,10 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
         const uint32_t lim_eff = act ? lim : 0;
         const uint8_t* D8 = reinterpret_cast<const uint8_t*>(L.data);
         uint32_t bestkey = 0;
-        for (uint32_t jb = 0;; jb += KD) {
-            // lanes that still need candidates jb + 1 ...: wave-uniform window length
-            uint32_t need = (act && nc > jb && (bestkey >> 15) < lim) ? min(nc - jb, (uint32_t)KD) : 0u;
+        for (uint32_t jb = 0, wl = K <= KD ? KD : W0;; jb += wl, wl = KD) {   // (bounded K <= KD: all in registers)
+            // lanes that still need candidates jb + 1 ...: wave-uniform window length (window
+            // 0: the W0 nearest candidates, by the register compare; then windows of KD)
+            uint32_t need = (act && nc > jb && (bestkey >> 15) < lim) ? min(nc - jb, wl) : 0u;
             need = max(need, dpp_shr(need, 1));
             need = max(need, dpp_shr(need, 2));
             need = max(need, dpp_shr(need, 4));
@@ -737,7 +741,7 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
                                       max(__builtin_amdgcn_readlane(need, 47), __builtin_amdgcn_readlane(need, 63)));
             if (jmax == 0) break;
             iters += jmax;
-            // halo of this window: lane l < KD holds entry k0 - 1 - jb - l
+            // halo of this window: lane l < KD holds entry k0 - 1 - jb - l (its bytes too in window 0)
             uint32_t hq = 0;
             uint64_t hv0 = 0;
             uint32_t h2 = 0;
@@ -749,10 +753,10 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
                 }
             }
             // lanes without a candidate j of this window: halo lanes before the block start
-            // (k0 < jb + KD), or a bounded chain longer than KD ending inside the window
-            // (K <= KD needs no mask: the window is at most K steps long)
+            // (k0 < jb + wl), or a bounded chain ending inside a later window (a bounded
+            // K <= KD has a single window, at most K steps long, and needs no mask)
             const uint32_t ncw = nc > jb ? nc - jb : 0u;
-            const bool guard = k0 < jb + KD || (K > KD && K < jb + KD);
+            const bool guard = k0 < jb + wl || (K > W0 && K < jb + wl);
             if (jb == 0) {
                 const uint32_t h0 = (uint32_t)hv0, h1 = (uint32_t)(hv0 >> 32);
                 {   // sort check: the predecessor (lane - 1, lane 0: halo 0) has a smaller (bucket, position)
