@@ -26,21 +26,25 @@
 
 #include "../../include/dmx.h"
 
-#define IW 32768          // window = LDS ring
-#define IM (IW - 1)
+#define IW 32768          // window = LDS ring (stream mode; the indexed mode's ring is IWX)
+#ifndef DMX_IWX
+#define DMX_IWX 16384     // indexed mode: a 16 KiB ring, older sources read back from HBM
+#endif
+#define IWX DMX_IWX
 #define IFB 10            // first-level table bits
-#define IFLUSH 16384      // stream mode: flush to HBM every IFLUSH bytes
+#define IFLUSH 16384      // stream mode: flush to HBM every IFLUSH bytes (half the ring)
 
 struct ITable {
-    uint16_t fast[1 << IFB];   // sym << 4 | len; ISLOW = code longer than IFB (or none)
+    uint32_t fast[1 << IFB];   // first-level entries (format: "Table entries" below)
     uint16_t first[16];        // first canonical code of each length
     uint16_t cnt[16];
     uint16_t offs[16];         // index into sym[] of the first symbol of each length
     uint16_t sym[288];         // symbols sorted by (length, symbol)
 };
 
+template <uint32_t W>
 struct InfLDS {
-    uint8_t win[IW];
+    uint8_t win[W];
     ITable lt, dt;
     uint8_t len[320];
     uint8_t seq[320];
@@ -52,31 +56,47 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t v) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Bit reader.  Coordinates are relative to the dword-aligned address at or below z, so the
-// fast refill is one aligned scalar dword load; words that are not wholly inside the
-// stream go through the byte path (zeros past the end, counted as overrun).
+// Bit reader.  Coordinates are relative to the dword-aligned address at or below z.  The
+// stream is staged in two VGPRs, one dword per lane: vcur holds words wb + lane, vnxt words
+// wb + 64 + lane, so a refill is one v_readlane; when the reader passes into vnxt the pair
+// advances and the load of the next 256 bytes is issued, 64 refills before it is needed.
+// Words that are not wholly inside the stream are assembled from bytes (zeros past the end).
 // ---------------------------------------------------------------------------------------
-typedef __attribute__((address_space(4))) const uint32_t cu32;   // constant space: scalar loads
+// global-space views: plain loads, not flat ones (a flat load counts in lgkmcnt too, so every
+// LDS wait would also wait for the stream prefetch)
+typedef __attribute__((address_space(1))) const uint8_t gu8;
+typedef __attribute__((address_space(1))) const uint32_t gu32;
 
 struct IBits {
-    cu32* w;
-    const uint8_t* zb;     // aligned base as bytes
+    gu8* zb;               // aligned base as bytes
     uint32_t lo, hi;       // valid byte range [lo, hi) relative to zb
-    uint32_t wi, wfast;    // next word; words < wfast are wholly inside the stream
+    uint32_t wfast;        // words < wfast are wholly inside the stream
+    uint32_t wb;           // word index of vcur's lane 0 (a multiple of 64)
+    uint32_t vcur, vnxt;   // per lane: word wb + lane, word wb + 64 + lane
+    uint32_t wi;           // next word
     uint32_t bc;
     uint64_t bb;
-    bool over;
 };
 
-__device__ __forceinline__ uint32_t ib_word(IBits& r, uint32_t wi) {
-    if (wi < r.wfast) return r.w[wi];
+__device__ __forceinline__ uint32_t ib_vload(const IBits& r, uint32_t w0) {   // word w0 + lane
+    const uint32_t wi = w0 + __lane_id();
+    if (wi < r.wfast) return reinterpret_cast<gu32*>(r.zb)[wi];
     uint32_t v = 0;
     for (uint32_t j = 0; j < 4; j++) {
         const uint32_t b = wi * 4 + j;
         if (b >= r.lo && b < r.hi) v |= (uint32_t)r.zb[b] << (8 * j);
     }
-    if (wi * 4 >= r.hi + 8) r.over = true;
-    return rfl(v);
+    return v;
+}
+__device__ __forceinline__ uint32_t ib_word(IBits& r, uint32_t wi) {   // wi: sequential from the seek
+    uint32_t k = wi - r.wb;
+    if (k >= 64) {
+        r.vcur = r.vnxt;
+        r.wb += 64;
+        r.vnxt = ib_vload(r, r.wb + 64);
+        k -= 64;
+    }
+    return __builtin_amdgcn_readlane(r.vcur, k);
 }
 __device__ __forceinline__ void ib_refill(IBits& r) {   // afterwards bc >= 32
     if (r.bc <= 32) {
@@ -85,22 +105,26 @@ __device__ __forceinline__ void ib_refill(IBits& r) {   // afterwards bc >= 32
         r.bc += 32;
     }
 }
+// a word read that starts 8 or more bytes past the end of the stream (word wi - 1 was the last read)
+__device__ __forceinline__ bool ib_over(const IBits& r) { return (uint64_t)r.wi * 4 >= (uint64_t)r.hi + 12; }
 __device__ __forceinline__ void ib_seek(IBits& r, uint64_t bit) {   // bit: relative to z
     const uint64_t ab = bit + (uint64_t)r.lo * 8;
     r.wi = (uint32_t)(ab >> 5);
+    r.wb = r.wi & ~63u;
+    r.vcur = ib_vload(r, r.wb);
+    r.vnxt = ib_vload(r, r.wb + 64);
     r.bb = (uint64_t)ib_word(r, r.wi) >> (ab & 31);
     r.bc = 32 - (uint32_t)(ab & 31);
     r.wi++;
 }
 __device__ __forceinline__ void ib_init(IBits& r, const uint8_t* z, uint64_t zbytes) {
     const uintptr_t a = (uintptr_t)z;
-    r.zb = (const uint8_t*)(a & ~(uintptr_t)3);
-    r.w = (cu32*)r.zb;
+    r.zb = (gu8*)(a & ~(uintptr_t)3);
     r.lo = (uint32_t)(a & 3);
     r.hi = r.lo + (uint32_t)zbytes;
     r.wfast = r.hi >> 2;
-    r.over = false;
-    r.wi = 0;
+    r.wi = r.wb = 0;
+    r.vcur = r.vnxt = 0;
     r.bb = 0;
     r.bc = 0;
 }
@@ -119,17 +143,52 @@ __device__ __forceinline__ uint64_t ib_bytepos(const IBits& r) {   // after ib_a
     return (uint64_t)r.wi * 4 - r.bc / 8 - r.lo;
 }
 
+#define ISLOW 0xFFFFu
+
+// DEFLATE length / distance bases by arithmetic (RFC 1951 3.2.5), no table loads.
+__device__ __forceinline__ uint32_t len_extra(uint32_t li) { return li < 8 || li == 28 ? 0 : (li - 4) >> 2; }
+__device__ __forceinline__ uint32_t len_base(uint32_t li) {
+    return li < 8 ? li + 3 : li == 28 ? 258 : ((4 + (li & 3)) << ((li - 4) >> 2)) + 3;
+}
+__device__ __forceinline__ uint32_t dist_extra(uint32_t d) { return d < 4 ? 0 : (d - 2) >> 1; }
+__device__ __forceinline__ uint32_t dist_base(uint32_t d) { return d < 4 ? d + 1 : ((2 + (d & 1)) << ((d - 2) >> 1)) + 1; }
+
+// Table entries (32-bit).  The symbol loop looks its codes up in 1024-entry tables held in 16
+// VGPRs (entry x in lane x & 63 of register x >> 6: an indexed v_mov + v_readlane, no LDS round
+// trip), with the length / distance base and extra-bit count resolved into the entry:
+//   literal/length: literal  sym << 8 | clen                      (< 0x80000000)
+//                   length   0x80000000 | base << 16 | extra << 4 | clen
+//                   EOB      0xC0000000 | clen;  invalid (286, 287) 0xE0000000 | clen
+//   distance:       base << 16 | extra << 4 | clen;  IVBAD invalid (30, 31)
+//   both:           IVSLOW: a code longer than IFB bits (or none) -- the canonical slow path
+#define IVSLOW 0xFFFFFFFFu
+#define IVBAD 0xFFFFFFFEu
+__device__ __forceinline__ uint32_t iv_ll(uint32_t e) {   // from a sym << 4 | clen entry
+    if (e == ISLOW) return IVSLOW;
+    const uint32_t sym = e >> 4, l = e & 15u;
+    if (sym < 256) return (sym << 8) | l;
+    if (sym == 256) return 0xC0000000u | l;
+    const uint32_t li = sym - 257;
+    if (li >= 29) return 0xE0000000u | l;
+    return 0x80000000u | (len_base(li) << 16) | (len_extra(li) << 4) | l;
+}
+__device__ __forceinline__ uint32_t iv_d(uint32_t e) {
+    if (e == ISLOW) return IVSLOW;
+    const uint32_t ds = e >> 4;
+    if (ds >= 30) return IVBAD;
+    return (dist_base(ds) << 16) | (dist_extra(ds) << 4) | (e & 15u);
+}
+
 // ---------------------------------------------------------------------------------------
 // Huffman tables.  Lane l (1..15) owns code length l: it counts its symbols, then assigns
-// their canonical codes in symbol order and fills their first-level entries.  Entries are
-// sym << 4 | len; ISLOW marks a code longer than IFB bits (or no code), so "literal" is the
-// single test e < 256 << 4.  Returns 0 complete, 1 incomplete, -1 over-subscribed.
+// their canonical codes in symbol order and fills their first-level entries, in the 32-bit
+// format above (DIST: a distance table; otherwise literal/length, which also serves the code
+// length code: its symbols 0..18 take the literal form); IVSLOW marks a code longer than IFB
+// bits (or no code).  Returns 0 complete, 1 incomplete, -1 over-subscribed.
 // ---------------------------------------------------------------------------------------
-#define ISLOW 0xFFFFu
-#define ILIT (256u << 4)
-
-__device__ __forceinline__ int itable_build(InfLDS& S, ITable& T, int n, uint32_t lane) {
-    for (int k = (int)lane; k < (1 << IFB); k += 64) T.fast[k] = (uint16_t)ISLOW;
+template <bool DIST, uint32_t W>
+__device__ __forceinline__ int itable_build(InfLDS<W>& S, ITable& T, int n, uint32_t lane) {
+    for (int k = (int)lane; k < (1 << IFB); k += 64) T.fast[k] = IVSLOW;
     uint32_t c = 0;
     if (lane >= 1 && lane < 16)
         for (int s = 0; s < n; s++) c += S.len[s] == lane;
@@ -160,7 +219,8 @@ __device__ __forceinline__ int itable_build(InfLDS& S, ITable& T, int n, uint32_
             T.sym[offl + k] = (uint16_t)s;
             if (lane <= IFB) {
                 const uint32_t rv = __brev(firstl + k) >> (32 - lane);
-                const uint16_t e = (uint16_t)((s << 4) | lane);
+                const uint32_t e16 = ((uint32_t)s << 4) | lane;
+                const uint32_t e = DIST ? iv_d(e16) : iv_ll(e16);
                 for (uint32_t j = 0; j < (1u << (IFB - lane)); j++) T.fast[rv | (j << lane)] = e;
             }
             k++;
@@ -181,18 +241,11 @@ __device__ __forceinline__ uint32_t ientry_slow(const IBits& r, const ITable& T)
     }
     return ISLOW;
 }
-__device__ __forceinline__ uint32_t ientry(const IBits& r, const ITable& T) {
+// the code length code (symbols 0..18, in the literal form): sym << 4 | len, or ISLOW
+__device__ __forceinline__ uint32_t ientry_cl(const IBits& r, const ITable& T) {
     const uint32_t e = rfl(T.fast[ib_peek(r, IFB)]);
-    return e != ISLOW ? e : ientry_slow(r, T);
+    return e != IVSLOW ? ((e >> 8) << 4) | (e & 15u) : ientry_slow(r, T);
 }
-
-// DEFLATE length / distance bases by arithmetic (RFC 1951 3.2.5), no table loads.
-__device__ __forceinline__ uint32_t len_extra(uint32_t li) { return li < 8 || li == 28 ? 0 : (li - 4) >> 2; }
-__device__ __forceinline__ uint32_t len_base(uint32_t li) {
-    return li < 8 ? li + 3 : li == 28 ? 258 : ((4 + (li & 3)) << ((li - 4) >> 2)) + 3;
-}
-__device__ __forceinline__ uint32_t dist_extra(uint32_t d) { return d < 4 ? 0 : (d - 2) >> 1; }
-__device__ __forceinline__ uint32_t dist_base(uint32_t d) { return d < 4 ? d + 1 : ((2 + (d & 1)) << ((d - 2) >> 1)) + 1; }
 
 __constant__ uint8_t c_iclorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
@@ -200,7 +253,21 @@ __constant__ uint8_t c_iclorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 
 // Output.  Positions are 32-bit and relative to ob (a multiple of IW, so the window index
 // of a position is pos & IM); stream mode moves ob forward as it flushes.
 // ---------------------------------------------------------------------------------------
+// DMX_INF_STAMPS (diagnostic builds only): per-workgroup cycle totals of the decode phases
+#ifdef DMX_INF_STAMPS
+#define INF_NST 8
+__device__ unsigned long long dmx_inf_st[1 << 16][INF_NST];
+#define IST_NOW() __builtin_amdgcn_s_memtime()
+#define IST_ADD(o, k, v) ((o).st[k] += (v))
+#else
+#define IST_NOW() 0ull
+#define IST_ADD(o, k, v) ((void)0)
+#endif
+
 struct IOut {
+#ifdef DMX_INF_STAMPS
+    unsigned long long st[INF_NST];   // 0 header + tables, 1 symbol loop, 2 flushes, 3 matches, 4 far matches, 5 match bytes, 6 blocks
+#endif
     uint8_t* out;     // + base + ob = position 0
     uint64_t base, ob, cap;   // cap: absolute output capacity
     uint32_t op, fl;  // produced / flushed (relative)
@@ -218,9 +285,11 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
     return v;
 }
 
-// Write window bytes [fl, upto) to HBM (upto - fl <= IW).  ADLER: fold them into (a, b).
-template <bool ADLER>
-__device__ __forceinline__ void io_flush(InfLDS& S, IOut& o, uint32_t upto, uint32_t lane) {
+// Write window bytes [fl, upto) to HBM (upto - fl <= W).  ADLER: fold them into (a, b).
+template <bool ADLER, uint32_t W>
+__device__ __forceinline__ void io_flush(InfLDS<W>& S, IOut& o, uint32_t upto, uint32_t lane) {
+    constexpr uint32_t IM = W - 1;
+    [[maybe_unused]] const unsigned long long ts0 = IST_NOW();
     __syncthreads();
     uint8_t* dst = o.out + o.base + o.ob;
     const uint32_t n = upto - o.fl;
@@ -283,19 +352,269 @@ __device__ __forceinline__ void io_flush(InfLDS& S, IOut& o, uint32_t upto, uint
         o.b = rfl((uint32_t)b2);
     }
     o.fl = upto;
-    if (o.fl >= IRENORM) {   // keep relative positions small (ob stays a multiple of IW)
+    __builtin_amdgcn_s_waitcnt(0);   // the stores are done: far-match reads see them
+    if (o.fl >= IRENORM) {   // keep relative positions small (ob stays a multiple of W)
         o.ob += IRENORM;
         o.op -= IRENORM;
         o.fl -= IRENORM;
     }
     __syncthreads();
+    IST_ADD(o, 2, IST_NOW() - ts0);
+}
+
+// LDS byte address of a __shared__ object (ds_* instructions address LDS from 0)
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// ---------------------------------------------------------------------------------------
+// The symbol loop's common path, hand-scheduled.  Compiled code for this state machine spent
+// ~100 instructions a token (the structurizer's branch flags, copies of the stream registers
+// that waited for their prefetch); this one spends ~20 on a literal and ~60 on a match.
+// In SGPRs: the 64-bit bit buffer (s[94:95]), bc, wi, op; the two tables come from LDS into
+// v96..v111 (literal/length) and v112..v127 (distance) and are read by an indexed v_mov
+// (s_set_gpr_idx_on) + v_readlane.  A literal is one ds_write_b8 (every lane stores the same
+// byte); a match inside the ring with distance >= length or >= 64 is a copy of 64 bytes a
+// round (lane t: byte src + t, read before the round's writes).  Returns at the first event
+// it leaves to the caller, with nothing of the current token consumed unless noted:
+//   IX_SYM   a long, end-of-block or invalid literal/length code
+//   IX_SEG   a refill at a token start that needs a stream segment it does not rotate into
+//            (the segment after next is not wholly inside the stream)
+//   IX_LIM   op >= lim at a literal or length (flush, or the capacity limit)
+//   IX_DIST  length decoded into len; the distance code is long or invalid
+//   IX_MATCH len and dist decoded: an error, a source older than the ring, or a short period
+// Hazards: a lane select written by SALU is 4+ instructions old at each v_readlane (s_nop 3
+// where it is not); the stream prefetch is waited for before it is read and before return;
+// m0 (written by s_set_gpr_idx_on) is restored.
+// ---------------------------------------------------------------------------------------
+#define IX_SYM 1u
+#define IX_SEG 2u
+#define IX_LIM 3u
+#define IX_DIST 4u
+#define IX_MATCH 5u
+
+template <uint32_t W>
+__device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t lim, uint32_t capr, uint32_t dfl,
+                                             uint32_t tla, uint32_t tda, uint32_t lane, uint32_t& len,
+                                             uint32_t& dist) {
+    uint32_t ex;
+    const int32_t wrl = (int32_t)r.wfast - 192;   // rotate while the new segment is wholly inside
+    const uint64_t zb = (uint64_t)(uintptr_t)r.zb;
+    asm volatile(
+        "s_mov_b64 s[94:95], %[bb]\n"
+        "s_mov_b32 s89, m0\n"
+        "ds_read_b32 v96, %[tla]\n"
+        "ds_read_b32 v97, %[tla] offset:256\n"
+        "ds_read_b32 v98, %[tla] offset:512\n"
+        "ds_read_b32 v99, %[tla] offset:768\n"
+        "ds_read_b32 v100, %[tla] offset:1024\n"
+        "ds_read_b32 v101, %[tla] offset:1280\n"
+        "ds_read_b32 v102, %[tla] offset:1536\n"
+        "ds_read_b32 v103, %[tla] offset:1792\n"
+        "ds_read_b32 v104, %[tla] offset:2048\n"
+        "ds_read_b32 v105, %[tla] offset:2304\n"
+        "ds_read_b32 v106, %[tla] offset:2560\n"
+        "ds_read_b32 v107, %[tla] offset:2816\n"
+        "ds_read_b32 v108, %[tla] offset:3072\n"
+        "ds_read_b32 v109, %[tla] offset:3328\n"
+        "ds_read_b32 v110, %[tla] offset:3584\n"
+        "ds_read_b32 v111, %[tla] offset:3840\n"
+        "ds_read_b32 v112, %[tda]\n"
+        "ds_read_b32 v113, %[tda] offset:256\n"
+        "ds_read_b32 v114, %[tda] offset:512\n"
+        "ds_read_b32 v115, %[tda] offset:768\n"
+        "ds_read_b32 v116, %[tda] offset:1024\n"
+        "ds_read_b32 v117, %[tda] offset:1280\n"
+        "ds_read_b32 v118, %[tda] offset:1536\n"
+        "ds_read_b32 v119, %[tda] offset:1792\n"
+        "ds_read_b32 v120, %[tda] offset:2048\n"
+        "ds_read_b32 v121, %[tda] offset:2304\n"
+        "ds_read_b32 v122, %[tda] offset:2560\n"
+        "ds_read_b32 v123, %[tda] offset:2816\n"
+        "ds_read_b32 v124, %[tda] offset:3072\n"
+        "ds_read_b32 v125, %[tda] offset:3328\n"
+        "ds_read_b32 v126, %[tda] offset:3584\n"
+        "ds_read_b32 v127, %[tda] offset:3840\n"
+        "s_mov_b32 s97, 0\n"
+        "s_mov_b32 %[len], 0\n"
+        "s_mov_b32 %[dist], 0\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        // ---- token start: refill (rotating the stream segments when the word is in vnxt)
+        "L_tok%=:\n"
+        "s_cmp_gt_u32 %[bc], 32\n"
+        "s_cbranch_scc1 L_look%=\n"
+        "s_sub_u32 s98, %[wi], %[wb]\n"
+        "s_cmp_lt_u32 s98, 64\n"
+        "s_cbranch_scc1 L_rd%=\n"
+        "s_cmp_le_i32 %[wb], %[wrl]\n"
+        "s_cbranch_scc0 L_xseg%=\n"
+        "s_waitcnt vmcnt(0)\n"
+        "v_mov_b32 %[vc], %[vn]\n"
+        "s_add_u32 %[wb], %[wb], 64\n"
+        "s_sub_u32 s98, s98, 64\n"
+        "s_add_u32 s99, %[wb], 64\n"
+        "v_add_lshl_u32 v129, %[lane], s99, 2\n"
+        "global_load_dword %[vn], v129, %[zb]\n"
+        "L_rd%=:\n"
+        "s_nop 3\n"
+        "v_readlane_b32 s96, %[vc], s98\n"
+        "s_lshl_b64 s[92:93], s[96:97], %[bc]\n"
+        "s_or_b64 s[94:95], s[94:95], s[92:93]\n"
+        "s_add_u32 %[wi], %[wi], 1\n"
+        "s_add_u32 %[bc], %[bc], 32\n"
+        // ---- literal/length lookup
+        "L_look%=:\n"
+        "s_bfe_u32 s98, s94, 0x40006\n"
+        "s_set_gpr_idx_on s98, gpr_idx(SRC0)\n"
+        "v_mov_b32 v128, v96\n"
+        "s_set_gpr_idx_off\n"
+        "v_readlane_b32 s99, v128, s94\n"
+        "s_cmp_lt_i32 s99, 0\n"
+        "s_cbranch_scc1 L_nl%=\n"
+        // literal
+        "s_cmp_ge_u32 %[op], %[lim]\n"
+        "s_cbranch_scc1 L_xlim%=\n"
+        "s_and_b32 s98, s99, 15\n"
+        "s_lshr_b64 s[94:95], s[94:95], s98\n"
+        "s_sub_u32 %[bc], %[bc], s98\n"
+        "s_lshr_b32 s99, s99, 8\n"
+        "s_and_b32 s98, %[op], %[im]\n"
+        "v_mov_b32 v129, s98\n"
+        "v_mov_b32 v130, s99\n"
+        "ds_write_b8 v129, v130\n"
+        "s_add_u32 %[op], %[op], 1\n"
+        "s_branch L_tok%=\n"
+        // ---- length
+        "L_nl%=:\n"
+        "s_cmp_lt_u32 s99, 0xC0000000\n"
+        "s_cbranch_scc0 L_xsym%=\n"
+        "s_cmp_ge_u32 %[op], %[lim]\n"
+        "s_cbranch_scc1 L_xlim%=\n"
+        "s_and_b32 s98, s99, 15\n"
+        "s_lshr_b64 s[92:93], s[94:95], s98\n"
+        "s_bfe_u32 s90, s99, 0x40004\n"
+        "s_bfm_b32 s91, s90, 0\n"
+        "s_and_b32 s91, s92, s91\n"
+        "s_bfe_u32 %[len], s99, 0x90010\n"
+        "s_add_u32 %[len], %[len], s91\n"
+        "s_add_u32 s98, s98, s90\n"
+        "s_lshr_b64 s[94:95], s[94:95], s98\n"
+        "s_sub_u32 %[bc], %[bc], s98\n"
+        // refill inside the token: the word is in vcur or vnxt
+        "s_cmp_gt_u32 %[bc], 32\n"
+        "s_cbranch_scc1 L_dl%=\n"
+        "s_sub_u32 s98, %[wi], %[wb]\n"
+        "s_cmp_lt_u32 s98, 64\n"
+        "s_cbranch_scc0 L_rn%=\n"
+        "s_nop 3\n"
+        "v_readlane_b32 s96, %[vc], s98\n"
+        "s_branch L_rdd%=\n"
+        "L_rn%=:\n"
+        "s_sub_u32 s98, s98, 64\n"
+        "s_waitcnt vmcnt(0)\n"
+        "s_nop 3\n"
+        "v_readlane_b32 s96, %[vn], s98\n"
+        "L_rdd%=:\n"
+        "s_lshl_b64 s[92:93], s[96:97], %[bc]\n"
+        "s_or_b64 s[94:95], s[94:95], s[92:93]\n"
+        "s_add_u32 %[wi], %[wi], 1\n"
+        "s_add_u32 %[bc], %[bc], 32\n"
+        // ---- distance
+        "L_dl%=:\n"
+        "s_bfe_u32 s98, s94, 0x40006\n"
+        "s_set_gpr_idx_on s98, gpr_idx(SRC0)\n"
+        "v_mov_b32 v128, v112\n"
+        "s_set_gpr_idx_off\n"
+        "v_readlane_b32 s99, v128, s94\n"
+        "s_cmp_ge_u32 s99, 0xFFFFFFFE\n"
+        "s_cbranch_scc1 L_xdist%=\n"
+        "s_and_b32 s98, s99, 15\n"
+        "s_lshr_b64 s[92:93], s[94:95], s98\n"
+        "s_bfe_u32 s90, s99, 0x40004\n"
+        "s_bfm_b32 s91, s90, 0\n"
+        "s_and_b32 s91, s92, s91\n"
+        "s_lshr_b32 %[dist], s99, 16\n"
+        "s_add_u32 %[dist], %[dist], s91\n"
+        "s_add_u32 s98, s98, s90\n"
+        "s_lshr_b64 s[94:95], s[94:95], s98\n"
+        "s_sub_u32 %[bc], %[bc], s98\n"
+        // ---- the copy, or the caller for errors, far sources and short periods
+        "s_add_u32 s98, %[op], %[dfl]\n"
+        "s_cmp_gt_u32 %[dist], s98\n"
+        "s_cbranch_scc1 L_xmatch%=\n"
+        "s_sub_u32 s98, %[capr], %[op]\n"
+        "s_cmp_gt_u32 %[len], s98\n"
+        "s_cbranch_scc1 L_xmatch%=\n"
+        "s_cmp_gt_u32 %[dist], %[wmax]\n"
+        "s_cbranch_scc1 L_xmatch%=\n"
+        "s_cmp_ge_u32 %[dist], %[len]\n"
+        "s_cbranch_scc1 L_cp%=\n"
+        "s_cmp_lt_u32 %[dist], 64\n"
+        "s_cbranch_scc1 L_xmatch%=\n"
+        "L_cp%=:\n"
+        "s_sub_u32 s98, %[op], %[dist]\n"
+        "v_add_u32 v129, s98, %[lane]\n"
+        "v_add_u32 v130, %[op], %[lane]\n"
+        "s_mov_b32 s99, %[len]\n"
+        "L_cr%=:\n"
+        "v_cmp_gt_u32 vcc, s99, %[lane]\n"
+        "s_and_saveexec_b64 s[92:93], vcc\n"
+        "v_and_b32 v131, %[im], v129\n"
+        "ds_read_u8 v131, v131\n"
+        "v_and_b32 v128, %[im], v130\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "ds_write_b8 v128, v131\n"
+        "s_mov_b64 exec, s[92:93]\n"
+        "s_sub_u32 s99, s99, 64\n"
+        "s_cmp_gt_i32 s99, 0\n"
+        "s_cbranch_scc0 L_cd%=\n"
+        "v_add_u32 v129, 64, v129\n"
+        "v_add_u32 v130, 64, v130\n"
+        "s_branch L_cr%=\n"
+        "L_cd%=:\n"
+        "s_add_u32 %[op], %[op], %[len]\n"
+        "s_branch L_tok%=\n"
+        // ---- exits
+        "L_xsym%=:\n"
+        "s_mov_b32 %[ex], 1\n"
+        "s_branch L_end%=\n"
+        "L_xseg%=:\n"
+        "s_mov_b32 %[ex], 2\n"
+        "s_branch L_end%=\n"
+        "L_xlim%=:\n"
+        "s_mov_b32 %[ex], 3\n"
+        "s_branch L_end%=\n"
+        "L_xdist%=:\n"
+        "s_mov_b32 %[ex], 4\n"
+        "s_branch L_end%=\n"
+        "L_xmatch%=:\n"
+        "s_mov_b32 %[ex], 5\n"
+        "L_end%=:\n"
+        "s_waitcnt vmcnt(0) lgkmcnt(0)\n"
+        "s_mov_b32 m0, s89\n"
+        "s_mov_b64 %[bb], s[94:95]\n"
+        : [bb] "+s"(r.bb), [bc] "+s"(r.bc), [wi] "+s"(r.wi), [wb] "+s"(r.wb), [vc] "+v"(r.vcur),
+          [vn] "+v"(r.vnxt), [op] "+s"(op), [ex] "=&s"(ex), [len] "=&s"(len), [dist] "=&s"(dist)
+        : [lim] "s"(lim), [capr] "s"(capr), [dfl] "s"(dfl), [tla] "v"(tla), [tda] "v"(tda), [lane] "v"(lane),
+          [wrl] "s"(wrl), [zb] "s"(zb), [im] "n"(W - 1), [wmax] "n"(W)
+        : "memory", "vcc", "scc", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99",
+          "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108",
+          "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120",
+          "v121", "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131");
+    return ex;
 }
 
 // ---------------------------------------------------------------------------------------
 // One DEFLATE block at the reader.  Returns 0 / -E_*; last = BFINAL.
 // ---------------------------------------------------------------------------------------
-template <bool RING>
-__device__ __forceinline__ int iblock(InfLDS& S, IBits& r, IOut& o, uint32_t lane, bool& last) {
+// RING: flush to HBM every half ring (ADLER: folding the Adler-32 sums; the stream mode);
+// otherwise the whole output stays in the window.  W < 32 KiB: matches farther than the ring
+// read their source from the output already flushed to HBM.
+template <bool RING, bool ADLER, uint32_t W>
+__device__ __forceinline__ int iblock(InfLDS<W>& S, IBits& r, IOut& o, uint32_t lane, bool& last) {
+    constexpr uint32_t IM = W - 1, FL = W / 2;
+    [[maybe_unused]] const unsigned long long ts0 = IST_NOW();
+    IST_ADD(o, 6, 1);
     last = ib_bits(r, 1) != 0;
     const uint32_t bt = ib_bits(r, 2);
     if (bt == 0) {   // stored
@@ -305,10 +624,10 @@ __device__ __forceinline__ int iblock(InfLDS& S, IBits& r, IOut& o, uint32_t lan
         if (len > io_caprel(o) - o.op) return -(int)E_SZ;
         const uint64_t src = ib_bytepos(r);   // relative to z
         if (src + len + r.lo > r.hi) return -(int)E_LEN;
-        const uint8_t* zs = r.zb + r.lo + src;
-        for (uint32_t c0 = 0; c0 < len; c0 += IFLUSH) {   // pieces the ring can hold
-            if (RING && o.op - o.fl > IW - IFLUSH) io_flush<true>(S, o, o.op, lane);
-            const uint32_t ce = min(len, c0 + (uint32_t)IFLUSH);
+        gu8* zs = r.zb + r.lo + src;
+        for (uint32_t c0 = 0; c0 < len; c0 += FL) {   // pieces the ring can hold
+            if (RING && o.op - o.fl > W - FL) io_flush<ADLER>(S, o, o.op, lane);
+            const uint32_t ce = min(len, c0 + FL);
             for (uint32_t j = c0 + lane; j < ce; j += 64) S.win[(o.op + (j - c0)) & IM] = zs[j];
             o.op += ce - c0;
         }
@@ -333,12 +652,12 @@ __device__ __forceinline__ int iblock(InfLDS& S, IBits& r, IOut& o, uint32_t lan
             if (lane == 0) S.len[c_iclorder[k]] = (uint8_t)v;
         }
         __syncthreads();
-        if (itable_build(S, S.lt, 19, lane) != 0) return -(int)E_HUFAMB;
+        if (itable_build<false>(S, S.lt, 19, lane) != 0) return -(int)E_HUFAMB;
         uint32_t prev = 0;
         int idx = 0, err = 0;
         while (idx < nlen + ndist) {
             ib_refill(r);
-            const uint32_t e = ientry(r, S.lt);
+            const uint32_t e = ientry_cl(r, S.lt);
             if (e == ISLOW) { err = -(int)E_HUFINV; break; }
             ib_drop(r, e & 15u);
             const uint32_t sy = e >> 4;
@@ -370,59 +689,96 @@ __device__ __forceinline__ int iblock(InfLDS& S, IBits& r, IOut& o, uint32_t lan
     // literal/length table from seq[0, nlen), distance table from seq[nlen, nlen + ndist)
     for (int s = (int)lane; s < 288; s += 64) S.len[s] = s < nlen ? S.seq[s] : 0;
     __syncthreads();
-    int e = itable_build(S, S.lt, nlen, lane);
+    int e = itable_build<false>(S, S.lt, nlen, lane);
     if (e < 0 || (e > 0 && bt == 2 && rfl(S.lt.offs[15] + S.lt.cnt[15]) != 1)) return -(int)E_HUFAMB;
     for (int s = (int)lane; s < 32; s += 64) S.len[s] = s < ndist ? S.seq[nlen + s] : 0;
     __syncthreads();
-    e = itable_build(S, S.dt, ndist, lane);
+    e = itable_build<true>(S, S.dt, ndist, lane);
     if (e < 0 || (e > 0 && bt == 2 && rfl(S.dt.offs[15] + S.dt.cnt[15]) > 1)) return -(int)E_HUFAMB;
 
-    // symbols.  The inner loop is the literal run: one lookup, one compare, one byte store.
+    // symbols: the common path in isym_run (literals, lengths and distances with table codes,
+    // matches inside the ring without overlap or with a period >= 64); the rest here.
     uint32_t op = o.op;
     uint32_t capr = io_caprel(o);
     int err = 0;
+    [[maybe_unused]] const unsigned long long ts1 = IST_NOW();
+    IST_ADD(o, 0, ts1 - ts0);
+    if (lds_addr(S.win) != 0) return -(int)E_RANGE;   // isym_run addresses the ring from LDS 0
+    const uint32_t tla = lds_addr(S.lt.fast) + lane * 4, tda = lds_addr(S.dt.fast) + lane * 4;
+    const uint32_t dfl = o.ob != 0 ? 0x40000000u : 0u;   // stream mode: sources before ob exist
     for (;;) {
-        const uint32_t lim = RING ? min(capr, o.fl + IFLUSH) : capr;
-        uint32_t en;
-        for (;;) {
+        const uint32_t lim = RING ? min(capr, o.fl + FL) : capr;
+        uint32_t len, dist;
+        const uint32_t ex = isym_run<W>(r, op, lim, capr, dfl, tla, tda, lane, len, dist);
+        if (ex == IX_SEG) {   // a refill at a token start that the run does not rotate into
             ib_refill(r);
-            en = rfl(S.lt.fast[ib_peek(r, IFB)]);
-            if (en >= ILIT || op >= lim) break;
-            ib_drop(r, en & 15u);
-            if (lane == 0) S.win[op & IM] = (uint8_t)(en >> 4);
-            op++;
+            continue;
         }
-        if (RING && op - o.fl >= IFLUSH) {
+        if (ex == IX_LIM && RING && op - o.fl >= FL) {
             o.op = op;
-            io_flush<true>(S, o, o.fl + IFLUSH, lane);
+            io_flush<ADLER>(S, o, o.fl + FL, lane);
             op = o.op;
             capr = io_caprel(o);
             continue;
         }
-        if (en == ISLOW) en = ientry_slow(r, S.lt);
-        if (en == ISLOW) { err = -(int)E_HUFINV; break; }
-        ib_drop(r, en & 15u);
-        const uint32_t sy = en >> 4;
-        if (sy < 256) {   // a literal at the capacity limit
-            if (op >= capr) { err = -(int)E_SZ; break; }
-            if (lane == 0) S.win[op & IM] = (uint8_t)sy;
-            op++;
-            continue;
+        uint32_t en = 0;
+        if (ex == IX_SYM || ex == IX_LIM) {   // one symbol the general way (nothing consumed)
+            ib_refill(r);
+            en = rfl(S.lt.fast[ib_peek(r, IFB)]);
+            if (en == IVSLOW) {
+                const uint32_t e16 = ientry_slow(r, S.lt);
+                if (e16 == ISLOW) { err = -(int)E_HUFINV; break; }
+                en = iv_ll(e16);
+            }
+            ib_drop(r, en & 15u);
+            if (en < 0x80000000u) {   // a literal: at the capacity limit, or a long code
+                if (op >= capr) { err = -(int)E_SZ; break; }
+                S.win[op & IM] = (uint8_t)(en >> 8);
+                op++;
+                continue;
+            }
+            if (en >= 0xC0000000u) {
+                if (en & 0x20000000u) err = -(int)E_HUFVAL;
+                break;   // end of block
+            }
+            const uint32_t lx = (en >> 4) & 15u;
+            len = ((en >> 16) & 0x1FFu) + ((uint32_t)r.bb & ((1u << lx) - 1));
+            ib_drop(r, lx);
         }
-        if (sy == 256) break;
-        const uint32_t li = sy - 257;
-        if (li >= 29) { err = -(int)E_HUFVAL; break; }
-        const uint32_t len = len_base(li) + ib_bits(r, len_extra(li));
-        ib_refill(r);
-        const uint32_t ed = ientry(r, S.dt);
-        const uint32_t ds = ed >> 4;
-        if (ed == ISLOW || ds >= 30) { err = -(int)E_HUFVAL; break; }
-        ib_drop(r, ed & 15u);
-        const uint32_t dist = dist_base(ds) + ib_bits(r, dist_extra(ds));
+        if (ex != IX_MATCH) {   // the distance the general way
+            ib_refill(r);
+            uint32_t ed = rfl(S.dt.fast[ib_peek(r, IFB)]);
+            if (ed >= IVBAD) {
+                const uint32_t e16 = ed == IVSLOW ? ientry_slow(r, S.dt) : ISLOW;
+                ed = e16 == ISLOW ? IVBAD : iv_d(e16);
+                if (ed == IVBAD) { err = -(int)E_HUFVAL; break; }
+            }
+            const uint32_t dc = ed & 15u, dx = (ed >> 4) & 15u;
+            dist = (ed >> 16) + ((uint32_t)(r.bb >> dc) & ((1u << dx) - 1));
+            ib_drop(r, dc + dx);
+        }
         if (o.ob == 0 && dist > op) { err = -(int)E_HUFDIS; break; }
         if (len > capr - op) { err = -(int)E_SZ; break; }
+        if (RING && op - o.fl >= FL) {   // half the ring is due before this match
+            o.op = op;
+            io_flush<ADLER>(S, o, o.fl + FL, lane);
+            op = o.op;
+            capr = io_caprel(o);
+        }
         const uint32_t src = op - dist;
-        if (dist >= 64 || dist >= len) {   // every read is of bytes written before its round
+        IST_ADD(o, 3, 1);
+        if (W < IW && dist > W) {
+            IST_ADD(o, 4, 1);
+            // older than the ring: from the output in HBM, flushed before this match (op - fl
+            // stays below W / 2 + 258, so every source byte lies below fl).  Agent-scope loads
+            // go to L2, past any vector-L1 copy of a line that was flushed in two pieces.
+            const uintptr_t g = (uintptr_t)(o.out + o.base + o.ob);
+            for (uint32_t t = lane; t < len; t += 64) {
+                const uintptr_t a = g + src + t;
+                const uint32_t w = __hip_atomic_load((gu32*)(a & ~(uintptr_t)3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                S.win[(op + t) & IM] = (uint8_t)(w >> (8 * (a & 3)));
+            }
+        } else if (dist >= 64 || dist >= len) {   // every read is of bytes written before its round
             for (uint32_t t = lane; t < len; t += 64) S.win[(op + t) & IM] = S.win[(src + t) & IM];
         } else {   // short period: byte t repeats byte t mod dist
             const float inv = 1.0f / (float)dist;
@@ -437,8 +793,9 @@ __device__ __forceinline__ int iblock(InfLDS& S, IBits& r, IOut& o, uint32_t lan
         op += len;
     }
     o.op = op;
+    IST_ADD(o, 1, IST_NOW() - ts1);
     if (err) return err;
-    if (r.over) return -(int)E_LEN;
+    if (ib_over(r)) return -(int)E_LEN;
     return 0;
 }
 
@@ -446,7 +803,7 @@ __global__ __launch_bounds__(64) void dmx_inflate_index_kernel(const uint8_t* __
                                                                const dmx_iblock* __restrict__ index,
                                                                uint8_t* __restrict__ out, uint64_t out_cap,
                                                                dmx_inflate_status* __restrict__ st) {
-    __shared__ InfLDS S;
+    __shared__ InfLDS<IWX> S;   // 16 KiB ring: 7 workgroups per CU (a 32 KiB window allowed 4)
     const uint32_t lane = threadIdx.x;
     IBits r;
     ib_init(r, z, zbytes);
@@ -454,6 +811,9 @@ __global__ __launch_bounds__(64) void dmx_inflate_index_kernel(const uint8_t* __
     const uint64_t off = rfl64(index[blockIdx.x].out_off);
     const uint32_t olen = rfl(index[blockIdx.x].out_len);
     IOut o;
+#ifdef DMX_INF_STAMPS
+    for (int k = 0; k < INF_NST; k++) o.st[k] = 0;
+#endif
     o.out = out;
     o.base = off;
     o.ob = 0;
@@ -468,23 +828,29 @@ __global__ __launch_bounds__(64) void dmx_inflate_index_kernel(const uint8_t* __
         ib_seek(r, bit);
         bool last = false;
         do {   // one sw block may be several DEFLATE blocks (DMX_F_SPLIT)
-            err = iblock<false>(S, r, o, lane, last);
+            err = iblock<true, false, IWX>(S, r, o, lane, last);
         } while (!err && o.op < olen && !last);
         if (!err && o.op != olen) err = -(int)E_SZ;
         if (!err) io_flush<false>(S, o, o.op, lane);
     }
     if (lane == 0 && err) atomicCAS(&st->status, 0, err);
     if (lane == 0 && !err) atomicAdd((unsigned long long*)&st->out_len, (unsigned long long)o.op);
+#ifdef DMX_INF_STAMPS
+    if (lane < INF_NST && blockIdx.x < (1u << 16)) dmx_inf_st[blockIdx.x][lane] = o.st[lane];
+#endif
 }
 
 __global__ __launch_bounds__(64) void dmx_inflate_stream_kernel(const uint8_t* __restrict__ z, uint64_t zbytes,
                                                                 uint8_t* __restrict__ out, uint64_t out_cap,
                                                                 dmx_inflate_status* __restrict__ st) {
-    __shared__ InfLDS S;
+    __shared__ InfLDS<IW> S;
     const uint32_t lane = threadIdx.x;
     IBits r;
     ib_init(r, z, zbytes);
     IOut o;
+#ifdef DMX_INF_STAMPS
+    for (int k = 0; k < INF_NST; k++) o.st[k] = 0;
+#endif
     o.out = out;
     o.base = 0;
     o.ob = 0;
@@ -505,14 +871,14 @@ __global__ __launch_bounds__(64) void dmx_inflate_stream_kernel(const uint8_t* _
     if (!err) {
         ib_seek(r, 16);
         bool last = false;
-        while (!err && !last) err = iblock<true>(S, r, o, lane, last);
+        while (!err && !last) err = iblock<true, true, IW>(S, r, o, lane, last);
     }
     if (!err) {
         io_flush<true>(S, o, o.op, lane);
         ib_drop(r, r.bc & 7);   // Adler-32 trailer, MSB first
         uint32_t want = 0;
         for (int k = 0; k < 4; k++) want = (want << 8) | ib_bits(r, 8);
-        if (r.over) err = -(int)E_LEN;
+        if (ib_over(r)) err = -(int)E_LEN;
         else if (((o.b << 16) | o.a) != want) err = -(int)E_ZADL32;
     }
     if (lane == 0) {
@@ -540,3 +906,11 @@ extern "C" int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_ibl
     if (hipGetLastError() != hipSuccess) return -(int)E_DEVICE;
     return 0;
 }
+
+#ifdef DMX_INF_STAMPS
+// diagnostic builds: copy the per-workgroup phase totals of the last indexed launch
+extern "C" int dmx_inflate_stamps(void* host, uint64_t bytes) {
+    if (bytes > sizeof(dmx_inf_st)) bytes = sizeof(dmx_inf_st);
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(dmx_inf_st), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
