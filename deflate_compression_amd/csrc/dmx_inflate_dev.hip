@@ -9,17 +9,18 @@
 //   * stream (dmx_inflate_stream_kernel): one workgroup decodes a whole zlib stream
 //     (header, blocks until BFINAL, Adler-32 check) -- any RFC 1950 stream, e.g. PNG IDAT.
 //
-// The decoder is wave-uniform and lives in scalar registers: the 64-bit bit buffer, the
-// stream word index and the output position are SGPRs (table entries come back through
-// readfirstlane), the stream is read with scalar loads, and the whole decode is one inlined
-// loop -- no calls, no scratch.  Lane 0 stores literals; a match is copied by the whole wave
-// from the periodic extension of its source (byte i of a match at distance d is the byte at
-// op - d + i mod d), so every lane reads data that existed before the match and a match of
-// up to 258 bytes is at most five independent LDS read/write rounds.  Output is assembled
-// in a 32 KiB LDS window and written to HBM in 16-byte-per-lane coalesced stores (stream
-// mode flushes every 16 KiB and folds the Adler-32 sums into the same pass).
-// Tables: 10-bit first-level lookup of 16-bit entries (symbol << 4 | code length); codes
-// longer than 10 bits take a canonical slow path (first code / count / offset per length).
+// The decoder is wave-uniform: the 64-bit bit buffer, the stream word index and the output
+// position are SGPRs; the compressed stream is staged in two VGPRs (one dword per lane, the
+// next 256 bytes prefetched), so a refill is a v_readlane.  The common path of the symbol loop
+// is hand-scheduled (isym_run): the literal/length and distance tables live in VGPRs during it
+// (an indexed v_mov + v_readlane per lookup, no LDS round trip), each entry carries its base
+// and is the s_bfe control of its own extra bits, a literal is one LDS byte store, and a match
+// is copied by the whole wave, 64 bytes a round (periodic sources by residue; sources older
+// than the ring from the output already flushed to HBM).  Output is assembled in an LDS ring
+// and written to HBM in 16-byte-per-lane coalesced stores every half ring (indexed mode: an
+// 8 KiB ring, so 8 workgroups fit a CU; stream mode: the 32 KiB window, folding the Adler-32
+// sums into the same pass).  Tables: 10-bit first level, built lane-parallel (ballot counts
+// and ranks); longer codes take a canonical slow path (first code / count / offset per length).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -28,7 +29,7 @@
 
 #define IW 32768          // window = LDS ring (stream mode; the indexed mode's ring is IWX)
 #ifndef DMX_IWX
-#define DMX_IWX 16384     // indexed mode: a 16 KiB ring, older sources read back from HBM
+#define DMX_IWX 8192      // indexed mode: an 8 KiB ring, older sources read back from HBM
 #endif
 #define IWX DMX_IWX
 #define IFB 10            // first-level table bits
@@ -155,75 +156,117 @@ __device__ __forceinline__ uint32_t dist_base(uint32_t d) { return d < 4 ? d + 1
 
 // Table entries (32-bit).  The symbol loop looks its codes up in 1024-entry tables held in 16
 // VGPRs (entry x in lane x & 63 of register x >> 6: an indexed v_mov + v_readlane, no LDS round
-// trip), with the length / distance base and extra-bit count resolved into the entry:
-//   literal/length: literal  sym << 8 | clen                      (< 0x80000000)
-//                   length   0x80000000 | base << 16 | extra << 4 | clen
-//                   EOB      0xC0000000 | clen;  invalid (286, 287) 0xE0000000 | clen
-//   distance:       base << 16 | extra << 4 | clen;  IVBAD invalid (30, 31)
+// trip).  A length or distance entry is laid out so that it is itself the s_bfe control that
+// extracts its extra bits from the bit buffer: bits [4:0] the code length (the field's offset),
+// [22:16] the extra-bit count (its width); [12:8] code + extra bits (the bits to drop).
+//   literal/length: literal  sym << 16 | clen                      (bit 15 clear)
+//                   length   base << 23 | extra << 16 | 0x8000 | (clen + extra) << 8 | clen
+//                   EOB      0xC000 | clen;  invalid (286, 287) 0xE000 | clen  (bit 14 set)
+//   distance:       m << 28 | extra << 16 | (clen + extra) << 8 | clen, where base - 1 = m << extra
+//                   (m = code for codes 0..3, 2 + (code & 1) above);  IVBAD invalid (30, 31)
 //   both:           IVSLOW: a code longer than IFB bits (or none) -- the canonical slow path
 #define IVSLOW 0xFFFFFFFFu
 #define IVBAD 0xFFFFFFFEu
 __device__ __forceinline__ uint32_t iv_ll(uint32_t e) {   // from a sym << 4 | clen entry
     if (e == ISLOW) return IVSLOW;
     const uint32_t sym = e >> 4, l = e & 15u;
-    if (sym < 256) return (sym << 8) | l;
-    if (sym == 256) return 0xC0000000u | l;
+    if (sym < 256) return (sym << 16) | l;
+    if (sym == 256) return 0xC000u | l;
     const uint32_t li = sym - 257;
-    if (li >= 29) return 0xE0000000u | l;
-    return 0x80000000u | (len_base(li) << 16) | (len_extra(li) << 4) | l;
+    if (li >= 29) return 0xE000u | l;
+    const uint32_t x = len_extra(li);
+    return (len_base(li) << 23) | (x << 16) | 0x8000u | ((l + x) << 8) | l;
 }
 __device__ __forceinline__ uint32_t iv_d(uint32_t e) {
     if (e == ISLOW) return IVSLOW;
-    const uint32_t ds = e >> 4;
+    const uint32_t ds = e >> 4, l = e & 15u;
     if (ds >= 30) return IVBAD;
-    return (dist_base(ds) << 16) | (dist_extra(ds) << 4) | (e & 15u);
+    const uint32_t x = dist_extra(ds), m = ds < 4 ? ds : 2 + (ds & 1);
+    return (m << 28) | (x << 16) | ((l + x) << 8) | l;
 }
+// the value of a length / distance entry's field (its extra bits at the reader) and its base
+__device__ __forceinline__ uint32_t iv_extra(uint64_t bb, uint32_t e) {
+    return (uint32_t)(bb >> (e & 31u)) & ((1u << ((e >> 16) & 15u)) - 1);
+}
+__device__ __forceinline__ uint32_t iv_dbase(uint32_t e) { return ((e >> 28) << ((e >> 16) & 15u)) + 1; }
 
 // ---------------------------------------------------------------------------------------
-// Huffman tables.  Lane l (1..15) owns code length l: it counts its symbols, then assigns
-// their canonical codes in symbol order and fills their first-level entries, in the 32-bit
-// format above (DIST: a distance table; otherwise literal/length, which also serves the code
-// length code: its symbols 0..18 take the literal form); IVSLOW marks a code longer than IFB
-// bits (or no code).  Returns 0 complete, 1 incomplete, -1 over-subscribed.
+// Huffman tables, lane-parallel over symbols (lane t holds symbols t, t + 64, ...): counts per
+// code length by ballots, the canonical first codes and offsets (uniform), then each symbol's
+// rank among the symbols of its length (mbcnt of the same ballots) gives its code and its slot
+// in the length-sorted list; every lane then fills its symbol's first-level entries at once,
+// in the 32-bit format above (DIST: a distance table; otherwise literal/length, which also
+// serves the code length code: its symbols 0..18 take the literal form).  IVSLOW marks a code
+// longer than IFB bits (or no code).  Returns 0 complete, 1 incomplete, -1 over-subscribed.
 // ---------------------------------------------------------------------------------------
 template <bool DIST, uint32_t W>
 __device__ __forceinline__ int itable_build(InfLDS<W>& S, ITable& T, int n, uint32_t lane) {
+    const int nc = (n + 63) >> 6;   // symbol chunks, <= 5
+    uint32_t lc[5];
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+        const int s = c * 64 + (int)lane;
+        lc[c] = (c < nc && s < n) ? S.len[s] : 0u;
+    }
     for (int k = (int)lane; k < (1 << IFB); k += 64) T.fast[k] = IVSLOW;
-    uint32_t c = 0;
-    if (lane >= 1 && lane < 16)
-        for (int s = 0; s < n; s++) c += S.len[s] == lane;
-    // Kraft check, first codes and offsets (uniform, unrolled)
-    int left = 1, res = 0;
-    uint32_t code = 0, off = 0, firstl = 0, offl = 0, cprev = 0;
+    uint32_t cnt[16], first[16], offs[16];
+#pragma unroll
     for (int l = 1; l < 16; l++) {
-        const uint32_t cl = rfl(__builtin_amdgcn_readlane(c, l));
-        left = 2 * left - (int)cl;
+        uint32_t t = 0;
+#pragma unroll
+        for (int c = 0; c < 5; c++)
+            if (c < nc) t += (uint32_t)__popcll(__ballot(lc[c] == (uint32_t)l));
+        cnt[l] = t;
+    }
+    // Kraft check, first codes and offsets (uniform)
+    int left = 1, res = 0;
+    uint32_t code = 0, off = 0, cprev = 0;
+#pragma unroll
+    for (int l = 1; l < 16; l++) {
+        left = 2 * left - (int)cnt[l];
         if (left < 0) res = -1;
         code = (code + cprev) << 1;
-        if ((uint32_t)l == lane) { firstl = code; offl = off; }
+        first[l] = code;
+        offs[l] = off;
         if (lane == 0) {
             T.first[l] = (uint16_t)code;
-            T.cnt[l] = (uint16_t)cl;
+            T.cnt[l] = (uint16_t)cnt[l];
             T.offs[l] = (uint16_t)off;
         }
-        off += cl;
-        cprev = cl;
+        off += cnt[l];
+        cprev = cnt[l];
     }
     if (res == 0 && left > 0) res = 1;
     if (off == 0) res = 1;   // no codes at all
-    __syncthreads();
-    if (res >= 0 && lane >= 1 && lane < 16 && c) {
-        uint32_t k = 0;
-        for (int s = 0; s < n; s++) {
-            if (S.len[s] != lane) continue;
-            T.sym[offl + k] = (uint16_t)s;
-            if (lane <= IFB) {
-                const uint32_t rv = __brev(firstl + k) >> (32 - lane);
-                const uint32_t e16 = ((uint32_t)s << 4) | lane;
-                const uint32_t e = DIST ? iv_d(e16) : iv_ll(e16);
-                for (uint32_t j = 0; j < (1u << (IFB - lane)); j++) T.fast[rv | (j << lane)] = e;
+    if (res >= 0) {
+        uint32_t run[16];
+#pragma unroll
+        for (int l = 1; l < 16; l++) run[l] = 0;
+#pragma unroll
+        for (int c = 0; c < 5; c++) {
+            if (c >= nc) break;
+            const uint32_t l0 = lc[c];
+            uint32_t mycode = 0, myoff = 0;
+#pragma unroll
+            for (int l = 1; l < 16; l++) {
+                const uint64_t m = __ballot(l0 == (uint32_t)l);
+                const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                if (l0 == (uint32_t)l) {
+                    mycode = first[l] + run[l] + below;
+                    myoff = offs[l] + run[l] + below;
+                }
+                run[l] += (uint32_t)__popcll(m);
             }
-            k++;
+            if (l0) {
+                const uint32_t s = c * 64 + lane;
+                T.sym[myoff] = (uint16_t)s;
+                if (l0 <= IFB) {
+                    const uint32_t rv = __brev(mycode) >> (32 - l0);
+                    const uint32_t e16 = (s << 4) | l0;
+                    const uint32_t e = DIST ? iv_d(e16) : iv_ll(e16);
+                    for (uint32_t j = 0; j < (1u << (IFB - l0)); j++) T.fast[rv | (j << l0)] = e;
+                }
+            }
         }
     }
     __syncthreads();
@@ -244,7 +287,7 @@ __device__ __forceinline__ uint32_t ientry_slow(const IBits& r, const ITable& T)
 // the code length code (symbols 0..18, in the literal form): sym << 4 | len, or ISLOW
 __device__ __forceinline__ uint32_t ientry_cl(const IBits& r, const ITable& T) {
     const uint32_t e = rfl(T.fast[ib_peek(r, IFB)]);
-    return e != IVSLOW ? ((e >> 8) << 4) | (e & 15u) : ientry_slow(r, T);
+    return e != IVSLOW ? (((e >> 16) & 0xFFu) << 4) | (e & 15u) : ientry_slow(r, T);
 }
 
 __constant__ uint8_t c_iclorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
@@ -255,7 +298,7 @@ __constant__ uint8_t c_iclorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 
 // ---------------------------------------------------------------------------------------
 // DMX_INF_STAMPS (diagnostic builds only): per-workgroup cycle totals of the decode phases
 #ifdef DMX_INF_STAMPS
-#define INF_NST 8
+#define INF_NST 12
 __device__ unsigned long long dmx_inf_st[1 << 16][INF_NST];
 #define IST_NOW() __builtin_amdgcn_s_memtime()
 #define IST_ADD(o, k, v) ((o).st[k] += (v))
@@ -266,7 +309,8 @@ __device__ unsigned long long dmx_inf_st[1 << 16][INF_NST];
 
 struct IOut {
 #ifdef DMX_INF_STAMPS
-    unsigned long long st[INF_NST];   // 0 header + tables, 1 symbol loop, 2 flushes, 3 matches, 4 far matches, 5 match bytes, 6 blocks
+    unsigned long long st[INF_NST];   // 0 header + tables, 1 symbol loop, 2 flushes, 3 matches, 4 far matches, 5 -, 6 blocks,
+                                      // 7 code length table, 8 code lengths, 9 literal/length table, 10 distance table
 #endif
     uint8_t* out;     // + base + ob = position 0
     uint64_t base, ob, cap;   // cap: absolute output capacity
@@ -374,15 +418,16 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // In SGPRs: the 64-bit bit buffer (s[94:95]), bc, wi, op; the two tables come from LDS into
 // v96..v111 (literal/length) and v112..v127 (distance) and are read by an indexed v_mov
 // (s_set_gpr_idx_on) + v_readlane.  A literal is one ds_write_b8 (every lane stores the same
-// byte); a match inside the ring with distance >= length or >= 64 is a copy of 64 bytes a
-// round (lane t: byte src + t, read before the round's writes).  Returns at the first event
-// it leaves to the caller, with nothing of the current token consumed unless noted:
+// byte); a match is 64 bytes a round (lane t: byte src + t, read before the round's writes,
+// when distance >= length or >= 64; byte src + t mod distance for a shorter period; a
+// source older than the ring from the flushed output in HBM).  Returns at the first event it
+// leaves to the caller, with nothing of the current token consumed unless noted:
 //   IX_SYM   a long, end-of-block or invalid literal/length code
 //   IX_SEG   a refill at a token start that needs a stream segment it does not rotate into
 //            (the segment after next is not wholly inside the stream)
-//   IX_LIM   op >= lim at a literal or length (flush, or the capacity limit)
+//   IX_LIM   op >= lim at a literal or op >= limm at a length (flush, or near the capacity)
 //   IX_DIST  length decoded into len; the distance code is long or invalid
-//   IX_MATCH len and dist decoded: an error, a source older than the ring, or a short period
+//   IX_MATCH len and dist decoded: a distance before the output
 // Hazards: a lane select written by SALU is 4+ instructions old at each v_readlane (s_nop 3
 // where it is not); the stream prefetch is waited for before it is read and before return;
 // m0 (written by s_set_gpr_idx_on) is restored.
@@ -394,10 +439,12 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 #define IX_MATCH 5u
 
 template <uint32_t W>
-__device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t lim, uint32_t capr, uint32_t dfl,
-                                             uint32_t tla, uint32_t tda, uint32_t lane, uint32_t& len,
-                                             uint32_t& dist) {
+__device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t lim, uint32_t limm, uint32_t dfl,
+                                             uint32_t tla, uint32_t tda, uint32_t lane, uint64_t gpos0,
+                                             uint32_t& len, uint32_t& dist) {
     uint32_t ex;
+    const uint64_t galn = gpos0 & ~3ull;   // output position 0 in HBM, as an aligned base + 0..3
+    const uint32_t gmis = (uint32_t)gpos0 & 3u;
     const int32_t wrl = (int32_t)r.wfast - 192;   // rotate while the new segment is wholly inside
     const uint64_t zb = (uint64_t)(uintptr_t)r.zb;
     asm volatile(
@@ -439,6 +486,71 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
         "s_mov_b32 %[len], 0\n"
         "s_mov_b32 %[dist], 0\n"
         "s_waitcnt lgkmcnt(0)\n"
+        // distance bases (m << extra) + 1 beside the distance entries, in v128..v143
+        "v_bfe_u32 v148, v112, 28, 2\n"
+        "v_bfe_u32 v149, v112, 16, 4\n"
+        "v_lshlrev_b32 v148, v149, v148\n"
+        "v_add_u32 v128, 1, v148\n"
+        "v_bfe_u32 v148, v113, 28, 2\n"
+        "v_bfe_u32 v149, v113, 16, 4\n"
+        "v_lshlrev_b32 v148, v149, v148\n"
+        "v_add_u32 v129, 1, v148\n"
+        "v_bfe_u32 v148, v114, 28, 2\n"
+        "v_bfe_u32 v149, v114, 16, 4\n"
+        "v_lshlrev_b32 v148, v149, v148\n"
+        "v_add_u32 v130, 1, v148\n"
+        "v_bfe_u32 v148, v115, 28, 2\n"
+        "v_bfe_u32 v149, v115, 16, 4\n"
+        "v_lshlrev_b32 v148, v149, v148\n"
+        "v_add_u32 v131, 1, v148\n"
+        "v_bfe_u32 v148, v116, 28, 2\n"
+        "v_bfe_u32 v149, v116, 16, 4\n"
+        "v_lshlrev_b32 v148, v149, v148\n"
+        "v_add_u32 v132, 1, v148\n"
+        "v_bfe_u32 v148, v117, 28, 2\n"
+        "v_bfe_u32 v149, v117, 16, 4\n"
+        "v_lshlrev_b32 v148, v149, v148\n"
+        "v_add_u32 v133, 1, v148\n"
+        "v_bfe_u32 v148, v118, 28, 2\n"
+        "v_bfe_u32 v149, v118, 16, 4\n"
+        "v_lshlrev_b32 v148, v149, v148\n"
+        "v_add_u32 v134, 1, v148\n"
+        "v_bfe_u32 v148, v119, 28, 2\n"
+        "v_bfe_u32 v149, v119, 16, 4\n"
+        "v_lshlrev_b32 v148, v149, v148\n"
+        "v_add_u32 v135, 1, v148\n"
+        "v_bfe_u32 v148, v120, 28, 2\n"
+        "v_bfe_u32 v149, v120, 16, 4\n"
+        "v_lshlrev_b32 v148, v149, v148\n"
+        "v_add_u32 v136, 1, v148\n"
+        "v_bfe_u32 v148, v121, 28, 2\n"
+        "v_bfe_u32 v149, v121, 16, 4\n"
+        "v_lshlrev_b32 v148, v149, v148\n"
+        "v_add_u32 v137, 1, v148\n"
+        "v_bfe_u32 v148, v122, 28, 2\n"
+        "v_bfe_u32 v149, v122, 16, 4\n"
+        "v_lshlrev_b32 v148, v149, v148\n"
+        "v_add_u32 v138, 1, v148\n"
+        "v_bfe_u32 v148, v123, 28, 2\n"
+        "v_bfe_u32 v149, v123, 16, 4\n"
+        "v_lshlrev_b32 v148, v149, v148\n"
+        "v_add_u32 v139, 1, v148\n"
+        "v_bfe_u32 v148, v124, 28, 2\n"
+        "v_bfe_u32 v149, v124, 16, 4\n"
+        "v_lshlrev_b32 v148, v149, v148\n"
+        "v_add_u32 v140, 1, v148\n"
+        "v_bfe_u32 v148, v125, 28, 2\n"
+        "v_bfe_u32 v149, v125, 16, 4\n"
+        "v_lshlrev_b32 v148, v149, v148\n"
+        "v_add_u32 v141, 1, v148\n"
+        "v_bfe_u32 v148, v126, 28, 2\n"
+        "v_bfe_u32 v149, v126, 16, 4\n"
+        "v_lshlrev_b32 v148, v149, v148\n"
+        "v_add_u32 v142, 1, v148\n"
+        "v_bfe_u32 v148, v127, 28, 2\n"
+        "v_bfe_u32 v149, v127, 16, 4\n"
+        "v_lshlrev_b32 v148, v149, v148\n"
+        "v_add_u32 v143, 1, v148\n"
         // ---- token start: refill (rotating the stream segments when the word is in vnxt)
         "L_tok%=:\n"
         "s_cmp_gt_u32 %[bc], 32\n"
@@ -453,8 +565,8 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
         "s_add_u32 %[wb], %[wb], 64\n"
         "s_sub_u32 s98, s98, 64\n"
         "s_add_u32 s99, %[wb], 64\n"
-        "v_add_lshl_u32 v129, %[lane], s99, 2\n"
-        "global_load_dword %[vn], v129, %[zb]\n"
+        "v_add_lshl_u32 v146, %[lane], s99, 2\n"
+        "global_load_dword %[vn], v146, %[zb]\n"
         "L_rd%=:\n"
         "s_nop 3\n"
         "v_readlane_b32 s96, %[vc], s98\n"
@@ -466,38 +578,33 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
         "L_look%=:\n"
         "s_bfe_u32 s98, s94, 0x40006\n"
         "s_set_gpr_idx_on s98, gpr_idx(SRC0)\n"
-        "v_mov_b32 v128, v96\n"
+        "v_mov_b32 v144, v96\n"
         "s_set_gpr_idx_off\n"
-        "v_readlane_b32 s99, v128, s94\n"
-        "s_cmp_lt_i32 s99, 0\n"
+        "v_readlane_b32 s99, v144, s94\n"
+        "s_bitcmp1_b32 s99, 15\n"
         "s_cbranch_scc1 L_nl%=\n"
-        // literal
+        // literal: sym in bits 23:16 (ds_write_b8_d16_hi), every lane the same byte
         "s_cmp_ge_u32 %[op], %[lim]\n"
         "s_cbranch_scc1 L_xlim%=\n"
-        "s_and_b32 s98, s99, 15\n"
+        "s_and_b32 s98, s99, 31\n"
         "s_lshr_b64 s[94:95], s[94:95], s98\n"
         "s_sub_u32 %[bc], %[bc], s98\n"
-        "s_lshr_b32 s99, s99, 8\n"
-        "s_and_b32 s98, %[op], %[im]\n"
-        "v_mov_b32 v129, s98\n"
-        "v_mov_b32 v130, s99\n"
-        "ds_write_b8 v129, v130\n"
+        "v_mov_b32 v146, %[op]\n"
+        "v_and_b32 v146, %[im], v146\n"
+        "v_mov_b32 v147, s99\n"
+        "ds_write_b8_d16_hi v146, v147\n"
         "s_add_u32 %[op], %[op], 1\n"
         "s_branch L_tok%=\n"
-        // ---- length
+        // ---- length (the entry is the s_bfe control of its extra bits)
         "L_nl%=:\n"
-        "s_cmp_lt_u32 s99, 0xC0000000\n"
-        "s_cbranch_scc0 L_xsym%=\n"
-        "s_cmp_ge_u32 %[op], %[lim]\n"
+        "s_bitcmp1_b32 s99, 14\n"
+        "s_cbranch_scc1 L_xsym%=\n"
+        "s_cmp_ge_u32 %[op], %[limm]\n"
         "s_cbranch_scc1 L_xlim%=\n"
-        "s_and_b32 s98, s99, 15\n"
-        "s_lshr_b64 s[92:93], s[94:95], s98\n"
-        "s_bfe_u32 s90, s99, 0x40004\n"
-        "s_bfm_b32 s91, s90, 0\n"
-        "s_and_b32 s91, s92, s91\n"
-        "s_bfe_u32 %[len], s99, 0x90010\n"
+        "s_bfe_u32 s91, s94, s99\n"
+        "s_lshr_b32 %[len], s99, 23\n"
         "s_add_u32 %[len], %[len], s91\n"
-        "s_add_u32 s98, s98, s90\n"
+        "s_bfe_u32 s98, s99, 0x50008\n"
         "s_lshr_b64 s[94:95], s[94:95], s98\n"
         "s_sub_u32 %[bc], %[bc], s98\n"
         // refill inside the token: the word is in vcur or vnxt
@@ -519,61 +626,126 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
         "s_or_b64 s[94:95], s[94:95], s[92:93]\n"
         "s_add_u32 %[wi], %[wi], 1\n"
         "s_add_u32 %[bc], %[bc], 32\n"
-        // ---- distance
+        // ---- distance: entry and base by the same index
         "L_dl%=:\n"
         "s_bfe_u32 s98, s94, 0x40006\n"
         "s_set_gpr_idx_on s98, gpr_idx(SRC0)\n"
-        "v_mov_b32 v128, v112\n"
+        "v_mov_b32 v144, v112\n"
+        "v_mov_b32 v145, v128\n"
         "s_set_gpr_idx_off\n"
-        "v_readlane_b32 s99, v128, s94\n"
-        "s_cmp_ge_u32 s99, 0xFFFFFFFE\n"
+        "v_readlane_b32 s99, v144, s94\n"
+        "v_readlane_b32 s90, v145, s94\n"
+        "s_cmp_lt_i32 s99, 0\n"
         "s_cbranch_scc1 L_xdist%=\n"
-        "s_and_b32 s98, s99, 15\n"
-        "s_lshr_b64 s[92:93], s[94:95], s98\n"
-        "s_bfe_u32 s90, s99, 0x40004\n"
-        "s_bfm_b32 s91, s90, 0\n"
-        "s_and_b32 s91, s92, s91\n"
-        "s_lshr_b32 %[dist], s99, 16\n"
-        "s_add_u32 %[dist], %[dist], s91\n"
-        "s_add_u32 s98, s98, s90\n"
+        "s_bfe_u32 s91, s94, s99\n"
+        "s_add_u32 %[dist], s90, s91\n"
+        "s_bfe_u32 s98, s99, 0x50008\n"
         "s_lshr_b64 s[94:95], s[94:95], s98\n"
         "s_sub_u32 %[bc], %[bc], s98\n"
-        // ---- the copy, or the caller for errors, far sources and short periods
+        // ---- the copy (op < limm: the length fits), or the caller for a distance before the output
         "s_add_u32 s98, %[op], %[dfl]\n"
         "s_cmp_gt_u32 %[dist], s98\n"
         "s_cbranch_scc1 L_xmatch%=\n"
-        "s_sub_u32 s98, %[capr], %[op]\n"
-        "s_cmp_gt_u32 %[len], s98\n"
-        "s_cbranch_scc1 L_xmatch%=\n"
         "s_cmp_gt_u32 %[dist], %[wmax]\n"
-        "s_cbranch_scc1 L_xmatch%=\n"
+        "s_cbranch_scc1 L_far%=\n"
         "s_cmp_ge_u32 %[dist], %[len]\n"
         "s_cbranch_scc1 L_cp%=\n"
         "s_cmp_lt_u32 %[dist], 64\n"
-        "s_cbranch_scc1 L_xmatch%=\n"
+        "s_cbranch_scc1 L_per%=\n"
         "L_cp%=:\n"
         "s_sub_u32 s98, %[op], %[dist]\n"
-        "v_add_u32 v129, s98, %[lane]\n"
-        "v_add_u32 v130, %[op], %[lane]\n"
+        "v_add_u32 v144, s98, %[lane]\n"
+        "v_add_u32 v145, %[op], %[lane]\n"
         "s_mov_b32 s99, %[len]\n"
         "L_cr%=:\n"
         "v_cmp_gt_u32 vcc, s99, %[lane]\n"
         "s_and_saveexec_b64 s[92:93], vcc\n"
-        "v_and_b32 v131, %[im], v129\n"
-        "ds_read_u8 v131, v131\n"
-        "v_and_b32 v128, %[im], v130\n"
+        "v_and_b32 v146, %[im], v144\n"
+        "ds_read_u8 v146, v146\n"
+        "v_and_b32 v147, %[im], v145\n"
         "s_waitcnt lgkmcnt(0)\n"
-        "ds_write_b8 v128, v131\n"
+        "ds_write_b8 v147, v146\n"
         "s_mov_b64 exec, s[92:93]\n"
         "s_sub_u32 s99, s99, 64\n"
         "s_cmp_gt_i32 s99, 0\n"
         "s_cbranch_scc0 L_cd%=\n"
-        "v_add_u32 v129, 64, v129\n"
-        "v_add_u32 v130, 64, v130\n"
+        "v_add_u32 v144, 64, v144\n"
+        "v_add_u32 v145, 64, v145\n"
         "s_branch L_cr%=\n"
         "L_cd%=:\n"
         "s_add_u32 %[op], %[op], %[len]\n"
         "s_branch L_tok%=\n"
+        // ---- short period (dist < 64, dist < len): byte t is source byte t mod dist; lane
+        // residues start at lane mod dist (float reciprocal, corrected) and advance 64 mod dist
+        "L_per%=:\n"
+        "s_sub_u32 s98, %[op], %[dist]\n"
+        "v_cvt_f32_u32 v146, %[dist]\n"
+        "v_rcp_f32 v146, v146\n"
+        "v_cvt_f32_u32 v144, %[lane]\n"
+        "v_mul_f32 v144, v144, v146\n"
+        "v_cvt_u32_f32 v144, v144\n"
+        "v_mul_lo_u32 v144, v144, %[dist]\n"
+        "v_sub_u32 v144, %[lane], v144\n"
+        "v_cmp_gt_i32 vcc, 0, v144\n"
+        "v_add_u32 v146, %[dist], v144\n"
+        "v_cndmask_b32 v144, v144, v146, vcc\n"
+        "v_subrev_u32 v146, %[dist], v144\n"
+        "v_cmp_le_u32 vcc, %[dist], v144\n"
+        "v_cndmask_b32 v144, v144, v146, vcc\n"
+        "s_mov_b32 s91, 64\n"
+        "L_pm%=:\n"
+        "s_cmp_lt_u32 s91, %[dist]\n"
+        "s_cbranch_scc1 L_pmd%=\n"
+        "s_sub_u32 s91, s91, %[dist]\n"
+        "s_branch L_pm%=\n"
+        "L_pmd%=:\n"
+        "v_add_u32 v145, %[op], %[lane]\n"
+        "s_mov_b32 s99, %[len]\n"
+        "L_pr%=:\n"
+        "v_cmp_gt_u32 vcc, s99, %[lane]\n"
+        "s_and_saveexec_b64 s[92:93], vcc\n"
+        "v_add_u32 v146, s98, v144\n"
+        "v_and_b32 v146, %[im], v146\n"
+        "ds_read_u8 v146, v146\n"
+        "v_and_b32 v147, %[im], v145\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "ds_write_b8 v147, v146\n"
+        "s_mov_b64 exec, s[92:93]\n"
+        "s_sub_u32 s99, s99, 64\n"
+        "s_cmp_gt_i32 s99, 0\n"
+        "s_cbranch_scc0 L_cd%=\n"
+        "v_add_u32 v145, 64, v145\n"
+        "v_add_u32 v144, s91, v144\n"
+        "v_subrev_u32 v146, %[dist], v144\n"
+        "v_cmp_le_u32 vcc, %[dist], v144\n"
+        "v_cndmask_b32 v144, v144, v146, vcc\n"
+        "s_branch L_pr%=\n"
+        // ---- a source older than the ring: from the output already in HBM (flushed, the
+        // stores complete), agent-scope dword loads (to L2, past the vector L1)
+        "L_far%=:\n"
+        "s_sub_u32 s98, %[op], %[dist]\n"
+        "s_add_u32 s98, s98, %[gmis]\n"
+        "v_add_u32 v144, s98, %[lane]\n"
+        "v_add_u32 v145, %[op], %[lane]\n"
+        "s_mov_b32 s99, %[len]\n"
+        "L_fr%=:\n"
+        "v_cmp_gt_u32 vcc, s99, %[lane]\n"
+        "s_and_saveexec_b64 s[92:93], vcc\n"
+        "v_and_b32 v146, -4, v144\n"
+        "global_load_dword v146, v146, %[galn] sc1\n"
+        "v_and_b32 v147, 3, v144\n"
+        "v_lshlrev_b32 v147, 3, v147\n"
+        "s_waitcnt vmcnt(0)\n"
+        "v_lshrrev_b32 v146, v147, v146\n"
+        "v_and_b32 v147, %[im], v145\n"
+        "ds_write_b8 v147, v146\n"
+        "s_mov_b64 exec, s[92:93]\n"
+        "s_sub_u32 s99, s99, 64\n"
+        "s_cmp_gt_i32 s99, 0\n"
+        "s_cbranch_scc0 L_cd%=\n"
+        "v_add_u32 v144, 64, v144\n"
+        "v_add_u32 v145, 64, v145\n"
+        "s_branch L_fr%=\n"
         // ---- exits
         "L_xsym%=:\n"
         "s_mov_b32 %[ex], 1\n"
@@ -595,12 +767,10 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
         "s_mov_b64 %[bb], s[94:95]\n"
         : [bb] "+s"(r.bb), [bc] "+s"(r.bc), [wi] "+s"(r.wi), [wb] "+s"(r.wb), [vc] "+v"(r.vcur),
           [vn] "+v"(r.vnxt), [op] "+s"(op), [ex] "=&s"(ex), [len] "=&s"(len), [dist] "=&s"(dist)
-        : [lim] "s"(lim), [capr] "s"(capr), [dfl] "s"(dfl), [tla] "v"(tla), [tda] "v"(tda), [lane] "v"(lane),
-          [wrl] "s"(wrl), [zb] "s"(zb), [im] "n"(W - 1), [wmax] "n"(W)
+        : [lim] "s"(lim), [limm] "s"(limm), [dfl] "s"(dfl), [tla] "v"(tla), [tda] "v"(tda), [lane] "v"(lane),
+          [wrl] "s"(wrl), [zb] "s"(zb), [galn] "s"(galn), [gmis] "s"(gmis), [im] "n"(W - 1), [wmax] "n"(W)
         : "memory", "vcc", "scc", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99",
-          "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108",
-          "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120",
-          "v121", "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131");
+          "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149");
     return ex;
 }
 
@@ -652,7 +822,10 @@ __device__ __forceinline__ int iblock(InfLDS<W>& S, IBits& r, IOut& o, uint32_t 
             if (lane == 0) S.len[c_iclorder[k]] = (uint8_t)v;
         }
         __syncthreads();
+        [[maybe_unused]] const unsigned long long tc0 = IST_NOW();
         if (itable_build<false>(S, S.lt, 19, lane) != 0) return -(int)E_HUFAMB;
+        [[maybe_unused]] const unsigned long long tc1 = IST_NOW();
+        IST_ADD(o, 7, tc1 - tc0);
         uint32_t prev = 0;
         int idx = 0, err = 0;
         while (idx < nlen + ndist) {
@@ -689,11 +862,16 @@ __device__ __forceinline__ int iblock(InfLDS<W>& S, IBits& r, IOut& o, uint32_t 
     // literal/length table from seq[0, nlen), distance table from seq[nlen, nlen + ndist)
     for (int s = (int)lane; s < 288; s += 64) S.len[s] = s < nlen ? S.seq[s] : 0;
     __syncthreads();
+    [[maybe_unused]] const unsigned long long tl0 = IST_NOW();
+    IST_ADD(o, 8, tl0 - ts0);
     int e = itable_build<false>(S, S.lt, nlen, lane);
+    [[maybe_unused]] const unsigned long long tl1 = IST_NOW();
+    IST_ADD(o, 9, tl1 - tl0);
     if (e < 0 || (e > 0 && bt == 2 && rfl(S.lt.offs[15] + S.lt.cnt[15]) != 1)) return -(int)E_HUFAMB;
     for (int s = (int)lane; s < 32; s += 64) S.len[s] = s < ndist ? S.seq[nlen + s] : 0;
     __syncthreads();
     e = itable_build<true>(S, S.dt, ndist, lane);
+    IST_ADD(o, 10, IST_NOW() - tl1);
     if (e < 0 || (e > 0 && bt == 2 && rfl(S.dt.offs[15] + S.dt.cnt[15]) > 1)) return -(int)E_HUFAMB;
 
     // symbols: the common path in isym_run (literals, lengths and distances with table codes,
@@ -706,10 +884,12 @@ __device__ __forceinline__ int iblock(InfLDS<W>& S, IBits& r, IOut& o, uint32_t 
     if (lds_addr(S.win) != 0) return -(int)E_RANGE;   // isym_run addresses the ring from LDS 0
     const uint32_t tla = lds_addr(S.lt.fast) + lane * 4, tda = lds_addr(S.dt.fast) + lane * 4;
     const uint32_t dfl = o.ob != 0 ? 0x40000000u : 0u;   // stream mode: sources before ob exist
+    const uint64_t gpos0 = (uint64_t)(uintptr_t)(o.out + o.base + o.ob);
     for (;;) {
         const uint32_t lim = RING ? min(capr, o.fl + FL) : capr;
+        const uint32_t limm = rfl(min(lim, capr >= 258 ? capr - 258 : 0u));   // below it any length fits
         uint32_t len, dist;
-        const uint32_t ex = isym_run<W>(r, op, lim, capr, dfl, tla, tda, lane, len, dist);
+        const uint32_t ex = isym_run<W>(r, op, lim, limm, dfl, tla, tda, lane, gpos0, len, dist);
         if (ex == IX_SEG) {   // a refill at a token start that the run does not rotate into
             ib_refill(r);
             continue;
@@ -730,20 +910,20 @@ __device__ __forceinline__ int iblock(InfLDS<W>& S, IBits& r, IOut& o, uint32_t 
                 if (e16 == ISLOW) { err = -(int)E_HUFINV; break; }
                 en = iv_ll(e16);
             }
-            ib_drop(r, en & 15u);
-            if (en < 0x80000000u) {   // a literal: at the capacity limit, or a long code
+            if (!(en & 0x8000u)) {   // a literal: at the capacity limit, or a long code
+                ib_drop(r, en & 31u);
                 if (op >= capr) { err = -(int)E_SZ; break; }
-                S.win[op & IM] = (uint8_t)(en >> 8);
+                S.win[op & IM] = (uint8_t)(en >> 16);
                 op++;
                 continue;
             }
-            if (en >= 0xC0000000u) {
-                if (en & 0x20000000u) err = -(int)E_HUFVAL;
+            if (en & 0x4000u) {
+                ib_drop(r, en & 31u);
+                if (en & 0x2000u) err = -(int)E_HUFVAL;
                 break;   // end of block
             }
-            const uint32_t lx = (en >> 4) & 15u;
-            len = ((en >> 16) & 0x1FFu) + ((uint32_t)r.bb & ((1u << lx) - 1));
-            ib_drop(r, lx);
+            len = (en >> 23) + iv_extra(r.bb, en);
+            ib_drop(r, (en >> 8) & 31u);
         }
         if (ex != IX_MATCH) {   // the distance the general way
             ib_refill(r);
@@ -753,9 +933,8 @@ __device__ __forceinline__ int iblock(InfLDS<W>& S, IBits& r, IOut& o, uint32_t 
                 ed = e16 == ISLOW ? IVBAD : iv_d(e16);
                 if (ed == IVBAD) { err = -(int)E_HUFVAL; break; }
             }
-            const uint32_t dc = ed & 15u, dx = (ed >> 4) & 15u;
-            dist = (ed >> 16) + ((uint32_t)(r.bb >> dc) & ((1u << dx) - 1));
-            ib_drop(r, dc + dx);
+            dist = iv_dbase(ed) + iv_extra(r.bb, ed);
+            ib_drop(r, (ed >> 8) & 31u);
         }
         if (o.ob == 0 && dist > op) { err = -(int)E_HUFDIS; break; }
         if (len > capr - op) { err = -(int)E_SZ; break; }
@@ -803,7 +982,7 @@ __global__ __launch_bounds__(64) void dmx_inflate_index_kernel(const uint8_t* __
                                                                const dmx_iblock* __restrict__ index,
                                                                uint8_t* __restrict__ out, uint64_t out_cap,
                                                                dmx_inflate_status* __restrict__ st) {
-    __shared__ InfLDS<IWX> S;   // 16 KiB ring: 7 workgroups per CU (a 32 KiB window allowed 4)
+    __shared__ InfLDS<IWX> S;   // 8 KiB ring: 18 KiB of LDS, 8 workgroups per CU (a 32 KiB window allowed 4)
     const uint32_t lane = threadIdx.x;
     IBits r;
     ib_init(r, z, zbytes);

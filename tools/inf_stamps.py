@@ -32,15 +32,17 @@ assert L.dmx_inflate_async(out.data_ptr(), out.numel(), ix.data_ptr(), nb, dec.d
                            s.cuda_stream) == 0
 e1.record(s)
 torch.cuda.synchronize()
-a = np.zeros((nb, 8), np.uint64)
+a = np.zeros((nb, 12), np.uint64)
 assert L.dmx_inflate_stamps(a.ctypes.data, a.nbytes) == 0
 a = a.astype(np.float64)
 tot = a[:, 0] + a[:, 1]
 print(json.dumps({"lib": os.path.basename(D.LIB_PATH), "ms": round(e0.elapsed_time(e1), 3),
                   "bit_exact": bool(torch.equal(dec, data)), "blocks": nb,
                   "hdr_tables_kcyc": round(a[:, 0].mean() / 1e3, 1), "symbols_kcyc": round(a[:, 1].mean() / 1e3, 1),
-                  "flush_kcyc": round(a[:, 2].mean() / 1e3, 1), "matches": round(a[:, 3].mean(), 1),
-                  "far_matches": round(a[:, 4].mean(), 1), "match_bytes": round(a[:, 5].mean(), 1),
-                  "deflate_blocks": round(a[:, 6].mean(), 2), "total_kcyc_max": round(tot.max() / 1e3, 1),
-                  "cyc_per_match_all": round(a[:, 1].mean() / max(a[:, 3].mean(), 1), 1)}))
+                  "flush_kcyc": round(a[:, 2].mean() / 1e3, 1), "cpp_path_matches": round(a[:, 3].mean(), 1),
+                  "cpp_path_far": round(a[:, 4].mean(), 1), "deflate_blocks": round(a[:, 6].mean(), 2),
+                  "cl_table_kcyc": round(a[:, 7].mean() / 1e3, 1),
+                  "header_to_ll_table_kcyc": round(a[:, 8].mean() / 1e3, 1),
+                  "ll_table_kcyc": round(a[:, 9].mean() / 1e3, 1), "dist_table_kcyc": round(a[:, 10].mean() / 1e3, 1),
+                  "total_kcyc_max": round(tot.max() / 1e3, 1)}))
 enc.close()
