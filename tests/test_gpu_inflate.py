@@ -118,3 +118,52 @@ def test_indexed_matches_bulk_decode_at_scale():
         assert torch.equal(dec, t)
     finally:
         enc.close()
+
+
+def _ring_edge_inputs():
+    """Inputs aimed at the symbol loop's paths (isym_run): sources at and across the indexed
+    ring's edge (8 KiB) and the stream ring's (32 KiB), short periods 1..63 and periods 64..257
+    under 258-byte matches, and a skewed literal alphabet whose rare literals get codes longer
+    than the 10-bit first-level table (the slow path)."""
+    rng = np.random.default_rng(77)
+    out = {}
+    for d in (4095, 4096, 4097, 8191, 8192, 8193, 16384, 24576, 32767):
+        head = rng.integers(0, 256, d, dtype=np.uint8).tobytes()
+        out[f"dist{d}"] = head + head[:32768 - d] + head[:1000]
+    per = b""
+    for p in list(range(1, 64)) + [64, 65, 100, 129, 200, 257]:
+        unit = rng.integers(0, 256, p, dtype=np.uint8).tobytes()
+        per += rng.integers(0, 256, 7, dtype=np.uint8).tobytes() + (unit * (600 // p + 2))[:600]
+    out["periods"] = per
+    geo = np.minimum(rng.geometric(0.18, 120_000), 255).astype(np.uint8)   # literal codes up to 15 bits
+    out["skewed"] = geo.tobytes()
+    words = [bytes(rng.integers(97, 123, rng.integers(2, 9), dtype=np.uint8)) for _ in range(300)]
+    out["skewed_text"] = b" ".join(words[min(int(rng.geometric(0.02)), 299)] for _ in range(30000))
+    return out
+
+
+@pytest.mark.parametrize("lazy", [False, True])
+@pytest.mark.parametrize("k", [0, 8])
+def test_indexed_ring_edges(k, lazy):
+    enc = D.Encoder(0, 1 << 20)
+    try:
+        for name, data in _ring_edge_inputs().items():
+            t = _dev(data)
+            opts = D.Opts(32768, k, D.DMX_ZLIB | (D.DMX_F_LAZY if lazy else 0), 0)
+            out, r = enc.compress_tensor(t[:len(data)], opts=opts)
+            assert zlib.decompress(out.cpu().numpy().tobytes()) == data, name
+            ix, n = enc.block_index()
+            dec, st = D.inflate_gpu(out, len(data), ix, n)
+            assert st == 0, (name, st)
+            assert dec.cpu().numpy().tobytes() == data, name
+    finally:
+        enc.close()
+
+
+@pytest.mark.parametrize("level", [1, 9])
+def test_stream_ring_edges(level):
+    for name, data in _ring_edge_inputs().items():
+        z = zlib.compress(data, level)
+        dec, st = D.inflate_gpu(_dev(z), len(data) + 16)
+        assert st == 0, (name, level, st)
+        assert dec.cpu().numpy().tobytes() == data, (name, level)
