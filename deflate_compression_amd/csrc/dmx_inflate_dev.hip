@@ -13,7 +13,7 @@
 // position are SGPRs; the compressed stream is staged in two VGPRs (one dword per lane, the
 // next 256 bytes prefetched), so a refill is a v_readlane.  The common path of the symbol loop
 // is hand-scheduled (isym_run): the literal/length and distance tables live in VGPRs during it
-// (an indexed v_mov + v_readlane per lookup, no LDS round trip), each entry carries its base
+// (a v_readlane under the VGPR index mode per lookup, no LDS round trip), each entry carries its base
 // and is the s_bfe control of its own extra bits, a literal is one LDS byte store, and a match
 // is copied by the whole wave, 64 bytes a round (periodic sources by residue; sources older
 // than the ring from the output already flushed to HBM).  Output is assembled in an LDS ring
@@ -155,7 +155,7 @@ __device__ __forceinline__ uint32_t dist_extra(uint32_t d) { return d < 4 ? 0 : 
 __device__ __forceinline__ uint32_t dist_base(uint32_t d) { return d < 4 ? d + 1 : ((2 + (d & 1)) << ((d - 2) >> 1)) + 1; }
 
 // Table entries (32-bit).  The symbol loop looks its codes up in 1024-entry tables held in 16
-// VGPRs (entry x in lane x & 63 of register x >> 6: an indexed v_mov + v_readlane, no LDS round
+// VGPRs (entry x in lane x & 63 of register x >> 6: a v_readlane under the index mode, no LDS round
 // trip).  A length or distance entry is laid out so that it is itself the s_bfe control that
 // extracts its extra bits from the bit buffer: bits [4:0] the code length (the field's offset),
 // [22:16] the extra-bit count (its width); [12:8] code + extra bits (the bits to drop).
@@ -416,8 +416,8 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // ~100 instructions a token (the structurizer's branch flags, copies of the stream registers
 // that waited for their prefetch); this one spends ~20 on a literal and ~60 on a match.
 // In SGPRs: the 64-bit bit buffer (s[94:95]), bc, wi, op; the two tables come from LDS into
-// v96..v111 (literal/length) and v112..v127 (distance) and are read by an indexed v_mov
-// (s_set_gpr_idx_on) + v_readlane.  A literal is one ds_write_b8 (every lane stores the same
+// v96..v111 (literal/length) and v112..v127 (distance, bases in v128..v143) and are read by
+// v_readlane under s_set_gpr_idx_on.  A literal is one ds_write_b8 (every lane stores the same
 // byte); a match is 64 bytes a round (lane t: byte src + t, read before the round's writes,
 // when distance >= length or >= 64; byte src + t mod distance for a shorter period; a
 // source older than the ring from the flushed output in HBM).  Returns at the first event it
@@ -432,6 +432,25 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // where it is not); the stream prefetch is waited for before it is read and before return;
 // m0 (written by s_set_gpr_idx_on) is restored.
 // ---------------------------------------------------------------------------------------
+// diagnostic timing builds only (the output is wrong): DMX_INF_NOFAR copies far sources from
+// the ring instead of HBM, DMX_INF_NOWAIT writes a copy round without waiting for its reads
+#ifdef DMX_INF_NOFAR
+#define IFAR_BRANCH "s_cbranch_scc1 L_cp%=\n"
+#else
+#define IFAR_BRANCH "s_cbranch_scc1 L_far%=\n"
+#endif
+#ifdef DMX_INF_NOWAIT
+#define ICOPY_WAIT
+#else
+#define ICOPY_WAIT "s_waitcnt lgkmcnt(0)\n"
+#endif
+// table lookups: lane s94 & 63 of register v96 + (s94 >> 6 & 15) (v112 + for distances, their
+// bases at v128 +), read by v_readlane under the index mode: the mode indexes the readlane's
+// VGPR source too (tools/gpridx_test.hip checks it on the device), so a lookup is s_bfe,
+// s_set_gpr_idx_on, v_readlane, s_set_gpr_idx_off -- no VGPR copy of the indexed register
+#define ILOOK_LL "s_set_gpr_idx_on s98, gpr_idx(SRC0)\n" "v_readlane_b32 s99, v96, s94\n" "s_set_gpr_idx_off\n"
+#define ILOOK_D "s_set_gpr_idx_on s98, gpr_idx(SRC0)\n" "v_readlane_b32 s99, v112, s94\n" \
+                "v_readlane_b32 s90, v128, s94\n" "s_set_gpr_idx_off\n"
 #define IX_SYM 1u
 #define IX_SEG 2u
 #define IX_LIM 3u
@@ -577,10 +596,7 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
         // ---- literal/length lookup
         "L_look%=:\n"
         "s_bfe_u32 s98, s94, 0x40006\n"
-        "s_set_gpr_idx_on s98, gpr_idx(SRC0)\n"
-        "v_mov_b32 v144, v96\n"
-        "s_set_gpr_idx_off\n"
-        "v_readlane_b32 s99, v144, s94\n"
+        ILOOK_LL
         "s_bitcmp1_b32 s99, 15\n"
         "s_cbranch_scc1 L_nl%=\n"
         // literal: sym in bits 23:16 (ds_write_b8_d16_hi), every lane the same byte
@@ -594,6 +610,8 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
         "v_mov_b32 v147, s99\n"
         "ds_write_b8_d16_hi v146, v147\n"
         "s_add_u32 %[op], %[op], 1\n"
+        "s_cmp_gt_u32 %[bc], 32\n"
+        "s_cbranch_scc1 L_look%=\n"
         "s_branch L_tok%=\n"
         // ---- length (the entry is the s_bfe control of its extra bits)
         "L_nl%=:\n"
@@ -629,12 +647,7 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
         // ---- distance: entry and base by the same index
         "L_dl%=:\n"
         "s_bfe_u32 s98, s94, 0x40006\n"
-        "s_set_gpr_idx_on s98, gpr_idx(SRC0)\n"
-        "v_mov_b32 v144, v112\n"
-        "v_mov_b32 v145, v128\n"
-        "s_set_gpr_idx_off\n"
-        "v_readlane_b32 s99, v144, s94\n"
-        "v_readlane_b32 s90, v145, s94\n"
+        ILOOK_D
         "s_cmp_lt_i32 s99, 0\n"
         "s_cbranch_scc1 L_xdist%=\n"
         "s_bfe_u32 s91, s94, s99\n"
@@ -647,7 +660,7 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
         "s_cmp_gt_u32 %[dist], s98\n"
         "s_cbranch_scc1 L_xmatch%=\n"
         "s_cmp_gt_u32 %[dist], %[wmax]\n"
-        "s_cbranch_scc1 L_far%=\n"
+        IFAR_BRANCH
         "s_cmp_ge_u32 %[dist], %[len]\n"
         "s_cbranch_scc1 L_cp%=\n"
         "s_cmp_lt_u32 %[dist], 64\n"
@@ -656,6 +669,21 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
         "s_sub_u32 s98, %[op], %[dist]\n"
         "v_add_u32 v144, s98, %[lane]\n"
         "v_add_u32 v145, %[op], %[lane]\n"
+        "s_cmp_gt_u32 %[len], 64\n"
+        "s_cbranch_scc1 L_cpl%=\n"
+        "v_cmp_gt_u32 vcc, %[len], %[lane]\n"      // one round: lanes t < len
+        "s_and_saveexec_b64 s[92:93], vcc\n"
+        "v_and_b32 v146, %[im], v144\n"
+        "ds_read_u8 v146, v146\n"
+        "v_and_b32 v147, %[im], v145\n"
+        ICOPY_WAIT
+        "ds_write_b8 v147, v146\n"
+        "s_mov_b64 exec, s[92:93]\n"
+        "s_add_u32 %[op], %[op], %[len]\n"
+        "s_cmp_gt_u32 %[bc], 32\n"
+        "s_cbranch_scc1 L_look%=\n"
+        "s_branch L_tok%=\n"
+        "L_cpl%=:\n"
         "s_mov_b32 s99, %[len]\n"
         "L_cr%=:\n"
         "v_cmp_gt_u32 vcc, s99, %[lane]\n"
@@ -663,7 +691,7 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
         "v_and_b32 v146, %[im], v144\n"
         "ds_read_u8 v146, v146\n"
         "v_and_b32 v147, %[im], v145\n"
-        "s_waitcnt lgkmcnt(0)\n"
+        ICOPY_WAIT
         "ds_write_b8 v147, v146\n"
         "s_mov_b64 exec, s[92:93]\n"
         "s_sub_u32 s99, s99, 64\n"
