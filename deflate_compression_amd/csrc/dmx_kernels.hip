@@ -47,6 +47,20 @@ __device__ __forceinline__ uint32_t dmx_hash(uint32_t tri) { return (tri * 0x9E3
 // the vector registers of the match kernel, which otherwise spills them).
 __device__ __forceinline__ uint32_t wave_of(uint32_t tid) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6)); }
 __device__ __forceinline__ uint32_t sort_key(uint32_t w, uint32_t p) { return (dmx_hash(w & 0xFFFFFFu) << 15) | p; }
+// NB-byte chains (the exhaustive parse, NB = 4 or 5; 3 = the trigram chains): the bucket of
+// the first NB bytes of w (position order, byte 0 in the low byte)
+__device__ __forceinline__ uint32_t dmx_hash4(uint32_t w) { return (w * 0x9E3779B1u) >> DMX_HASH_SHIFT; }
+template <int NB>
+__device__ __forceinline__ uint32_t bucket_of(uint64_t w) {
+    if (NB == 3) return dmx_hash((uint32_t)w & 0xFFFFFFu);
+    if (NB == 4) return dmx_hash4((uint32_t)w);
+    return (uint32_t)(((w & 0xFFFFFFFFFFull) * 0x9E3779B97F4A7C15ull) >> (64 - 13));
+}
+template <int NB>
+__device__ __forceinline__ uint32_t sort_key_h(uint64_t w, uint32_t p) { return (bucket_of<NB>(w) << 15) | p; }
+// the first NB bytes at p (NB <= 4: one dword)
+template <int NB>
+__device__ __forceinline__ uint64_t ldg(const uint32_t* W, uint32_t p);
 
 // RFC 1951 §3.2.5 length -> symbol 257..285, extra-bit count, extra value
 __device__ __forceinline__ void len_sym(uint32_t len, uint32_t& sym, uint32_t& eb, uint32_t& ev) {
@@ -157,6 +171,8 @@ __device__ __forceinline__ uint64_t ld8(const uint32_t* W, uint32_t p) {   // by
 __device__ __forceinline__ uint32_t ld4(const uint32_t* W, uint32_t p) {   // bytes p..p+3
     return __builtin_amdgcn_alignbyte(W[(p >> 2) + 1], W[p >> 2], p & 3);
 }
+template <int NB>
+__device__ __forceinline__ uint64_t ldg(const uint32_t* W, uint32_t p) { return NB > 4 ? ld8(W, p) : (uint64_t)ld4(W, p); }
 
 __device__ __forceinline__ uint32_t adv_of(const MatchLDS& L, uint32_t p) {
     return ((L.lit[p >> 5] >> (p & 31)) & 1u) ? 1u : (uint32_t)L.len8[p] + 3u;
@@ -614,9 +630,11 @@ __device__ __forceinline__ void ext_queue(MatchLDS& L, uint32_t bn, uint32_t K, 
     __builtin_amdgcn_wave_barrier();
 }
 
-template <bool DICT, bool RUNS>
+template <bool DICT, bool RUNS, int NB = 3>
 __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint16_t* __restrict__ pg,
-                                     uint32_t tid, bool stamp, uint64_t& tdef, const uint32_t* __restrict__ hbk) {
+                                     uint32_t tid, bool stamp, uint64_t& tdef, const uint32_t* __restrict__ hbk,
+                                     const uint32_t* __restrict__ seeds = nullptr) {
+    constexpr bool H4 = NB > 3;   // NB-byte chains seeded with the shorter matches (P0')
     const uint32_t lane = tid & 63, wave = wave_of(tid);
     const uint32_t K = max_chain > 0 ? (uint32_t)max_chain : 0xFFFFFFFFu;
     const uint32_t nvalid = bn > 2 ? bn - 2 : 0;   // positions with a full trigram = entries of S
@@ -722,13 +740,14 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
             // bounded mode (K <= KD) needs no bucket rank: the K entries below k are examined
             // and those of other buckets never reach 3 equal bytes (cand_steps); only the
             // first K entries of the block lack K predecessors.  Longer chains need the rank.
-            nc = K <= KD ? min(k, K) : min(k - (uint32_t)L.bstart[dmx_hash((uint32_t)iv0 & 0xFFFFFFu)], K);
+            nc = K <= KD ? min(k, K) : min(k - (uint32_t)L.bstart[bucket_of<NB>(iv0)], K);
             lim = (bn - i) < MAXLEN ? (bn - i) : MAXLEN;
         }
         const uint32_t i0 = (uint32_t)iv0, i1 = (uint32_t)(iv0 >> 32);
         const uint32_t lim_eff = act ? lim : 0;
         const uint8_t* D8 = reinterpret_cast<const uint8_t*>(L.data);
         uint32_t bestkey = 0;
+        if (H4 && act) bestkey = seeds[i];   // the best match shorter than NB (P0', in HBM)
         for (uint32_t jb = 0, wl = K <= KD ? KD : W0;; jb += wl, wl = KD) {   // (bounded K <= KD: all in registers)
             // lanes that still need candidates jb + 1 ...: wave-uniform window length (window
             // 0: the W0 nearest candidates, by the register compare; then windows of KD)
@@ -756,12 +775,14 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
             // (k0 < jb + wl), or a bounded chain ending inside a later window (a bounded
             // K <= KD has a single window, at most K steps long, and needs no mask)
             const uint32_t ncw = nc > jb ? nc - jb : 0u;
-            const bool guard = k0 < jb + wl || (K > W0 && K < jb + wl);
+            // H4: an entry before the bucket start can still share the trigram (3 bytes, from
+            // any position, later ones too), so 4-byte chains are always masked at their end
+            const bool guard = H4 || k0 < jb + wl || (K > W0 && K < jb + wl);
             if (jb == 0) {
                 const uint32_t h0 = (uint32_t)hv0, h1 = (uint32_t)(hv0 >> 32);
                 {   // sort check: the predecessor (lane - 1, lane 0: halo 0) has a smaller (bucket, position)
-                    const uint32_t sk = sort_key(i0, i);
-                    const uint32_t pk = wshr(sk, __builtin_amdgcn_readlane(sort_key(h0, hq), 0));
+                    const uint32_t sk = sort_key_h<NB>(iv0, i);
+                    const uint32_t pk = wshr(sk, __builtin_amdgcn_readlane(sort_key_h<NB>(hv0, hq), 0));
                     if (__ballot(act && k >= 1 && pk > sk)) L.sortbad = 1;
                 }
                 uint32_t x0 = i0, x1 = i1, x2 = i2;   // the candidate streams
@@ -771,7 +792,7 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
                 if (lim_eff <= CB) full = 0;
                 // the window's register best in position form
                 if (act && (jkey >> 8) >= 3)
-                    bestkey = ((jkey >> 8) << 15) | (uint32_t)L.sorted[k - (255u - (jkey & 255u))];
+                    bestkey = max(bestkey, ((jkey >> 8) << 15) | (uint32_t)L.sorted[k - (255u - (jkey & 255u))]);
                 const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
                 bestkey = resolve_full<false, false>(L, bn, lane, wave, k, i, lim_eff, bestkey, full, k0);
                 if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
@@ -940,7 +961,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(MatchLDS& L, uint32_t v, uin
 // RUNCHK: count_add / atomic_rank first test whether all lanes of a step share one digit
 // (runs), which turns a 64-way same-address atomic into one add; blocks that are not
 // run-dominated (counted while staging) skip that test (correct either way).
-template <bool EXACT, bool RUNCHK = true>
+template <bool EXACT, bool RUNCHK = true, int NB = 3>
 __device__ __forceinline__ void sort_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint32_t tid, bool stamp,
                                                uint64_t* tp0) {
     const uint32_t lane = tid & 63, wave = wave_of(tid);
@@ -967,8 +988,8 @@ __device__ __forceinline__ void sort_positions(MatchLDS& L, uint32_t bn, int32_t
 #pragma unroll
     for (int st = 0; st < 32; st += 2) {
         const uint32_t xa = x0l + ((uint32_t)st << 6), xb = xa + 64;
-        const uint32_t ha = xa < nvl ? dmx_hash(ld4(L.data, xa) & 0xFFFFFFu) : 0u;
-        const uint32_t hb = xb < nvl ? dmx_hash(ld4(L.data, xb) & 0xFFFFFFu) : 0u;
+        const uint32_t ha = xa < nvl ? bucket_of<NB>(ldg<NB>(L.data, xa)) : 0u;
+        const uint32_t hb = xb < nvl ? bucket_of<NB>(ldg<NB>(L.data, xb)) : 0u;
         hh[st >> 1] = ha | (hb << 16);
         if ((st & 7) == 6) __builtin_amdgcn_sched_barrier(0);   // 8 loads in flight per group
     }
@@ -1061,13 +1082,102 @@ __device__ __forceinline__ void sort_positions(MatchLDS& L, uint32_t bn, int32_t
     for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) L.lit[k] = 0;
     if (need_starts) {   // bucket starts: entries whose bucket differs from the previous one
         for (uint32_t k = tid; k < nvalid; k += MT) {
-            const uint32_t h = dmx_hash(ld4(L.data, L.sorted[k]) & 0xFFFFFFu);
-            const uint32_t hp = k ? dmx_hash(ld4(L.data, L.sorted[k - 1]) & 0xFFFFFFu) : 0xFFFFFFFFu;
+            const uint32_t h = bucket_of<NB>(ldg<NB>(L.data, L.sorted[k]));
+            const uint32_t hp = k ? bucket_of<NB>(ldg<NB>(L.data, L.sorted[k - 1])) : 0xFFFFFFFFu;
             if (h != hp) L.bstart[h] = (uint16_t)k;
         }
     }
     __syncthreads();
     if (stamp && tid == 0) tp0[2] = __builtin_amdgcn_s_memtime();
+}
+
+
+// P0' (the exhaustive parse on NB-byte chains): with S sorted by NG-byte buckets, the nearest
+// earlier position with the same first NG bytes of every entry (NG < NB), as a seed key
+// NG << 15 | q (NG = 3 writes every seed, 0 = none; NG = 4 only the entries it finds, whose
+// keys beat the 3-byte ones).  Entries k - 1 .. k - PW stream through the lanes (wave
+// shifts; lane 0 from a halo of the PW entries below the chunk); entries whose bucket goes on
+// past PW colliding entries (a rare gram in a bucket it shares with a common one) are listed
+// and walked afterwards a wave per entry, 64 entries a step.  Returns this thread's
+// sort-order check (an entry before its predecessor).
+template <int NG>
+__device__ __forceinline__ uint32_t gram_pass(MatchLDS& L, uint32_t nv, uint32_t tid, uint32_t* __restrict__ seeds,
+                                              uint32_t& ndefer, uint64_t& tsweep) {
+#ifndef DMX_GRAM_PW
+    constexpr uint32_t PW = 9;
+#else
+    constexpr uint32_t PW = DMX_GRAM_PW;   // (diagnostic builds)
+#endif
+    constexpr uint32_t GM = NG == 3 ? 0xFFFFFFu : 0xFFFFFFFFu;
+    const uint32_t lane = tid & 63, wave = wave_of(tid);
+    uint32_t* UL = L.tsm;   // tsm + exitp: 2048 slots, free until the next sort
+    uint32_t bad = 0;
+    if (tid == 0) L.ntok = 0;
+    __syncthreads();
+    for (uint32_t kb = wave << 6; kb < nv; kb += MT) {
+        const uint32_t k = kb + lane;
+        const bool act = k < nv;
+        const uint32_t i = act ? (uint32_t)L.sorted[k] : 0u, w = act ? ld4(L.data, i) : 0u;
+        const uint32_t t = w & GM, hb = bucket_of<NG>(t);
+        uint32_t hi = 0xFFFFu, hw = 0;   // halo: lane l < PW holds entry kb - 1 - l
+        if (lane < PW && kb >= lane + 1) { hi = L.sorted[kb - 1 - lane]; hw = ld4(L.data, hi); }
+        uint32_t ip = i, wp = w, q = 0xFFFFu;
+        bool open = act && k > 0;   // still looking
+        for (uint32_t st = 1; st <= PW; st++) {
+            if (st > 1 && !__ballot(open)) break;   // most chunks: every lane found at step 1
+            ip = wshr(ip, __builtin_amdgcn_readlane(hi, (int)st - 1));
+            wp = wshr(wp, __builtin_amdgcn_readlane(hw, (int)st - 1));
+            if (st == 1 && open && sort_key_h<NG>(wp, ip) > sort_key_h<NG>(w, i)) bad = 1;
+            if (open && k >= st) {
+                if ((wp & GM) == t) { q = ip; open = false; }
+                else if (bucket_of<NG>(wp & GM) != hb) open = false;   // the bucket start is passed
+            } else {
+                open = false;
+            }
+        }
+        if (open && k > PW) {   // more of the bucket to walk: later, a wave per entry
+            const uint32_t u = atomicAdd(&L.ntok, 1u);
+            if (u < 2 * (DMX_BLK / 32)) {
+                UL[u] = ((k - PW) << 16) | k;
+            } else {
+                const uint32_t k0 = L.bstart[hb];
+                for (uint32_t j = k - PW; j > k0; j--) {
+                    const uint32_t c = L.sorted[j - 1];
+                    if ((ld4(L.data, c) & GM) == t) { q = c; break; }
+                }
+            }
+        }
+        // (a gram that runs past the block's end is a match of fewer bytes: the 3-byte seed stays)
+#ifndef DMX_H4_NOSTORE
+        if (act && (NG == 3 || (q != 0xFFFFu && i + NG <= nv + 2))) seeds[i] = q != 0xFFFFu ? ((uint32_t)NG << 15) | q : 0u;
+#else
+        if (act && q == 0x1234u) seeds[i] = q;   // (diagnostic timing builds: the output is wrong)
+#endif
+    }
+    __syncthreads();
+    tsweep += __builtin_amdgcn_s_memtime();   // (diagnostic stamps: the sweep's end)
+    const uint32_t nul = min(L.ntok, 2u * (DMX_BLK / 32));
+    ndefer += L.ntok;
+    for (uint32_t u = wave; u < nul; u += MW) {
+        const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)UL[u]);
+        const uint32_t k = e & 0xFFFFu, i = L.sorted[k], t = ld4(L.data, i) & GM;
+        const uint32_t k0 = L.bstart[bucket_of<NG>(t)];
+        uint32_t q = 0xFFFFu;
+        for (int jb = (int)(e >> 16); jb > (int)k0; jb -= 64) {
+            const int j = jb - 1 - (int)lane;
+            const uint32_t c = j >= (int)k0 ? (uint32_t)L.sorted[j] : 0u;
+            const uint64_t m = __ballot(j >= (int)k0 && (ld4(L.data, c) & GM) == t);
+            if (m) {   // the lowest lane holds the nearest
+                q = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)__builtin_ctzll(m));
+                break;
+            }
+        }
+        if (lane == 0 && (NG == 3 || (q != 0xFFFFu && i + NG <= nv + 2))) seeds[i] = q != 0xFFFFu ? ((uint32_t)NG << 15) | q : 0u;
+    }
+    // every store complete (in L2) before the caller's barrier: the search's loads of the
+    // seeds come from other waves, and a workgroup barrier alone does not wait for stores
+    __builtin_amdgcn_s_waitcnt(0);
+    return bad;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1638,14 +1748,19 @@ __device__ __forceinline__ bool dbg_stop(uint32_t mflags, uint32_t phase, dmx_bl
     return true;
 }
 
-template <bool DICT>
+// NBX > 3: the exhaustive parse without a dictionary (max_chain = 0) on NBX-byte chains
+// (P0'); a separate instantiation, so the bounded modes' code and registers are untouched
+#ifndef DMX_NBX
+#define DMX_NBX 4   // the exhaustive parse's chain length in bytes (4; 5 measured slower: a second gram pass and sort)
+#endif
+template <bool DICT, int NBX = 3>
 __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
                                                        int32_t max_chain, uint32_t mflags, uint16_t* __restrict__ dist_g,
                                                        const uint16_t* __restrict__ chs, uint32_t* __restrict__ tok_g,
                                                        uint32_t* __restrict__ hist_g,
                                                        dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg) {
     __shared__ MatchLDS L;
-    __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def, tp0[3], st_rounds, st_p3a;
+    __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def, tp0[3], st_rounds, st_p3a, st_h4[3];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = wave_of(tid);
     const uint32_t b = blockIdx.x;
     if ((mflags & 4u) && info[b].prestored) return;   // stored by the noise check (K0)
@@ -1754,6 +1869,40 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         if (lane == 0) { atomicAdd(&L.adl_s, (unsigned long long)s); atomicAdd(&L.adl_t, (unsigned long long)t); }
     }
 
+    // ---- P0' (the exhaustive parse, no dictionary): 4-byte chains.  Every match of 4 or
+    // more bytes is between positions with the same first 4 bytes, so the exhaustive search
+    // runs over the chains of a second sort by a hash of 4 bytes (text: 17 candidates per
+    // position on average instead of 39).  A match of exactly 3 is then the nearest earlier
+    // position with the same trigram: read from the 3-byte sort first (the nearest entry of
+    // the trigram's bucket with equal bytes; hash collisions are skipped) and kept in HBM,
+    // in this block's token slots, until the search merges it (longest, then nearest).
+    constexpr bool h4 = NBX > 3 && !DICT;   // launched only with max_chain == 0
+    uint32_t* seeds = tok_g + (uint64_t)b * DMX_BLK;   // this block's token slots, free until P3
+    if constexpr (h4) {
+        const uint32_t nv = bn > 2 ? bn - 2 : 0;
+        const uint32_t hook = L.sortbad;   // the exact-sort test hook (mflags & 2)
+        uint32_t npass = 0, ndefer = 0;
+        uint64_t tsw = 0;
+        for (uint32_t pass = 0;; pass++) {   // 3-byte grams from P0's sort (checked here)
+            npass++;
+            if (!__syncthreads_or(gram_pass<3>(L, nv, tid, seeds, ndefer, tsw)) || pass) break;
+            sort_positions<true>(L, bn, max_chain, tid, false, tp0);   // never observed on gfx950
+        }
+        if constexpr (NBX > 4) {   // 4-byte grams from a 4-byte sort
+            for (uint32_t pass = 0;; pass++) {
+                npass++;
+                if (hook || pass) sort_positions<true, true, 4>(L, bn, max_chain, tid, false, tp0);
+                else sort_positions<false, true, 4>(L, bn, max_chain, tid, false, tp0);
+                if (!__syncthreads_or(gram_pass<4>(L, nv, tid, seeds, ndefer, tsw)) || pass || hook) break;
+            }
+        }
+        if (dbg && tid == 0) st_h4[0] = (__builtin_amdgcn_s_memtime() - tbeg) | ((uint64_t)npass << 48);
+        if (dbg && tid == 0) st_h4[2] = tsw - tbeg;   // the 3-byte sweep's end (before its listed walks)
+        if (hook) sort_positions<true, true, NBX>(L, bn, max_chain, tid, false, tp0);
+        else sort_positions<false, true, NBX>(L, bn, max_chain, tid, false, tp0);
+        if (dbg && tid == 0) st_h4[1] = (__builtin_amdgcn_s_memtime() - tbeg) | ((uint64_t)min(ndefer, 65535u) << 48);
+    }
+
     // ---- P1: longest match of every position ----
     const uint64_t t0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t tdef = 0;
@@ -1770,6 +1919,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
             __syncthreads();
         }
         const uint32_t its = runs ? search_positions<DICT, true>(L, bn, max_chain, pg, tid, dbg != nullptr, tdef, hbk)
+                             : h4 ? search_positions<DICT, false, (h4 ? NBX : 3)>(L, bn, max_chain, pg, tid, dbg != nullptr, tdef, hbk, seeds)
                                   : search_positions<DICT, false>(L, bn, max_chain, pg, tid, dbg != nullptr, tdef, hbk);
         if (dbg && lane == 0 && attempt == 0) {
             atomicAdd((unsigned long long*)&st_iters, (unsigned long long)its);
@@ -1779,7 +1929,8 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         __syncthreads();
         if (!L.sortbad || attempt) break;
         // never observed on gfx950: redo the block with the match-any sort (stable by construction)
-        sort_positions<true>(L, bn, max_chain, tid, dbg != nullptr, tp0);
+        if (h4) sort_positions<true, true, (h4 ? NBX : 3)>(L, bn, max_chain, tid, dbg != nullptr, tp0);
+        else sort_positions<true>(L, bn, max_chain, tid, dbg != nullptr, tp0);
     }
     const uint64_t t1 = dbg ? __builtin_amdgcn_s_memtime() : 0;
     if (dbg_stop(mflags, 2, info, hist_g, b, bn, tid)) return;
@@ -2031,8 +2182,10 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         dbg[(uint64_t)b * DMX_STAMPS + 10] = tp0[2] - tbeg;  //   pass 2 done
         dbg[(uint64_t)b * DMX_STAMPS + 11] = st_rounds;      // walk: Jacobi rounds (JR = not converged)
         if (!DICT) {   // (12, 13 are the history kernel's with DMX_F_DICT)
-            dbg[(uint64_t)b * DMX_STAMPS + 12] = st_p3a;     // P3: token list built (token-major path)
+            dbg[(uint64_t)b * DMX_STAMPS + 12] = h4 ? st_h4[2] : st_p3a;   // P3: token list built (exhaustive: sweep end)
             dbg[(uint64_t)b * DMX_STAMPS + 13] = p3b;        // P3: tokens and histograms done
+            dbg[(uint64_t)b * DMX_STAMPS + 14] = h4 ? st_h4[0] : 0;   // exhaustive: nearest-trigram pass done
+            dbg[(uint64_t)b * DMX_STAMPS + 15] = h4 ? st_h4[1] : 0;   //   4-byte sort done
         }
     }
     if (tid == 0) {
@@ -3518,6 +3671,9 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                              ((o.flags & DMX_F_STORE_CHECK) ? 4u : 0u) | (dstop ? ((uint32_t)atoi(dstop) & 3u) << 8 : 0u);
         if (o.flags & DMX_F_DICT)
             hipLaunchKernelGGL(dmx_match_kernel<true>, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n,
+                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg);
+        else if (o.max_chain == 0)
+            hipLaunchKernelGGL((dmx_match_kernel<false, DMX_NBX>), dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n,
                                (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg);
         else
             hipLaunchKernelGGL(dmx_match_kernel<false>, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n,
