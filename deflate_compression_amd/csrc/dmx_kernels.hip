@@ -194,6 +194,9 @@ __device__ __forceinline__ uint32_t adv_of(const MatchLDS& L, uint32_t p) {
 // (:249-263).  A lane stops comparing once its best is the longest possible length.
 #define KD 32
 #define W0 8    // long chains: candidates of the first window, compared in registers (the rest filtered)
+#ifndef DMX_W0H4
+#define DMX_W0H4 8   // the same on the exhaustive parse's 4-byte chains
+#endif
 #define CB 12   // bytes compared in registers per candidate step; longer matches extend from LDS
 #define KE 8    // chains up to KE candidates use chunks with the halo embedded (64-K owned entries)
 #define JR 8    // Jacobi rounds of the walk before the serial fallback
@@ -748,7 +751,8 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
         const uint8_t* D8 = reinterpret_cast<const uint8_t*>(L.data);
         uint32_t bestkey = 0;
         if (H4 && act) bestkey = seeds[i];   // the best match shorter than NB (P0', in HBM)
-        for (uint32_t jb = 0, wl = K <= KD ? KD : W0;; jb += wl, wl = KD) {   // (bounded K <= KD: all in registers)
+        constexpr uint32_t W0X = H4 ? DMX_W0H4 : W0;
+        for (uint32_t jb = 0, wl = K <= KD ? KD : W0X;; jb += wl, wl = KD) {   // (bounded K <= KD: all in registers)
             // lanes that still need candidates jb + 1 ...: wave-uniform window length (window
             // 0: the W0 nearest candidates, by the register compare; then windows of KD)
             uint32_t need = (act && nc > jb && (bestkey >> 15) < lim) ? min(nc - jb, wl) : 0u;
