@@ -451,6 +451,21 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 #define ILOOK_LL "s_set_gpr_idx_on s98, gpr_idx(SRC0)\n" "v_readlane_b32 s99, v96, s94\n" "s_set_gpr_idx_off\n"
 #define ILOOK_D "s_set_gpr_idx_on s98, gpr_idx(SRC0)\n" "v_readlane_b32 s99, v112, s94\n" \
                 "v_readlane_b32 s90, v128, s94\n" "s_set_gpr_idx_off\n"
+// A copy of one round (length <= 64) is left pending: its LDS read (or HBM load, for a source
+// older than the ring) is issued and the wave goes on decoding the next token while it is in
+// flight; the write (lanes in s[84:85], data v148 >> v150, address v149) is issued before
+// the next read of the ring, the next copy, or the return.  Literal stores in between touch
+// other positions.
+#define IFLUSH_PENDING(N) \
+    "s_cmp_eq_u64 s[84:85], 0\n" \
+    "s_cbranch_scc1 L_nf" #N "%=\n" \
+    "s_waitcnt vmcnt(0) lgkmcnt(0)\n" \
+    "s_mov_b64 exec, s[84:85]\n" \
+    "v_lshrrev_b32 v148, v150, v148\n" \
+    "ds_write_b8 v149, v148\n" \
+    "s_mov_b64 exec, s[86:87]\n" \
+    "s_mov_b64 s[84:85], 0\n" \
+    "L_nf" #N "%=:\n"
 #define IX_SYM 1u
 #define IX_SEG 2u
 #define IX_LIM 3u
@@ -469,6 +484,8 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
     asm volatile(
         "s_mov_b64 s[94:95], %[bb]\n"
         "s_mov_b32 s89, m0\n"
+        "s_mov_b64 s[86:87], exec\n"
+        "s_mov_b64 s[84:85], 0\n"
         "ds_read_b32 v96, %[tla]\n"
         "ds_read_b32 v97, %[tla] offset:256\n"
         "ds_read_b32 v98, %[tla] offset:512\n"
@@ -666,19 +683,20 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
         "s_cmp_lt_u32 %[dist], 64\n"
         "s_cbranch_scc1 L_per%=\n"
         "L_cp%=:\n"
+        IFLUSH_PENDING(1)
         "s_sub_u32 s98, %[op], %[dist]\n"
         "v_add_u32 v144, s98, %[lane]\n"
         "v_add_u32 v145, %[op], %[lane]\n"
         "s_cmp_gt_u32 %[len], 64\n"
         "s_cbranch_scc1 L_cpl%=\n"
-        "v_cmp_gt_u32 vcc, %[len], %[lane]\n"      // one round: lanes t < len
+        "v_cmp_gt_u32 vcc, %[len], %[lane]\n"      // one round: lanes t < len, left pending
         "s_and_saveexec_b64 s[92:93], vcc\n"
         "v_and_b32 v146, %[im], v144\n"
-        "ds_read_u8 v146, v146\n"
-        "v_and_b32 v147, %[im], v145\n"
-        ICOPY_WAIT
-        "ds_write_b8 v147, v146\n"
+        "ds_read_u8 v148, v146\n"
+        "v_and_b32 v149, %[im], v145\n"
+        "v_mov_b32 v150, 0\n"
         "s_mov_b64 exec, s[92:93]\n"
+        "s_mov_b64 s[84:85], vcc\n"
         "s_add_u32 %[op], %[op], %[len]\n"
         "s_cmp_gt_u32 %[bc], 32\n"
         "s_cbranch_scc1 L_look%=\n"
@@ -706,6 +724,7 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
         // ---- short period (dist < 64, dist < len): byte t is source byte t mod dist; lane
         // residues start at lane mod dist (float reciprocal, corrected) and advance 64 mod dist
         "L_per%=:\n"
+        IFLUSH_PENDING(2)
         "s_sub_u32 s98, %[op], %[dist]\n"
         "v_cvt_f32_u32 v146, %[dist]\n"
         "v_rcp_f32 v146, v146\n"
@@ -751,10 +770,27 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
         // ---- a source older than the ring: from the output already in HBM (flushed, the
         // stores complete), agent-scope dword loads (to L2, past the vector L1)
         "L_far%=:\n"
+        IFLUSH_PENDING(3)
         "s_sub_u32 s98, %[op], %[dist]\n"
         "s_add_u32 s98, s98, %[gmis]\n"
         "v_add_u32 v144, s98, %[lane]\n"
         "v_add_u32 v145, %[op], %[lane]\n"
+        "s_cmp_gt_u32 %[len], 64\n"
+        "s_cbranch_scc1 L_farl%=\n"
+        "v_cmp_gt_u32 vcc, %[len], %[lane]\n"      // one round, left pending
+        "s_and_saveexec_b64 s[92:93], vcc\n"
+        "v_and_b32 v146, -4, v144\n"
+        "global_load_dword v148, v146, %[galn] sc1\n"
+        "v_and_b32 v150, 3, v144\n"
+        "v_lshlrev_b32 v150, 3, v150\n"
+        "v_and_b32 v149, %[im], v145\n"
+        "s_mov_b64 exec, s[92:93]\n"
+        "s_mov_b64 s[84:85], vcc\n"
+        "s_add_u32 %[op], %[op], %[len]\n"
+        "s_cmp_gt_u32 %[bc], 32\n"
+        "s_cbranch_scc1 L_look%=\n"
+        "s_branch L_tok%=\n"
+        "L_farl%=:\n"
         "s_mov_b32 s99, %[len]\n"
         "L_fr%=:\n"
         "v_cmp_gt_u32 vcc, s99, %[lane]\n"
@@ -790,6 +826,7 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
         "L_xmatch%=:\n"
         "s_mov_b32 %[ex], 5\n"
         "L_end%=:\n"
+        IFLUSH_PENDING(4)
         "s_waitcnt vmcnt(0) lgkmcnt(0)\n"
         "s_mov_b32 m0, s89\n"
         "s_mov_b64 %[bb], s[94:95]\n"
@@ -797,8 +834,8 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
           [vn] "+v"(r.vnxt), [op] "+s"(op), [ex] "=&s"(ex), [len] "=&s"(len), [dist] "=&s"(dist)
         : [lim] "s"(lim), [limm] "s"(limm), [dfl] "s"(dfl), [tla] "v"(tla), [tda] "v"(tda), [lane] "v"(lane),
           [wrl] "s"(wrl), [zb] "s"(zb), [galn] "s"(galn), [gmis] "s"(gmis), [im] "n"(W - 1), [wmax] "n"(W)
-        : "memory", "vcc", "scc", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99",
-          "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149");
+        : "memory", "vcc", "scc", "s84", "s85", "s86", "s87", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99",
+          "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149", "v150");
     return ex;
 }
 
