@@ -11,23 +11,20 @@ OUT = os.path.join(R, "build", "exp")
 
 VARIANTS = {
     "base": [],
-    "nogroup": [("    const uint64_t vm = __ballot(valid);\n    if (vm == 0) return 0;\n    const uint32_t v0 = __builtin_amdgcn_readlane(v, (int)__builtin_ctzll(vm));",
-                 "    const uint64_t vm = __ballot(valid);\n    return valid ? (1ull << (threadIdx.x & 63)) : 0ull;\n    const uint32_t v0 = __builtin_amdgcn_readlane(v, (int)__builtin_ctzll(vm));")],
-    "_ballot7": [("    uint64_t eq = 0;\n    if (valid) {\n        __hip_atomic_fetch_or(",
-                 "    uint64_t eq = vm;\n#pragma unroll\n    for (int bit = 0; bit < 7; bit++) { const bool hb = (v >> bit) & 1u; const uint64_t mk = __ballot(hb); eq &= hb ? mk : ~mk; }\n    return valid ? eq : 0ull;\n    if (valid) {\n        __hip_atomic_fetch_or(")],
-    "nocheck": [("                const bool bad = act && ei >= 1 && pn > i && dmx_hash(dn & 0xFFFFFFu) == dmx_hash(i0 & 0xFFFFFFu);\n                if (__ballot(bad)) L.sortbad = 1;\n", "")],
-    "noqueue": [("    const uint32_t cnt = __popc(full);\n    const uint32_t incl = wave_incl_scan(cnt);", "    return bestkey;\n    const uint32_t cnt = __popc(full);\n    const uint32_t incl = wave_incl_scan(cnt);")],
-    "nodeferred": [("    if (__ballot(full != 0) == 0) return bestkey;", "    return bestkey;")],
-    "nocount": [("__device__ __forceinline__ void count_add(uint32_t* T, uint32_t v, bool valid, bool pair16) {\n",
-                 "__device__ __forceinline__ void count_add(uint32_t* T, uint32_t v, bool valid, bool pair16) {\n    return;\n")],
-    "noscatter": [("                L.sorted[dst] = (uint16_t)x;\n                D2[dst] = (uint8_t)(h >> 7);\n", ""),
-                  ("                L.sorted[c + (uint32_t)__popcll(eq & lt)] = (uint16_t)p;\n", "")],
+    # P0 knockouts (round 2): what each LDS operation of the two sort passes costs
+    "nocnt1": [("        count_add<RUNCHK>(C + (wave << 7), h & 127u, x < nvl, false);\n", "")],
+    "nocnt2": [("        count_add<RUNCHK>(C2, ((dst >> 11) << 6) | (h >> 7), valid, false);   // pass 2: (wave, digit)\n", "")],
+    "nosc1": [("            L.sorted[dst] = (uint16_t)x;\n            D2[dst] = (uint8_t)(h >> 7);\n", "")],
+    "nosc2": [("            if (valid) L.sorted[dst] = (uint16_t)p;\n", "            if (valid && dst == 0xFFFFu) L.sorted[0] = (uint16_t)p;\n")],
+    "norank": [("    if (!RUNCHK) return valid ? atomicAdd(&T[v], 1u) : 0u;", "    if (!RUNCHK) return valid ? ((T[v] + (threadIdx.x & 63)) & 32767u) : 0u;")],
 }
 
 def build():
     os.makedirs(OUT, exist_ok=True)
     base = open(os.path.join(SRC, "dmx_kernels.hip")).read()
-    for name, reps in VARIANTS.items():
+    names = sys.argv[2].split(",") if len(sys.argv) > 2 else list(VARIANTS)
+    for name in names:
+        reps = VARIANTS[name]
         s = base
         if any(a not in s for a, _ in reps):
             print("skip", name, "(pattern no longer in the source)")
@@ -39,7 +36,7 @@ def build():
         obj = os.path.join(OUT, f"k_{name}.o")
         subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-fPIC", "--offload-arch=gfx950", "-std=c++17",
                                "-I", SRC, "-I", os.path.join(R, "include"), "-c", "-o", obj, src])
-        objs = [os.path.join(R, "build", "dmx", f) for f in ("dmx_host.o", "dmx_inflate.o", "dmx_gen.o")]
+        objs = [os.path.join(R, "build", "dmx", f) for f in ("dmx_host.o", "dmx_inflate.o", "dmx_gen.o", "dmx_inflate_dev.o")]
         subprocess.check_call(["/opt/rocm/bin/hipcc", "-shared", "-fPIC", "--offload-arch=gfx950", "-o",
                                os.path.join(OUT, f"libdmx_{name}.so"), obj] + objs + ["-lm", "-lpthread"])
         print("built", name)
@@ -57,7 +54,7 @@ def one(name):
     D.LIB_PATH = os.path.join(OUT, f"libdmx_{name}.so")
     n = 20_000_000
     t = torch.from_numpy(D.gen_text(n, 0xE5818)).cuda()
-    e = D.Encoder(0, n, max_chain=8, flags=D.DMX_ZLIB | D.DMX_F_LAZY)
+    e = D.Encoder(0, n, max_chain=int(os.environ.get("EXP_K", "6")), flags=D.DMX_ZLIB | D.DMX_F_LAZY)
     for _ in range(2):
         out, r = e.compress_tensor(t)
     st = e.stamps(r.nblocks).astype(np.float64)

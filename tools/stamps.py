@@ -28,10 +28,10 @@ def run(kind, n, mc, flags=D.DMX_ZLIB | D.DMX_F_LAZY):
                       **({"hist_staged_kcyc": round(st[1:, 12].mean() / 1e3, 1), "hist_total_kcyc": round(st[1:, 13].mean() / 1e3, 1)}
                          if flags & D.DMX_F_DICT else {})}))
 
-# args: kind:max_chain[:d]  (d = with the cross-block dictionary, DMX_F_DICT)
+# args: kind:max_chain[:opts]  (opts: d = with the cross-block dictionary, DMX_F_DICT; g = greedy, no lazy)
 cfgs = [("text", 1, ""), ("text", 16, ""), ("text", 0, ""), ("random", 0, ""), ("zeros", 0, "")]
 if len(sys.argv) > 1:
     cfgs = [(a.split(":") + [""])[:3] for a in sys.argv[1:]]
 for kind, mc, opt in cfgs:
-    fl = D.DMX_ZLIB | D.DMX_F_LAZY | (D.DMX_F_DICT if "d" in opt else 0)
+    fl = D.DMX_ZLIB | (0 if "g" in opt else D.DMX_F_LAZY) | (D.DMX_F_DICT if "d" in opt else 0)
     run(kind, 20_000_000 if kind == "text" else 64 << 20, int(mc), fl)
