@@ -17,6 +17,11 @@ VARIANTS = {
     "nosc1": [("            L.sorted[dst] = (uint16_t)x;\n            D2[dst] = (uint8_t)(h >> 7);\n", "")],
     "nosc2": [("            if (valid) L.sorted[dst] = (uint16_t)p;\n", "            if (valid && dst == 0xFFFFu) L.sorted[0] = (uint16_t)p;\n")],
     "norank": [("    if (!RUNCHK) return valid ? atomicAdd(&T[v], 1u) : 0u;", "    if (!RUNCHK) return valid ? ((T[v] + (threadIdx.x & 63)) & 32767u) : 0u;")],
+    # walk: the distance permute's random reads (winner entries) and scatter stores
+    "noperm_rd": [("                    else if (jj) dist = ((pw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu) - (uint32_t)L.sorted[kk - jj];",
+                   "                    else if (jj) dist = jj;")],
+    "noperm_st": [("                    L.sorted[(pw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu] = (uint16_t)(dw[e >> 1] >> (16 * (e & 1)));",
+                   "                    L.sorted[kk] = (uint16_t)(dw[e >> 1] >> (16 * (e & 1)));")],
 }
 
 def build():
@@ -59,7 +64,7 @@ def one(name):
         out, r = e.compress_tensor(t)
     st = e.stamps(r.nblocks).astype(np.float64)
     e.close()
-    print(json.dumps({"p0": round(st[:, 0].mean() / 1e3, 1), "pass1_end": round(st[:, 9].mean() / 1e3, 1),
+    print(json.dumps({"w1": round(st[:, 5].mean() / 1e3, 1), "walk": round(st[:, 2].mean() / 1e3, 1), "p0": round(st[:, 0].mean() / 1e3, 1), "pass1_end": round(st[:, 9].mean() / 1e3, 1),
                       "pass2_end": round(st[:, 10].mean() / 1e3, 1), "search": round(st[:, 1].mean() / 1e3, 1),
                       "total": round(st[:, 7].mean() / 1e3, 1)}))
 
