@@ -81,6 +81,9 @@ def parse_args(argv=None):
                     help="run the pipelined gather loop at N = 1 too (single-rank process group; tests the path)")
     ap.add_argument("--cpu-budget", type=float, default=8.0,
                     help="seconds per CPU baseline leg (0 = skip the CPU legs)")
+    ap.add_argument("--real-text", type=int, default=1,
+                    help="N = 1, text workload: also encode the reference's corpus tiled to 100 MB "
+                         "(reported under 'real_text'; 0 = skip)")
     ap.add_argument("--long-run", type=float, default=1.0,
                     help="N = 1: after the timed steps, time further steps for about this many seconds "
                          "(reported under 'long_run'; 0 = skip)")
@@ -159,43 +162,48 @@ def cpu_info():
         aff = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         aff = os.cpu_count()
-    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or aff
-    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity": aff, "threads": threads}
+    share = int(os.environ.get("OMP_NUM_THREADS") or 0) or aff
+    # the CPU legs run on every core this process may use (SURVEY §8d ii: all cores); the
+    # box's nominal share (OMP_NUM_THREADS) is reported as a second figure
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity": aff, "threads": aff, "share_threads": share}
 
 
 def cpu_baselines(data, args, budget_s: float):
     """CPU legs on rank 0 (SURVEY §8d ii), on the GPU box's host cores, in the same run:
       same_parse  -- oracle/dmx_oracle.c (C port of the reference parse + our Huffman/emitter)
-                     with the GPU line's parse flags, blocks in parallel on all the threads the
-                     box gives this job (OpenMP; OMP_NUM_THREADS), over the workload in pieces
-                     until the budget is spent;
-      exhaustive  -- the same port with the reference's own exhaustive parse, all threads: its
-                     size over the whole input is S_ref, the size the GPU stream is compared with;
+                     with the GPU line's parse flags, blocks in parallel on every core of the
+                     process's affinity (OpenMP), over the whole workload when the budget allows
+                     (else a bounded sample); its stream over the whole input is kept as the
+                     full-size parity witness of the GPU stream;
+      share       -- the same leg on the box's nominal CPU share (OMP_NUM_THREADS), a sample;
+      exhaustive  -- the same port with the reference's own exhaustive parse, all cores: its
+                     stream over the whole input is S_ref, the size the GPU stream is compared
+                     with, and the parity witness of the GPU's exhaustive stream;
       reference   -- the reference encoder itself (oracle/_ref, built from /root/reference's own
                      sources), one process per 32 KiB block, 1 core, with its per-token estimator
                      (only where it was built).
     """
     from oracle import oracle as O
     info = cpu_info()
-    thr = info["threads"]
     out = {}
     n = int(data.size)
     sw = 32768
 
-    def leg(max_chain, lazy, split, dct, store, budget, name):
+    def leg(max_chain, lazy, split, dct, store, budget, name, thr, want_full):
         kw = dict(lazy=lazy, split=split, dict=dct, store_check=store, threads=thr)
         piece = min(n, sw * max(4 * thr, 32))
         t0 = time.perf_counter()
         O.compress_par(data[:piece], sw, max_chain, flags=5, **kw)   # probe: the first piece
         tp = time.perf_counter() - t0
+        z = None
         if piece and tp / piece * n <= 2 * budget:
             # the whole workload in one call: one stream, its exact size
             t0 = time.perf_counter()
             z = O.compress_par(data, sw, max_chain, flags=7, **kw)
             dt = time.perf_counter() - t0
-            done, zb, how = n, len(z), "all"
+            done, how = n, "all"
         else:   # a bounded sample: pieces until the budget is spent (first piece included)
-            done, zb, dt = piece, None, tp
+            done, dt = piece, tp
             while done < n and dt < budget:
                 hi = min(n, done + piece)
                 q0 = time.perf_counter()
@@ -203,21 +211,28 @@ def cpu_baselines(data, args, budget_s: float):
                 dt += time.perf_counter() - q0
                 done = hi
             how = "first"
+            if want_full and tp / piece * n <= 8 * budget:   # the parity witness, untimed
+                z = O.compress_par(data, sw, max_chain, flags=7, **kw)
         return {"value": round(done / dt / 1e9, 6), "unit": "GB/s", "cores": thr, "kind": "port",
                 "sample": f"{how} {done} B of the workload, oracle/dmx_oracle.c {name}, blocks in parallel on "
                           f"{thr} OpenMP threads (dmx_oracle_compress_par)",
-                "cpu_model": info["cpu_model"], "nproc": info["nproc"]}, done, zb
+                "cpu_model": info["cpu_model"], "nproc": info["nproc"]}, done, z
 
     parse = parse_str(args)
-    r, _, _ = leg(args.max_chain, bool(args.lazy), bool(args.split), bool(args.dict), bool(args.store_check),
-                  budget_s, f"compress ({parse}: the GPU line's parse)")
+    same = (args.max_chain, bool(args.lazy), bool(args.split), bool(args.dict), bool(args.store_check))
+    r, _, z = leg(*same, budget_s, f"compress ({parse}: the GPU line's parse)", info["threads"], True)
     r["parse"] = parse
     out["same_parse"] = r
-    r, done, zb = leg(0, False, False, False, False, budget_s,
-                      "compress (the reference's exhaustive greedy parse + Huffman/emitter)")
+    out["same_parse_stream"] = z
+    if info["share_threads"] != info["threads"]:
+        r, _, _ = leg(*same, budget_s / 2, f"compress ({parse}: the GPU line's parse)", info["share_threads"], False)
+        r["parse"] = parse
+        out["share"] = r
+    r, done, z = leg(0, False, False, False, False, budget_s,
+                     "compress (the reference's exhaustive greedy parse + Huffman/emitter)", info["threads"], True)
     r["parse"] = "exhaustive, greedy (reference semantics)"
     out["exhaustive"] = r
-    out["s_ref"] = (done, zb)   # the reference parse's stream over the whole input (None: sampled)
+    out["s_ref_stream"] = z   # the reference parse's stream over the whole input (None: too slow here)
     if O.ref_available():
         t0 = time.perf_counter()
         done = 0
@@ -231,6 +246,49 @@ def cpu_baselines(data, args, budget_s: float):
                                       "1 process at a time, incl. its per-token estimator",
                             "cpu_model": info["cpu_model"]}
     return out, info
+
+
+def real_text_leg(enc_flags, args, dev, local, stream):
+    """Representativeness check: real text instead of the seeded generator -- the
+    reference's own corpus (tests/golden/bee_movie_script.txt, 57 641 B of CRLF text) tiled to
+    100 MB and cut into independent 32 KiB blocks (every block starts at a different offset of
+    the corpus), encoded with the bench's parse; GB/s over 5 steps, size vs its own S_ref (the
+    port's exhaustive stream, all cores) and byte parity with the port at the same parse."""
+    import numpy as np
+    import torch
+    import deflate_compression_amd as D
+    from oracle import oracle as O
+    bee = np.frombuffer(open(os.path.join(REPO, "tests", "golden", "bee_movie_script.txt"), "rb").read(),
+                        dtype=np.uint8)
+    n = 100_000_000
+    host = np.resize(bee, n)
+    thr = cpu_info()["threads"]
+    e = D.Encoder(local, n, 32768, args.max_chain, enc_flags)
+    try:
+        d_in = torch.from_numpy(host).to(dev)
+        cap = D.max_compressed(n)
+        d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+        e.encode_async(d_in.data_ptr(), n, d_out.data_ptr(), cap, stream)
+        r = e.result(stream)
+        z = d_out[:int(r.out_len)].cpu().numpy().tobytes()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(5):
+            e.encode_async(d_in.data_ptr(), n, d_out.data_ptr(), cap, stream)
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t0) / 5
+    finally:
+        e.close()
+    port = O.compress_par(host, 32768, args.max_chain, lazy=bool(args.lazy), split=bool(args.split),
+                          dict=bool(args.dict), store_check=bool(args.store_check), threads=thr)
+    sref = O.compress_par(host, 32768, 0, threads=thr)
+    return {"value": round(n / dt / 1e9, 3), "unit": "GB/s", "ms_per_step": round(dt * 1e3, 4), "steps": 5,
+            "input": "tests/golden/bee_movie_script.txt (the reference's corpus) tiled to 100 000 000 B, "
+                     "independent 32 KiB blocks", "parse": parse_str(args),
+            "ratio": round(len(z) / n, 5), "s_ref_bytes": len(sref),
+            "size_vs_ref_pct": round((len(z) / len(sref) - 1) * 100, 3),
+            "parity_vs_port": z == port, "inflates": zlib.decompress(z) == host.tobytes(),
+            "nsortfallback_total": int(r.nsortfallback_total)}
 
 
 def end_to_end(host, args):
@@ -454,6 +512,7 @@ def main() -> int:
     out_len = int(res.out_len)
     ok = True
     stitched = None
+    z = None
     if world == 1:
         z = d_out[:out_len].cpu().numpy().tobytes()
         ok = zlib.decompress(z) == host.tobytes()
@@ -548,6 +607,7 @@ def main() -> int:
     stage_ms, nstage = enc.stage_times()
     enc.set_timing(False)
     dt = t1 - t0
+    fb_total = int(enc.result(stream).nsortfallback_total)   # every encode of this context so far
     # a longer run of the same step (outside the timed region): the timed region above is what
     # the driver asked for; this shows the rate holds over about a second of back-to-back steps
     long_run = None
@@ -579,6 +639,7 @@ def main() -> int:
             tradeoff.append({"max_chain": kc, "value": round(n * 5 / (q1 - q0) / 1e9, 3), "unit": "GB/s",
                              "ratio": round(t_len / n, 5), "compressed_bytes": t_len, "steps": 5})
     exh = None
+    exh_stream = None
     if world == 1 and args.max_chain != 0 and args.exhaustive_steps > 0:
         # the reference's own parse (every earlier position of the bucket), same input
         ex = D.Encoder(local, n, 32768, 0, flags & ~(D.DMX_F_LAZY | D.DMX_F_DICT | D.DMX_F_SPLIT | D.DMX_F_STORE_CHECK))
@@ -590,9 +651,12 @@ def main() -> int:
             ex.encode_async(d_in.data_ptr(), n, d_out.data_ptr(), cap, stream)
         torch.cuda.synchronize(dev)
         e1 = time.perf_counter()
+        ex_res = ex.result(stream)
+        exh_stream = d_out[:ex_len].cpu().numpy().tobytes()
         ex.close()
         exh = {"value": round(n * args.exhaustive_steps / (e1 - e0) / 1e9, 3), "unit": "GB/s",
-               "ratio": round(ex_len / n, 5), "compressed_bytes": ex_len, "steps": args.exhaustive_steps}
+               "ratio": round(ex_len / n, 5), "compressed_bytes": ex_len, "steps": args.exhaustive_steps,
+               "nsortfallback_total": int(ex_res.nsortfallback_total)}
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -646,7 +710,7 @@ def main() -> int:
                         "source": f"SQ_INSTS_VALU per block from {ctr['source']} x this launch's parsed blocks, "
                                   "divided by this run's HIP-event launch time"}
         cpu, info = ({}, cpu_info())
-        e2e = zl6 = None
+        e2e = zl6 = real = None
         if world == 1 and args.cpu_budget > 0:
             cpu, info = cpu_baselines(host, args, args.cpu_budget)
             try:
@@ -654,13 +718,33 @@ def main() -> int:
             except Exception as e:  # pragma: no cover
                 log("end-to-end fd API leg failed:", e)
             zl6 = len(zlib.compress(host.tobytes(), 6))   # context: zlib -6 on the same input
+            if args.real_text and args.workload == "text":
+                real = real_text_leg(flags, args, dev, local, stream)
+                if not (real["parity_vs_port"] and real["inflates"]):
+                    log("ERROR: real-text stream differs from the port's or does not inflate")
+                    ok = False
         base = cpu.get("same_parse")
         size_pct = s_ref_bytes = None
-        if "s_ref" in cpu and cpu["s_ref"][0] == n and cpu["s_ref"][1]:
-            s_ref_bytes = cpu["s_ref"][1]
+        # full-size parity witness: the port's stream at the GPU line's exact parse,
+        # over the whole input, must equal the GPU stream byte for byte; a mismatch fails the run
+        parity = parity_exh = None
+        if cpu.get("same_parse_stream") is not None and z is not None:
+            parity = cpu["same_parse_stream"] == z
+            if not parity:
+                log("ERROR: GPU stream differs from the CPU port's stream at the same parse")
+                ok = False
+        sref = cpu.get("s_ref_stream")
+        if sref is not None:
+            s_ref_bytes = len(sref)
             size_pct = round((out_len / s_ref_bytes - 1) * 100, 3)
             for t in tradeoff:
                 t["size_vs_ref_pct"] = round((t["compressed_bytes"] / s_ref_bytes - 1) * 100, 3)
+            if exh_stream is not None:
+                parity_exh = exh_stream == sref
+                exh["parity_vs_port"] = parity_exh
+                if not parity_exh:
+                    log("ERROR: GPU exhaustive stream differs from the CPU port's (the reference parse)")
+                    ok = False
         line = {
             "metric": "encode GB/s (uncompressed in) + compression ratio vs CPU ref, 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -684,6 +768,8 @@ def main() -> int:
                                + (", pipelined" if pipelined else ""),
             },
             "ratio": round(out_len / n, 5),
+            "parity_vs_port": parity,
+            "nsortfallback": fb_total,
             "size_vs_ref_pct": size_pct,
             "s_ref_bytes": s_ref_bytes,
             "exhaustive": exh,
@@ -716,7 +802,9 @@ def main() -> int:
             "zlib6": None if zl6 is None else {"ratio": round(zl6 / n, 5), "compressed_bytes": zl6,
                                                  "ours_vs_zlib6_pct": round((out_len / zl6 - 1) * 100, 3)},
             "cpu_baseline": base,
+            "cpu_baseline_share": cpu.get("share"),
             "cpu_baseline_exhaustive": cpu.get("exhaustive"),
+            "real_text": real,
             "cpu_baseline_reference": cpu.get("reference"),
             "host": info,
         }

@@ -23,7 +23,7 @@ import struct
 __all__ = [
     "DeflateError", "Opts", "Result", "Encoder", "lib", "compress", "deflate_compress",
     "deflate_decompress", "max_compressed", "adler32_combine", "gen_text", "gen_random",
-    "COMPRESS_STATS", "E", "DMX_F_HEADER", "DMX_F_TRAILER", "DMX_F_FINAL", "DMX_ZLIB", "DMX_F_LAZY", "DMX_F_EXACT_SORT", "DMX_F_SPLIT", "DMX_F_DICT", "DMX_F_STORE_CHECK", "inflate_gpu",
+    "COMPRESS_STATS", "E", "DMX_F_HEADER", "DMX_F_TRAILER", "DMX_F_FINAL", "DMX_ZLIB", "DMX_F_LAZY", "DMX_F_EXACT_SORT", "DMX_F_SPLIT", "DMX_F_DICT", "DMX_F_STORE_CHECK", "inflate_gpu", "ref_estimates",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -69,7 +69,8 @@ class Result(ctypes.Structure):
     _fields_ = [("out_len", ctypes.c_uint64), ("end_bits", ctypes.c_uint64), ("n", ctypes.c_uint64),
                 ("ntokens", ctypes.c_uint64), ("adler", ctypes.c_uint32), ("status", ctypes.c_int32),
                 ("nblocks", ctypes.c_uint32), ("nstored", ctypes.c_uint32), ("nfixed", ctypes.c_uint32),
-                ("ndynamic", ctypes.c_uint32), ("pad", ctypes.c_uint32 * 2)]
+                ("ndynamic", ctypes.c_uint32), ("nsortfallback", ctypes.c_uint32),
+                ("nsortfallback_total", ctypes.c_uint32)]
 
 
 class _StringLen(ctypes.Structure):
@@ -124,6 +125,9 @@ def lib() -> ctypes.CDLL:
         "dmx_inflate_async": ([vp, u64, vp, u32, vp, u64, vp, vp], ctypes.c_int),
         "dmx_gen_text": ([vp, u64, u64], None),
         "dmx_gen_random": ([vp, u64, u64], None),
+        "dmx_refest_create": ([], vp),
+        "dmx_refest_destroy": ([vp], None),
+        "dmx_refest_feed": ([vp, u32p, u32, vp, u32p], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -224,6 +228,27 @@ def inflate_gpu(z, out_cap: int, index=None, nblk: int = 0, stream=None):
 def fault_set(spec: str | None) -> int:
     """Fault injection (tests): "malloc:N" / "launch:N" / None (dmx_fault_set)."""
     return int(lib().dmx_fault_set(spec.encode() if spec else None))
+
+
+def ref_estimates(tokens, state=None):
+    """The reference's estimate fields (tree_bits, ll_bits, d_bits) of every token's
+    compress_stats record (deflate_compress.c:290-298), from libdmx's host restatement of its
+    adaptive Huffman trees (csrc/dmx_refstats.c).  tokens: uint32 (byte | dist << 9 | len) in
+    stream order.  Returns int32[ntok, 3].  Pure host code: no GPU needed."""
+    import numpy as np
+    t = np.ascontiguousarray(tokens, dtype=np.uint32)
+    L = lib()
+    e = L.dmx_refest_create() if state is None else state
+    rec = np.zeros((t.size, 6), dtype=np.int32)
+    nf = ctypes.c_uint32(0)
+    try:
+        r = L.dmx_refest_feed(e, t.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), t.size,
+                              ctypes.c_void_p(rec.ctypes.data), ctypes.byref(nf))
+    finally:
+        if state is None:
+            L.dmx_refest_destroy(e)
+    _check(r, "dmx_refest_feed")
+    return rec[:, 1:4].copy()
 
 
 def adler32_combine(a: int, b: int, len_b: int) -> int:

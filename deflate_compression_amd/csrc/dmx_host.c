@@ -10,6 +10,7 @@
  * longjmps.  There is no CPU encode path: the encode runs on the GPU or fails.
  */
 #include <errno.h>
+#include <limits.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -100,69 +101,94 @@ static void h_dist_sym(int dist, int* sym, int* eb) {
     *eb = e - 1;
 }
 
-/* One compress_stats record per token (deflate_compress.c:290-309), with the reference's
- * accumulation: in the reference ll_bits / d_bits are the adaptive-Huffman scores of every
- * token so far (ll_aht.score / d_aht.score, :297-298, aht.c:239-277) and tree_bits the cost
- * of describing the current codes (h_tree_d_lens + the code-length tree, :292-295), so
- * (tree_bits + ll_bits + d_bits) / bytes is the stream's rate so far.  Here the same sums
- * are exact instead of estimated, over the whole stream:
- *   tree_bits = header bits of every DEFLATE block begun so far (its own included: BFINAL /
- *               BTYPE, and for dynamic blocks the code-length and code descriptions);
- *   ll_bits   = lit/len code bits + length extra bits of every token so far (stored blocks:
- *               8 per byte);
- *   d_bits    = distance code bits + distance extra bits of every match so far.
- * With DMX_F_SPLIT an sw block holds up to four DEFLATE blocks, each with its own codes.
- * (Round 1 restarted the sums at every block) */
+/* One compress_stats record per token (deflate_compress.c:290-309): bytes = 1 + the token's
+ * input offset, ll / d = the token.  The *_bits fields (DMX_STATS, include/dmx.h):
+ *   "ref" (default): the reference's estimates -- its adaptive-Huffman scores ll_aht.score /
+ *       d_aht.score (:297-298, aht.c:239-277) and the cost of describing the current codes
+ *       (h_tree_d_lens + the code-length tree, :292-295), restated in dmx_refstats.c and
+ *       running over the whole stream as the reference's trees do;
+ *   "exact": this stream's exact costs, over the whole stream --
+ *       tree_bits = header bits of every DEFLATE block begun so far (its own included:
+ *                   BFINAL / BTYPE, and for dynamic blocks the code-length and code
+ *                   descriptions; with DMX_F_SPLIT an sw block holds up to four),
+ *       ll_bits   = lit/len code bits + length extra bits of every token so far (stored
+ *                   blocks: 8 per byte),
+ *       d_bits    = distance code bits + distance extra bits of every match so far.
+ * The fields are int (deflate_ext.h:19-31).  A record whose bytes or *_bits would exceed
+ * INT_MAX is never written: the records before it are, and the call returns -E_RANGE. */
 static int write_stats(dmx_ctx* c, int fd, uint64_t n, int sw) {
     const uint32_t nblk = (uint32_t)((n + (uint64_t)sw - 1) / (uint64_t)sw);
     if (!nblk) return 0;
+    const char* mode = getenv("DMX_STATS");
+    const int exact = mode && strcmp(mode, "exact") == 0;
+    if (mode && *mode && !exact && strcmp(mode, "ref") != 0) return -E_INVAL;
     uint32_t* tok = (uint32_t*)malloc(sizeof(uint32_t) * DMX_BLK);
     struct compress_stats* rec = (struct compress_stats*)malloc(sizeof(struct compress_stats) * DMX_BLK);
+    dmx_refest* est = exact ? NULL : dmx_refest_create();
     int r = 0;
-    long long tree_bits = 0, ll_bits = 0, d_bits = 0;   /* over the whole stream */
-    if (!tok || !rec) r = -E_MALLOC;
+    long long tree_bits = 0, ll_bits = 0, d_bits = 0;   /* exact: over the whole stream */
+    if (!tok || !rec || (!exact && !est)) r = -E_MALLOC;
     for (uint32_t b = 0; !r && b < nblk; b++) {
         int nt = dmx_last_tokens(c, b, tok, DMX_BLK);
         if (nt < 0) { r = nt; break; }
+        uint32_t lim = (uint32_t)nt;   /* records of this block that fit the int fields */
         uint64_t pos = (uint64_t)b * (uint64_t)sw;
-        int nsub = 1;
-        for (int sb = 0; !r && sb < nsub; sb++) {
-            uint8_t lens[316];
-            uint32_t range[2], bt = 0, hb = 0;
-            nsub = dmx_last_subblock(c, b, (uint32_t)sb, range, &bt, &hb, lens);
-            if (nsub < 0) { r = nsub; break; }
-            tree_bits += bt == 2 ? (long long)hb : 3;
-            for (uint32_t k = range[0]; k < range[1]; k++) {
-                uint32_t t = tok[k];
-                struct compress_stats* cs = rec + k;
-                cs->bytes = (int)(pos + 1);
-                cs->tree_bits = (int)tree_bits;
-                if ((t >> 9) == 0) {
-                    cs->ll = (int)(t & 0xFF);
-                    cs->d = 0;
-                    ll_bits += bt == 0 ? 8 : (long long)lens[t & 0xFF];
-                    pos += 1;
-                } else {
-                    int len = (int)(t & 0x1FF), dist = (int)(t >> 9), sy, eb;
-                    cs->ll = len;
-                    cs->d = dist;
-                    if (bt == 0) {          /* stored block: the bytes themselves */
-                        ll_bits += 8 * len;
-                    } else {
-                        h_len_sym(len, &sy, &eb);
-                        ll_bits += lens[sy] + eb;
-                        h_dist_sym(dist, &sy, &eb);
-                        d_bits += lens[DMX_DIST0 + sy] + eb;
-                    }
-                    pos += (uint64_t)len;
-                }
-                cs->ll_bits = (int)ll_bits;
-                cs->d_bits = (int)d_bits;
+        for (uint32_t k = 0; k < (uint32_t)nt; k++) {
+            const uint32_t t = tok[k];
+            if (pos + 1 > (uint64_t)INT_MAX) { lim = k; break; }
+            rec[k].bytes = (int)(pos + 1);
+            if ((t >> 9) == 0) {
+                rec[k].ll = (int)(t & 0xFF);
+                rec[k].d = 0;
+                pos += 1;
+            } else {
+                rec[k].ll = (int)(t & 0x1FF);
+                rec[k].d = (int)(t >> 9);
+                pos += t & 0x1FF;
             }
         }
-        if (!r) r = write_all(fd, rec, sizeof(struct compress_stats) * (uint64_t)nt);
+        if (!exact) {
+            uint32_t nf = 0;
+            const int e = dmx_refest_feed(est, tok, lim, rec, &nf);
+            if (e && e != -E_RANGE) { r = e; break; }
+            lim = nf;
+        } else {
+            int nsub = 1;
+            for (int sb = 0; !r && sb < nsub; sb++) {
+                uint8_t lens[316];
+                uint32_t range[2], bt = 0, hb = 0;
+                nsub = dmx_last_subblock(c, b, (uint32_t)sb, range, &bt, &hb, lens);
+                if (nsub < 0) { r = nsub; break; }
+                tree_bits += bt == 2 ? (long long)hb : 3;
+                for (uint32_t k = range[0]; k < range[1] && k < lim; k++) {
+                    const uint32_t t = tok[k];
+                    if ((t >> 9) == 0) {
+                        ll_bits += bt == 0 ? 8 : (long long)lens[t & 0xFF];
+                    } else {
+                        const int len = (int)(t & 0x1FF), dist = (int)(t >> 9);
+                        int sy, eb;
+                        if (bt == 0) {          /* stored block: the bytes themselves */
+                            ll_bits += 8 * len;
+                        } else {
+                            h_len_sym(len, &sy, &eb);
+                            ll_bits += lens[sy] + eb;
+                            h_dist_sym(dist, &sy, &eb);
+                            d_bits += lens[DMX_DIST0 + sy] + eb;
+                        }
+                    }
+                    if (tree_bits > INT_MAX || ll_bits > INT_MAX || d_bits > INT_MAX) { lim = k; break; }
+                    rec[k].tree_bits = (int)tree_bits;
+                    rec[k].ll_bits = (int)ll_bits;
+                    rec[k].d_bits = (int)d_bits;
+                }
+            }
+            if (r) break;
+        }
+        r = write_all(fd, rec, sizeof(struct compress_stats) * (uint64_t)lim);
+        if (!r && lim < (uint32_t)nt) r = -E_RANGE;
     }
     free(tok); free(rec);
+    dmx_refest_destroy(est);
     return r;
 }
 

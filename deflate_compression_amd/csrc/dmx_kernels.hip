@@ -1241,7 +1241,8 @@ __device__ __forceinline__ const uint8_t* hist_of(const uint8_t* in, uint32_t sw
 
 __global__ __launch_bounds__(MT) void dmx_chain_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
                                                        const uint8_t* __restrict__ pre, uint32_t npre,
-                                                       uint16_t* __restrict__ chs, uint16_t* __restrict__ che) {
+                                                       uint16_t* __restrict__ chs, uint16_t* __restrict__ che,
+                                                       uint32_t* __restrict__ nfallback) {
     __shared__ MatchLDS L;
     __shared__ uint64_t tp0[3];
     const uint32_t tid = threadIdx.x;
@@ -1280,6 +1281,7 @@ __global__ __launch_bounds__(MT) void dmx_chain_kernel(const uint8_t* __restrict
             }
         }
         if (!__syncthreads_or(bad) || attempt) break;
+        if (tid == 0) atomicAdd(nfallback, 1u);
     }
     for (uint32_t k = tid; k < (nv + 7) / 8; k += MT)   // 8 entries per 16-byte store
         reinterpret_cast<uint4*>(S)[k] = reinterpret_cast<const uint4*>(L.sorted)[k];
@@ -1762,7 +1764,8 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
                                                        int32_t max_chain, uint32_t mflags, uint16_t* __restrict__ dist_g,
                                                        const uint16_t* __restrict__ chs, uint32_t* __restrict__ tok_g,
                                                        uint32_t* __restrict__ hist_g,
-                                                       dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg) {
+                                                       dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg,
+                                                       uint32_t* __restrict__ nfallback) {
     __shared__ MatchLDS L;
     __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def, tp0[3], st_rounds, st_p3a, st_h4[3];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = wave_of(tid);
@@ -1890,6 +1893,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         for (uint32_t pass = 0;; pass++) {   // 3-byte grams from P0's sort (checked here)
             npass++;
             if (!__syncthreads_or(gram_pass<3>(L, nv, tid, seeds, ndefer, tsw)) || pass) break;
+            if (tid == 0) atomicAdd(nfallback, 1u);   // counted in dmx_result.nsortfallback
             sort_positions<true>(L, bn, max_chain, tid, false, tp0);   // never observed on gfx950
         }
         if constexpr (NBX > 4) {   // 4-byte grams from a 4-byte sort
@@ -1898,6 +1902,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
                 if (hook || pass) sort_positions<true, true, 4>(L, bn, max_chain, tid, false, tp0);
                 else sort_positions<false, true, 4>(L, bn, max_chain, tid, false, tp0);
                 if (!__syncthreads_or(gram_pass<4>(L, nv, tid, seeds, ndefer, tsw)) || pass || hook) break;
+                if (tid == 0) atomicAdd(nfallback, 1u);
             }
         }
         if (dbg && tid == 0) st_h4[0] = (__builtin_amdgcn_s_memtime() - tbeg) | ((uint64_t)npass << 48);
@@ -1932,7 +1937,9 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         }
         __syncthreads();
         if (!L.sortbad || attempt) break;
-        // never observed on gfx950: redo the block with the match-any sort (stable by construction)
+        // never observed on gfx950: redo the block with the match-any sort (stable by construction);
+        // counted (dmx_result.nsortfallback) so that every run shows it did not happen
+        if (tid == 0) atomicAdd(nfallback, 1u);
         if (h4) sort_positions<true, true, (h4 ? NBX : 3)>(L, bn, max_chain, tid, dbg != nullptr, tp0);
         else sort_positions<true>(L, bn, max_chain, tid, dbg != nullptr, tp0);
     }
@@ -3013,7 +3020,8 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_tile_kernel(dmx_blkinfo* _
 
 __global__ __launch_bounds__(ST) void dmx_scan_kernel(ScanTile* __restrict__ tiles, uint32_t nblk, uint64_t n,
                                                       uint32_t flags, uint64_t out_cap,
-                                                      uint32_t* __restrict__ out32, dmx_result* __restrict__ res) {
+                                                      uint32_t* __restrict__ out32, dmx_result* __restrict__ res,
+                                                      uint32_t* __restrict__ nfallback) {
     __shared__ Mono wtot[ST / 64];
     __shared__ Mono carry_s;
     __shared__ uint64_t red[ST / 64][5];
@@ -3097,6 +3105,10 @@ __global__ __launch_bounds__(ST) void dmx_scan_kernel(ScanTile* __restrict__ til
         res->nstored = (uint32_t)ns;
         res->nfixed = (uint32_t)nf;
         res->ndynamic = nblk - (uint32_t)ns - (uint32_t)nf;
+        res->nsortfallback = nfallback[0];   // this encode's sort fallbacks; zeroed for the next
+        nfallback[1] += nfallback[0];       // and the context's running total
+        res->nsortfallback_total = nfallback[1];
+        nfallback[0] = 0;
         s_end = end;
         s_T = T;
         s_adler = adler;
@@ -3384,6 +3396,7 @@ struct dmx_ctx {
     dmx_blkinfo* info;
     ScanTile* tiles;  // cap_blocks / SCAN_TILE + 1: per-tile aggregates and prefixes (scan)
     dmx_result* res;
+    uint32_t* nfb;        // [0] sort fallbacks of the encode in flight (kernels add, K3's scan reads and zeroes), [1] total
     uint64_t* dbg;        // optional per-block phase stamps (DMX_STAMPS=1)
     uint64_t dbg_cap;
     // last encode (introspection)
@@ -3435,19 +3448,21 @@ extern "C" int dmx_fault_set(const char* spec) {
         if (n <= 0) return -(int)E_RANGE;
     }
     pthread_mutex_lock(&g_fault_mu);
-    g_fault_kind = kind;
     g_fault_left = n;
+    __atomic_store_n(&g_fault_kind, kind, __ATOMIC_RELEASE);
     pthread_mutex_unlock(&g_fault_mu);
     return 0;
 }
 __attribute__((constructor)) static void dmx_fault_env(void) { (void)dmx_fault_set(getenv("DMX_FAULT")); }
 static bool fault_hit(int kind) {
-    if (!g_fault_kind) return false;
+    // several host threads allocate and launch at once (dmx_encode_fd_multi): the unlocked
+    // fast-path read is atomic, the update under the lock
+    if (!__atomic_load_n(&g_fault_kind, __ATOMIC_ACQUIRE)) return false;
     pthread_mutex_lock(&g_fault_mu);
     bool hit = false;
     if (g_fault_kind == kind && g_fault_left > 0 && --g_fault_left == 0) {
         hit = true;
-        g_fault_kind = 0;
+        __atomic_store_n(&g_fault_kind, 0, __ATOMIC_RELEASE);
     }
     pthread_mutex_unlock(&g_fault_mu);
     return hit;
@@ -3553,6 +3568,10 @@ extern "C" int dmx_ctx_create(int device, uint64_t max_input, dmx_ctx** out) {
     c->device = device;
     if (hip_fail(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate")) { c->stream = NULL; dmx_ctx_destroy(c); return -(int)E_DEVICE; }
     if (hip_fail(dmx_malloc(&c->res, sizeof(dmx_result)), "hipMalloc(res)")) { dmx_ctx_destroy(c); return -(int)E_DEVICE; }
+    if (hip_fail(dmx_malloc(&c->nfb, 16), "hipMalloc(nfb)") || hip_fail(hipMemset(c->nfb, 0, 16), "hipMemset(nfb)")) {
+        dmx_ctx_destroy(c);
+        return -(int)E_DEVICE;
+    }
     for (int j = 0; j < DMX_EV_RING; j++)
         for (int k = 0; k < 6; k++) (void)hipEventCreate(&c->ev[j][k]);
     const uint64_t nb = (max_input + DMX_BLK - 1) / DMX_BLK;
@@ -3588,6 +3607,7 @@ extern "C" void dmx_ctx_destroy(dmx_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     ctx_free_ws(c);
     if (c->res) (void)hipFree(c->res);
+    if (c->nfb) (void)hipFree(c->nfb);
     if (c->dbg) (void)hipFree(c->dbg);
     if (c->d_in) (void)hipFree(c->d_in);
     if (c->d_out) (void)hipFree(c->d_out);
@@ -3660,7 +3680,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         // the dict's) and the history search; otherwise the match kernel sorts its own block
         if (o.flags & DMX_F_DICT) {
             hipLaunchKernelGGL(dmx_chain_kernel, dim3(nblk + 1), dim3(MT), 0, s, (const uint8_t*)d_in, n,
-                               (uint32_t)o.sw, (const uint8_t*)o.dict, dict_len, c->chs, c->che);
+                               (uint32_t)o.sw, (const uint8_t*)o.dict, dict_len, c->chs, c->che, c->nfb);
             hipLaunchKernelGGL((o.max_chain >= 1 && o.max_chain <= 6) ? dmx_hist_kernel_t<6> : dmx_hist_kernel_t<8>,
                                dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw,
                                o.max_chain, (const uint8_t*)o.dict, dict_len, c->chs, c->che, c->tok, dbg);
@@ -3675,13 +3695,13 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                              ((o.flags & DMX_F_STORE_CHECK) ? 4u : 0u) | (dstop ? ((uint32_t)atoi(dstop) & 3u) << 8 : 0u);
         if (o.flags & DMX_F_DICT)
             hipLaunchKernelGGL(dmx_match_kernel<true>, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n,
-                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg);
+                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb);
         else if (o.max_chain == 0)
             hipLaunchKernelGGL((dmx_match_kernel<false, DMX_NBX>), dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n,
-                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg);
+                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb);
         else
             hipLaunchKernelGGL(dmx_match_kernel<false>, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n,
-                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg);
+                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb);
         if (ev) (void)hipEventRecord(ev[2], s);
         if (o.flags & DMX_F_SPLIT)
             {
@@ -3706,7 +3726,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         hipLaunchKernelGGL(dmx_scan_tile_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, n, (uint32_t)o.sw,
                            c->tiles);
     hipLaunchKernelGGL(dmx_scan_kernel, dim3(1), dim3(ST), 0, s, c->tiles, nblk, n, o.flags, out_cap,
-                       (uint32_t*)d_out, c->res);
+                       (uint32_t*)d_out, c->res, c->nfb);
     if (nblk)
         hipLaunchKernelGGL(dmx_scan_apply_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, o.flags, c->tiles,
                            (uint32_t*)d_out, (const dmx_result*)c->res);
@@ -4261,21 +4281,24 @@ static void* multi_worker(void* a) {
 }
 
 // DMX_DEVICES: "0,1,2,3" (a device may repeat: one context each) or "all"; the number of
-// entries written to devs, 0 when unset or empty.
+// entries written to devs, 0 when unset or empty; -E_INVAL for a malformed list, -E_RANGE
+// for more than cap entries, -E_NEXIST when "all" finds no device.
 extern "C" int dmx_devices_from_env(int* devs, int cap) {
     const char* e = getenv("DMX_DEVICES");
     if (!e || !*e) return 0;
     if (!strcmp(e, "all")) {
         int nd = 0;
-        if (hipGetDeviceCount(&nd) != hipSuccess || nd <= 0) return 0;
-        for (int k = 0; k < nd && k < cap; k++) devs[k] = k;
-        return nd < cap ? nd : cap;
+        if (hipGetDeviceCount(&nd) != hipSuccess || nd <= 0) return -(int)E_NEXIST;
+        if (nd > cap) return -(int)E_RANGE;
+        for (int k = 0; k < nd; k++) devs[k] = k;
+        return nd;
     }
     int n = 0;
-    for (const char* p = e; *p && n < cap;) {
+    for (const char* p = e; *p;) {
         char* end = NULL;
         const long v = strtol(p, &end, 10);
         if (end == p) return -(int)E_INVAL;
+        if (n == cap) return -(int)E_RANGE;
         devs[n++] = (int)v;
         p = *end == ',' ? end + 1 : end;
         if (*end && *end != ',') return -(int)E_INVAL;
@@ -4290,6 +4313,9 @@ extern "C" int dmx_encode_fd_multi(int fd_in, int fd_out, const dmx_opts* opts, 
     if (hipGetDeviceCount(&nd) != hipSuccess || nd <= 0) return -(int)E_NEXIST;
     for (int w = 0; w < ndev; w++)
         if (devices[w] < 0 || devices[w] >= nd) return -(int)E_RANGE;
+    // one device: the single-device streaming path (read-ahead and writer threads overlap
+    // the encode), not one worker doing every step in turn
+    if (ndev == 1) return encode_fd_on(devices[0], fd_in, fd_out, opts, chunk);
     dmx_opts o = {0, 0, DMX_ZLIB, 0, NULL, 0};
     if (opts) o = *opts;
     if (o.sw == 0) o.sw = DMX_BLK;

@@ -61,10 +61,20 @@ int deflate_decompress(struct string_len* decompr_dat, struct string_len* compr_
 
 /* deflate_ext.h:19-31 -- per-token record written to fd_stats.
  * bytes = 1 + input offset of the token; ll/d = literal byte (d == 0) or length/
- * distance.  The reference's *_bits fields were adaptive-Huffman running
- * estimates; here they are the exact costs of the block the token is in:
- * tree_bits = header bits of the block, ll_bits / d_bits = running lit/len and
- * distance bits (codes + extra bits) inside the block up to this token. */
+ * distance.  The *_bits fields depend on DMX_STATS in the environment:
+ *   unset / "ref"  the reference's own estimates (deflate_compress.c:290-298): tree_bits =
+ *                  the code-length description cost of its adaptive Huffman trees
+ *                  (h_tree.c:75-148) + the code-length code's weighted depth (:242-302),
+ *                  ll_bits / d_bits = the adaptive trees' scores after this token
+ *                  (aht.c:239-277), running over the whole stream as in the reference.
+ *                  Same records as the reference for the same tokens (dmx_refest_*).
+ *   "exact"        exact costs of this stream, running over the whole stream: tree_bits =
+ *                  header bits of every DEFLATE block begun so far (its own included),
+ *                  ll_bits = lit/len code + length extra bits of every token so far (8 per
+ *                  byte in stored blocks), d_bits = distance code + extra bits so far.
+ * The fields are int, as in the reference: deflate_compress returns -E_RANGE, after the
+ * complete stream to fd_out and every record before it, at the first record whose bytes
+ * or *_bits would exceed INT_MAX (inputs past 2 GiB, or about 2^31 bits of running sum). */
 struct compress_stats {
     int bytes;
     int tree_bits;
@@ -158,7 +168,11 @@ typedef struct {
     int32_t status;     /* 0 or -E_* */
     uint32_t nblocks;
     uint32_t nstored, nfixed, ndynamic;
-    uint32_t pad[2];
+    uint32_t nsortfallback; /* blocks of this encode whose lane-ordered radix sort failed its
+                               order check and were re-sorted with the match-any grouping
+                               (DESIGN.md §3); the DMX_F_EXACT_SORT test hook forces one per
+                               searched block */
+    uint32_t nsortfallback_total; /* the same, summed over every encode of the context */
 } dmx_result;
 
 typedef struct dmx_ctx dmx_ctx;
@@ -264,6 +278,19 @@ int dmx_ctx_stage_times(dmx_ctx* ctx, double* ms6, uint32_t* count);
 /* Diagnostic: per-block match-kernel phase stamps (cycles) of the last encode, when the
  * process runs with DMX_STAMPS=1: 16 x u64 per block (see dmx_kernels.hip). */
 int dmx_debug_stamps(dmx_ctx* ctx, uint64_t* out16, uint32_t nblk);
+
+/* The reference's estimate fields of struct compress_stats (DMX_STATS=ref, the default of
+ * deflate_compress's fd_stats channel): a host restatement of its two adaptive Huffman trees
+ * and code-length pricing (csrc/dmx_refstats.c).  create() starts a stream (the end-of-block
+ * code counted once, deflate_compress.c:234); feed() takes tokens in stream order (t = byte,
+ * or dist << 9 | len) and fills rec[k].tree_bits / ll_bits / d_bits after token k (the other
+ * fields untouched).  Returns 0, -E_INVAL, or -E_RANGE at the first token whose fields would
+ * exceed INT_MAX or that is not a valid token; *nfilled = records filled.  Host only. */
+typedef struct dmx_refest dmx_refest;
+dmx_refest* dmx_refest_create(void);
+void dmx_refest_destroy(dmx_refest* e);
+int dmx_refest_feed(dmx_refest* e, const uint32_t* tok, uint32_t ntok, struct compress_stats* rec,
+                    uint32_t* nfilled);
 
 /* Adler-32 combine (RFC 1950 math): adler of A||B from adler(A), adler(B), len(B). */
 uint32_t dmx_adler32_combine(uint32_t a, uint32_t b, uint64_t len_b);

@@ -43,6 +43,9 @@
  *    literal  : t = byte                       (t >> 9 == 0)
  *    match    : t = (dist << 9) | len          (1 <= dist <= 32768, 3 <= len <= 258)
  */
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -824,7 +827,12 @@ long long dmx_oracle_compress_par(const uint8_t* in, size_t n, int sw, int max_c
     uint64_t* bits = (uint64_t*)calloc(nblk ? nblk : 1, sizeof(uint64_t));
     int bad = 0;
     if (!bb || !bits) { free(bb); free(bits); return -3; }
-#pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1) if (nthreads != 1)
+#ifdef _OPENMP
+    const int nth = nthreads > 0 ? nthreads : omp_get_max_threads();   /* 0: the OpenMP default */
+#else
+    const int nth = 1;
+#endif
+#pragma omp parallel num_threads(nth) if (nth != 1)
     {
         uint32_t* tok = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)sw);
         orc_plan* P = (orc_plan*)malloc(sizeof(orc_plan));
@@ -838,7 +846,10 @@ long long dmx_oracle_compress_par(const uint8_t* in, size_t n, int sw, int max_c
                       flags & ORC_F_FINAL, tok, P, SP, NULL);
             const uint64_t nb = orc_bitpos(&w);
             orc_align(&w);   /* flush the partial byte into buf */
-            if (w.overflow) bad = 1;
+            if (w.overflow) {
+#pragma omp atomic write
+                bad = 1;
+            }
             bits[b] = nb;
         }
         free(tok);

@@ -7,6 +7,9 @@
  *     it and on single-bit flips at a stride: each call returns 0 or -E_*, never faults;
  *   - dmx_adler32_combine against a direct Adler-32 over split buffers;
  *   - dmx_gen_text / dmx_gen_random determinism;
+ *   - dmx_refest_* (the reference's stats estimates) over 200 000 pseudo-random tokens of
+ *     every kind (literals, lengths 3..258, distances 1..32768, all 30 distance codes, so
+ *     the last split of a full alphabet is exercised) and its invalid-token error;
  *   - the boundary's error paths: deflate_compress without a GPU (-E_NEXIST), sw out of
  *     range (-E_RANGE), spawn / init / deinit.
  * Exit status 0 = no failed check (the sanitizers abort on their own findings).
@@ -87,6 +90,29 @@ int main(int argc, char** argv) {
     dmx_gen_random(buf, 99999, 7);
     dmx_gen_random(b2, 99999, 7);
     if (memcmp(buf, b2, 99999)) { fprintf(stderr, "gen_random not deterministic\n"); fails++; }
+    {
+        enum { NT = 200000 };
+        uint32_t* tk = (uint32_t*)malloc(sizeof(uint32_t) * NT);
+        struct compress_stats* rc = (struct compress_stats*)calloc(NT, sizeof(struct compress_stats));
+        uint64_t x = 0x9E3779B97F4A7C15ull;
+        for (int k = 0; k < NT; k++) {
+            x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+            const uint32_t len = 3 + (uint32_t)(x % 256), dist = 1 + (uint32_t)((x >> 20) % 32768);
+            tk[k] = (x >> 60) < 9 ? (uint32_t)((x >> 8) & 0xFF) : (dist << 9) | len;
+        }
+        dmx_refest* e = dmx_refest_create();
+        uint32_t nf = 0;
+        if (!e || dmx_refest_feed(e, tk, NT, rc, &nf) != 0 || nf != NT || rc[NT - 1].ll_bits <= 0 ||
+            rc[NT - 1].d_bits <= 0 || rc[NT - 1].tree_bits <= 0) {
+            fprintf(stderr, "refest feed\n");
+            fails++;
+        }
+        tk[0] = (40000u << 9) | 5u;
+        if (dmx_refest_feed(e, tk, 1, rc, &nf) != -E_RANGE || nf != 0) { fprintf(stderr, "refest range\n"); fails++; }
+        dmx_refest_destroy(e);
+        free(tk);
+        free(rc);
+    }
     free(buf);
     free(b2);
     /* boundary error paths without a GPU */

@@ -38,8 +38,9 @@ def test_stats_replay_links(built):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("stats", ["ref", "exact"])
 @pytest.mark.parametrize("case", ["bee", "text", "mixed", "sw4096"])
-def test_stats_replay_on_gpu(built, tmp_path, case):
+def test_stats_replay_on_gpu(built, tmp_path, case, stats):
     import deflate_compression_amd as D
     text = D.gen_text(150000, 5).tobytes()
     data = {"bee": open(os.path.join(GOLD, "bee_movie_script.txt"), "rb").read(), "text": text,
@@ -48,6 +49,6 @@ def test_stats_replay_on_gpu(built, tmp_path, case):
     fi = tmp_path / "in"
     fi.write_bytes(data)
     args = [os.path.join(built, "stats_replay"), str(fi)] + (["4096"] if case == "sw4096" else [])
-    p = subprocess.run(args, capture_output=True, text=True, timeout=120)
+    p = subprocess.run(args, capture_output=True, text=True, timeout=120, env=dict(os.environ, DMX_STATS=stats))
     assert p.returncode == 0, p.stdout + p.stderr
     assert "stats_replay ok" in p.stdout

@@ -75,11 +75,22 @@ def oracle_records(data: bytes, sw: int = 32768):
     return np.array(recs, dtype=np.int64).reshape(-1, 6)
 
 
-def _stats(tmp_path, data: bytes, sw: int = 32768):
+def _stats(tmp_path, data: bytes, sw: int = 32768, mode: str | None = "exact", raw: bool = False):
+    """deflate_compress with fd_stats; mode = DMX_STATS (None: unset, the reference's estimates)."""
     fi, fo, fs = tmp_path / "in", tmp_path / "out", tmp_path / "st"
     fi.write_bytes(data)
-    with open(fi, "rb") as a, open(fo, "wb") as b, open(fs, "wb") as c:
-        assert D.deflate_compress(a.fileno(), b.fileno(), c.fileno(), sw, 0) == 0
+    old = os.environ.pop("DMX_STATS", None)
+    if mode is not None:
+        os.environ["DMX_STATS"] = mode
+    try:
+        with open(fi, "rb") as a, open(fo, "wb") as b, open(fs, "wb") as c:
+            assert D.deflate_compress(a.fileno(), b.fileno(), c.fileno(), sw, 0) == 0
+    finally:
+        os.environ.pop("DMX_STATS", None)
+        if old is not None:
+            os.environ["DMX_STATS"] = old
+    if raw:
+        return fo.read_bytes(), fs.read_bytes()
     return fo.read_bytes(), np.frombuffer(fs.read_bytes(), dtype="<i4").reshape(-1, 6).astype(np.int64)
 
 
@@ -101,11 +112,24 @@ def test_stats_records_equal_oracle(tmp_path, case):
     assert 0.9 * (len(z) - 6) * 8 < tot <= (len(z) - 6) * 8
 
 
+@pytest.mark.parametrize("mode", [None, "ref"])
+def test_stats_records_identical_to_reference(tmp_path, golden_cases, mode):
+    """Default fd_stats channel (DMX_STATS unset or "ref"): the whole 24-byte record stream
+    of every golden block is byte-identical to the one the reference's own encoder wrote
+    (tests/golden/manifest.json records_sha256, from oracle/_ref): bytes, the token, and its
+    adaptive-Huffman estimates tree_bits / ll_bits / d_bits (deflate_compress.c:290-309)."""
+    import hashlib
+    man = json.load(open(os.path.join(GOLD, "manifest.json")))["cases"]
+    for name, data in golden_cases.items():
+        _, st = _stats(tmp_path, data, mode=mode, raw=True)
+        assert hashlib.sha256(st).hexdigest() == man[name]["records_sha256"], name
+
+
 def test_stats_last_record_vs_reference_golden(tmp_path, golden_cases):
-    """The reference's own last record of every golden block (tests/golden/manifest.json,
-    written by its encoder): bytes, ll and d are equal; its *_bits fields are adaptive-
-    Huffman estimates without extra bits (aht.c:239-277, h_tree.c:75-148), ours the exact
-    running costs, so only their order of magnitude is compared."""
+    """DMX_STATS=exact against the reference's own last record of every golden block: bytes,
+    ll and d are equal; its *_bits fields are adaptive-Huffman estimates without extra bits
+    (aht.c:239-277, h_tree.c:75-148), the exact mode's the exact running costs, so only their
+    order of magnitude is compared."""
     man = json.load(open(os.path.join(GOLD, "manifest.json")))["cases"]
     for name, data in golden_cases.items():
         _, st = _stats(tmp_path, data)
@@ -114,6 +138,74 @@ def test_stats_last_record_vs_reference_golden(tmp_path, golden_cases):
         ours, theirs = int(st[-1, 1] + st[-1, 2] + st[-1, 3]), last[1] + last[2] + last[3]
         if len(data) >= 1000:   # tiny blocks: the reference's estimate is mostly its tree description
             assert theirs / 3 < ours < 3 * theirs, (name, ours, theirs)
+
+
+def test_stats_ref_mode_multi_block_equals_host_restatement(tmp_path):
+    """Past one window the reference's own encoder breaks; its trees would
+    keep running over the stream.  The default records over a 5-block input equal the host
+    restatement fed with the GPU's tokens in stream order (one tree state), and the
+    bytes / ll / d fields replay the input."""
+    bee = open(os.path.join(GOLD, "bee_movie_script.txt"), "rb").read()
+    data = bee + D.gen_text(90000, 23).tobytes()
+    _, st = _stats(tmp_path, data, mode=None)
+    toks = np.concatenate([O.parse_block(data[o:o + 32768]) for o in range(0, len(data), 32768)])
+    assert st.shape[0] == toks.size
+    assert np.array_equal(st[:, 1:4], D.ref_estimates(toks))
+    assert O.replay(np.where(st[:, 5] == 0, st[:, 4], (st[:, 5] << 9) | st[:, 4]).astype(np.uint32)) == data
+
+
+def test_stats_overflow_returns_range(tmp_path):
+    """compress_stats fields are int (deflate_ext.h:19-31).  300 MB of splitmix64 bytes go out
+    stored (8 bits per byte of ll_bits in the exact mode), so the running ll_bits passes
+    INT_MAX after ~268 MB: deflate_compress writes the whole stream, every record up to the
+    last one that fits, and returns -E_RANGE (never a wrapped, negative record)."""
+    import threading
+    n = 300_000_000
+    data = D.gen_random(n, 0x5EED)
+    fi, fo = tmp_path / "in", tmp_path / "out"
+    data.tofile(fi)
+    rfd, wfd = os.pipe()
+    seen = {"n": 0, "last": None, "bad": None}
+
+    def reader():
+        rec, carry, prev = 24, b"", None
+        with os.fdopen(rfd, "rb", buffering=0) as f:
+            while True:
+                buf = f.read(1 << 24)
+                if not buf:
+                    break
+                buf = carry + buf
+                m = len(buf) // rec
+                carry = buf[m * rec:]
+                a = np.frombuffer(buf[:m * rec], dtype="<i4").reshape(-1, 6).astype(np.int64)
+                if prev is not None:
+                    a2 = np.vstack([prev, a])
+                else:
+                    a2 = a
+                if seen["bad"] is None and ((a < 0).any() or (np.diff(a2[:, 0]) <= 0).any() or
+                                            (np.diff(a2[:, 2]) < 0).any() or (np.diff(a2[:, 1]) < 0).any()):
+                    seen["bad"] = seen["n"]
+                seen["n"] += m
+                prev = a[-1:]
+                seen["last"] = a[-1].copy()
+
+    th = threading.Thread(target=reader)
+    th.start()
+    os.environ["DMX_STATS"] = "exact"
+    try:
+        with open(fi, "rb") as a, open(fo, "wb") as b:
+            rc = D.deflate_compress(a.fileno(), b.fileno(), wfd, 32768, 0)
+    finally:
+        os.environ.pop("DMX_STATS", None)
+        os.close(wfd)
+        th.join()
+    assert rc == -D.E["E_RANGE"], rc
+    assert seen["bad"] is None, seen
+    last = seen["last"]
+    assert 2 ** 31 - 1 - 8 * 258 < last[2] <= 2 ** 31 - 1, last
+    assert 250_000_000 < seen["n"] < n
+    z = fo.read_bytes()
+    assert zlib.decompress(z) == data.tobytes()
 
 
 def _fd_encode(tmp_path, data: bytes, env: dict, name="out"):

@@ -121,13 +121,19 @@ def test_lazy_parity(enc, golden_cases, k):
 @pytest.mark.parametrize("k", [0, 6, 8, 16])
 def test_exact_sort_fallback_parity(enc, golden_cases, k):
     """The match-any sort (the fallback if lane-ordered LDS atomics ever misorder) gives the
-    same stream as the fast sort and the oracle."""
+    same stream as the fast sort and the oracle.  dmx_result.nsortfallback counts the
+    fallbacks: none on the fast path, at least one per searched block under the test hook
+    (which forces the fallback), and the context total adds them up."""
     data = golden_cases["bee0"] + D.gen_text(150000, 21).tobytes() + bytes(3000) + golden_cases["runs32k"]
     for lazy in (False, True):
         f = D.DMX_ZLIB | (D.DMX_F_LAZY if lazy else 0)
-        z_fast, _ = enc.compress_bytes(data, max_chain=k, flags=f)
-        z_exact, _ = enc.compress_bytes(data, max_chain=k, flags=f | D.DMX_F_EXACT_SORT)
+        z_fast, r_fast = enc.compress_bytes(data, max_chain=k, flags=f)
+        tot0 = r_fast.nsortfallback_total
+        z_exact, r_ex = enc.compress_bytes(data, max_chain=k, flags=f | D.DMX_F_EXACT_SORT)
         assert z_fast == z_exact == O.compress(data, max_chain=k, lazy=lazy)
+        assert r_fast.nsortfallback == 0
+        assert r_ex.nsortfallback >= r_ex.nblocks == 7
+        assert r_ex.nsortfallback_total == tot0 + r_ex.nsortfallback
 
 
 def test_lazy_tokens_and_edges(enc, golden_cases):

@@ -3,7 +3,8 @@
 Bar: the GPU stream equals the oracle's split stream byte for byte (same quarter cut
 points, same per-group Huffman plans, same cheapest-cut choice and tie-break), it inflates
 with zlib, our CPU inflate and the GPU inflate, and it is never larger than the unsplit
-stream.  The compress_stats side channel restarts its running sums at every DEFLATE block.
+stream.  In DMX_STATS=exact the compress_stats side channel follows every DEFLATE block's
+own codes and header, in running sums over the whole stream.
 """
 import zlib
 
@@ -128,6 +129,7 @@ def test_split_stats(tmp_path, enc, monkeypatch):
     fi.write_bytes(data)
     monkeypatch.setenv("DMX_SPLIT", "1")
     monkeypatch.setenv("DMX_MAX_CHAIN", "8")
+    monkeypatch.setenv("DMX_STATS", "exact")
     with open(fi, "rb") as a, open(fo, "wb") as b, open(fs, "wb") as c:
         assert D.deflate_compress(a.fileno(), b.fileno(), c.fileno(), 32768, 0) == 0
     assert fo.read_bytes() == O.compress(data, max_chain=8, split=True)

@@ -8,6 +8,9 @@
    compress_stats stream (deflate_ext.h:19-31) is converted to the token encoding
    (t = byte | dist<<9 | len) and stored in ref_tokens.npz; manifest.json keeps
    the token count + SHA-256 and the stats' last-record estimate fields.
+   ref_stats.npz keeps every record's estimate fields (tree_bits, ll_bits, d_bits;
+   deflate_compress.c:292-298) as int32 first differences, SHA-256 of the whole
+   24-byte record stream in the manifest (`records_sha256`).
 3. The zlib streams inside the reference's PNG fixtures (png/img/*.png, util/*.png)
    are extracted to idat/*.zlib with the length + SHA-256 of their inflation
    (Python zlib 1.2.11 is the decoder of record; pngtest.png's 52 bytes are also
@@ -55,21 +58,24 @@ def main() -> None:
     subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "oracle"), "-f", "Makefile.ref",
                            f"REF={REF}"])
     assert O.ref_available()
-    toks, man = {}, {"cases": {}, "idat": {}}
+    toks, ests, man = {}, {}, {"cases": {}, "idat": {}}
     for name, data in golden_inputs.cases().items():
         st = O.ref_stats(data)
         t = O.ref_tokens(data)
         assert O.replay(t) == data, f"reference replay mismatch on {name}"
         toks[name] = t
+        ests[name] = np.diff(st[:, 1:4].astype(np.int64), axis=0, prepend=0).astype(np.int32)
         man["cases"][name] = {
             "n": len(data),
             "ntok": int(t.size),
             "tokens_sha256": hashlib.sha256(t.astype("<u4").tobytes()).hexdigest(),
             "input_sha256": hashlib.sha256(data).hexdigest(),
             "ref_last_record": [int(x) for x in st[-1]],
+            "records_sha256": hashlib.sha256(st.astype("<i4").tobytes()).hexdigest(),
         }
         print(f"{name:14s} n={len(data):6d} ntok={t.size}")
     np.savez_compressed(os.path.join(GOLD, "ref_tokens.npz"), **toks)
+    np.savez_compressed(os.path.join(GOLD, "ref_stats.npz"), **ests)
     for rel in ["png/img/pngtest.png", "png/img/pngtest2.png", "png/img/pngtest3.png",
                 "util/image.png", "util/image1.png", "util/sunset.png"]:
         z = png_idat(os.path.join(REF, rel))
