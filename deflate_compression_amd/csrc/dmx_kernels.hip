@@ -3411,9 +3411,12 @@ struct dmx_ctx {
     // dmx_encode_fd streaming buffers, kept across calls (pinning ~100 MB costs ms)
     uint8_t* fd_hin[2];   // pinned input chunks
     uint8_t* fd_hout[2];  // pinned output chunks
-    void* fd_din[2];      // device input chunks (the previous one is the next chunk's history)
-    void* fd_dout;
-    dmx_result* fd_hres;  // pinned
+    void* fd_din[2];      // device input chunks (the previous one is the next chunk's history);
+                          // DMX_BLK bytes in front of the chunk hold a multi-GPU worker's history
+    void* fd_dout[2];     // device output chunks (a multi-GPU worker copies one while encoding into the other)
+    dmx_result* fd_hres[2];  // pinned
+    hipStream_t fd_cs;    // multi-GPU worker: D2H copies beside the next encode
+    hipEvent_t fd_ev[2];  // multi-GPU worker: encode i done
     uint64_t fd_chunk, fd_ocap;
     uint16_t* chs;        // DMX_F_DICT: (cap_chain) x DMX_BLK bucket-sorted positions per block (+ the dict)
     uint16_t* che;        // DMX_F_DICT: (cap_chain) x DMX_NBUCKET bucket ends
@@ -3617,8 +3620,12 @@ extern "C" void dmx_ctx_destroy(dmx_ctx* c) {
         if (c->fd_hout[k]) (void)hipHostFree(c->fd_hout[k]);
         if (c->fd_din[k]) (void)hipFree(c->fd_din[k]);
     }
-    if (c->fd_dout) (void)hipFree(c->fd_dout);
-    if (c->fd_hres) (void)hipHostFree(c->fd_hres);
+    for (int k = 0; k < 2; k++) {
+        if (c->fd_dout[k]) (void)hipFree(c->fd_dout[k]);
+        if (c->fd_hres[k]) (void)hipHostFree(c->fd_hres[k]);
+        if (c->fd_ev[k]) (void)hipEventDestroy(c->fd_ev[k]);
+    }
+    if (c->fd_cs) (void)hipStreamDestroy(c->fd_cs);
     if (c->chs) (void)hipFree(c->chs);
     if (c->che) (void)hipFree(c->che);
     if (c->split) (void)hipFree(c->split);
@@ -4064,20 +4071,27 @@ static int fd_buffers(dmx_ctx* c, uint64_t chunk, uint64_t ocap) {
         if (c->fd_hin[k]) (void)hipHostFree(c->fd_hin[k]);
         if (c->fd_hout[k]) (void)hipHostFree(c->fd_hout[k]);
         if (c->fd_din[k]) (void)hipFree(c->fd_din[k]);
+        if (c->fd_dout[k]) (void)hipFree(c->fd_dout[k]);
         c->fd_hin[k] = c->fd_hout[k] = NULL;
-        c->fd_din[k] = NULL;
+        c->fd_din[k] = c->fd_dout[k] = NULL;
     }
-    if (c->fd_dout) (void)hipFree(c->fd_dout);
-    c->fd_dout = NULL;
     c->fd_chunk = c->fd_ocap = 0;
-    for (int k = 0; k < 2; k++) {
-        if (hip_fail(dmx_host_malloc((void**)&c->fd_hin[k], chunk + 16), "hipHostMalloc")) return -(int)E_MALLOC;
+    for (int k = 0; k < 2; k++) {   // input buffers: DMX_BLK bytes of history room + the chunk
+        if (hip_fail(dmx_host_malloc((void**)&c->fd_hin[k], chunk + DMX_BLK + 16), "hipHostMalloc")) return -(int)E_MALLOC;
         if (hip_fail(dmx_host_malloc((void**)&c->fd_hout[k], ocap), "hipHostMalloc")) return -(int)E_MALLOC;
-        if (hip_fail(dmx_malloc(&c->fd_din[k], chunk + 16), "hipMalloc")) return -(int)E_DEVICE;
+        if (hip_fail(dmx_malloc(&c->fd_din[k], chunk + DMX_BLK + 16), "hipMalloc")) return -(int)E_DEVICE;
+        if (hip_fail(dmx_malloc(&c->fd_dout[k], ocap), "hipMalloc")) return -(int)E_DEVICE;
+        if (!c->fd_hres[k] && hip_fail(dmx_host_malloc((void**)&c->fd_hres[k], sizeof(dmx_result)), "hipHostMalloc"))
+            return -(int)E_MALLOC;
+        if (!c->fd_ev[k] && hip_fail(hipEventCreateWithFlags(&c->fd_ev[k], hipEventDisableTiming), "hipEventCreate")) {
+            c->fd_ev[k] = NULL;
+            return -(int)E_DEVICE;
+        }
     }
-    if (hip_fail(dmx_malloc(&c->fd_dout, ocap), "hipMalloc")) return -(int)E_DEVICE;
-    if (!c->fd_hres && hip_fail(dmx_host_malloc((void**)&c->fd_hres, sizeof(dmx_result)), "hipHostMalloc"))
-        return -(int)E_MALLOC;
+    if (!c->fd_cs && hip_fail(hipStreamCreateWithFlags(&c->fd_cs, hipStreamNonBlocking), "hipStreamCreate")) {
+        c->fd_cs = NULL;
+        return -(int)E_DEVICE;
+    }
     c->fd_chunk = chunk;
     c->fd_ocap = ocap;
     return 0;
@@ -4140,23 +4154,23 @@ static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts,
         }
         if (len && hip_fail(hipMemcpyAsync(c->fd_din[cur], c->fd_hin[cur], (size_t)len, hipMemcpyHostToDevice, s), "H2D"))
             r = -(int)E_DEVICE;
-        if (!r) r = dmx_encode_async(c, c->fd_din[cur], (uint64_t)len, c->fd_dout, ocap, &oc, s);
-        if (!r) r = dmx_encode_result_async(c, c->fd_hres, s);
+        if (!r) r = dmx_encode_async(c, c->fd_din[cur], (uint64_t)len, c->fd_dout[0], ocap, &oc, s);
+        if (!r) r = dmx_encode_result_async(c, c->fd_hres[0], s);
         int64_t nlen = 0;
         if (!r && !last) {   // the next chunk, read while the device encodes this one
             nlen = fd_read_chunk(&R, c->fd_hin[cur ^ 1], chunk);
             if (nlen < 0) r = (int)nlen;
         }
         if (!r && hip_fail(hipStreamSynchronize(s), "hipStreamSynchronize")) r = -(int)E_DEVICE;
-        if (!r && c->fd_hres->status) r = c->fd_hres->status;
-        const uint64_t olen = r ? 0 : c->fd_hres->out_len;
-        const uint32_t cadl = r ? 0 : c->fd_hres->adler;
+        if (!r && c->fd_hres[0]->status) r = c->fd_hres[0]->status;
+        const uint64_t olen = r ? 0 : c->fd_hres[0]->out_len;
+        const uint32_t cadl = r ? 0 : c->fd_hres[0]->adler;
         if (wact[cur]) {   // writer i-2 used this buffer (writer i-1 waited for it already)
             pthread_join(wt[cur], NULL);
             wact[cur] = false;
             if (!r && wj[cur].rc) r = wj[cur].rc;
         }
-        if (!r && hip_fail(hipMemcpy(c->fd_hout[cur], c->fd_dout, olen, hipMemcpyDeviceToHost), "D2H")) r = -(int)E_DEVICE;
+        if (!r && hip_fail(hipMemcpy(c->fd_hout[cur], c->fd_dout[0], olen, hipMemcpyDeviceToHost), "D2H")) r = -(int)E_DEVICE;
         if (wact[cur ^ 1]) {   // in order: writer i starts after writer i-1
             pthread_join(wt[cur ^ 1], NULL);
             wact[cur ^ 1] = false;
@@ -4233,50 +4247,79 @@ static void multi_fail(MultiJob* J, int r) {
     pthread_mutex_unlock(&J->mu);
 }
 
+// Worker pipeline over its chunks t = 0, 1, ... (file chunks w, w + ndev, ...), two of
+// everything: while the device encodes chunk t + 1 (input slot and output slot (t + 1) & 1),
+// the host copies chunk t back on the copy stream, waits for its turn and writes it, and
+// reads chunk t + 2 from the file.  With DMX_F_DICT each pread also takes the sw bytes before
+// the chunk (the first block's history) into the slot's front, one H2D for both.
+static int multi_enqueue(MultiJob* J, dmx_ctx* c, uint64_t i, uint64_t len, int k, uint64_t ocap) {
+    dmx_opts oc = J->o;
+    oc.flags = J->pflags | (i == 0 ? DMX_F_HEADER : 0u) | (i + 1 == J->nchunks ? DMX_F_FINAL : 0u);
+    const bool hist = (J->pflags & DMX_F_DICT) && i > 0;
+    const uint64_t front = hist ? J->sw : 0;
+    oc.dict = hist ? (const uint8_t*)c->fd_din[k] + (DMX_BLK - front) : NULL;
+    oc.dict_len = front;
+    hipStream_t s = c->stream;
+    if ((len || front) &&
+        hip_fail(hipMemcpyAsync((uint8_t*)c->fd_din[k] + (DMX_BLK - front), c->fd_hin[k] + (DMX_BLK - front),
+                                (size_t)(front + len), hipMemcpyHostToDevice, s), "H2D"))
+        return -(int)E_DEVICE;
+    int r = dmx_encode_async(c, (const uint8_t*)c->fd_din[k] + DMX_BLK, len, c->fd_dout[k], ocap, &oc, s);
+    if (!r) r = dmx_encode_result_async(c, c->fd_hres[k], s);
+    if (!r && hip_fail(hipEventRecord(c->fd_ev[k], s), "hipEventRecord")) r = -(int)E_DEVICE;
+    return r;
+}
+
+static int multi_read(MultiJob* J, dmx_ctx* c, uint64_t i, uint64_t len, int k) {
+    const uint64_t front = ((J->pflags & DMX_F_DICT) && i > 0) ? J->sw : 0;
+    if (!len && !front) return 0;
+    return pread_full(J->fd_in, c->fd_hin[k] + (DMX_BLK - front), front + len, J->off0 + i * J->chunk - front);
+}
+
 static void* multi_worker(void* a) {
     MultiWorker* W = (MultiWorker*)a;
     MultiJob* J = W->J;
     dmx_ctx* c = W->c;
     if (hip_fail(hipSetDevice(c->device), "hipSetDevice")) { multi_fail(J, -(int)E_DEVICE); return NULL; }
     const uint64_t ocap = dmx_max_compressed(J->chunk, (int32_t)J->sw);
-    hipStream_t s = c->stream;
-    for (uint64_t i = (uint64_t)W->w; i < J->nchunks; i += (uint64_t)J->ndev) {
+    const uint64_t step = (uint64_t)J->ndev;
+    auto chunk_len = [&](uint64_t i) {
+        const uint64_t lo = i * J->chunk, left = J->size - J->off0 - lo;
+        return left < J->chunk ? left : J->chunk;
+    };
+    uint64_t i = (uint64_t)W->w;
+    int r = 0;
+    if (i < J->nchunks) {
+        r = multi_read(J, c, i, chunk_len(i), 0);
+        if (!r) r = multi_enqueue(J, c, i, chunk_len(i), 0, ocap);
+    }
+    for (int k = 0; !r && i < J->nchunks; i += step, k ^= 1) {
         if (__atomic_load_n(&J->err, __ATOMIC_RELAXED)) break;
-        const uint64_t lo = i * J->chunk, len = (J->size - J->off0 - lo) < J->chunk ? (J->size - J->off0 - lo) : J->chunk;
-        dmx_opts oc = J->o;
-        oc.flags = J->pflags | (i == 0 ? DMX_F_HEADER : 0u) | (i + 1 == J->nchunks ? DMX_F_FINAL : 0u);
-        oc.dict = NULL;
-        oc.dict_len = 0;
-        int r = len ? pread_full(J->fd_in, c->fd_hin[0], len, J->off0 + lo) : 0;
-        if (!r && (J->pflags & DMX_F_DICT) && i > 0) {   // the previous chunk's last sw bytes
-            r = pread_full(J->fd_in, c->fd_hin[1], J->sw, J->off0 + lo - J->sw);
-            if (!r && hip_fail(hipMemcpyAsync(c->fd_din[1], c->fd_hin[1], J->sw, hipMemcpyHostToDevice, s), "H2D"))
-                r = -(int)E_DEVICE;
-            oc.dict = c->fd_din[1];
-            oc.dict_len = J->sw;
-        }
-        if (!r && len && hip_fail(hipMemcpyAsync(c->fd_din[0], c->fd_hin[0], len, hipMemcpyHostToDevice, s), "H2D"))
+        const uint64_t len = chunk_len(i), in = i + step;
+        const bool more = in < J->nchunks;
+        if (more) r = multi_read(J, c, in, chunk_len(in), k ^ 1);   // beside the device's work on chunk i
+        if (!r && hip_fail(hipEventSynchronize(c->fd_ev[k]), "hipEventSynchronize")) r = -(int)E_DEVICE;
+        if (!r && c->fd_hres[k]->status) r = c->fd_hres[k]->status;
+        const uint64_t olen = r ? 0 : c->fd_hres[k]->out_len;
+        const uint32_t cadl = r ? 0 : c->fd_hres[k]->adler;
+        if (!r && more) r = multi_enqueue(J, c, in, chunk_len(in), k ^ 1, ocap);   // the device goes on
+        if (!r && (hip_fail(hipMemcpyAsync(c->fd_hout[k], c->fd_dout[k], olen, hipMemcpyDeviceToHost, c->fd_cs), "D2H") ||
+                   hip_fail(hipStreamSynchronize(c->fd_cs), "hipStreamSynchronize")))
             r = -(int)E_DEVICE;
-        if (!r) r = dmx_encode_async(c, c->fd_din[0], len, c->fd_dout, ocap, &oc, s);
-        if (!r) r = dmx_encode_result_async(c, c->fd_hres, s);
-        if (!r && hip_fail(hipStreamSynchronize(s), "hipStreamSynchronize")) r = -(int)E_DEVICE;
-        if (!r && c->fd_hres->status) r = c->fd_hres->status;
-        const uint64_t olen = r ? 0 : c->fd_hres->out_len;
-        const uint32_t cadl = r ? 0 : c->fd_hres->adler;
-        if (!r && hip_fail(hipMemcpy(c->fd_hout[0], c->fd_dout, olen, hipMemcpyDeviceToHost), "D2H")) r = -(int)E_DEVICE;
-        if (r) { multi_fail(J, r); break; }
+        if (r) break;
         pthread_mutex_lock(&J->mu);   // in order: chunk i after chunk i - 1
         while (J->next != i && !J->err) pthread_cond_wait(&J->cv, &J->mu);
         if (!J->err) {
-            if (J->fd_out >= 0) r = write_full(J->fd_out, c->fd_hout[0], olen);
+            if (J->fd_out >= 0) r = write_full(J->fd_out, c->fd_hout[k], olen);
             J->adler = dmx_adler32_combine(J->adler, cadl, len);
             if (r) J->err = r;
             J->next = i + 1;
         }
         pthread_cond_broadcast(&J->cv);
         pthread_mutex_unlock(&J->mu);
-        if (r) break;
     }
+    if (r) multi_fail(J, r);
+    (void)hipStreamSynchronize(c->stream);   // nothing of this call left in flight
     return NULL;
 }
 
