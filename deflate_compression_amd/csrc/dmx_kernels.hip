@@ -1488,9 +1488,11 @@ __global__ __launch_bounds__(MT) void dmx_hist_kernel_t(const uint8_t* __restric
 //   pass 1: the whole block into registers (8 loads per thread in flight), Adler-32
 //           partial sums (v_sad_u8, v_dot4_u32_u8).
 //   pass 2 (noise-like blocks only; full blocks from the registers of pass 1): byte
-//           histogram of the even positions and 18-bit presence bitmap of the 4-grams
-//           sampled by content (bit 13 of their hash clear), LDS atomics (33 KB, several
-//           workgroups per CU); sampling halves the atomics, which bound this pass.
+//           histogram of every s-th position (s = 8 for full blocks: 4096 samples) and
+//           18-bit presence bitmap of the 4-grams sampled by content (bits 11..13 of their
+//           hash clear: an eighth), LDS atomics (33 KB, several workgroups per CU).  The
+//           atomics bound this pass: round 2 sampled every other position and half the
+//           4-grams (32 K atomics per block, 0.53 ms per GiB); now 8 K.
 // A block that passes gets its whole record here (stored, no tokens); the match kernel then
 // skips it and the Huffman kernels leave it alone.  Same integer rule as
 // dmx_oracle_store_check.
@@ -1676,14 +1678,16 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
     hist[tid] = 0;   // (8 padded sub-histograms by lane & 7 measured slower: 0.59 -> 0.77 ms per GiB)
     __syncthreads();
     uint32_t qn = 0;   // sampled 4-grams of this thread
+    // histogram stride s = 8 / 4 / 2 / 1 for blocks of >= 32768 / 16384 / 8192 / 4096 bytes
+    const uint32_t smask = bn >= 32768 ? 7u : bn >= 16384 ? 3u : bn >= 8192 ? 1u : 0u;
     auto chunk2 = [&](uint32_t p, const uint32_t* w) {   // 16 positions at block offset p (w[4]: next 4 bytes)
 #pragma unroll
         for (int j = 0; j < 16; j++) {
             const uint32_t lo = w[j >> 2], hi = w[(j >> 2) + 1];
             const uint32_t g4 = (j & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(j & 3)) : lo;
-            if ((j & 1) == 0 && p + j < bn) atomicAdd(&hist[(lo >> (8 * (j & 3))) & 0xFFu], 1u);   // even positions
+            if (((uint32_t)j & smask) == 0 && p + j < bn) atomicAdd(&hist[(lo >> (8 * (j & 3))) & 0xFFu], 1u);
             const uint32_t x = g4 * 0x9E3779B1u;
-            if (p + j + 4 <= bn && !(x & (1u << 13))) {   // sampled by content
+            if (p + j + 4 <= bn && !(x & (7u << 11))) {   // sampled by content
                 qn++;
                 atomicOr(&bm[x >> 19], 1u << ((x >> 14) & 31));
             }
@@ -1719,9 +1723,9 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
         for (int w = 0; w < SCT / 64; w++) {
             S += red[8][w]; T += red[9][w]; Dn += red[0][w]; S2 += red[1][w]; Q += red[2][w];
         }
-        const uint64_t m = ((uint64_t)bn + 1) / 2, m2 = m * m;
+        const uint64_t m = ((uint64_t)bn + smask) / (smask + 1), m2 = m * m;
         const uint64_t coll = Q - Dn;
-        const bool sto = 256 * S2 <= m2 + (m2 >> 4) + 256 * m && 4 * Q >= (uint64_t)bn && 64 * coll <= 5 * Q;
+        const bool sto = 256 * S2 <= m2 + (m2 >> 4) + 256 * m && 16 * Q >= (uint64_t)bn && 64 * coll <= 4 * Q;
         info[b].prestored = sto ? 1u : 0u;
         if (sto) {
             info[b].ntok = 0;

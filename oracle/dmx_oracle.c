@@ -660,25 +660,29 @@ int dmx_oracle_store_check(const uint8_t* d, int bn) {
         const int64_t dev = 2 * ones - 4096;
         if (8 * (dev < 0 ? -dev : dev) > 4096) return 0;
     }
+    /* byte histogram of every s-th position, s = 8 / 4 / 2 / 1 for blocks of at least
+     * 32768 / 16384 / 8192 / 4096 bytes (m = ceil(bn / s) >= 4096 samples) */
+    const int sh = bn >= 32768 ? 3 : bn >= 16384 ? 2 : bn >= 8192 ? 1 : 0;
     uint64_t h[256] = {0};
-    for (int k = 0; k < bn; k += 2) h[d[k]]++;
+    for (int k = 0; k < bn; k += 1 << sh) h[d[k]]++;
     uint64_t s2 = 0;
     for (int c = 0; c < 256; c++) s2 += h[c] * h[c];
-    const uint64_t m = (uint64_t)(bn + 1) / 2, m2 = m * m;
+    const uint64_t m = ((uint64_t)bn + (1u << sh) - 1) >> sh, m2 = m * m;
     if (256 * s2 > m2 + (m2 >> 4) + 256 * m) return 0;
+    /* 4-grams sampled by content: bits 11..13 of their hash clear (an eighth) */
     uint32_t* bm = (uint32_t*)calloc(1u << 13, sizeof(uint32_t));
     uint64_t q = 0, distinct = 0;
     for (int p = 0; p + 4 <= bn; p++) {
         const uint32_t w = (uint32_t)d[p] | (uint32_t)d[p + 1] << 8 | (uint32_t)d[p + 2] << 16 | (uint32_t)d[p + 3] << 24;
         const uint32_t x = w * 0x9E3779B1u;
-        if (x & (1u << 13)) continue;
+        if (x & (7u << 11)) continue;
         q++;
         const uint32_t g = x >> 14;
         if (!(bm[g >> 5] & (1u << (g & 31)))) { bm[g >> 5] |= 1u << (g & 31); distinct++; }
     }
     free(bm);
     const uint64_t coll = q - distinct;
-    return 4 * q >= (uint64_t)bn && 64 * coll <= 5 * q;
+    return 16 * q >= (uint64_t)bn && 64 * coll <= 4 * q;
 }
 
 /* ---- 8. whole stream ---------------------------------------------------------------- */

@@ -26,18 +26,19 @@ def np_store_check(block) -> bool:
     bits = np.unpackbits(b[:4096, None], axis=1)
     if np.any(8 * np.abs(2 * bits.sum(axis=0).astype(np.int64) - 4096) > 4096):
         return False
-    h = np.bincount(b[0::2], minlength=256).astype(np.uint64)
+    sh = 3 if n >= 32768 else 2 if n >= 16384 else 1 if n >= 8192 else 0
+    h = np.bincount(b[0::1 << sh], minlength=256).astype(np.uint64)
     s2 = int((h * h).sum())
-    m = (n + 1) // 2
+    m = (n + (1 << sh) - 1) >> sh
     if 256 * s2 > m * m + ((m * m) >> 4) + 256 * m:
         return False
     w = (b[:-3].astype(np.uint64) | b[1:-2].astype(np.uint64) << 8 | b[2:-1].astype(np.uint64) << 16
          | b[3:].astype(np.uint64) << 24)
     x = (w * 0x9E3779B1) & 0xFFFFFFFF
-    g = x[(x & (1 << 13)) == 0] >> 14
+    g = x[(x & (7 << 11)) == 0] >> 14
     q = g.size
     coll = q - np.unique(g).size
-    return 4 * q >= n and 64 * coll <= 5 * q
+    return 16 * q >= n and 64 * coll <= 4 * q
 
 
 def _noise(n, seed, alphabet=256):
