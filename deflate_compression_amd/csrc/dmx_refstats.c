@@ -62,12 +62,14 @@ typedef struct {
     int16_t nx[RS_SLOTS];     /* next node in the order list (heavier side), -1 at the end */
     int16_t pv[RS_SLOTS];     /* previous node in the order list */
     uint32_t score;           /* sum of weight x depth over the leaves, maintained incrementally */
+    int dirty;                /* a leaf's depth changed (or a leaf appeared) since tree_bits was priced */
     int nsym;
     int nyt;                  /* slot of the current NYT leaf */
 } rs_tree;
 
 struct dmx_refest {
     rs_tree ll, d;
+    uint32_t tree_bits;   /* the last price: unchanged while no leaf depth changes */
 };
 
 static void rs_init(rs_tree* t, int nsym) {
@@ -94,6 +96,7 @@ static void rs_redepth(rs_tree* t, int x, int d) {
     for (;;) {
         if (rs_leaf(t, x)) {
             t->score += (uint32_t)(d - t->dep[x]) * t->w[x];
+            t->dirty |= t->dep[x] != d;
             t->dep[x] = (int16_t)d;
             return;
         }
@@ -186,6 +189,7 @@ static void rs_swap(rs_tree* t, int a, int b) {
         t->up[b] = (int16_t)pa;
     }
     if (t->dep[a] != t->dep[b]) {
+        t->dirty = 1;
         t->score += (uint32_t)(t->dep[a] - t->dep[b]) * (t->w[b] - t->w[a]);
         const int16_t d = t->dep[a];
         t->dep[a] = t->dep[b];
@@ -220,6 +224,7 @@ static void rs_insert(rs_tree* t, int c) {
         t->nx[z] = (int16_t)c;
         t->pv[z] = -1;
         t->nyt = z;
+        t->dirty = 1;
         tail = c;
     } else {
         const int lead = rs_leader(t, c);
@@ -371,6 +376,8 @@ dmx_refest* dmx_refest_create(void) {
     rs_init(&e->ll, RS_LL);
     rs_init(&e->d, RS_D);
     rs_insert(&e->ll, 256);   /* the end-of-block code, counted once up front (deflate_compress.c:234) */
+    e->tree_bits = 0;
+    e->ll.dirty = 1;
     return e;
 }
 
@@ -390,7 +397,11 @@ int dmx_refest_feed(dmx_refest* e, const uint32_t* tok, uint32_t ntok, struct co
             rs_insert(&e->ll, rs_len_code(len));
             rs_insert(&e->d, rs_dist_code(dist));
         }
-        const uint32_t tb = rs_tree_bits(&e->ll, &e->d);
+        if (e->ll.dirty || e->d.dirty) {   /* the price depends on the leaves' depths only */
+            e->tree_bits = rs_tree_bits(&e->ll, &e->d);
+            e->ll.dirty = e->d.dirty = 0;
+        }
+        const uint32_t tb = e->tree_bits;
         if (tb > INT_MAX || e->ll.score > INT_MAX || e->d.score > INT_MAX) return -E_RANGE;
         rec[k].tree_bits = (int)tb;
         rec[k].ll_bits = (int)e->ll.score;
