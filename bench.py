@@ -551,27 +551,37 @@ def main() -> int:
         ok = bool(flag.item())
         del full
     # GPU inflate of the same stream: every block decoded in parallel from the
-    # encoder's block index, compared bit for bit with the input; timed with events
-    # (dict streams reference the previous block: the whole-stream decoder, one timed run)
-    indexed = not args.dict
-    ix, nblk = enc.block_index() if indexed else (None, 0)
+    # encoder's block index, compared bit for bit with the input; timed with events.  Dict
+    # streams reference the previous block: the chained decode (cells + pointer jumping,
+    # dmx_inflate_chained_async), also every block in parallel.
+    ix, nblk = enc.block_index()
     dec = torch.empty(n, dtype=torch.uint8, device=dev)
     ist = torch.zeros(16, dtype=torch.uint8, device=dev)
     Lib = D.lib()
     inf_src = last_buf[0]
+    chained = bool(args.dict)
+    work = None
+    if chained:
+        wb = int(Lib.dmx_inflate_chained_work(n))
+        work = torch.empty(wb + 256, dtype=torch.uint8, device=dev)
+        wptr = (work.data_ptr() + 255) & ~255
 
     def inflate():
-        rc = Lib.dmx_inflate_async(inf_src.data_ptr(), out_len, ix.data_ptr() if indexed else None, nblk,
-                                   dec.data_ptr(), n, ist.data_ptr(), stream)
+        if chained:
+            rc = Lib.dmx_inflate_chained_async(inf_src.data_ptr(), out_len, ix.data_ptr(), nblk, dec.data_ptr(), n,
+                                               wptr, wb, ist.data_ptr(), stream)
+        else:
+            rc = Lib.dmx_inflate_async(inf_src.data_ptr(), out_len, ix.data_ptr(), nblk, dec.data_ptr(), n,
+                                       ist.data_ptr(), stream)
         if rc != 0:
-            raise RuntimeError(f"dmx_inflate_async: {rc}")
+            raise RuntimeError(f"GPU inflate launch: {rc}")
 
-    if world == 1 or indexed:
+    if world == 1 or not chained:
         inflate()
     torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
-    inf_reps = 3 if indexed else (1 if world == 1 else 0)
+    inf_reps = 3 if (world == 1 or not chained) else 0
     for _ in range(inf_reps):
         inflate()
     ev1.record()
@@ -587,9 +597,12 @@ def main() -> int:
             log(f"ERROR: GPU inflate status {inf_status}, {inf_len} of {n} bytes, or a byte mismatch")
             ok = False
         gpu_inflate = {"GBps_out": round(n / inf_ms / 1e6, 3), "ms": round(inf_ms, 4), "bit_exact": inf_ok,
-                       "mode": "indexed: one single-wave workgroup per block" if indexed else
-                               "stream: one wave decodes the whole zlib stream (dict blocks chain)",
-                       "kernel": "dmx_inflate_index_kernel" if indexed else "dmx_inflate_stream_kernel"}
+                       "mode": "chained: every block in parallel into 16-bit cells (references to the bytes "
+                               "before the block), references resolved by pointer jumping" if chained else
+                               "indexed: one single-wave workgroup per block",
+                       "kernel": "dmx_inflate_index_kernel<true> + dmx_cells_*" if chained else
+                                 "dmx_inflate_index_kernel"}
+    del work
     del dec
     run(args.warmup)
     torch.cuda.synchronize(dev)

@@ -23,7 +23,7 @@ import struct
 __all__ = [
     "DeflateError", "Opts", "Result", "Encoder", "lib", "compress", "deflate_compress",
     "deflate_decompress", "max_compressed", "adler32_combine", "gen_text", "gen_random",
-    "COMPRESS_STATS", "E", "DMX_F_HEADER", "DMX_F_TRAILER", "DMX_F_FINAL", "DMX_ZLIB", "DMX_F_LAZY", "DMX_F_EXACT_SORT", "DMX_F_SPLIT", "DMX_F_DICT", "DMX_F_STORE_CHECK", "inflate_gpu", "ref_estimates",
+    "COMPRESS_STATS", "E", "DMX_F_HEADER", "DMX_F_TRAILER", "DMX_F_FINAL", "DMX_ZLIB", "DMX_F_LAZY", "DMX_F_EXACT_SORT", "DMX_F_SPLIT", "DMX_F_DICT", "DMX_F_STORE_CHECK", "inflate_gpu", "inflate_gpu_chained", "ref_estimates",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -125,6 +125,8 @@ def lib() -> ctypes.CDLL:
         "dmx_inflate_async": ([vp, u64, vp, u32, vp, u64, vp, vp], ctypes.c_int),
         "dmx_gen_text": ([vp, u64, u64], None),
         "dmx_gen_random": ([vp, u64, u64], None),
+        "dmx_inflate_chained_async": ([vp, u64, vp, u32, vp, u64, vp, u64, vp, vp], ctypes.c_int),
+        "dmx_inflate_chained_work": ([u64], u64),
         "dmx_refest_create": ([], vp),
         "dmx_refest_destroy": ([vp], None),
         "dmx_refest_feed": ([vp, u32p, u32, vp, u32p], ctypes.c_int),
@@ -218,6 +220,33 @@ def inflate_gpu(z, out_cap: int, index=None, nblk: int = 0, stream=None):
     r = L.dmx_inflate_async(z.data_ptr(), z.numel(), index.data_ptr() if index is not None else None,
                             nblk, out.data_ptr(), out_cap, st.data_ptr(), s)
     _check(r, "dmx_inflate_async")
+    torch.cuda.synchronize(dev)
+    h = st.cpu().numpy()
+    status = int(np.frombuffer(h[:4].tobytes(), np.int32)[0])
+    olen = int(np.frombuffer(h[8:16].tobytes(), np.uint64)[0])
+    return out[:olen], status
+
+
+def inflate_gpu_chained(z, out_cap: int, index, nblk: int, stream=None, work=None):
+    """Inflate on the GPU a stream whose blocks may reference the block before them
+    (DMX_F_DICT streams), all blocks in parallel: each decodes into 16-bit cells with
+    references for the bytes before it, then pointer jumping resolves the references
+    (dmx_inflate_chained_async).  index: Encoder.block_index().  work: optional uint8 CUDA
+    scratch of dmx_inflate_chained_work(out_cap) bytes.  Returns (uint8 tensor, status)."""
+    import numpy as np
+    import torch
+    L = lib()
+    dev = z.device
+    out = torch.empty(max(out_cap, 1), dtype=torch.uint8, device=dev)
+    st = torch.zeros(16, dtype=torch.uint8, device=dev)
+    wb = int(L.dmx_inflate_chained_work(out_cap))
+    if work is None or work.numel() < wb:
+        work = torch.empty(wb + 256, dtype=torch.uint8, device=dev)
+    wp = (work.data_ptr() + 255) & ~255
+    s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    r = L.dmx_inflate_chained_async(z.data_ptr(), z.numel(), index.data_ptr(), nblk, out.data_ptr(), out_cap,
+                                    wp, work.numel() - (wp - work.data_ptr()), st.data_ptr(), s)
+    _check(r, "dmx_inflate_chained_async")
     torch.cuda.synchronize(dev)
     h = st.cpu().numpy()
     status = int(np.frombuffer(h[:4].tobytes(), np.int32)[0])

@@ -23,6 +23,7 @@
 // and ranks); longer codes take a canonical slow path (first code / count / offset per length).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 #include <stdio.h>
 
 #include "../../include/dmx.h"
@@ -43,9 +44,12 @@ struct ITable {
     uint16_t sym[288];         // symbols sorted by (length, symbol)
 };
 
-template <uint32_t W>
+// T = uint8_t: the output bytes; T = uint16_t: cells of the chained decode (a byte value, or
+// 0x100 + b - 1 for the byte b positions before the sw block's first output byte, resolved
+// afterwards: dmx_inflate_chained_async)
+template <uint32_t W, typename T = uint8_t>
 struct InfLDS {
-    uint8_t win[W];
+    T win[W];
     ITable lt, dt;
     uint8_t len[320];
     uint8_t seq[320];
@@ -199,8 +203,8 @@ __device__ __forceinline__ uint32_t iv_dbase(uint32_t e) { return ((e >> 28) << 
 // serves the code length code: its symbols 0..18 take the literal form).  IVSLOW marks a code
 // longer than IFB bits (or no code).  Returns 0 complete, 1 incomplete, -1 over-subscribed.
 // ---------------------------------------------------------------------------------------
-template <bool DIST, uint32_t W>
-__device__ __forceinline__ int itable_build(InfLDS<W>& S, ITable& T, int n, uint32_t lane) {
+template <bool DIST, uint32_t W, typename TW>
+__device__ __forceinline__ int itable_build(InfLDS<W, TW>& S, ITable& T, int n, uint32_t lane) {
     const int nc = (n + 63) >> 6;   // symbol chunks, <= 5
     uint32_t lc[5];
 #pragma unroll
@@ -330,8 +334,47 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 }
 
 // Write window bytes [fl, upto) to HBM (upto - fl <= W).  ADLER: fold them into (a, b).
-template <bool ADLER, uint32_t W>
-__device__ __forceinline__ void io_flush(InfLDS<W>& S, IOut& o, uint32_t upto, uint32_t lane) {
+// Cells: window positions [fl, upto) to the cell buffer (2 bytes a position), 8 cells (16
+// bytes) per lane where the destination is 16-byte aligned.
+template <uint32_t W>
+__device__ __forceinline__ void io_flush_cells(InfLDS<W, uint16_t>& S, IOut& o, uint32_t upto, uint32_t lane) {
+    constexpr uint32_t IM = W - 1;
+    __syncthreads();
+    uint16_t* dst = reinterpret_cast<uint16_t*>(o.out) + o.base + o.ob;
+    uint32_t p = o.fl;
+    const uint32_t head = min(upto - p, (uint32_t)(((16 - (((uintptr_t)(dst + p)) & 15)) & 15) >> 1));
+    if (lane < head) dst[p + lane] = S.win[(p + lane) & IM];
+    p += head;
+    for (; p + 8 <= upto; p += 512) {
+        const uint32_t q = p + lane * 8;
+        if (q + 8 <= upto) {
+            uint32_t w[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                w[k] = (uint32_t)S.win[(q + 2 * k) & IM] | ((uint32_t)S.win[(q + 2 * k + 1) & IM] << 16);
+            *(uint4*)&dst[q] = make_uint4(w[0], w[1], w[2], w[3]);
+        } else if (q < upto) {
+            for (uint32_t t = q; t < upto; t++) dst[t] = S.win[t & IM];
+        }
+    }
+    if (p < upto && lane == 0)
+        for (uint32_t t = p; t < upto; t++) dst[t] = S.win[t & IM];
+    o.fl = upto;
+    __builtin_amdgcn_s_waitcnt(0);   // the stores are done: far-match reads see them
+    if (o.fl >= IRENORM) {
+        o.ob += IRENORM;
+        o.op -= IRENORM;
+        o.fl -= IRENORM;
+    }
+    __syncthreads();
+}
+
+template <bool ADLER, uint32_t W, typename TW>
+__device__ __forceinline__ void io_flush(InfLDS<W, TW>& S, IOut& o, uint32_t upto, uint32_t lane) {
+    if constexpr (sizeof(TW) == 2) {
+        io_flush_cells<W>(S, o, upto, lane);
+        return;
+    } else {
     constexpr uint32_t IM = W - 1;
     [[maybe_unused]] const unsigned long long ts0 = IST_NOW();
     __syncthreads();
@@ -404,6 +447,7 @@ __device__ __forceinline__ void io_flush(InfLDS<W>& S, IOut& o, uint32_t upto, u
     }
     __syncthreads();
     IST_ADD(o, 2, IST_NOW() - ts0);
+    }
 }
 
 // LDS byte address of a __shared__ object (ds_* instructions address LDS from 0)
@@ -462,7 +506,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
     "s_waitcnt vmcnt(0) lgkmcnt(0)\n" \
     "s_mov_b64 exec, s[84:85]\n" \
     "v_lshrrev_b32 v148, v150, v148\n" \
-    "ds_write_b8 v149, v148\n" \
+    IWR " v149, v148\n" \
     "s_mov_b64 exec, s[86:87]\n" \
     "s_mov_b64 s[84:85], 0\n" \
     "L_nf" #N "%=:\n"
@@ -472,7 +516,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 #define IX_DIST 4u
 #define IX_MATCH 5u
 
-template <uint32_t W>
+template <uint32_t W, bool CELL>
 __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t lim, uint32_t limm, uint32_t dfl,
                                              uint32_t tla, uint32_t tda, uint32_t lane, uint64_t gpos0,
                                              uint32_t& len, uint32_t& dist) {
@@ -481,361 +525,15 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
     const uint32_t gmis = (uint32_t)gpos0 & 3u;
     const int32_t wrl = (int32_t)r.wfast - 192;   // rotate while the new segment is wholly inside
     const uint64_t zb = (uint64_t)(uintptr_t)r.zb;
-    asm volatile(
-        "s_mov_b64 s[94:95], %[bb]\n"
-        "s_mov_b32 s89, m0\n"
-        "s_mov_b64 s[86:87], exec\n"
-        "s_mov_b64 s[84:85], 0\n"
-        "ds_read_b32 v96, %[tla]\n"
-        "ds_read_b32 v97, %[tla] offset:256\n"
-        "ds_read_b32 v98, %[tla] offset:512\n"
-        "ds_read_b32 v99, %[tla] offset:768\n"
-        "ds_read_b32 v100, %[tla] offset:1024\n"
-        "ds_read_b32 v101, %[tla] offset:1280\n"
-        "ds_read_b32 v102, %[tla] offset:1536\n"
-        "ds_read_b32 v103, %[tla] offset:1792\n"
-        "ds_read_b32 v104, %[tla] offset:2048\n"
-        "ds_read_b32 v105, %[tla] offset:2304\n"
-        "ds_read_b32 v106, %[tla] offset:2560\n"
-        "ds_read_b32 v107, %[tla] offset:2816\n"
-        "ds_read_b32 v108, %[tla] offset:3072\n"
-        "ds_read_b32 v109, %[tla] offset:3328\n"
-        "ds_read_b32 v110, %[tla] offset:3584\n"
-        "ds_read_b32 v111, %[tla] offset:3840\n"
-        "ds_read_b32 v112, %[tda]\n"
-        "ds_read_b32 v113, %[tda] offset:256\n"
-        "ds_read_b32 v114, %[tda] offset:512\n"
-        "ds_read_b32 v115, %[tda] offset:768\n"
-        "ds_read_b32 v116, %[tda] offset:1024\n"
-        "ds_read_b32 v117, %[tda] offset:1280\n"
-        "ds_read_b32 v118, %[tda] offset:1536\n"
-        "ds_read_b32 v119, %[tda] offset:1792\n"
-        "ds_read_b32 v120, %[tda] offset:2048\n"
-        "ds_read_b32 v121, %[tda] offset:2304\n"
-        "ds_read_b32 v122, %[tda] offset:2560\n"
-        "ds_read_b32 v123, %[tda] offset:2816\n"
-        "ds_read_b32 v124, %[tda] offset:3072\n"
-        "ds_read_b32 v125, %[tda] offset:3328\n"
-        "ds_read_b32 v126, %[tda] offset:3584\n"
-        "ds_read_b32 v127, %[tda] offset:3840\n"
-        "s_mov_b32 s97, 0\n"
-        "s_mov_b32 %[len], 0\n"
-        "s_mov_b32 %[dist], 0\n"
-        "s_waitcnt lgkmcnt(0)\n"
-        // distance bases (m << extra) + 1 beside the distance entries, in v128..v143
-        "v_bfe_u32 v148, v112, 28, 2\n"
-        "v_bfe_u32 v149, v112, 16, 4\n"
-        "v_lshlrev_b32 v148, v149, v148\n"
-        "v_add_u32 v128, 1, v148\n"
-        "v_bfe_u32 v148, v113, 28, 2\n"
-        "v_bfe_u32 v149, v113, 16, 4\n"
-        "v_lshlrev_b32 v148, v149, v148\n"
-        "v_add_u32 v129, 1, v148\n"
-        "v_bfe_u32 v148, v114, 28, 2\n"
-        "v_bfe_u32 v149, v114, 16, 4\n"
-        "v_lshlrev_b32 v148, v149, v148\n"
-        "v_add_u32 v130, 1, v148\n"
-        "v_bfe_u32 v148, v115, 28, 2\n"
-        "v_bfe_u32 v149, v115, 16, 4\n"
-        "v_lshlrev_b32 v148, v149, v148\n"
-        "v_add_u32 v131, 1, v148\n"
-        "v_bfe_u32 v148, v116, 28, 2\n"
-        "v_bfe_u32 v149, v116, 16, 4\n"
-        "v_lshlrev_b32 v148, v149, v148\n"
-        "v_add_u32 v132, 1, v148\n"
-        "v_bfe_u32 v148, v117, 28, 2\n"
-        "v_bfe_u32 v149, v117, 16, 4\n"
-        "v_lshlrev_b32 v148, v149, v148\n"
-        "v_add_u32 v133, 1, v148\n"
-        "v_bfe_u32 v148, v118, 28, 2\n"
-        "v_bfe_u32 v149, v118, 16, 4\n"
-        "v_lshlrev_b32 v148, v149, v148\n"
-        "v_add_u32 v134, 1, v148\n"
-        "v_bfe_u32 v148, v119, 28, 2\n"
-        "v_bfe_u32 v149, v119, 16, 4\n"
-        "v_lshlrev_b32 v148, v149, v148\n"
-        "v_add_u32 v135, 1, v148\n"
-        "v_bfe_u32 v148, v120, 28, 2\n"
-        "v_bfe_u32 v149, v120, 16, 4\n"
-        "v_lshlrev_b32 v148, v149, v148\n"
-        "v_add_u32 v136, 1, v148\n"
-        "v_bfe_u32 v148, v121, 28, 2\n"
-        "v_bfe_u32 v149, v121, 16, 4\n"
-        "v_lshlrev_b32 v148, v149, v148\n"
-        "v_add_u32 v137, 1, v148\n"
-        "v_bfe_u32 v148, v122, 28, 2\n"
-        "v_bfe_u32 v149, v122, 16, 4\n"
-        "v_lshlrev_b32 v148, v149, v148\n"
-        "v_add_u32 v138, 1, v148\n"
-        "v_bfe_u32 v148, v123, 28, 2\n"
-        "v_bfe_u32 v149, v123, 16, 4\n"
-        "v_lshlrev_b32 v148, v149, v148\n"
-        "v_add_u32 v139, 1, v148\n"
-        "v_bfe_u32 v148, v124, 28, 2\n"
-        "v_bfe_u32 v149, v124, 16, 4\n"
-        "v_lshlrev_b32 v148, v149, v148\n"
-        "v_add_u32 v140, 1, v148\n"
-        "v_bfe_u32 v148, v125, 28, 2\n"
-        "v_bfe_u32 v149, v125, 16, 4\n"
-        "v_lshlrev_b32 v148, v149, v148\n"
-        "v_add_u32 v141, 1, v148\n"
-        "v_bfe_u32 v148, v126, 28, 2\n"
-        "v_bfe_u32 v149, v126, 16, 4\n"
-        "v_lshlrev_b32 v148, v149, v148\n"
-        "v_add_u32 v142, 1, v148\n"
-        "v_bfe_u32 v148, v127, 28, 2\n"
-        "v_bfe_u32 v149, v127, 16, 4\n"
-        "v_lshlrev_b32 v148, v149, v148\n"
-        "v_add_u32 v143, 1, v148\n"
-        // ---- token start: refill (rotating the stream segments when the word is in vnxt)
-        "L_tok%=:\n"
-        "s_cmp_gt_u32 %[bc], 32\n"
-        "s_cbranch_scc1 L_look%=\n"
-        "s_sub_u32 s98, %[wi], %[wb]\n"
-        "s_cmp_lt_u32 s98, 64\n"
-        "s_cbranch_scc1 L_rd%=\n"
-        "s_cmp_le_i32 %[wb], %[wrl]\n"
-        "s_cbranch_scc0 L_xseg%=\n"
-        "s_waitcnt vmcnt(0)\n"
-        "v_mov_b32 %[vc], %[vn]\n"
-        "s_add_u32 %[wb], %[wb], 64\n"
-        "s_sub_u32 s98, s98, 64\n"
-        "s_add_u32 s99, %[wb], 64\n"
-        "v_add_lshl_u32 v146, %[lane], s99, 2\n"
-        "global_load_dword %[vn], v146, %[zb]\n"
-        "L_rd%=:\n"
-        "s_nop 3\n"
-        "v_readlane_b32 s96, %[vc], s98\n"
-        "s_lshl_b64 s[92:93], s[96:97], %[bc]\n"
-        "s_or_b64 s[94:95], s[94:95], s[92:93]\n"
-        "s_add_u32 %[wi], %[wi], 1\n"
-        "s_add_u32 %[bc], %[bc], 32\n"
-        // ---- literal/length lookup
-        "L_look%=:\n"
-        "s_bfe_u32 s98, s94, 0x40006\n"
-        ILOOK_LL
-        "s_bitcmp1_b32 s99, 15\n"
-        "s_cbranch_scc1 L_nl%=\n"
-        // literal: sym in bits 23:16 (ds_write_b8_d16_hi), every lane the same byte
-        "s_cmp_ge_u32 %[op], %[lim]\n"
-        "s_cbranch_scc1 L_xlim%=\n"
-        "s_and_b32 s98, s99, 31\n"
-        "s_lshr_b64 s[94:95], s[94:95], s98\n"
-        "s_sub_u32 %[bc], %[bc], s98\n"
-        "v_mov_b32 v146, %[op]\n"
-        "v_and_b32 v146, %[im], v146\n"
-        "v_mov_b32 v147, s99\n"
-        "ds_write_b8_d16_hi v146, v147\n"
-        "s_add_u32 %[op], %[op], 1\n"
-        "s_cmp_gt_u32 %[bc], 32\n"
-        "s_cbranch_scc1 L_look%=\n"
-        "s_branch L_tok%=\n"
-        // ---- length (the entry is the s_bfe control of its extra bits)
-        "L_nl%=:\n"
-        "s_bitcmp1_b32 s99, 14\n"
-        "s_cbranch_scc1 L_xsym%=\n"
-        "s_cmp_ge_u32 %[op], %[limm]\n"
-        "s_cbranch_scc1 L_xlim%=\n"
-        "s_bfe_u32 s91, s94, s99\n"
-        "s_lshr_b32 %[len], s99, 23\n"
-        "s_add_u32 %[len], %[len], s91\n"
-        "s_bfe_u32 s98, s99, 0x50008\n"
-        "s_lshr_b64 s[94:95], s[94:95], s98\n"
-        "s_sub_u32 %[bc], %[bc], s98\n"
-        // refill inside the token: the word is in vcur or vnxt
-        "s_cmp_gt_u32 %[bc], 32\n"
-        "s_cbranch_scc1 L_dl%=\n"
-        "s_sub_u32 s98, %[wi], %[wb]\n"
-        "s_cmp_lt_u32 s98, 64\n"
-        "s_cbranch_scc0 L_rn%=\n"
-        "s_nop 3\n"
-        "v_readlane_b32 s96, %[vc], s98\n"
-        "s_branch L_rdd%=\n"
-        "L_rn%=:\n"
-        "s_sub_u32 s98, s98, 64\n"
-        "s_waitcnt vmcnt(0)\n"
-        "s_nop 3\n"
-        "v_readlane_b32 s96, %[vn], s98\n"
-        "L_rdd%=:\n"
-        "s_lshl_b64 s[92:93], s[96:97], %[bc]\n"
-        "s_or_b64 s[94:95], s[94:95], s[92:93]\n"
-        "s_add_u32 %[wi], %[wi], 1\n"
-        "s_add_u32 %[bc], %[bc], 32\n"
-        // ---- distance: entry and base by the same index
-        "L_dl%=:\n"
-        "s_bfe_u32 s98, s94, 0x40006\n"
-        ILOOK_D
-        "s_cmp_lt_i32 s99, 0\n"
-        "s_cbranch_scc1 L_xdist%=\n"
-        "s_bfe_u32 s91, s94, s99\n"
-        "s_add_u32 %[dist], s90, s91\n"
-        "s_bfe_u32 s98, s99, 0x50008\n"
-        "s_lshr_b64 s[94:95], s[94:95], s98\n"
-        "s_sub_u32 %[bc], %[bc], s98\n"
-        // ---- the copy (op < limm: the length fits), or the caller for a distance before the output
-        "s_add_u32 s98, %[op], %[dfl]\n"
-        "s_cmp_gt_u32 %[dist], s98\n"
-        "s_cbranch_scc1 L_xmatch%=\n"
-        "s_cmp_gt_u32 %[dist], %[wmax]\n"
-        IFAR_BRANCH
-        "s_cmp_ge_u32 %[dist], %[len]\n"
-        "s_cbranch_scc1 L_cp%=\n"
-        "s_cmp_lt_u32 %[dist], 64\n"
-        "s_cbranch_scc1 L_per%=\n"
-        "L_cp%=:\n"
-        IFLUSH_PENDING(1)
-        "s_sub_u32 s98, %[op], %[dist]\n"
-        "v_add_u32 v144, s98, %[lane]\n"
-        "v_add_u32 v145, %[op], %[lane]\n"
-        "s_cmp_gt_u32 %[len], 64\n"
-        "s_cbranch_scc1 L_cpl%=\n"
-        "v_cmp_gt_u32 vcc, %[len], %[lane]\n"      // one round: lanes t < len, left pending
-        "s_and_saveexec_b64 s[92:93], vcc\n"
-        "v_and_b32 v146, %[im], v144\n"
-        "ds_read_u8 v148, v146\n"
-        "v_and_b32 v149, %[im], v145\n"
-        "v_mov_b32 v150, 0\n"
-        "s_mov_b64 exec, s[92:93]\n"
-        "s_mov_b64 s[84:85], vcc\n"
-        "s_add_u32 %[op], %[op], %[len]\n"
-        "s_cmp_gt_u32 %[bc], 32\n"
-        "s_cbranch_scc1 L_look%=\n"
-        "s_branch L_tok%=\n"
-        "L_cpl%=:\n"
-        "s_mov_b32 s99, %[len]\n"
-        "L_cr%=:\n"
-        "v_cmp_gt_u32 vcc, s99, %[lane]\n"
-        "s_and_saveexec_b64 s[92:93], vcc\n"
-        "v_and_b32 v146, %[im], v144\n"
-        "ds_read_u8 v146, v146\n"
-        "v_and_b32 v147, %[im], v145\n"
-        ICOPY_WAIT
-        "ds_write_b8 v147, v146\n"
-        "s_mov_b64 exec, s[92:93]\n"
-        "s_sub_u32 s99, s99, 64\n"
-        "s_cmp_gt_i32 s99, 0\n"
-        "s_cbranch_scc0 L_cd%=\n"
-        "v_add_u32 v144, 64, v144\n"
-        "v_add_u32 v145, 64, v145\n"
-        "s_branch L_cr%=\n"
-        "L_cd%=:\n"
-        "s_add_u32 %[op], %[op], %[len]\n"
-        "s_branch L_tok%=\n"
-        // ---- short period (dist < 64, dist < len): byte t is source byte t mod dist; lane
-        // residues start at lane mod dist (float reciprocal, corrected) and advance 64 mod dist
-        "L_per%=:\n"
-        IFLUSH_PENDING(2)
-        "s_sub_u32 s98, %[op], %[dist]\n"
-        "v_cvt_f32_u32 v146, %[dist]\n"
-        "v_rcp_f32 v146, v146\n"
-        "v_cvt_f32_u32 v144, %[lane]\n"
-        "v_mul_f32 v144, v144, v146\n"
-        "v_cvt_u32_f32 v144, v144\n"
-        "v_mul_lo_u32 v144, v144, %[dist]\n"
-        "v_sub_u32 v144, %[lane], v144\n"
-        "v_cmp_gt_i32 vcc, 0, v144\n"
-        "v_add_u32 v146, %[dist], v144\n"
-        "v_cndmask_b32 v144, v144, v146, vcc\n"
-        "v_subrev_u32 v146, %[dist], v144\n"
-        "v_cmp_le_u32 vcc, %[dist], v144\n"
-        "v_cndmask_b32 v144, v144, v146, vcc\n"
-        "s_mov_b32 s91, 64\n"
-        "L_pm%=:\n"
-        "s_cmp_lt_u32 s91, %[dist]\n"
-        "s_cbranch_scc1 L_pmd%=\n"
-        "s_sub_u32 s91, s91, %[dist]\n"
-        "s_branch L_pm%=\n"
-        "L_pmd%=:\n"
-        "v_add_u32 v145, %[op], %[lane]\n"
-        "s_mov_b32 s99, %[len]\n"
-        "L_pr%=:\n"
-        "v_cmp_gt_u32 vcc, s99, %[lane]\n"
-        "s_and_saveexec_b64 s[92:93], vcc\n"
-        "v_add_u32 v146, s98, v144\n"
-        "v_and_b32 v146, %[im], v146\n"
-        "ds_read_u8 v146, v146\n"
-        "v_and_b32 v147, %[im], v145\n"
-        "s_waitcnt lgkmcnt(0)\n"
-        "ds_write_b8 v147, v146\n"
-        "s_mov_b64 exec, s[92:93]\n"
-        "s_sub_u32 s99, s99, 64\n"
-        "s_cmp_gt_i32 s99, 0\n"
-        "s_cbranch_scc0 L_cd%=\n"
-        "v_add_u32 v145, 64, v145\n"
-        "v_add_u32 v144, s91, v144\n"
-        "v_subrev_u32 v146, %[dist], v144\n"
-        "v_cmp_le_u32 vcc, %[dist], v144\n"
-        "v_cndmask_b32 v144, v144, v146, vcc\n"
-        "s_branch L_pr%=\n"
-        // ---- a source older than the ring: from the output already in HBM (flushed, the
-        // stores complete), agent-scope dword loads (to L2, past the vector L1)
-        "L_far%=:\n"
-        IFLUSH_PENDING(3)
-        "s_sub_u32 s98, %[op], %[dist]\n"
-        "s_add_u32 s98, s98, %[gmis]\n"
-        "v_add_u32 v144, s98, %[lane]\n"
-        "v_add_u32 v145, %[op], %[lane]\n"
-        "s_cmp_gt_u32 %[len], 64\n"
-        "s_cbranch_scc1 L_farl%=\n"
-        "v_cmp_gt_u32 vcc, %[len], %[lane]\n"      // one round, left pending
-        "s_and_saveexec_b64 s[92:93], vcc\n"
-        "v_and_b32 v146, -4, v144\n"
-        "global_load_dword v148, v146, %[galn] sc1\n"
-        "v_and_b32 v150, 3, v144\n"
-        "v_lshlrev_b32 v150, 3, v150\n"
-        "v_and_b32 v149, %[im], v145\n"
-        "s_mov_b64 exec, s[92:93]\n"
-        "s_mov_b64 s[84:85], vcc\n"
-        "s_add_u32 %[op], %[op], %[len]\n"
-        "s_cmp_gt_u32 %[bc], 32\n"
-        "s_cbranch_scc1 L_look%=\n"
-        "s_branch L_tok%=\n"
-        "L_farl%=:\n"
-        "s_mov_b32 s99, %[len]\n"
-        "L_fr%=:\n"
-        "v_cmp_gt_u32 vcc, s99, %[lane]\n"
-        "s_and_saveexec_b64 s[92:93], vcc\n"
-        "v_and_b32 v146, -4, v144\n"
-        "global_load_dword v146, v146, %[galn] sc1\n"
-        "v_and_b32 v147, 3, v144\n"
-        "v_lshlrev_b32 v147, 3, v147\n"
-        "s_waitcnt vmcnt(0)\n"
-        "v_lshrrev_b32 v146, v147, v146\n"
-        "v_and_b32 v147, %[im], v145\n"
-        "ds_write_b8 v147, v146\n"
-        "s_mov_b64 exec, s[92:93]\n"
-        "s_sub_u32 s99, s99, 64\n"
-        "s_cmp_gt_i32 s99, 0\n"
-        "s_cbranch_scc0 L_cd%=\n"
-        "v_add_u32 v144, 64, v144\n"
-        "v_add_u32 v145, 64, v145\n"
-        "s_branch L_fr%=\n"
-        // ---- exits
-        "L_xsym%=:\n"
-        "s_mov_b32 %[ex], 1\n"
-        "s_branch L_end%=\n"
-        "L_xseg%=:\n"
-        "s_mov_b32 %[ex], 2\n"
-        "s_branch L_end%=\n"
-        "L_xlim%=:\n"
-        "s_mov_b32 %[ex], 3\n"
-        "s_branch L_end%=\n"
-        "L_xdist%=:\n"
-        "s_mov_b32 %[ex], 4\n"
-        "s_branch L_end%=\n"
-        "L_xmatch%=:\n"
-        "s_mov_b32 %[ex], 5\n"
-        "L_end%=:\n"
-        IFLUSH_PENDING(4)
-        "s_waitcnt vmcnt(0) lgkmcnt(0)\n"
-        "s_mov_b32 m0, s89\n"
-        "s_mov_b64 %[bb], s[94:95]\n"
-        : [bb] "+s"(r.bb), [bc] "+s"(r.bc), [wi] "+s"(r.wi), [wb] "+s"(r.wb), [vc] "+v"(r.vcur),
-          [vn] "+v"(r.vnxt), [op] "+s"(op), [ex] "=&s"(ex), [len] "=&s"(len), [dist] "=&s"(dist)
-        : [lim] "s"(lim), [limm] "s"(limm), [dfl] "s"(dfl), [tla] "v"(tla), [tda] "v"(tda), [lane] "v"(lane),
-          [wrl] "s"(wrl), [zb] "s"(zb), [galn] "s"(galn), [gmis] "s"(gmis), [im] "n"(W - 1), [wmax] "n"(W)
-        : "memory", "vcc", "scc", "s84", "s85", "s86", "s87", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99",
-          "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149", "v150");
+    if constexpr (!CELL) {
+#define ISYM_CELL 0
+#include "dmx_isym.inc"
+#undef ISYM_CELL
+    } else {
+#define ISYM_CELL 1
+#include "dmx_isym.inc"
+#undef ISYM_CELL
+    }
     return ex;
 }
 
@@ -845,9 +543,13 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
 // RING: flush to HBM every half ring (ADLER: folding the Adler-32 sums; the stream mode);
 // otherwise the whole output stays in the window.  W < 32 KiB: matches farther than the ring
 // read their source from the output already flushed to HBM.
-template <bool RING, bool ADLER, uint32_t W>
-__device__ __forceinline__ int iblock(InfLDS<W>& S, IBits& r, IOut& o, uint32_t lane, bool& last) {
+// CELL: the chained decode of dictionary streams -- the window and the output hold 16-bit
+// cells; a match reaching before the sw block's first byte writes reference cells there.
+template <bool RING, bool ADLER, uint32_t W, bool CELL = false>
+__device__ __forceinline__ int iblock(InfLDS<W, typename std::conditional<CELL, uint16_t, uint8_t>::type>& S, IBits& r,
+                                      IOut& o, uint32_t lane, bool& last) {
     constexpr uint32_t IM = W - 1, FL = W / 2;
+    constexpr uint32_t CS = CELL ? 2 : 1;   // bytes per output position
     [[maybe_unused]] const unsigned long long ts0 = IST_NOW();
     IST_ADD(o, 6, 1);
     last = ib_bits(r, 1) != 0;
@@ -949,12 +651,12 @@ __device__ __forceinline__ int iblock(InfLDS<W>& S, IBits& r, IOut& o, uint32_t 
     if (lds_addr(S.win) != 0) return -(int)E_RANGE;   // isym_run addresses the ring from LDS 0
     const uint32_t tla = lds_addr(S.lt.fast) + lane * 4, tda = lds_addr(S.dt.fast) + lane * 4;
     const uint32_t dfl = o.ob != 0 ? 0x40000000u : 0u;   // stream mode: sources before ob exist
-    const uint64_t gpos0 = (uint64_t)(uintptr_t)(o.out + o.base + o.ob);
+    const uint64_t gpos0 = (uint64_t)(uintptr_t)(o.out + CS * (o.base + o.ob));
     for (;;) {
         const uint32_t lim = RING ? min(capr, o.fl + FL) : capr;
         const uint32_t limm = rfl(min(lim, capr >= 258 ? capr - 258 : 0u));   // below it any length fits
         uint32_t len, dist;
-        const uint32_t ex = isym_run<W>(r, op, lim, limm, dfl, tla, tda, lane, gpos0, len, dist);
+        const uint32_t ex = isym_run<W, CELL>(r, op, lim, limm, dfl, tla, tda, lane, gpos0, len, dist);
         if (ex == IX_SEG) {   // a refill at a token start that the run does not rotate into
             ib_refill(r);
             continue;
@@ -978,7 +680,7 @@ __device__ __forceinline__ int iblock(InfLDS<W>& S, IBits& r, IOut& o, uint32_t 
             if (!(en & 0x8000u)) {   // a literal: at the capacity limit, or a long code
                 ib_drop(r, en & 31u);
                 if (op >= capr) { err = -(int)E_SZ; break; }
-                S.win[op & IM] = (uint8_t)(en >> 16);
+                S.win[op & IM] = (uint8_t)(en >> 16);   // (a byte value in a cell, too)
                 op++;
                 continue;
             }
@@ -1001,7 +703,7 @@ __device__ __forceinline__ int iblock(InfLDS<W>& S, IBits& r, IOut& o, uint32_t 
             dist = iv_dbase(ed) + iv_extra(r.bb, ed);
             ib_drop(r, (ed >> 8) & 31u);
         }
-        if (o.ob == 0 && dist > op) { err = -(int)E_HUFDIS; break; }
+        if (o.ob == 0 && dist > op && (!CELL || dist - op > o.base)) { err = -(int)E_HUFDIS; break; }
         if (len > capr - op) { err = -(int)E_SZ; break; }
         if (RING && op - o.fl >= FL) {   // half the ring is due before this match
             o.op = op;
@@ -1011,16 +713,36 @@ __device__ __forceinline__ int iblock(InfLDS<W>& S, IBits& r, IOut& o, uint32_t 
         }
         const uint32_t src = op - dist;
         IST_ADD(o, 3, 1);
-        if (W < IW && dist > W) {
+        if (CELL && dist > op) {   // (o.ob == 0 here) from before the sw block: reference cells
+            const uintptr_t g = (uintptr_t)(o.out + CS * o.base);
+            auto cell_at = [&](uint32_t t) -> uint32_t {   // output position op + t
+                const int32_t sp = (int32_t)op - (int32_t)dist + (int32_t)t;
+                if (sp < 0) return 0xFFu + (uint32_t)(-sp);   // 0x100 + (back - 1)
+                if (t >= dist) return S.win[(op + t - dist) & IM];   // this match's own output
+                if (W < IW && dist > W) {   // flushed: from the cell buffer
+                    const uintptr_t a = g + CS * (uintptr_t)sp;
+                    const uint32_t w = __hip_atomic_load((gu32*)(a & ~(uintptr_t)3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    return (w >> (8 * (a & 3))) & 0xFFFFu;
+                }
+                return S.win[(uint32_t)sp & IM];
+            };
+            if (len <= dist) {
+                for (uint32_t t = lane; t < len; t += 64) S.win[(op + t) & IM] = cell_at(t);
+            } else {   // the match overlaps itself (rare): in order, one lane
+                if (lane == 0)
+                    for (uint32_t t = 0; t < len; t++) S.win[(op + t) & IM] = cell_at(t);
+            }
+            __syncthreads();
+        } else if (W < IW && dist > W) {
             IST_ADD(o, 4, 1);
             // older than the ring: from the output in HBM, flushed before this match (op - fl
             // stays below W / 2 + 258, so every source byte lies below fl).  Agent-scope loads
             // go to L2, past any vector-L1 copy of a line that was flushed in two pieces.
-            const uintptr_t g = (uintptr_t)(o.out + o.base + o.ob);
+            const uintptr_t g = (uintptr_t)(o.out + CS * (o.base + o.ob));
             for (uint32_t t = lane; t < len; t += 64) {
-                const uintptr_t a = g + src + t;
+                const uintptr_t a = g + CS * (uintptr_t)(src + t);
                 const uint32_t w = __hip_atomic_load((gu32*)(a & ~(uintptr_t)3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                S.win[(op + t) & IM] = (uint8_t)(w >> (8 * (a & 3)));
+                S.win[(op + t) & IM] = CELL ? (w >> (8 * (a & 3))) & 0xFFFFu : (w >> (8 * (a & 3))) & 0xFFu;
             }
         } else if (dist >= 64 || dist >= len) {   // every read is of bytes written before its round
             for (uint32_t t = lane; t < len; t += 64) S.win[(op + t) & IM] = S.win[(src + t) & IM];
@@ -1043,11 +765,15 @@ __device__ __forceinline__ int iblock(InfLDS<W>& S, IBits& r, IOut& o, uint32_t 
     return 0;
 }
 
+// CELL: out is the cell buffer (2 bytes a position), out_cap in positions
+template <bool CELL>
 __global__ __launch_bounds__(64) void dmx_inflate_index_kernel(const uint8_t* __restrict__ z, uint64_t zbytes,
                                                                const dmx_iblock* __restrict__ index,
                                                                uint8_t* __restrict__ out, uint64_t out_cap,
                                                                dmx_inflate_status* __restrict__ st) {
-    __shared__ InfLDS<IWX> S;   // 8 KiB ring: 18 KiB of LDS, 8 workgroups per CU (a 32 KiB window allowed 4)
+    // bytes: an 8 KiB ring, 18 KiB of LDS, 8 workgroups per CU (a 32 KiB window allowed 4);
+    // cells: 16 KiB of ring, 26 KiB, 6 per CU
+    __shared__ InfLDS<IWX, typename std::conditional<CELL, uint16_t, uint8_t>::type> S;
     const uint32_t lane = threadIdx.x;
     IBits r;
     ib_init(r, z, zbytes);
@@ -1072,7 +798,7 @@ __global__ __launch_bounds__(64) void dmx_inflate_index_kernel(const uint8_t* __
         ib_seek(r, bit);
         bool last = false;
         do {   // one sw block may be several DEFLATE blocks (DMX_F_SPLIT)
-            err = iblock<true, false, IWX>(S, r, o, lane, last);
+            err = iblock<true, false, IWX, CELL>(S, r, o, lane, last);
         } while (!err && o.op < olen && !last);
         if (!err && o.op != olen) err = -(int)E_SZ;
         if (!err) io_flush<false>(S, o, o.op, lane);
@@ -1142,11 +868,149 @@ extern "C" int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_ibl
     hipStream_t s = (hipStream_t)stream;
     if (hipMemsetAsync(d_status, 0, sizeof(dmx_inflate_status), s) != hipSuccess) return -(int)E_DEVICE;
     if (d_index)
-        hipLaunchKernelGGL(dmx_inflate_index_kernel, dim3(nblk), dim3(64), 0, s, (const uint8_t*)d_z, zbytes,
+        hipLaunchKernelGGL(dmx_inflate_index_kernel<false>, dim3(nblk), dim3(64), 0, s, (const uint8_t*)d_z, zbytes,
                            d_index, (uint8_t*)d_out, out_cap, d_status);
     else
         hipLaunchKernelGGL(dmx_inflate_stream_kernel, dim3(1), dim3(64), 0, s, (const uint8_t*)d_z, zbytes,
                            (uint8_t*)d_out, out_cap, d_status);
+    if (hipGetLastError() != hipSuccess) return -(int)E_DEVICE;
+    return 0;
+}
+
+// ------------------------------------------------------------------------------------
+// Chained decode (dictionary streams, DMX_F_DICT: a block's matches may reach into the block
+// before it).  Three steps, all blocks in parallel:
+//   1. dmx_inflate_index_kernel<true>: every sw block decodes on its own into 16-bit cells; a
+//      byte it cannot know yet (a match source before the block's first output byte, or a
+//      copy of such a cell) becomes a reference cell 0x100 + b - 1 = the byte b positions
+//      before the block's start.  Copies inside the block copy cells, so a reference always
+//      names a byte of an EARLIER block.
+//   2. dmx_cells_prep_kernel: each reference becomes an absolute source position P[j]; the
+//      cell is marked unresolved (0xFFFF).
+//      dmx_cells_jump_kernel, about log2(nblk) + 2 launches: every unresolved j looks at its
+//      source s = P[j]: a resolved cell is copied, otherwise P[j] = P[s] (pointer jumping:
+//      chains of references through many blocks -- a run carried across every block, say --
+//      halve each launch).  In place: a stale read only delays resolution, never changes
+//      the value (P moves along the chain, a resolved cell stays).  A launch whose
+//      predecessor left nothing unresolved returns at once.
+//   3. dmx_cells_final_kernel: cells -> bytes; any cell still unresolved is an error.
+// ------------------------------------------------------------------------------------
+#define CHAIN_ROUNDS_MAX 40
+struct ChainWork {   // the head of the work buffer: unresolved counts per round
+    uint32_t left[CHAIN_ROUNDS_MAX + 1];
+};
+
+__global__ __launch_bounds__(256) void dmx_cells_prep_kernel(const dmx_iblock* __restrict__ index, uint16_t* __restrict__ cells,
+                                                            uint32_t* __restrict__ P, ChainWork* __restrict__ W,
+                                                            dmx_inflate_status* __restrict__ st) {
+    const uint64_t off = index[blockIdx.x].out_off;
+    const uint32_t len = index[blockIdx.x].out_len;
+    uint32_t nl = 0;
+    bool bad = false;
+    for (uint32_t j = threadIdx.x; j < len; j += 256) {
+        const uint32_t c = cells[off + j];
+        if (c >= 0x100u) {
+            const uint64_t back = (uint64_t)(c - 0xFFu) + j;   // positions before j
+            if (back > off + j) { bad = true; continue; }
+            P[off + j] = (uint32_t)(off + j - back);
+            cells[off + j] = 0xFFFFu;
+            nl++;
+        }
+    }
+    nl = __reduce_add_sync(~0ull, nl);
+    if ((threadIdx.x & 63) == 0 && nl) atomicAdd(&W->left[0], nl);
+    if (bad) atomicCAS(&st->status, 0, -(int32_t)E_HUFDIS);
+}
+
+__global__ __launch_bounds__(256) void dmx_cells_jump_kernel(uint16_t* __restrict__ cells, uint32_t* __restrict__ P,
+                                                            uint64_t n, ChainWork* __restrict__ W, uint32_t round) {
+    if (__hip_atomic_load(&W->left[round], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+    uint32_t nl = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * 8;
+    for (uint64_t j0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 8; j0 < n; j0 += stride) {
+        uint16_t c[8];
+        const bool full = j0 + 8 <= n;
+        if (full) {
+            const uint4 v = *reinterpret_cast<const uint4*>(cells + j0);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 8; k++) c[k] = (uint16_t)(w[k >> 1] >> (16 * (k & 1)));
+        } else {
+            for (int k = 0; k < 8; k++) c[k] = j0 + k < n ? cells[j0 + k] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            if (c[k] != 0xFFFFu) continue;
+            const uint64_t j = j0 + k;
+            const uint32_t sp = P[j];
+            if ((uint64_t)sp >= j) continue;   // never from a well-formed prep (sources precede): stays unresolved
+            const uint16_t cs = __hip_atomic_load(cells + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cs != 0xFFFFu) {
+                cells[j] = cs;
+            } else {
+                P[j] = __hip_atomic_load(P + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                nl++;
+            }
+        }
+    }
+    nl = __reduce_add_sync(~0ull, nl);
+    if ((threadIdx.x & 63) == 0 && nl) atomicAdd(&W->left[round + 1], nl);
+}
+
+__global__ __launch_bounds__(256) void dmx_cells_final_kernel(const uint16_t* __restrict__ cells, uint8_t* __restrict__ out,
+                                                             uint64_t n, dmx_inflate_status* __restrict__ st) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * 16;
+    bool bad = false;
+    for (uint64_t j0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16; j0 < n; j0 += stride) {
+        if (j0 + 16 <= n && ((uintptr_t)(out + j0) & 15) == 0) {
+            const uint4 a = *reinterpret_cast<const uint4*>(cells + j0), b = *reinterpret_cast<const uint4*>(cells + j0 + 8);
+            const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+            uint32_t o[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t lo = w[2 * k], hi = w[2 * k + 1];
+                bad = bad || ((lo | hi) & 0xFF00FF00u) != 0;
+                o[k] = (lo & 0xFFu) | ((lo >> 8) & 0xFF00u) | ((hi & 0xFFu) << 16) | ((hi >> 8) & 0xFF000000u);
+            }
+            *reinterpret_cast<uint4*>(out + j0) = make_uint4(o[0], o[1], o[2], o[3]);
+        } else {
+            for (uint64_t j = j0; j < n && j < j0 + 16; j++) {
+                bad = bad || cells[j] > 0xFFu;
+                out[j] = (uint8_t)cells[j];
+            }
+        }
+    }
+    if (bad) atomicCAS(&st->status, 0, -(int32_t)E_HUFDIS);
+}
+
+extern "C" uint64_t dmx_inflate_chained_work(uint64_t out_cap) {
+    return 256 + ((2 * out_cap + 255) & ~255ull) + 4 * out_cap;
+}
+
+extern "C" int dmx_inflate_chained_async(const void* d_z, uint64_t zbytes, const dmx_iblock* d_index, uint32_t nblk,
+                                         void* d_out, uint64_t out_cap, void* d_work, uint64_t work_bytes,
+                                         dmx_inflate_status* d_status, void* stream) {
+    if (!d_z || !d_out || !d_status || !d_index || !nblk || !d_work) return -(int)E_INVAL;
+    if (zbytes > 0xFFFFFFF0ull || out_cap > 0xFFFFFFF0ull) return -(int)E_RANGE;   // 32-bit positions
+    if (work_bytes < dmx_inflate_chained_work(out_cap) || ((uintptr_t)d_work & 255)) return -(int)E_SZ;
+    hipStream_t s = (hipStream_t)stream;
+    ChainWork* W = (ChainWork*)d_work;
+    uint16_t* cells = (uint16_t*)((uint8_t*)d_work + 256);
+    uint32_t* P = (uint32_t*)((uint8_t*)cells + ((2 * out_cap + 255) & ~255ull));
+    if (hipMemsetAsync(d_status, 0, sizeof(dmx_inflate_status), s) != hipSuccess) return -(int)E_DEVICE;
+    if (hipMemsetAsync(W, 0, sizeof(ChainWork), s) != hipSuccess) return -(int)E_DEVICE;
+    hipLaunchKernelGGL(dmx_inflate_index_kernel<true>, dim3(nblk), dim3(64), 0, s, (const uint8_t*)d_z, zbytes, d_index,
+                       (uint8_t*)cells, out_cap, d_status);
+    hipLaunchKernelGGL(dmx_cells_prep_kernel, dim3(nblk), dim3(256), 0, s, d_index, cells, P, W, d_status);
+    uint32_t rounds = 2;   // pointer jumping: a chain through k blocks takes ~log2(k) + 1 rounds
+    while ((1ull << (rounds - 2)) < (uint64_t)nblk && rounds < CHAIN_ROUNDS_MAX) rounds++;
+    const uint64_t g0 = (out_cap + 2047) / 2048;
+    const uint32_t g = (uint32_t)(g0 < 4096 ? g0 : 4096);
+    for (uint32_t rd = 0; rd < rounds; rd++)
+        hipLaunchKernelGGL(dmx_cells_jump_kernel, dim3(g ? g : 1), dim3(256), 0, s, cells, P, out_cap, W, rd);
+    const uint64_t gf0 = (out_cap + 4095) / 4096;
+    const uint32_t gf = (uint32_t)(gf0 < 4096 ? gf0 : 4096);
+    hipLaunchKernelGGL(dmx_cells_final_kernel, dim3(gf ? gf : 1), dim3(256), 0, s, cells, (uint8_t*)d_out, out_cap, d_status);
     if (hipGetLastError() != hipSuccess) return -(int)E_DEVICE;
     return 0;
 }

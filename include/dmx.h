@@ -256,6 +256,18 @@ int dmx_block_index(dmx_ctx* ctx, dmx_iblock* d_index, uint32_t cap, void* strea
 int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_iblock* d_index, uint32_t nblk, void* d_out,
                       uint64_t out_cap, dmx_inflate_status* d_status, void* stream);
 
+/* Chained GPU inflate: the blocks listed in d_index decoded in parallel although a block's
+ * matches may reach into the blocks before it (DMX_F_DICT streams; any stream cut at block
+ * starts).  Each block decodes into 16-bit cells -- a byte, or a reference to a position
+ * before the block -- and pointer jumping over the references, about log2(nblk) + 2 short
+ * launches, resolves them; then the cells become bytes in d_out.  d_work: device scratch of
+ * dmx_inflate_chained_work(out_cap) bytes, 256-byte aligned.  Status in d_status (out_len =
+ * bytes decoded; a reference before the output start is -E_HUFDIS).  Returns 0 or -E_*. */
+uint64_t dmx_inflate_chained_work(uint64_t out_cap);
+int dmx_inflate_chained_async(const void* d_z, uint64_t zbytes, const dmx_iblock* d_index, uint32_t nblk, void* d_out,
+                              uint64_t out_cap, void* d_work, uint64_t work_bytes, dmx_inflate_status* d_status,
+                              void* stream);
+
 /* Introspection of the last encode of ctx (tests / fd_stats): per-block token
  * counts and the token stream (t = byte | dist << 9 | len),
  * per-block BTYPE, and the lit/len + distance code lengths (286 + 30 per block). */

@@ -124,6 +124,47 @@ def test_dict_gpu_inflate_stream_mode(enc):
         assert D.deflate_decompress(z) == data
 
 
+def chained(enc, z: bytes, n: int):
+    dz = torch.frombuffer(bytearray(z), dtype=torch.uint8).cuda()
+    ix, nblk = enc.block_index()
+    out, st = D.inflate_gpu_chained(dz, n, ix, nblk)
+    return out.cpu().numpy().tobytes(), st
+
+
+@pytest.mark.parametrize("K", [0, 6])
+@pytest.mark.parametrize("lazy", [False, True])
+def test_dict_gpu_inflate_chained(enc, K, lazy):
+    """Dict streams decoded with every block in parallel (dmx_inflate_chained_async: cells with
+    references to the bytes before the block, resolved by pointer jumping), bit-exact on the
+    streams of every dict input, K in {0, 6}, greedy and lazy; with DMX_F_SPLIT too."""
+    flags = D.DMX_ZLIB | D.DMX_F_DICT | (D.DMX_F_LAZY if lazy else 0)
+    for name, data in _inputs().items():
+        for f in (flags, flags | D.DMX_F_SPLIT):
+            z, _ = enc.compress_bytes(data, max_chain=K, flags=f)
+            out, st = chained(enc, z, len(data))
+            assert st == 0 and out == data, (name, K, lazy, f)
+
+
+def test_dict_gpu_inflate_chained_edges(enc):
+    """Chains through every block (runs carried across blocks: each block's bytes come from
+    the one before), distance 32768, small windows, edge sizes, a plain (no-dict) stream."""
+    text = D.gen_text(300000, 41).tobytes()
+    cases = [bytes(700000), (b"xy" * 7) * 60000, text[:32768] * 9, text[:32768] + text[:32768],
+             text[:1], text[:32769], text[:65537], bytes(32768) + text[:1000]]
+    for data in cases:
+        z, _ = enc.compress_bytes(data, max_chain=6, flags=D.DMX_ZLIB | D.DMX_F_DICT | D.DMX_F_LAZY)
+        out, st = chained(enc, z, len(data))
+        assert st == 0 and out == data, len(data)
+    for sw in (1024, 5000):
+        data = text[:120000]
+        z, _ = enc.compress_bytes(data, sw=sw, max_chain=6, flags=D.DMX_ZLIB | D.DMX_F_DICT | D.DMX_F_LAZY)
+        out, st = chained(enc, z, len(data))
+        assert st == 0 and out == data, sw
+    z, _ = enc.compress_bytes(text, max_chain=6, flags=D.DMX_ZLIB | D.DMX_F_LAZY)   # no references at all
+    out, st = chained(enc, z, len(text))
+    assert st == 0 and out == text
+
+
 def test_dict_max_distance_tokens(enc):
     """A block equal to its predecessor: position 0 matches at distance exactly 32768."""
     text = D.gen_text(40000, 13).tobytes()
@@ -134,6 +175,8 @@ def test_dict_max_distance_tokens(enc):
     assert int(np.where(t >> 9, t & 0x1FF, 1).sum()) == 32768
     assert z == O.compress(data, max_chain=0, dict=True)
     out, st = gpu_inflate_stream(z, len(data))
+    assert st == 0 and out == data
+    out, st = chained(enc, z, len(data))
     assert st == 0 and out == data
     assert zlib.decompress(z) == data
 
