@@ -970,7 +970,7 @@ __global__ __launch_bounds__(256) void dmx_cells_final_kernel(const uint16_t* __
             for (int k = 0; k < 4; k++) {
                 const uint32_t lo = w[2 * k], hi = w[2 * k + 1];
                 bad = bad || ((lo | hi) & 0xFF00FF00u) != 0;
-                o[k] = (lo & 0xFFu) | ((lo >> 8) & 0xFF00u) | ((hi & 0xFFu) << 16) | ((hi >> 8) & 0xFF000000u);
+                o[k] = (lo & 0xFFu) | ((lo >> 8) & 0xFF00u) | ((hi & 0xFFu) << 16) | ((hi << 8) & 0xFF000000u);
             }
             *reinterpret_cast<uint4*>(out + j0) = make_uint4(o[0], o[1], o[2], o[3]);
         } else {
