@@ -1546,10 +1546,42 @@ __device__ __forceinline__ uint32_t uniform_parse(uint32_t bn, uint32_t c, uint3
 }
 
 // prestored: 0 = parse in K1; 1 = stored by the noise check; 2 = a block of one repeated
-// byte, parsed here in closed form (K1 skips it, the Huffman kernels code it).
+// byte, parsed here in closed form (K1 skips it, the Huffman kernels code it); 3 = stored,
+// and its interior already written to the stream at the offset it has when every block
+// before it is stored too (below; the pack kernel then writes only the rest).
+//
+// The speculative copy: block b of a stream whose blocks 0..b-1 are all stored starts at bit
+// start + 8 b (sw + 5) (each stored block: one header byte with its 3 bits, LEN/NLEN, sw data
+// bytes).  A stored block copies itself there -- the whole 16-byte output quads the pack
+// kernel would copy (dmx_pack_kernel's stored path, same quads, same condition) -- while its
+// input is still in L2 from the check, so on noise the input crosses HBM once and the pack
+// kernel only writes the edges.  If an earlier block is not stored, the scan gives this block
+// another offset; the pack kernel then writes the whole block and every other block writes
+// all of its words, so a misplaced quad inside the stream is overwritten (words shared
+// between blocks are zeroed by the scan first), and one past the stream's end is outside it.
+__device__ __forceinline__ uint64_t spec_stored_bit(uint32_t b, uint32_t sw, uint32_t flags) {
+    return ((flags & DMX_F_HEADER) ? 16ull : 0ull) + 8ull * (uint64_t)b * ((uint64_t)sw + 5);
+}
+// the stored block's 16-byte output quads with a whole 20-byte input window (the pack
+// kernel's fast path); calls f(k, o0) for every such quad: output word gw0 + k, input offset o0
+template <typename F>
+__device__ __forceinline__ void stored_quads(uint64_t O, uint32_t bn, bool dal, uint32_t tid, uint32_t nthr, F f) {
+    const uint32_t s0 = (uint32_t)(O & 31);
+    const uint32_t P = (s0 + 3 + 7) & ~7u, B0 = (P + 32) >> 3;   // as the pack kernel: LEN/NLEN at P / 8, data at B0
+    const uint32_t nwords = (uint32_t)(((uint64_t)P + 32 + 8ull * bn + 31) >> 5);   // (s0 + len_bits + 31) / 32
+    const uint64_t gw0 = O >> 5;
+    const uint32_t ks = 4 - (uint32_t)(gw0 & 3);
+    const uint32_t nq = (dal && nwords > ks + 1) ? (nwords - 1 - ks) >> 2 : 0;
+    for (uint32_t j = tid; j < nq; j += nthr) {
+        const uint32_t k = ks + 4 * j;
+        const int64_t o0 = (int64_t)(4 * k) - (int64_t)B0;
+        if (o0 >= 0 && (uint64_t)((o0 & ~3ll) + 20) <= bn) f(k, o0);
+    }
+}
 __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
                                                               dmx_blkinfo* __restrict__ info, uint32_t* __restrict__ tok_g,
-                                                              uint32_t* __restrict__ hist_g, uint32_t uni_ok) {
+                                                              uint32_t* __restrict__ hist_g, uint32_t uni_ok, uint32_t flags,
+                                                              uint32_t* __restrict__ out32, uint64_t out_cap) {
     __shared__ uint32_t bm[1u << 13];
     __shared__ uint32_t hist[256];
     __shared__ uint64_t red[10][SCT / 64];
@@ -1726,7 +1758,10 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
         const uint64_t m = ((uint64_t)bn + smask) / (smask + 1), m2 = m * m;
         const uint64_t coll = Q - Dn;
         const bool sto = 256 * S2 <= m2 + (m2 >> 4) + 256 * m && 16 * Q >= (uint64_t)bn && 64 * coll <= 4 * Q;
-        info[b].prestored = sto ? 1u : 0u;
+        // the speculative copy (above) when the whole block fits the output at that offset
+        const bool spec = sto && (spec_stored_bit(b, sw, flags) >> 3) + (uint64_t)bn + 16 <= out_cap;
+        info[b].prestored = sto ? (spec ? 3u : 1u) : 0u;
+        pass_s = spec ? 1u : 0u;
         if (sto) {
             info[b].ntok = 0;
             info[b].n = bn;
@@ -1737,6 +1772,22 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
             info[b].body_bits = 0;
             info[b].nsub = 1;
         }
+    }
+    __syncthreads();
+    if (pass_s) {
+        const uint64_t O = spec_stored_bit(b, sw, flags);
+        const bool dal = (reinterpret_cast<uintptr_t>(d) & 3) == 0;
+        stored_quads(O, bn, dal, tid, SCT, [&](uint32_t k, int64_t o0) {
+            const uint32_t* p32 = reinterpret_cast<const uint32_t*>(d + (o0 & ~3ll));
+            const uint32_t w0 = p32[0], w1 = p32[1], w2 = p32[2], w3 = p32[3], w4 = p32[4];
+            const uint32_t sh = (uint32_t)(o0 & 3);
+            uint4 v;
+            v.x = sh ? __builtin_amdgcn_alignbyte(w1, w0, sh) : w0;
+            v.y = sh ? __builtin_amdgcn_alignbyte(w2, w1, sh) : w1;
+            v.z = sh ? __builtin_amdgcn_alignbyte(w3, w2, sh) : w2;
+            v.w = sh ? __builtin_amdgcn_alignbyte(w4, w3, sh) : w3;
+            *reinterpret_cast<uint4*>(&out32[(O >> 5) + k]) = v;
+        });
     }
 }
 
@@ -2659,7 +2710,7 @@ __global__ __launch_bounds__(64) void dmx_huff_kernel(const uint32_t* __restrict
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x;
     const uint32_t* hg = hist_g + (uint64_t)b * DMX_HIST;
-    if (info[b].prestored == 1) return;   // K0 wrote the stored record
+    if (info[b].prestored & 1u) return;   // K0 wrote the stored record (1, 3)
     const uint32_t bn = info[b].n;
     const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1) ? 1u : 0u;
 
@@ -2727,7 +2778,7 @@ __global__ __launch_bounds__(SHT) void dmx_split_hist_kernel(const uint32_t* __r
     __shared__ uint32_t qt[5], wsum[SHT / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t b = blockIdx.x;
-    if (info[b].prestored == 1) return;   // K0 wrote the stored record
+    if (info[b].prestored & 1u) return;   // K0 wrote the stored record (1, 3)
     const uint32_t ntok = info[b].ntok, bn = info[b].n;
     for (uint32_t k = tid; k < 4 * DMX_HIST; k += SHT) (&qh[0][0])[k] = 0;
     if (tid < 5) qt[tid] = tid == 4 ? ntok : 0u;
@@ -2789,7 +2840,7 @@ __global__ __launch_bounds__(64) void dmx_split_plan_kernel(SplitScratch* __rest
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x / SPW, g = blockIdx.x % SPW;
     SplitScratch& o = sp[b];
-    if (info[b].prestored == 1) return;
+    if (info[b].prestored & 1u) return;
     const uint32_t bn = info[b].n;
     const uint32_t i = c_gi[g], j = c_gj[g];
     const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1 && j == 3) ? 1u : 0u;
@@ -2830,7 +2881,7 @@ __global__ __launch_bounds__(64) void dmx_split_choose_kernel(const SplitScratch
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x;
     const SplitScratch& o = sp[b];
-    if (info[b].prestored == 1) return;
+    if (info[b].prestored & 1u) return;
     if (lane == 0) {   // cheapest cut mask: bit k = a cut after quarter k
         int best = -1;
         uint64_t bestc = 0;
@@ -3229,12 +3280,15 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
             else out32[gw0 + k] = v;
         };
         const bool dal = (reinterpret_cast<uintptr_t>(d) & 3) == 0;
+        // K0's speculative copy landed where the scan put the block: its quads are written
+        const bool spec = bi.prestored == 3 && O == spec_stored_bit(b, sw, flags);
         const uint32_t ks = 4 - (uint32_t)(gw0 & 3);                      // first quad: (gw0 + ks) % 4 == 0, ks >= 1
         const uint32_t nq = (dal && nwords > ks + 1) ? (nwords - 1 - ks) >> 2 : 0;   // quads short of the last word
         for (uint32_t j = tid; j < nq; j += PT) {
             const uint32_t k = ks + 4 * j;
             const int64_t o0 = (int64_t)(4 * k) - (int64_t)B0;
             if (o0 >= 0 && (uint64_t)((o0 & ~3ll) + 20) <= bn) {
+                if (spec) continue;
                 const uint32_t* p32 = reinterpret_cast<const uint32_t*>(d + (o0 & ~3ll));
                 const uint32_t w0 = p32[0], w1 = p32[1], w2 = p32[2], w3 = p32[3], w4 = p32[4];
                 const uint32_t sh = (uint32_t)(o0 & 3);
@@ -3699,7 +3753,8 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         // stage 0 also holds K0, the noise check (DMX_F_STORE_CHECK)
         if (o.flags & DMX_F_STORE_CHECK)
             hipLaunchKernelGGL(dmx_store_check_kernel, dim3(nblk), dim3(SCT), 0, s, (const uint8_t*)d_in, n,
-                               (uint32_t)o.sw, c->info, c->tok, c->hist, (o.flags & DMX_F_DICT) ? 0u : 1u);
+                               (uint32_t)o.sw, c->info, c->tok, c->hist, (o.flags & DMX_F_DICT) ? 0u : 1u, o.flags,
+                               (uint32_t*)d_out, out_cap);
         if (ev) (void)hipEventRecord(ev[1], s);
         const char* dstop = getenv("DMX_DEBUG_STOP");   // diagnostic only (dbg_stop)
         const uint32_t mfl = ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u) |
