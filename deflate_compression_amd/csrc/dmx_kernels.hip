@@ -1143,11 +1143,11 @@ __device__ __forceinline__ uint32_t gram_pass(MatchLDS& L, uint32_t nv, uint32_t
             const uint32_t u = atomicAdd(&L.ntok, 1u);
             if (u < 2 * (DMX_BLK / 32)) {
                 UL[u] = ((k - PW) << 16) | k;
-            } else {
-                const uint32_t k0 = L.bstart[hb];
-                for (uint32_t j = k - PW; j > k0; j--) {
-                    const uint32_t c = L.sorted[j - 1];
-                    if ((ld4(L.data, c) & GM) == t) { q = c; break; }
+            } else {   // (the list is full) walk down to the bucket's first entry here
+                for (uint32_t j = k - PW; j > 0; j--) {
+                    const uint32_t c = L.sorted[j - 1], wc = ld4(L.data, c) & GM;
+                    if (wc == t) { q = c; break; }
+                    if (bucket_of<NG>(wc) != hb) break;
                 }
             }
         }
@@ -1165,16 +1165,21 @@ __device__ __forceinline__ uint32_t gram_pass(MatchLDS& L, uint32_t nv, uint32_t
     for (uint32_t u = wave; u < nul; u += MW) {
         const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)UL[u]);
         const uint32_t k = e & 0xFFFFu, i = L.sorted[k], t = ld4(L.data, i) & GM;
-        const uint32_t k0 = L.bstart[bucket_of<NG>(t)];
+        const uint32_t hb = bucket_of<NG>(t);
         uint32_t q = 0xFFFFu;
-        for (int jb = (int)(e >> 16); jb > (int)k0; jb -= 64) {
+        // down the bucket, 64 entries a step, to its first entry (where the bucket changes;
+        // the sort computes no bucket starts for this pass)
+        for (int jb = (int)(e >> 16); jb > 0; jb -= 64) {
             const int j = jb - 1 - (int)lane;
-            const uint32_t c = j >= (int)k0 ? (uint32_t)L.sorted[j] : 0u;
-            const uint64_t m = __ballot(j >= (int)k0 && (ld4(L.data, c) & GM) == t);
-            if (m) {   // the lowest lane holds the nearest
-                q = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)__builtin_ctzll(m));
+            const uint32_t c = j >= 0 ? (uint32_t)L.sorted[j] : 0u, wc = ld4(L.data, c) & GM;
+            const bool inb = j >= 0 && bucket_of<NG>(wc) == hb;
+            const uint64_t m = __ballot(inb && wc == t), x = __ballot(!inb);
+            const uint64_t below = x ? ((1ull << __builtin_ctzll(x)) - 1ull) : ~0ull;   // lanes before the bucket's end
+            if (m & below) {   // the lowest lane holds the nearest
+                q = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)__builtin_ctzll(m & below));
                 break;
             }
+            if (x) break;
         }
         if (lane == 0 && (NG == 3 || (q != 0xFFFFu && i + NG <= nv + 2))) seeds[i] = q != 0xFFFFu ? ((uint32_t)NG << 15) | q : 0u;
     }
@@ -1909,8 +1914,11 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         uint32_t nrun0 = 0;
 #pragma unroll
         for (int w = 0; w < MW; w++) nrun0 += L.wexit[w];
-        if (nrun0 * 4 >= ((bn + 15) >> 4)) sort_positions<false, true>(L, bn, max_chain, tid, dbg != nullptr, tp0);
-        else sort_positions<false, false>(L, bn, max_chain, tid, dbg != nullptr, tp0);
+        // the exhaustive parse's first sort (trigram chains for the gram pass) needs no bucket
+        // starts: the 4-byte sort makes the search's (max_chain 1 here only skips them)
+        const int32_t mc0 = (NBX > 3 && !DICT) ? 1 : max_chain;
+        if (nrun0 * 4 >= ((bn + 15) >> 4)) sort_positions<false, true>(L, bn, mc0, tid, dbg != nullptr, tp0);
+        else sort_positions<false, false>(L, bn, mc0, tid, dbg != nullptr, tp0);
     }
 
     if (dbg_stop(mflags, 1, info, hist_g, b, bn, tid)) return;
@@ -1949,7 +1957,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
             npass++;
             if (!__syncthreads_or(gram_pass<3>(L, nv, tid, seeds, ndefer, tsw)) || pass) break;
             if (tid == 0) atomicAdd(nfallback, 1u);   // counted in dmx_result.nsortfallback
-            sort_positions<true>(L, bn, max_chain, tid, false, tp0);   // never observed on gfx950
+            sort_positions<true>(L, bn, 1, tid, false, tp0);   // never observed on gfx950 (no starts, as above)
         }
         if constexpr (NBX > 4) {   // 4-byte grams from a 4-byte sort
             for (uint32_t pass = 0;; pass++) {

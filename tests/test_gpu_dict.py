@@ -165,6 +165,36 @@ def test_dict_gpu_inflate_chained_edges(enc):
     assert st == 0 and out == text
 
 
+def test_dict_gpu_inflate_chained_corrupt(enc):
+    """Corrupted dict streams through the chained decode: every call ends with a status or
+    with a wrong output, never a fault or a hang (bit flips anywhere, a truncated stream, an
+    index whose first block claims history it does not have)."""
+    data = _inputs()["mixed"]
+    z, _ = enc.compress_bytes(data, max_chain=6, flags=D.DMX_ZLIB | D.DMX_F_DICT | D.DMX_F_LAZY)
+    ix, nblk = enc.block_index()
+    rng = np.random.default_rng(7)
+    bad = 0
+    for _ in range(40):
+        zz = bytearray(z)
+        for _ in range(int(rng.integers(1, 4))):
+            p = int(rng.integers(2, len(zz) - 4))
+            zz[p] ^= 1 << int(rng.integers(0, 8))
+        dz = torch.frombuffer(zz, dtype=torch.uint8).cuda()
+        out, st = D.inflate_gpu_chained(dz, len(data), ix, nblk)
+        bad += st != 0 or out.cpu().numpy().tobytes() != data
+    assert bad >= 30
+    dz = torch.frombuffer(bytearray(z[: len(z) // 2]), dtype=torch.uint8).cuda()
+    out, st = D.inflate_gpu_chained(dz, len(data), ix, nblk)
+    assert st != 0
+    # the second block alone, listed as if it were the first: its history references reach
+    # before the output start
+    ix2 = ix[24:48].clone()
+    ix2[8:16] = 0   # out_off = 0
+    dz = torch.frombuffer(bytearray(z), dtype=torch.uint8).cuda()
+    out, st = D.inflate_gpu_chained(dz, 32768, ix2, 1)
+    assert st == -D.E["E_HUFDIS"]
+
+
 def test_dict_max_distance_tokens(enc):
     """A block equal to its predecessor: position 0 matches at distance exactly 32768."""
     text = D.gen_text(40000, 13).tobytes()
