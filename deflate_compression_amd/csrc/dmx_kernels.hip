@@ -1779,7 +1779,46 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
         }
     }
     __syncthreads();
-    if (pass_s) {
+    if (pass_s && full) {
+        // full block: the quads from pass 1's registers.  Quad j (output word gw0 + ks + 4 j)
+        // holds input bytes [o0, o0 + 16), o0 = 16 j + R: chunk c = j (R >= 0) or j - 1 (R < 0)
+        // and the next chunk, which the next lane holds (DPP); lane 63's next chunk is in
+        // another wave, so its quads re-read the input (L2) as the general path does.
+        const uint64_t O = spec_stored_bit(b, sw, flags);
+        const uint32_t s0 = (uint32_t)(O & 31), P = (s0 + 3 + 7) & ~7u, B0 = (P + 32) >> 3;
+        const uint32_t nwords = (uint32_t)(((uint64_t)P + 32 + 8ull * bn + 31) >> 5);
+        const uint64_t gw0 = O >> 5;
+        const uint32_t ks = 4 - (uint32_t)(gw0 & 3);
+        const uint32_t nq = nwords > ks + 1 ? (nwords - 1 - ks) >> 2 : 0;
+        const int32_t R = (int32_t)(4 * ks) - (int32_t)B0;
+        const uint32_t r = (uint32_t)(R & 15), a4 = r >> 2, sh = r & 3, jadd = R < 0 ? 1u : 0u;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t c = tid + (uint32_t)i * SCT, j = c + jadd;
+            const int64_t o0 = 16 * (int64_t)j + R;
+            const uint32_t n0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[i].x, 0x130, 0xF, 0xF, false);
+            const uint32_t n1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[i].y, 0x130, 0xF, 0xF, false);
+            const uint32_t n2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[i].z, 0x130, 0xF, 0xF, false);
+            const uint32_t n3 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[i].w, 0x130, 0xF, 0xF, false);
+            if (j >= nq || o0 < 0 || (uint64_t)((o0 & ~3ll) + 20) > bn) continue;   // not one of the quads
+            uint32_t w[5];
+            if (lane != 63) {
+                const uint32_t e8[8] = {v[i].x, v[i].y, v[i].z, v[i].w, n0, n1, n2, n3};
+#pragma unroll
+                for (int q = 0; q < 5; q++) w[q] = a4 == 0 ? e8[q] : a4 == 1 ? e8[q + 1] : a4 == 2 ? e8[q + 2] : e8[q + 3];
+            } else {
+                const uint32_t* p32 = reinterpret_cast<const uint32_t*>(d + (o0 & ~3ll));
+#pragma unroll
+                for (int q = 0; q < 5; q++) w[q] = p32[q];
+            }
+            uint4 o;
+            o.x = sh ? __builtin_amdgcn_alignbyte(w[1], w[0], sh) : w[0];
+            o.y = sh ? __builtin_amdgcn_alignbyte(w[2], w[1], sh) : w[1];
+            o.z = sh ? __builtin_amdgcn_alignbyte(w[3], w[2], sh) : w[2];
+            o.w = sh ? __builtin_amdgcn_alignbyte(w[4], w[3], sh) : w[3];
+            *reinterpret_cast<uint4*>(&out32[gw0 + ks + 4 * j]) = o;
+        }
+    } else if (pass_s) {
         const uint64_t O = spec_stored_bit(b, sw, flags);
         const bool dal = (reinterpret_cast<uintptr_t>(d) & 3) == 0;
         stored_quads(O, bn, dal, tid, SCT, [&](uint32_t k, int64_t o0) {
