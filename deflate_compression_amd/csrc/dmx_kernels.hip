@@ -1494,8 +1494,8 @@ __global__ __launch_bounds__(MT) void dmx_hist_kernel_t(const uint8_t* __restric
 //           partial sums (v_sad_u8, v_dot4_u32_u8).
 //   pass 2 (noise-like blocks only; full blocks from the registers of pass 1): byte
 //           histogram of every s-th position (s = 8 for full blocks: 4096 samples) and
-//           18-bit presence bitmap of the 4-grams sampled by content (bits 11..13 of their
-//           hash clear: an eighth), LDS atomics (33 KB, several workgroups per CU).  The
+//           17-bit presence bitmap of the 4-grams sampled by content (bits 11..13 of their
+//           hash clear: an eighth), LDS atomics (17 KB: 8 workgroups per CU).  The
 //           atomics bound this pass: round 2 sampled every other position and half the
 //           4-grams (32 K atomics per block, 0.53 ms per GiB); now 8 K.
 // A block that passes gets its whole record here (stored, no tokens); the match kernel then
@@ -1587,7 +1587,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
                                                               dmx_blkinfo* __restrict__ info, uint32_t* __restrict__ tok_g,
                                                               uint32_t* __restrict__ hist_g, uint32_t uni_ok, uint32_t flags,
                                                               uint32_t* __restrict__ out32, uint64_t out_cap) {
-    __shared__ uint32_t bm[1u << 13];
+    __shared__ uint32_t bm[1u << 12];   // the 17-bit presence bitmap (16 KB: 8 workgroups per CU)
     __shared__ uint32_t hist[256];
     __shared__ uint64_t red[10][SCT / 64];
     __shared__ uint32_t pass_s;
@@ -1711,7 +1711,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
         red[9][wave] = t;
     }
     // ---- pass 2: byte histogram + 4-gram bitmap ----
-    for (uint32_t k = tid; k < (1u << 13) / 4; k += SCT) reinterpret_cast<uint4*>(bm)[k] = make_uint4(0, 0, 0, 0);
+    for (uint32_t k = tid; k < (1u << 12) / 4; k += SCT) reinterpret_cast<uint4*>(bm)[k] = make_uint4(0, 0, 0, 0);
     hist[tid] = 0;   // (8 padded sub-histograms by lane & 7 measured slower: 0.59 -> 0.77 ms per GiB)
     __syncthreads();
     uint32_t qn = 0;   // sampled 4-grams of this thread
@@ -1726,7 +1726,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
             const uint32_t x = g4 * 0x9E3779B1u;
             if (p + j + 4 <= bn && !(x & (7u << 11))) {   // sampled by content
                 qn++;
-                atomicOr(&bm[x >> 19], 1u << ((x >> 14) & 31));
+                atomicOr(&bm[x >> 20], 1u << ((x >> 15) & 31));
             }
         }
     };
@@ -1745,7 +1745,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
     }
     __syncthreads();
     uint64_t distinct = 0;
-    for (uint32_t k = tid; k < (1u << 13); k += SCT) distinct += __builtin_popcount(bm[k]);
+    for (uint32_t k = tid; k < (1u << 12); k += SCT) distinct += __builtin_popcount(bm[k]);
     const uint64_t hc = hist[tid];
     uint64_t s2 = hc * hc;
     distinct = wave_sum_u64(distinct);

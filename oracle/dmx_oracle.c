@@ -670,14 +670,14 @@ int dmx_oracle_store_check(const uint8_t* d, int bn) {
     const uint64_t m = ((uint64_t)bn + (1u << sh) - 1) >> sh, m2 = m * m;
     if (256 * s2 > m2 + (m2 >> 4) + 256 * m) return 0;
     /* 4-grams sampled by content: bits 11..13 of their hash clear (an eighth) */
-    uint32_t* bm = (uint32_t*)calloc(1u << 13, sizeof(uint32_t));
+    uint32_t* bm = (uint32_t*)calloc(1u << 12, sizeof(uint32_t));   /* 17-bit presence bitmap */
     uint64_t q = 0, distinct = 0;
     for (int p = 0; p + 4 <= bn; p++) {
         const uint32_t w = (uint32_t)d[p] | (uint32_t)d[p + 1] << 8 | (uint32_t)d[p + 2] << 16 | (uint32_t)d[p + 3] << 24;
         const uint32_t x = w * 0x9E3779B1u;
         if (x & (7u << 11)) continue;
         q++;
-        const uint32_t g = x >> 14;
+        const uint32_t g = x >> 15;
         if (!(bm[g >> 5] & (1u << (g & 31)))) { bm[g >> 5] |= 1u << (g & 31); distinct++; }
     }
     free(bm);

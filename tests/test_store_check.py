@@ -35,7 +35,7 @@ def np_store_check(block) -> bool:
     w = (b[:-3].astype(np.uint64) | b[1:-2].astype(np.uint64) << 8 | b[2:-1].astype(np.uint64) << 16
          | b[3:].astype(np.uint64) << 24)
     x = (w * 0x9E3779B1) & 0xFFFFFFFF
-    g = x[(x & (7 << 11)) == 0] >> 14
+    g = x[(x & (7 << 11)) == 0] >> 15
     q = g.size
     coll = q - np.unique(g).size
     return 16 * q >= n and 64 * coll <= 4 * q
