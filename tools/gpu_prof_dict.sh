@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 600 python3 -u -m pytest "$R/tests/test_store_check.py" "$R/tests/test_gpu_dict.py" -m gpu -x -q -p no:cacheprovider \
+timeout -k 10 600 python3 -u -m pytest "$R/tests/test_store_check.py" "$R/tests/test_gpu_dict.py" -m gpu -x -v -p no:cacheprovider \
     --timeout 240 --timeout-method thread > "$OUT/pytest.log" 2>&1 || { tail -20 "$OUT/pytest.log"; exit 1; }
 tail -1 "$OUT/pytest.log"
 Q="--cpu-budget 0 --exhaustive-steps 0 --tradeoff= --long-run 0 --real-text 0 --steps 5 --warmup 1"
