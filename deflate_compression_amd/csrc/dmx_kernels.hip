@@ -1858,17 +1858,17 @@ __device__ __forceinline__ bool dbg_stop(uint32_t mflags, uint32_t phase, dmx_bl
 #ifndef DMX_NBX
 #define DMX_NBX 4   // the exhaustive parse's chain length in bytes (4; 5 measured slower: a second gram pass and sort)
 #endif
-// One block b of the match kernel (the workgroup's whole LDS; every return is workgroup-uniform).
-template <bool DICT, int NBX>
-__device__ __forceinline__ void match_block(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
-                                            int32_t max_chain, uint32_t mflags, uint16_t* __restrict__ dist_g,
-                                            const uint16_t* __restrict__ chs, uint32_t* __restrict__ tok_g,
-                                            uint32_t* __restrict__ hist_g,
-                                            dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg,
-                                            uint32_t* __restrict__ nfallback, const uint32_t b) {
+template <bool DICT, int NBX = 3>
+__global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
+                                                       int32_t max_chain, uint32_t mflags, uint16_t* __restrict__ dist_g,
+                                                       const uint16_t* __restrict__ chs, uint32_t* __restrict__ tok_g,
+                                                       uint32_t* __restrict__ hist_g,
+                                                       dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg,
+                                                       uint32_t* __restrict__ nfallback) {
     __shared__ MatchLDS L;
     __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def, tp0[3], st_rounds, st_p3a, st_h4[3];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = wave_of(tid);
+    const uint32_t b = blockIdx.x;
     if ((mflags & 4u) && info[b].prestored) return;   // stored by the noise check (K0)
     const uint64_t off = (uint64_t)b * sw;
     const uint32_t bn = (uint32_t)((n - off) < sw ? (n - off) : sw);
@@ -2307,29 +2307,6 @@ __device__ __forceinline__ void match_block(const uint8_t* __restrict__ in, uint
         info[b].adl_s = L.adl_s;
         info[b].adl_w = (uint64_t)bn * L.adl_s - L.adl_t;
         info[b].prestored = 0;
-    }
-}
-
-// K1: one workgroup per CU (its LDS allows no second one) taking blocks from a work counter
-// (wq, zeroed by K3's scan for the next encode) until none is left: a block stored by K0 costs
-// one counter fetch instead of a workgroup launch (32 768 of them per GiB of noise took
-// 0.07 ms), and the CUs stay busy until the last blocks.
-template <bool DICT, int NBX = 3>
-__global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
-                                                       int32_t max_chain, uint32_t mflags, uint16_t* __restrict__ dist_g,
-                                                       const uint16_t* __restrict__ chs, uint32_t* __restrict__ tok_g,
-                                                       uint32_t* __restrict__ hist_g,
-                                                       dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg,
-                                                       uint32_t* __restrict__ nfallback, uint32_t nblk,
-                                                       uint32_t* __restrict__ wq) {
-    __shared__ uint32_t s_b;
-    for (;;) {
-        if (threadIdx.x == 0) s_b = atomicAdd(wq, 1u);
-        __syncthreads();   // (also: every thread is done with the previous block)
-        const uint32_t b = s_b;
-        __syncthreads();   // every thread has read s_b before thread 0 takes the next one
-        if (b >= nblk) break;
-        match_block<DICT, NBX>(in, n, sw, max_chain, mflags, dist_g, chs, tok_g, hist_g, info, dbg, nfallback, b);
     }
 }
 
@@ -3234,7 +3211,6 @@ __global__ __launch_bounds__(ST) void dmx_scan_kernel(ScanTile* __restrict__ til
         nfallback[1] += nfallback[0];       // and the context's running total
         res->nsortfallback_total = nfallback[1];
         nfallback[0] = 0;
-        nfallback[2] = 0;                   // the match kernel's work counter, for the next encode
         s_end = end;
         s_T = T;
         s_adler = adler;
@@ -3525,7 +3501,6 @@ struct dmx_ctx {
     dmx_blkinfo* info;
     ScanTile* tiles;  // cap_blocks / SCAN_TILE + 1: per-tile aggregates and prefixes (scan)
     dmx_result* res;
-    uint32_t ncu;         // compute units (the match kernel's grid)
     uint32_t* nfb;        // [0] sort fallbacks of the encode in flight (kernels add, K3's scan reads and zeroes), [1] total
     uint64_t* dbg;        // optional per-block phase stamps (DMX_STAMPS=1)
     uint64_t dbg_cap;
@@ -3699,11 +3674,6 @@ extern "C" int dmx_ctx_create(int device, uint64_t max_input, dmx_ctx** out) {
     dmx_ctx* c = (dmx_ctx*)calloc(1, sizeof(dmx_ctx));
     if (!c) return -(int)E_MALLOC;
     c->device = device;
-    {
-        int ncu = 0;
-        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0) ncu = 256;
-        c->ncu = (uint32_t)ncu;
-    }
     if (hip_fail(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate")) { c->stream = NULL; dmx_ctx_destroy(c); return -(int)E_DEVICE; }
     if (hip_fail(dmx_malloc(&c->res, sizeof(dmx_result)), "hipMalloc(res)")) { dmx_ctx_destroy(c); return -(int)E_DEVICE; }
     if (hip_fail(dmx_malloc(&c->nfb, 16), "hipMalloc(nfb)") || hip_fail(hipMemset(c->nfb, 0, 16), "hipMemset(nfb)")) {
@@ -3836,16 +3806,15 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         const char* dstop = getenv("DMX_DEBUG_STOP");   // diagnostic only (dbg_stop)
         const uint32_t mfl = ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u) |
                              ((o.flags & DMX_F_STORE_CHECK) ? 4u : 0u) | (dstop ? ((uint32_t)atoi(dstop) & 3u) << 8 : 0u);
-        const uint32_t k1g = nblk < c->ncu ? nblk : c->ncu;   // one workgroup per CU, blocks from a counter
         if (o.flags & DMX_F_DICT)
-            hipLaunchKernelGGL(dmx_match_kernel<true>, dim3(k1g), dim3(MT), 0, s, (const uint8_t*)d_in, n,
-                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb, nblk, c->nfb + 2);
+            hipLaunchKernelGGL(dmx_match_kernel<true>, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n,
+                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb);
         else if (o.max_chain == 0)
-            hipLaunchKernelGGL((dmx_match_kernel<false, DMX_NBX>), dim3(k1g), dim3(MT), 0, s, (const uint8_t*)d_in, n,
-                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb, nblk, c->nfb + 2);
+            hipLaunchKernelGGL((dmx_match_kernel<false, DMX_NBX>), dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n,
+                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb);
         else
-            hipLaunchKernelGGL(dmx_match_kernel<false>, dim3(k1g), dim3(MT), 0, s, (const uint8_t*)d_in, n,
-                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb, nblk, c->nfb + 2);
+            hipLaunchKernelGGL(dmx_match_kernel<false>, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n,
+                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb);
         if (ev) (void)hipEventRecord(ev[2], s);
         if (o.flags & DMX_F_SPLIT)
             {
