@@ -167,28 +167,39 @@ def test_stats_overflow_returns_range(tmp_path):
     rfd, wfd = os.pipe()
     seen = {"n": 0, "last": None, "bad": None}
 
+    hb = os.environ.get("DMX_TEST_HEARTBEAT")   # a long test tells a watchdog it is alive
+
     def reader():
-        rec, carry, prev = 24, b"", None
+        import fcntl
+        try:
+            fcntl.fcntl(rfd, 1031, 1 << 20)   # F_SETPIPE_SZ: 1 MiB pipe buffer
+        except OSError:
+            pass
+        rec, carry, prev, nbytes = 24, b"", None, 0
         with os.fdopen(rfd, "rb", buffering=0) as f:
             while True:
                 buf = f.read(1 << 24)
                 if not buf:
                     break
+                nbytes += len(buf)
+                if hb and nbytes % (1 << 30) < len(buf):
+                    with open(hb, "a") as h:
+                        h.write(f"stats overflow test: {nbytes >> 20} MiB of records\n")
                 buf = carry + buf
                 m = len(buf) // rec
                 carry = buf[m * rec:]
-                a = np.frombuffer(buf[:m * rec], dtype="<i4").reshape(-1, 6).astype(np.int64)
-                if prev is not None:
-                    a2 = np.vstack([prev, a])
-                else:
-                    a2 = a
+                a = np.frombuffer(buf[:m * rec], dtype="<i4").reshape(-1, 6)
+                a2 = a if prev is None else np.concatenate([prev, a[:, :3]])
                 if seen["bad"] is None and ((a < 0).any() or (np.diff(a2[:, 0]) <= 0).any() or
                                             (np.diff(a2[:, 2]) < 0).any() or (np.diff(a2[:, 1]) < 0).any()):
                     seen["bad"] = seen["n"]
                 seen["n"] += m
-                prev = a[-1:]
-                seen["last"] = a[-1].copy()
+                prev = a[-1:, :3].copy()
+                seen["last"] = a[-1].astype(np.int64)
 
+    if hb:
+        with open(hb, "a") as h:
+            h.write("stats overflow test: input written, encoding\n")
     th = threading.Thread(target=reader)
     th.start()
     os.environ["DMX_STATS"] = "exact"

@@ -11,6 +11,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+export DMX_TEST_HEARTBEAT=$OUT/heartbeat.txt   # long tests append progress here (the silence watchdog)
 KARG=()
 [ -n "$K" ] && KARG=(-k "$K")
 timeout -k 10 900 python3 -u -m pytest "$R/tests" -m gpu -x -v -p no:cacheprovider --timeout 240 \
