@@ -885,76 +885,92 @@ extern "C" int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_ibl
 //      copy of such a cell) becomes a reference cell 0x100 + b - 1 = the byte b positions
 //      before the block's start.  Copies inside the block copy cells, so a reference always
 //      names a byte of an EARLIER block.
-//   2. dmx_cells_prep_kernel: each reference becomes an absolute source position P[j]; the
-//      cell is marked unresolved (0xFFFF).
-//      dmx_cells_jump_kernel, about log2(nblk) + 2 launches: every unresolved j looks at its
-//      source s = P[j]: a resolved cell is copied, otherwise P[j] = P[s] (pointer jumping:
-//      chains of references through many blocks -- a run carried across every block, say --
-//      halve each launch).  In place: a stale read only delays resolution, never changes
-//      the value (P moves along the chain, a resolved cell stays).  A launch whose
-//      predecessor left nothing unresolved returns at once.
+//   2. dmx_cells_prep_kernel: each reference becomes an absolute source position s; a source
+//      that is already a byte is copied at once, otherwise P[j] = s, the cell is marked
+//      unresolved (0xFFFF) and j goes on a list (one atomic per wave: ballot + prefix count).
+//      dmx_cells_jump_kernel, about log2(nblk) + 2 launches, each over the list the one
+//      before it left: an unresolved j looks at s = P[j]: a resolved cell is copied,
+//      otherwise P[j] = P[s] and j goes on the next list (pointer jumping: chains of
+//      references through many blocks -- a run carried across every block, say -- halve each
+//      launch).  In place: a stale read only delays resolution, never changes the value (P
+//      moves along the chain, a resolved cell stays).  A launch whose list is empty returns
+//      at once, and none reads more than its list.
 //   3. dmx_cells_final_kernel: cells -> bytes; any cell still unresolved is an error.
 // ------------------------------------------------------------------------------------
 #define CHAIN_ROUNDS_MAX 40
-struct ChainWork {   // the head of the work buffer: unresolved counts per round
+struct ChainWork {   // the head of the work buffer: list lengths per round
     uint32_t left[CHAIN_ROUNDS_MAX + 1];
 };
 
+// Appends v for every lane with want set; the whole wave calls it.
+__device__ inline void chain_push(bool want, uint32_t v, uint32_t* __restrict__ list, uint32_t* cnt) {
+    const uint64_t m = __ballot(want);
+    if (!m) return;
+    const int lead = __ffsll((unsigned long long)m) - 1;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t base = 0;
+    if ((int)lane == lead) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+    base = __shfl(base, lead);
+    if (want) list[base + __popcll(m & ((1ull << lane) - 1))] = v;
+}
+
 __global__ __launch_bounds__(256) void dmx_cells_prep_kernel(const dmx_iblock* __restrict__ index, uint16_t* __restrict__ cells,
-                                                            uint32_t* __restrict__ P, ChainWork* __restrict__ W,
-                                                            dmx_inflate_status* __restrict__ st) {
+                                                            uint32_t* __restrict__ P, uint32_t* __restrict__ list,
+                                                            ChainWork* __restrict__ W, dmx_inflate_status* __restrict__ st) {
     const uint64_t off = index[blockIdx.x].out_off;
     const uint32_t len = index[blockIdx.x].out_len;
-    uint32_t nl = 0;
     bool bad = false;
-    for (uint32_t j = threadIdx.x; j < len; j += 256) {
-        const uint32_t c = cells[off + j];
-        if (c >= 0x100u) {
-            const uint64_t back = (uint64_t)(c - 0xFFu) + j;   // positions before j
-            if (back > off + j) { bad = true; continue; }
-            P[off + j] = (uint32_t)(off + j - back);
-            cells[off + j] = 0xFFFFu;
-            nl++;
+    for (uint32_t j0 = 0; j0 < len; j0 += 256) {   // uniform trip count: chain_push needs the whole wave
+        const uint32_t j = j0 + threadIdx.x;
+        bool want = false;
+        if (j < len) {
+            const uint32_t c = cells[off + j];
+            if (c >= 0x100u) {
+                const uint64_t back = (uint64_t)(c - 0xFFu) + j;   // positions before j
+                if (back > off + j) {
+                    bad = true;
+                } else {
+                    const uint32_t sp = (uint32_t)(off + j - back);
+                    // a byte cell never changes; a reference (raw or already marked) waits
+                    const uint16_t cs = __hip_atomic_load(cells + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (cs < 0x100u) {
+                        cells[off + j] = cs;
+                    } else {
+                        P[off + j] = sp;
+                        __hip_atomic_store(cells + off + j, (uint16_t)0xFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        want = true;
+                    }
+                }
+            }
         }
+        chain_push(want, (uint32_t)(off + j), list, &W->left[0]);
     }
-    nl = __reduce_add_sync(~0ull, nl);
-    if ((threadIdx.x & 63) == 0 && nl) atomicAdd(&W->left[0], nl);
     if (bad) atomicCAS(&st->status, 0, -(int32_t)E_HUFDIS);
 }
 
 __global__ __launch_bounds__(256) void dmx_cells_jump_kernel(uint16_t* __restrict__ cells, uint32_t* __restrict__ P,
-                                                            uint64_t n, ChainWork* __restrict__ W, uint32_t round) {
-    if (__hip_atomic_load(&W->left[round], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
-    uint32_t nl = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * 256 * 8;
-    for (uint64_t j0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 8; j0 < n; j0 += stride) {
-        uint16_t c[8];
-        const bool full = j0 + 8 <= n;
-        if (full) {
-            const uint4 v = *reinterpret_cast<const uint4*>(cells + j0);
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int k = 0; k < 8; k++) c[k] = (uint16_t)(w[k >> 1] >> (16 * (k & 1)));
-        } else {
-            for (int k = 0; k < 8; k++) c[k] = j0 + k < n ? cells[j0 + k] : 0;
-        }
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            if (c[k] != 0xFFFFu) continue;
-            const uint64_t j = j0 + k;
+                                                            const uint32_t* __restrict__ lin, uint32_t* __restrict__ lout,
+                                                            ChainWork* __restrict__ W, uint32_t round) {
+    const uint32_t cnt = W->left[round];
+    for (uint32_t u0 = blockIdx.x * 256; u0 < cnt; u0 += gridDim.x * 256) {
+        const uint32_t u = u0 + threadIdx.x;
+        bool want = false;
+        uint32_t j = 0;
+        if (u < cnt) {
+            j = lin[u];
             const uint32_t sp = P[j];
-            if ((uint64_t)sp >= j) continue;   // never from a well-formed prep (sources precede): stays unresolved
-            const uint16_t cs = __hip_atomic_load(cells + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (cs != 0xFFFFu) {
-                cells[j] = cs;
-            } else {
-                P[j] = __hip_atomic_load(P + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                nl++;
+            if (sp < j) {   // never otherwise from a well-formed prep (sources precede): stays unresolved
+                const uint16_t cs = __hip_atomic_load(cells + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (cs != 0xFFFFu) {
+                    cells[j] = cs;
+                } else {
+                    P[j] = __hip_atomic_load(P + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    want = true;
+                }
             }
         }
+        chain_push(want, j, lout, &W->left[round + 1]);
     }
-    nl = __reduce_add_sync(~0ull, nl);
-    if ((threadIdx.x & 63) == 0 && nl) atomicAdd(&W->left[round + 1], nl);
 }
 
 __global__ __launch_bounds__(256) void dmx_cells_final_kernel(const uint16_t* __restrict__ cells, uint8_t* __restrict__ out,
@@ -983,8 +999,11 @@ __global__ __launch_bounds__(256) void dmx_cells_final_kernel(const uint16_t* __
     if (bad) atomicCAS(&st->status, 0, -(int32_t)E_HUFDIS);
 }
 
+// work layout: [ChainWork 256 B][cells 2*cap, 256-aligned][P 4*cap][list A 4*cap][list B 4*cap]
+static inline uint64_t chain_cells_bytes(uint64_t cap) { return (2 * cap + 255) & ~255ull; }
+
 extern "C" uint64_t dmx_inflate_chained_work(uint64_t out_cap) {
-    return 256 + ((2 * out_cap + 255) & ~255ull) + 4 * out_cap;
+    return 256 + chain_cells_bytes(out_cap) + 12 * out_cap;
 }
 
 extern "C" int dmx_inflate_chained_async(const void* d_z, uint64_t zbytes, const dmx_iblock* d_index, uint32_t nblk,
@@ -996,18 +1015,19 @@ extern "C" int dmx_inflate_chained_async(const void* d_z, uint64_t zbytes, const
     hipStream_t s = (hipStream_t)stream;
     ChainWork* W = (ChainWork*)d_work;
     uint16_t* cells = (uint16_t*)((uint8_t*)d_work + 256);
-    uint32_t* P = (uint32_t*)((uint8_t*)cells + ((2 * out_cap + 255) & ~255ull));
+    uint32_t* P = (uint32_t*)((uint8_t*)cells + chain_cells_bytes(out_cap));
+    uint32_t* L[2] = {P + out_cap, P + 2 * out_cap};
     if (hipMemsetAsync(d_status, 0, sizeof(dmx_inflate_status), s) != hipSuccess) return -(int)E_DEVICE;
     if (hipMemsetAsync(W, 0, sizeof(ChainWork), s) != hipSuccess) return -(int)E_DEVICE;
     hipLaunchKernelGGL(dmx_inflate_index_kernel<true>, dim3(nblk), dim3(64), 0, s, (const uint8_t*)d_z, zbytes, d_index,
                        (uint8_t*)cells, out_cap, d_status);
-    hipLaunchKernelGGL(dmx_cells_prep_kernel, dim3(nblk), dim3(256), 0, s, d_index, cells, P, W, d_status);
+    hipLaunchKernelGGL(dmx_cells_prep_kernel, dim3(nblk), dim3(256), 0, s, d_index, cells, P, L[0], W, d_status);
     uint32_t rounds = 2;   // pointer jumping: a chain through k blocks takes ~log2(k) + 1 rounds
     while ((1ull << (rounds - 2)) < (uint64_t)nblk && rounds < CHAIN_ROUNDS_MAX) rounds++;
-    const uint64_t g0 = (out_cap + 2047) / 2048;
-    const uint32_t g = (uint32_t)(g0 < 4096 ? g0 : 4096);
+    const uint64_t g0 = (out_cap + 8191) / 8192;
+    const uint32_t g = (uint32_t)(g0 < 2048 ? g0 : 2048);
     for (uint32_t rd = 0; rd < rounds; rd++)
-        hipLaunchKernelGGL(dmx_cells_jump_kernel, dim3(g ? g : 1), dim3(256), 0, s, cells, P, out_cap, W, rd);
+        hipLaunchKernelGGL(dmx_cells_jump_kernel, dim3(g ? g : 1), dim3(256), 0, s, cells, P, L[rd & 1], L[(rd + 1) & 1], W, rd);
     const uint64_t gf0 = (out_cap + 4095) / 4096;
     const uint32_t gf = (uint32_t)(gf0 < 4096 ? gf0 : 4096);
     hipLaunchKernelGGL(dmx_cells_final_kernel, dim3(gf ? gf : 1), dim3(256), 0, s, cells, (uint8_t*)d_out, out_cap, d_status);
