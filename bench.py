@@ -577,7 +577,7 @@ def main() -> int:
     chained = bool(args.dict)
     work = None
     if chained:
-        wb = int(Lib.dmx_inflate_chained_work(n))
+        wb = int(Lib.dmx_inflate_chained_work(n, nblk))
         work = torch.empty(wb + 256, dtype=torch.uint8, device=dev)
         wptr = (work.data_ptr() + 255) & ~255
 

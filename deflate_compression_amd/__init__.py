@@ -126,7 +126,7 @@ def lib() -> ctypes.CDLL:
         "dmx_gen_text": ([vp, u64, u64], None),
         "dmx_gen_random": ([vp, u64, u64], None),
         "dmx_inflate_chained_async": ([vp, u64, vp, u32, vp, u64, vp, u64, vp, vp], ctypes.c_int),
-        "dmx_inflate_chained_work": ([u64], u64),
+        "dmx_inflate_chained_work": ([u64, u32], u64),
         "dmx_refest_create": ([], vp),
         "dmx_refest_destroy": ([vp], None),
         "dmx_refest_feed": ([vp, u32p, u32, vp, u32p], ctypes.c_int),
@@ -232,14 +232,14 @@ def inflate_gpu_chained(z, out_cap: int, index, nblk: int, stream=None, work=Non
     (DMX_F_DICT streams), all blocks in parallel: each decodes into 16-bit cells with
     references for the bytes before it, then pointer jumping resolves the references
     (dmx_inflate_chained_async).  index: Encoder.block_index().  work: optional uint8 CUDA
-    scratch of dmx_inflate_chained_work(out_cap) bytes.  Returns (uint8 tensor, status)."""
+    scratch of dmx_inflate_chained_work(out_cap, nblk) bytes.  Returns (uint8 tensor, status)."""
     import numpy as np
     import torch
     L = lib()
     dev = z.device
     out = torch.empty(max(out_cap, 1), dtype=torch.uint8, device=dev)
     st = torch.zeros(16, dtype=torch.uint8, device=dev)
-    wb = int(L.dmx_inflate_chained_work(out_cap))
+    wb = int(L.dmx_inflate_chained_work(out_cap, nblk))
     if work is None or work.numel() < wb:
         work = torch.empty(wb + 256, dtype=torch.uint8, device=dev)
     wp = (work.data_ptr() + 255) & ~255

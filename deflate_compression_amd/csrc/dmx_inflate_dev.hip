@@ -887,38 +887,48 @@ extern "C" int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_ibl
 //      names a byte of an EARLIER block.
 //   2. dmx_cells_prep_kernel: each reference becomes an absolute source position s; a source
 //      that is already a byte is copied at once, otherwise P[j] = s, the cell is marked
-//      unresolved (0xFFFF) and j goes on a list (one atomic per wave: ballot + prefix count).
-//      dmx_cells_jump_kernel, about log2(nblk) + 2 launches, each over the list the one
-//      before it left: an unresolved j looks at s = P[j]: a resolved cell is copied,
-//      otherwise P[j] = P[s] and j goes on the next list (pointer jumping: chains of
-//      references through many blocks -- a run carried across every block, say -- halve each
-//      launch).  In place: a stale read only delays resolution, never changes the value (P
-//      moves along the chain, a resolved cell stays).  A launch whose list is empty returns
-//      at once, and none reads more than its list.
+//      unresolved (0xFFFF) and j goes on its block's list.  The lists are per block -- block
+//      b's entries sit in [out_off, out_off + count) of a list buffer, so a workgroup appends
+//      with one LDS atomic per wave and no global atomic at all.
+//      dmx_cells_jump_kernel, about log2(nblk) + 2 launches of one workgroup per block, each
+//      over the list the one before it left: an unresolved j looks at s = P[j]: a resolved
+//      cell is copied, otherwise P[j] = P[s] and j goes on the next list (pointer jumping:
+//      chains of references through many blocks -- a run carried across every block, say --
+//      halve each launch).  In place: a stale read only delays resolution, never changes the
+//      value (P moves along the chain, a resolved cell stays).  A block whose list is empty
+//      returns at once.
 //   3. dmx_cells_final_kernel: cells -> bytes; any cell still unresolved is an error.
 // ------------------------------------------------------------------------------------
 #define CHAIN_ROUNDS_MAX 40
-struct ChainWork {   // the head of the work buffer: list lengths per round
-    uint32_t left[CHAIN_ROUNDS_MAX + 1];
-};
 
-// Appends v for every lane with want set; the whole wave calls it.
-__device__ inline void chain_push(bool want, uint32_t v, uint32_t* __restrict__ list, uint32_t* cnt) {
+// Appends v at list[*lds_cnt ...] for every lane with want set; the whole wave calls it.
+__device__ inline void chain_push(bool want, uint32_t v, uint32_t* __restrict__ list, uint32_t* lds_cnt) {
     const uint64_t m = __ballot(want);
     if (!m) return;
     const int lead = __ffsll((unsigned long long)m) - 1;
     const uint32_t lane = threadIdx.x & 63;
     uint32_t base = 0;
-    if ((int)lane == lead) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+    if ((int)lane == lead) base = atomicAdd(lds_cnt, (uint32_t)__popcll(m));
     base = __shfl(base, lead);
     if (want) list[base + __popcll(m & ((1ull << lane) - 1))] = v;
 }
 
 __global__ __launch_bounds__(256) void dmx_cells_prep_kernel(const dmx_iblock* __restrict__ index, uint16_t* __restrict__ cells,
                                                             uint32_t* __restrict__ P, uint32_t* __restrict__ list,
-                                                            ChainWork* __restrict__ W, dmx_inflate_status* __restrict__ st) {
+                                                            uint32_t* __restrict__ count, uint64_t cap,
+                                                            dmx_inflate_status* __restrict__ st) {
+    __shared__ uint32_t nl;
     const uint64_t off = index[blockIdx.x].out_off;
     const uint32_t len = index[blockIdx.x].out_len;
+    if (off > cap || len > cap - off) {   // the decode already failed this index; read nothing
+        if (threadIdx.x == 0) {
+            count[blockIdx.x] = 0;
+            atomicCAS(&st->status, 0, -(int32_t)E_RANGE);
+        }
+        return;
+    }
+    if (threadIdx.x == 0) nl = 0;
+    __syncthreads();
     bool bad = false;
     for (uint32_t j0 = 0; j0 < len; j0 += 256) {   // uniform trip count: chain_push needs the whole wave
         const uint32_t j = j0 + threadIdx.x;
@@ -943,21 +953,32 @@ __global__ __launch_bounds__(256) void dmx_cells_prep_kernel(const dmx_iblock* _
                 }
             }
         }
-        chain_push(want, (uint32_t)(off + j), list, &W->left[0]);
+        chain_push(want, (uint32_t)(off + j), list + off, &nl);
     }
+    __syncthreads();
+    if (threadIdx.x == 0) count[blockIdx.x] = nl;
     if (bad) atomicCAS(&st->status, 0, -(int32_t)E_HUFDIS);
 }
 
-__global__ __launch_bounds__(256) void dmx_cells_jump_kernel(uint16_t* __restrict__ cells, uint32_t* __restrict__ P,
-                                                            const uint32_t* __restrict__ lin, uint32_t* __restrict__ lout,
-                                                            ChainWork* __restrict__ W, uint32_t round) {
-    const uint32_t cnt = W->left[round];
-    for (uint32_t u0 = blockIdx.x * 256; u0 < cnt; u0 += gridDim.x * 256) {
+__global__ __launch_bounds__(256) void dmx_cells_jump_kernel(const dmx_iblock* __restrict__ index, uint16_t* __restrict__ cells,
+                                                            uint32_t* __restrict__ P, const uint32_t* __restrict__ lin,
+                                                            uint32_t* __restrict__ lout, const uint32_t* __restrict__ cin,
+                                                            uint32_t* __restrict__ cout) {
+    __shared__ uint32_t nl;
+    const uint32_t cnt = cin[blockIdx.x];
+    if (cnt == 0) {
+        if (threadIdx.x == 0) cout[blockIdx.x] = 0;
+        return;
+    }
+    const uint64_t off = index[blockIdx.x].out_off;
+    if (threadIdx.x == 0) nl = 0;
+    __syncthreads();
+    for (uint32_t u0 = 0; u0 < cnt; u0 += 256) {
         const uint32_t u = u0 + threadIdx.x;
         bool want = false;
         uint32_t j = 0;
         if (u < cnt) {
-            j = lin[u];
+            j = lin[off + u];
             const uint32_t sp = P[j];
             if (sp < j) {   // never otherwise from a well-formed prep (sources precede): stays unresolved
                 const uint16_t cs = __hip_atomic_load(cells + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -969,8 +990,10 @@ __global__ __launch_bounds__(256) void dmx_cells_jump_kernel(uint16_t* __restric
                 }
             }
         }
-        chain_push(want, j, lout, &W->left[round + 1]);
+        chain_push(want, j, lout + off, &nl);
     }
+    __syncthreads();
+    if (threadIdx.x == 0) cout[blockIdx.x] = nl;
 }
 
 __global__ __launch_bounds__(256) void dmx_cells_final_kernel(const uint16_t* __restrict__ cells, uint8_t* __restrict__ out,
@@ -999,11 +1022,11 @@ __global__ __launch_bounds__(256) void dmx_cells_final_kernel(const uint16_t* __
     if (bad) atomicCAS(&st->status, 0, -(int32_t)E_HUFDIS);
 }
 
-// work layout: [ChainWork 256 B][cells 2*cap, 256-aligned][P 4*cap][list A 4*cap][list B 4*cap]
-static inline uint64_t chain_cells_bytes(uint64_t cap) { return (2 * cap + 255) & ~255ull; }
+// work layout: [list lengths 2 x nblk, 256-aligned][cells 2*cap, 256-aligned][P 4*cap][list A 4*cap][list B 4*cap]
+static inline uint64_t chain_a256(uint64_t x) { return (x + 255) & ~255ull; }
 
-extern "C" uint64_t dmx_inflate_chained_work(uint64_t out_cap) {
-    return 256 + chain_cells_bytes(out_cap) + 12 * out_cap;
+extern "C" uint64_t dmx_inflate_chained_work(uint64_t out_cap, uint32_t nblk) {
+    return chain_a256(8ull * nblk) + chain_a256(2 * out_cap) + 12 * out_cap;
 }
 
 extern "C" int dmx_inflate_chained_async(const void* d_z, uint64_t zbytes, const dmx_iblock* d_index, uint32_t nblk,
@@ -1011,23 +1034,21 @@ extern "C" int dmx_inflate_chained_async(const void* d_z, uint64_t zbytes, const
                                          dmx_inflate_status* d_status, void* stream) {
     if (!d_z || !d_out || !d_status || !d_index || !nblk || !d_work) return -(int)E_INVAL;
     if (zbytes > 0xFFFFFFF0ull || out_cap > 0xFFFFFFF0ull) return -(int)E_RANGE;   // 32-bit positions
-    if (work_bytes < dmx_inflate_chained_work(out_cap) || ((uintptr_t)d_work & 255)) return -(int)E_SZ;
+    if (work_bytes < dmx_inflate_chained_work(out_cap, nblk) || ((uintptr_t)d_work & 255)) return -(int)E_SZ;
     hipStream_t s = (hipStream_t)stream;
-    ChainWork* W = (ChainWork*)d_work;
-    uint16_t* cells = (uint16_t*)((uint8_t*)d_work + 256);
-    uint32_t* P = (uint32_t*)((uint8_t*)cells + chain_cells_bytes(out_cap));
+    uint32_t* C[2] = {(uint32_t*)d_work, (uint32_t*)d_work + nblk};
+    uint16_t* cells = (uint16_t*)((uint8_t*)d_work + chain_a256(8ull * nblk));
+    uint32_t* P = (uint32_t*)((uint8_t*)cells + chain_a256(2 * out_cap));
     uint32_t* L[2] = {P + out_cap, P + 2 * out_cap};
     if (hipMemsetAsync(d_status, 0, sizeof(dmx_inflate_status), s) != hipSuccess) return -(int)E_DEVICE;
-    if (hipMemsetAsync(W, 0, sizeof(ChainWork), s) != hipSuccess) return -(int)E_DEVICE;
     hipLaunchKernelGGL(dmx_inflate_index_kernel<true>, dim3(nblk), dim3(64), 0, s, (const uint8_t*)d_z, zbytes, d_index,
                        (uint8_t*)cells, out_cap, d_status);
-    hipLaunchKernelGGL(dmx_cells_prep_kernel, dim3(nblk), dim3(256), 0, s, d_index, cells, P, L[0], W, d_status);
+    hipLaunchKernelGGL(dmx_cells_prep_kernel, dim3(nblk), dim3(256), 0, s, d_index, cells, P, L[0], C[0], out_cap, d_status);
     uint32_t rounds = 2;   // pointer jumping: a chain through k blocks takes ~log2(k) + 1 rounds
     while ((1ull << (rounds - 2)) < (uint64_t)nblk && rounds < CHAIN_ROUNDS_MAX) rounds++;
-    const uint64_t g0 = (out_cap + 8191) / 8192;
-    const uint32_t g = (uint32_t)(g0 < 2048 ? g0 : 2048);
     for (uint32_t rd = 0; rd < rounds; rd++)
-        hipLaunchKernelGGL(dmx_cells_jump_kernel, dim3(g ? g : 1), dim3(256), 0, s, cells, P, L[rd & 1], L[(rd + 1) & 1], W, rd);
+        hipLaunchKernelGGL(dmx_cells_jump_kernel, dim3(nblk), dim3(256), 0, s, d_index, cells, P, L[rd & 1],
+                           L[(rd + 1) & 1], C[rd & 1], C[(rd + 1) & 1]);
     const uint64_t gf0 = (out_cap + 4095) / 4096;
     const uint32_t gf = (uint32_t)(gf0 < 4096 ? gf0 : 4096);
     hipLaunchKernelGGL(dmx_cells_final_kernel, dim3(gf ? gf : 1), dim3(256), 0, s, cells, (uint8_t*)d_out, out_cap, d_status);
