@@ -900,6 +900,7 @@ extern "C" int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_ibl
 //   3. dmx_cells_final_kernel: cells -> bytes; any cell still unresolved is an error.
 // ------------------------------------------------------------------------------------
 #define CHAIN_ROUNDS_MAX 40
+#define CHAIN_WG 1024   // threads per block in prep and jump: a block's list is latency-bound
 
 // Appends v at list[*lds_cnt ...] for every lane with want set; the whole wave calls it.
 __device__ inline void chain_push(bool want, uint32_t v, uint32_t* __restrict__ list, uint32_t* lds_cnt) {
@@ -913,7 +914,7 @@ __device__ inline void chain_push(bool want, uint32_t v, uint32_t* __restrict__ 
     if (want) list[base + __popcll(m & ((1ull << lane) - 1))] = v;
 }
 
-__global__ __launch_bounds__(256) void dmx_cells_prep_kernel(const dmx_iblock* __restrict__ index, uint16_t* __restrict__ cells,
+__global__ __launch_bounds__(CHAIN_WG) void dmx_cells_prep_kernel(const dmx_iblock* __restrict__ index, uint16_t* __restrict__ cells,
                                                             uint32_t* __restrict__ P, uint32_t* __restrict__ list,
                                                             uint32_t* __restrict__ count, uint64_t cap,
                                                             dmx_inflate_status* __restrict__ st) {
@@ -930,7 +931,7 @@ __global__ __launch_bounds__(256) void dmx_cells_prep_kernel(const dmx_iblock* _
     if (threadIdx.x == 0) nl = 0;
     __syncthreads();
     bool bad = false;
-    for (uint32_t j0 = 0; j0 < len; j0 += 256) {   // uniform trip count: chain_push needs the whole wave
+    for (uint32_t j0 = 0; j0 < len; j0 += CHAIN_WG) {   // uniform trip count: chain_push needs the whole wave
         const uint32_t j = j0 + threadIdx.x;
         bool want = false;
         if (j < len) {
@@ -960,10 +961,10 @@ __global__ __launch_bounds__(256) void dmx_cells_prep_kernel(const dmx_iblock* _
     if (bad) atomicCAS(&st->status, 0, -(int32_t)E_HUFDIS);
 }
 
-__global__ __launch_bounds__(256) void dmx_cells_jump_kernel(const dmx_iblock* __restrict__ index, uint16_t* __restrict__ cells,
-                                                            uint32_t* __restrict__ P, const uint32_t* __restrict__ lin,
-                                                            uint32_t* __restrict__ lout, const uint32_t* __restrict__ cin,
-                                                            uint32_t* __restrict__ cout) {
+__global__ __launch_bounds__(CHAIN_WG) void dmx_cells_jump_kernel(const dmx_iblock* __restrict__ index, uint16_t* __restrict__ cells,
+                                                                 uint32_t* __restrict__ P, const uint32_t* __restrict__ lin,
+                                                                 uint32_t* __restrict__ lout, const uint32_t* __restrict__ cin,
+                                                                 uint32_t* __restrict__ cout) {
     __shared__ uint32_t nl;
     const uint32_t cnt = cin[blockIdx.x];
     if (cnt == 0) {
@@ -973,24 +974,39 @@ __global__ __launch_bounds__(256) void dmx_cells_jump_kernel(const dmx_iblock* _
     const uint64_t off = index[blockIdx.x].out_off;
     if (threadIdx.x == 0) nl = 0;
     __syncthreads();
-    for (uint32_t u0 = 0; u0 < cnt; u0 += 256) {
-        const uint32_t u = u0 + threadIdx.x;
-        bool want = false;
-        uint32_t j = 0;
-        if (u < cnt) {
-            j = lin[off + u];
-            const uint32_t sp = P[j];
-            if (sp < j) {   // never otherwise from a well-formed prep (sources precede): stays unresolved
-                const uint16_t cs = __hip_atomic_load(cells + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (cs != 0xFFFFu) {
-                    cells[j] = cs;
+    // two entries per thread, their dependent loads (list, P, cell, P) interleaved
+    for (uint32_t u0 = 0; u0 < cnt; u0 += 2 * CHAIN_WG) {
+        uint32_t j[2], sp[2];
+        uint16_t cs[2];
+        bool act[2], want[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const uint32_t u = u0 + k * CHAIN_WG + threadIdx.x;
+            act[k] = u < cnt;
+            j[k] = act[k] ? lin[off + u] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            sp[k] = act[k] ? P[j[k]] : 0;
+            act[k] = act[k] && sp[k] < j[k];   // never otherwise from a well-formed prep: stays unresolved
+        }
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+            cs[k] = act[k] ? __hip_atomic_load(cells + sp[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            want[k] = false;
+            if (act[k]) {
+                if (cs[k] != 0xFFFFu) {
+                    cells[j[k]] = cs[k];
                 } else {
-                    P[j] = __hip_atomic_load(P + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    want = true;
+                    P[j[k]] = __hip_atomic_load(P + sp[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    want[k] = true;
                 }
             }
         }
-        chain_push(want, j, lout + off, &nl);
+        chain_push(want[0], j[0], lout + off, &nl);
+        chain_push(want[1], j[1], lout + off, &nl);
     }
     __syncthreads();
     if (threadIdx.x == 0) cout[blockIdx.x] = nl;
@@ -1043,11 +1059,11 @@ extern "C" int dmx_inflate_chained_async(const void* d_z, uint64_t zbytes, const
     if (hipMemsetAsync(d_status, 0, sizeof(dmx_inflate_status), s) != hipSuccess) return -(int)E_DEVICE;
     hipLaunchKernelGGL(dmx_inflate_index_kernel<true>, dim3(nblk), dim3(64), 0, s, (const uint8_t*)d_z, zbytes, d_index,
                        (uint8_t*)cells, out_cap, d_status);
-    hipLaunchKernelGGL(dmx_cells_prep_kernel, dim3(nblk), dim3(256), 0, s, d_index, cells, P, L[0], C[0], out_cap, d_status);
+    hipLaunchKernelGGL(dmx_cells_prep_kernel, dim3(nblk), dim3(CHAIN_WG), 0, s, d_index, cells, P, L[0], C[0], out_cap, d_status);
     uint32_t rounds = 2;   // pointer jumping: a chain through k blocks takes ~log2(k) + 1 rounds
     while ((1ull << (rounds - 2)) < (uint64_t)nblk && rounds < CHAIN_ROUNDS_MAX) rounds++;
     for (uint32_t rd = 0; rd < rounds; rd++)
-        hipLaunchKernelGGL(dmx_cells_jump_kernel, dim3(nblk), dim3(256), 0, s, d_index, cells, P, L[rd & 1],
+        hipLaunchKernelGGL(dmx_cells_jump_kernel, dim3(nblk), dim3(CHAIN_WG), 0, s, d_index, cells, P, L[rd & 1],
                            L[(rd + 1) & 1], C[rd & 1], C[(rd + 1) & 1]);
     const uint64_t gf0 = (out_cap + 4095) / 4096;
     const uint32_t gf = (uint32_t)(gf0 < 4096 ? gf0 : 4096);
