@@ -3331,7 +3331,12 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
         const bool spec = bi.prestored == 3 && O == spec_stored_bit(b, sw, flags);
         const uint32_t ks = 4 - (uint32_t)(gw0 & 3);                      // first quad: (gw0 + ks) % 4 == 0, ks >= 1
         const uint32_t nq = (dal && nwords > ks + 1) ? (nwords - 1 - ks) >> 2 : 0;   // quads short of the last word
-        for (uint32_t j = tid; j < nq; j += PT) {
+        // With the copy in place only the first two and the last two quads can need words of
+        // their own: quad j >= 2 starts at byte >= 36 > B0 (<= 9), and quad j <= nq - 3 ends
+        // >= 44 bytes before the block's end, so both take the fast path, which K0 wrote.
+        const uint32_t nqv = spec ? (nq < 4 ? nq : 4u) : nq;
+        for (uint32_t t = tid; t < nqv; t += PT) {
+            const uint32_t j = (spec && t >= 2) ? nq - (nqv - t) : t;
             const uint32_t k = ks + 4 * j;
             const int64_t o0 = (int64_t)(4 * k) - (int64_t)B0;
             if (o0 >= 0 && (uint64_t)((o0 & ~3ll) + 20) <= bn) {

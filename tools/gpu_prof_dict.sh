@@ -24,3 +24,6 @@ for r in csv.DictReader(open('$OUT/kernel_stats_$c.csv')):
     print('  ', r['Name'][:60], r['Calls'], r['AverageNs'], r['TotalDurationNs'])
 "
 done
+if [ -x "$R/tools/copy_bw" ]; then
+    timeout -k 10 120 "$R/tools/copy_bw" > "$OUT/copy_bw.txt" 2>&1 && cat "$OUT/copy_bw.txt"
+fi
