@@ -22,6 +22,39 @@ VARIANTS = {
                    "                    else if (jj) dist = jj;")],
     "noperm_st": [("                    L.sorted[(pw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu] = (uint16_t)(dw[e >> 1] >> (16 * (e & 1)));",
                    "                    L.sorted[kk] = (uint16_t)(dw[e >> 1] >> (16 * (e & 1)));")],
+    # K0 (C4 noise): the 4-gram bitmap's LDS atomics, knocked out and compacted
+    "k0_nobm": [("                atomicOr(&bm[x >> 20], 1u << ((x >> 15) & 31));\n", "")],
+    "k0_compact": [("""#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const uint32_t lo = w[j >> 2], hi = w[(j >> 2) + 1];
+            const uint32_t g4 = (j & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(j & 3)) : lo;
+            if (((uint32_t)j & smask) == 0 && p + j < bn) atomicAdd(&hist[(lo >> (8 * (j & 3))) & 0xFFu], 1u);
+            const uint32_t x = g4 * 0x9E3779B1u;
+            if (p + j + 4 <= bn && !(x & (7u << 11))) {   // sampled by content
+                qn++;
+                atomicOr(&bm[x >> 20], 1u << ((x >> 15) & 31));
+            }
+        }
+""", """        uint32_t sm = 0;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const uint32_t lo = w[j >> 2], hi = w[(j >> 2) + 1];
+            const uint32_t g4 = (j & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(j & 3)) : lo;
+            if (((uint32_t)j & smask) == 0 && p + j < bn) atomicAdd(&hist[(lo >> (8 * (j & 3))) & 0xFFu], 1u);
+            const uint32_t x = g4 * 0x9E3779B1u;
+            if (p + j + 4 <= bn && !(x & (7u << 11))) sm |= 1u << j;
+        }
+        qn += (uint32_t)__builtin_popcount(sm);
+        while (sm) {
+            const uint32_t j = (uint32_t)__builtin_ctz(sm), q = j >> 2;
+            sm &= sm - 1;
+            const uint32_t lo = q == 0 ? w[0] : q == 1 ? w[1] : q == 2 ? w[2] : w[3];
+            const uint32_t hi = q == 0 ? w[1] : q == 1 ? w[2] : q == 2 ? w[3] : w[4];
+            const uint32_t x = __builtin_amdgcn_alignbyte(hi, lo, j & 3) * 0x9E3779B1u;
+            atomicOr(&bm[x >> 20], 1u << ((x >> 15) & 31));
+        }
+""")],
+    "k0_nohist": [("            if (((uint32_t)j & smask) == 0 && p + j < bn) atomicAdd(&hist[(lo >> (8 * (j & 3))) & 0xFFu], 1u);\n", "")],
 }
 
 def build():
@@ -41,7 +74,7 @@ def build():
         obj = os.path.join(OUT, f"k_{name}.o")
         subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-fPIC", "--offload-arch=gfx950", "-std=c++17",
                                "-I", SRC, "-I", os.path.join(R, "include"), "-c", "-o", obj, src])
-        objs = [os.path.join(R, "build", "dmx", f) for f in ("dmx_host.o", "dmx_inflate.o", "dmx_gen.o", "dmx_inflate_dev.o")]
+        objs = [os.path.join(R, "build", "dmx", f) for f in ("dmx_host.o", "dmx_inflate.o", "dmx_gen.o", "dmx_inflate_dev.o", "dmx_refstats.o")]
         subprocess.check_call(["/opt/rocm/bin/hipcc", "-shared", "-fPIC", "--offload-arch=gfx950", "-o",
                                os.path.join(OUT, f"libdmx_{name}.so"), obj] + objs + ["-lm", "-lpthread"])
         print("built", name)
@@ -50,6 +83,29 @@ def run():
     for name in (sys.argv[2].split(",") if len(sys.argv) > 2 else VARIANTS):
         r = subprocess.run([sys.executable, __file__, "one", name], capture_output=True, text=True, timeout=300)
         print(name, r.stdout.strip() or r.stderr[-300:])
+
+def one_k0(name):
+    """C4: 1 GiB of noise with the store check; K0's HIP-event time ('pre') and the stream's hash."""
+    sys.path.insert(0, R)
+    import hashlib, numpy as np, torch
+    import deflate_compression_amd as D
+    D.LIB_PATH = os.path.join(OUT, f"libdmx_{name}.so")
+    n = 1 << 30
+    t = torch.from_numpy(D.gen_random(n)).cuda()
+    e = D.Encoder(0, n, max_chain=6, flags=D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK)
+    out, r = e.compress_tensor(t)
+    e.set_timing(True)
+    for _ in range(10):
+        out, r = e.compress_tensor(t)
+    st = e.stage_times()
+    h = hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()[:16]
+    e.close()
+    print(json.dumps({"stage_ms": st, "bytes": int(out.numel()), "sha": h}))
+
+def run_k0():
+    for name in sys.argv[2].split(","):
+        r = subprocess.run([sys.executable, __file__, "one_k0", name], capture_output=True, text=True, timeout=300)
+        print(name, r.stdout.strip() or r.stderr[-300:], flush=True)
 
 def one(name):
     os.environ["DMX_STAMPS"] = "1"
@@ -69,4 +125,7 @@ def one(name):
                       "total": round(st[:, 7].mean() / 1e3, 1)}))
 
 if __name__ == "__main__":
-    {"build": build, "run": run}.get(sys.argv[1], lambda: one(sys.argv[2]))()
+    if sys.argv[1] == "one_k0":
+        one_k0(sys.argv[2])
+    else:
+        {"build": build, "run": run, "run_k0": run_k0}.get(sys.argv[1], lambda: one(sys.argv[2]))()

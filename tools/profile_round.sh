@@ -12,7 +12,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
 BA="--cpu-budget 0 --exhaustive-steps 0 --tradeoff= --long-run 0 $*"
-echo "[1/6] pytest -m gpu"; timeout -k 10 900 python3 -u -m pytest "$R/tests" -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+echo "[1/6] pytest -m gpu"; timeout -k 10 900 python3 -u -m pytest "$R/tests" -m gpu -x -v -p no:cacheprovider --timeout 240 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 tail -2 "$OUT/pytest_gpu.log"
 echo "[2/6] kernel trace"; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 $BA > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
 echo "[3/6] pmc FETCH_SIZE"; timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_f" -o f -- python3 "$R/bench.py" --steps 2 --warmup 0 $BA > "$OUT/bench_pmc_f.json" 2> "$OUT/pmc_f.err"
