@@ -33,11 +33,17 @@
 #define DMX_IWX 8192      // indexed mode: an 8 KiB ring, older sources read back from HBM
 #endif
 #define IWX DMX_IWX
+#define IWC 4096          // chained decode: a ring of 4 096 cells (8 KiB)
 #define IFB 10            // first-level table bits
+#define ITAB_WORDS 2048   // a workgroup's first-level tables in HBM: literal/length, then distance
 #define IFLUSH 16384      // stream mode: flush to HBM every IFLUSH bytes (half the ring)
 
+// The first-level entries (1 << IFB words per table, format "Table entries" below) live in
+// HBM, ITAB_WORDS per workgroup: the symbol loop holds them in VGPRs and reloads them at each
+// entry (agent-scope loads, L2), so LDS keeps only the ring and these small arrays -- 10 KB
+// a workgroup, and all 3 052 blocks of 100 MB resident at once (12 per CU, the VGPR limit)
+// instead of 2 048 (8 per CU with the tables in LDS).
 struct ITable {
-    uint32_t fast[1 << IFB];   // first-level entries (format: "Table entries" below)
     uint16_t first[16];        // first canonical code of each length
     uint16_t cnt[16];
     uint16_t offs[16];         // index into sym[] of the first symbol of each length
@@ -203,8 +209,16 @@ __device__ __forceinline__ uint32_t iv_dbase(uint32_t e) { return ((e >> 28) << 
 // serves the code length code: its symbols 0..18 take the literal form).  IVSLOW marks a code
 // longer than IFB bits (or no code).  Returns 0 complete, 1 incomplete, -1 over-subscribed.
 // ---------------------------------------------------------------------------------------
+// agent-scope load of a table word (to L2, past the vector L1, which may hold the words of the
+// previous block's table)
+__device__ __forceinline__ uint32_t gtab_ld(const uint32_t* p) {
+    return __hip_atomic_load((const __attribute__((address_space(1))) uint32_t*)p, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <bool DIST, uint32_t W, typename TW>
-__device__ __forceinline__ int itable_build(InfLDS<W, TW>& S, ITable& T, int n, uint32_t lane) {
+__device__ __forceinline__ int itable_build(InfLDS<W, TW>& S, ITable& T, uint32_t* __restrict__ fast, int n,
+                                            uint32_t lane) {
     const int nc = (n + 63) >> 6;   // symbol chunks, <= 5
     uint32_t lc[5];
 #pragma unroll
@@ -212,7 +226,7 @@ __device__ __forceinline__ int itable_build(InfLDS<W, TW>& S, ITable& T, int n, 
         const int s = c * 64 + (int)lane;
         lc[c] = (c < nc && s < n) ? S.len[s] : 0u;
     }
-    for (int k = (int)lane; k < (1 << IFB); k += 64) T.fast[k] = IVSLOW;
+    for (int k = (int)lane; k < (1 << IFB); k += 64) fast[k] = IVSLOW;
     uint32_t cnt[16], first[16], offs[16];
 #pragma unroll
     for (int l = 1; l < 16; l++) {
@@ -268,11 +282,12 @@ __device__ __forceinline__ int itable_build(InfLDS<W, TW>& S, ITable& T, int n, 
                     const uint32_t rv = __brev(mycode) >> (32 - l0);
                     const uint32_t e16 = (s << 4) | l0;
                     const uint32_t e = DIST ? iv_d(e16) : iv_ll(e16);
-                    for (uint32_t j = 0; j < (1u << (IFB - l0)); j++) T.fast[rv | (j << l0)] = e;
+                    for (uint32_t j = 0; j < (1u << (IFB - l0)); j++) fast[rv | (j << l0)] = e;
                 }
             }
         }
     }
+    __builtin_amdgcn_s_waitcnt(0);   // the table stores are done before anyone loads them
     __syncthreads();
     return res;
 }
@@ -289,8 +304,8 @@ __device__ __forceinline__ uint32_t ientry_slow(const IBits& r, const ITable& T)
     return ISLOW;
 }
 // the code length code (symbols 0..18, in the literal form): sym << 4 | len, or ISLOW
-__device__ __forceinline__ uint32_t ientry_cl(const IBits& r, const ITable& T) {
-    const uint32_t e = rfl(T.fast[ib_peek(r, IFB)]);
+__device__ __forceinline__ uint32_t ientry_cl(const IBits& r, const ITable& T, const uint32_t* fast) {
+    const uint32_t e = rfl(gtab_ld(fast + ib_peek(r, IFB)));
     return e != IVSLOW ? (((e >> 16) & 0xFFu) << 4) | (e & 15u) : ientry_slow(r, T);
 }
 
@@ -518,7 +533,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 
 template <uint32_t W, bool CELL>
 __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t lim, uint32_t limm, uint32_t dfl,
-                                             uint32_t tla, uint32_t tda, uint32_t lane, uint64_t gpos0,
+                                             uint64_t tgl, uint64_t tgd, uint32_t toff, uint32_t lane, uint64_t gpos0,
                                              uint32_t& len, uint32_t& dist) {
     uint32_t ex;
     const uint64_t galn = gpos0 & ~3ull;   // output position 0 in HBM, as an aligned base + 0..3
@@ -547,7 +562,7 @@ __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t li
 // cells; a match reaching before the sw block's first byte writes reference cells there.
 template <bool RING, bool ADLER, uint32_t W, bool CELL = false>
 __device__ __forceinline__ int iblock(InfLDS<W, typename std::conditional<CELL, uint16_t, uint8_t>::type>& S, IBits& r,
-                                      IOut& o, uint32_t lane, bool& last) {
+                                      IOut& o, uint32_t* __restrict__ gt, uint32_t lane, bool& last) {
     constexpr uint32_t IM = W - 1, FL = W / 2;
     constexpr uint32_t CS = CELL ? 2 : 1;   // bytes per output position
     [[maybe_unused]] const unsigned long long ts0 = IST_NOW();
@@ -590,14 +605,14 @@ __device__ __forceinline__ int iblock(InfLDS<W, typename std::conditional<CELL, 
         }
         __syncthreads();
         [[maybe_unused]] const unsigned long long tc0 = IST_NOW();
-        if (itable_build<false>(S, S.lt, 19, lane) != 0) return -(int)E_HUFAMB;
+        if (itable_build<false>(S, S.lt, gt, 19, lane) != 0) return -(int)E_HUFAMB;
         [[maybe_unused]] const unsigned long long tc1 = IST_NOW();
         IST_ADD(o, 7, tc1 - tc0);
         uint32_t prev = 0;
         int idx = 0, err = 0;
         while (idx < nlen + ndist) {
             ib_refill(r);
-            const uint32_t e = ientry_cl(r, S.lt);
+            const uint32_t e = ientry_cl(r, S.lt, gt);
             if (e == ISLOW) { err = -(int)E_HUFINV; break; }
             ib_drop(r, e & 15u);
             const uint32_t sy = e >> 4;
@@ -631,13 +646,13 @@ __device__ __forceinline__ int iblock(InfLDS<W, typename std::conditional<CELL, 
     __syncthreads();
     [[maybe_unused]] const unsigned long long tl0 = IST_NOW();
     IST_ADD(o, 8, tl0 - ts0);
-    int e = itable_build<false>(S, S.lt, nlen, lane);
+    int e = itable_build<false>(S, S.lt, gt, nlen, lane);
     [[maybe_unused]] const unsigned long long tl1 = IST_NOW();
     IST_ADD(o, 9, tl1 - tl0);
     if (e < 0 || (e > 0 && bt == 2 && rfl(S.lt.offs[15] + S.lt.cnt[15]) != 1)) return -(int)E_HUFAMB;
     for (int s = (int)lane; s < 32; s += 64) S.len[s] = s < ndist ? S.seq[nlen + s] : 0;
     __syncthreads();
-    e = itable_build<true>(S, S.dt, ndist, lane);
+    e = itable_build<true>(S, S.dt, gt + (1u << IFB), ndist, lane);
     IST_ADD(o, 10, IST_NOW() - tl1);
     if (e < 0 || (e > 0 && bt == 2 && rfl(S.dt.offs[15] + S.dt.cnt[15]) > 1)) return -(int)E_HUFAMB;
 
@@ -649,14 +664,14 @@ __device__ __forceinline__ int iblock(InfLDS<W, typename std::conditional<CELL, 
     [[maybe_unused]] const unsigned long long ts1 = IST_NOW();
     IST_ADD(o, 0, ts1 - ts0);
     if (lds_addr(S.win) != 0) return -(int)E_RANGE;   // isym_run addresses the ring from LDS 0
-    const uint32_t tla = lds_addr(S.lt.fast) + lane * 4, tda = lds_addr(S.dt.fast) + lane * 4;
+    const uint64_t tgl = (uint64_t)(uintptr_t)gt, tgd = tgl + 4 * (1u << IFB);   // the tables' words, 4 bytes a lane
     const uint32_t dfl = o.ob != 0 ? 0x40000000u : 0u;   // stream mode: sources before ob exist
     const uint64_t gpos0 = (uint64_t)(uintptr_t)(o.out + CS * (o.base + o.ob));
     for (;;) {
         const uint32_t lim = RING ? min(capr, o.fl + FL) : capr;
         const uint32_t limm = rfl(min(lim, capr >= 258 ? capr - 258 : 0u));   // below it any length fits
         uint32_t len, dist;
-        const uint32_t ex = isym_run<W, CELL>(r, op, lim, limm, dfl, tla, tda, lane, gpos0, len, dist);
+        const uint32_t ex = isym_run<W, CELL>(r, op, lim, limm, dfl, tgl, tgd, lane * 4, lane, gpos0, len, dist);
         if (ex == IX_SEG) {   // a refill at a token start that the run does not rotate into
             ib_refill(r);
             continue;
@@ -671,7 +686,7 @@ __device__ __forceinline__ int iblock(InfLDS<W, typename std::conditional<CELL, 
         uint32_t en = 0;
         if (ex == IX_SYM || ex == IX_LIM) {   // one symbol the general way (nothing consumed)
             ib_refill(r);
-            en = rfl(S.lt.fast[ib_peek(r, IFB)]);
+            en = rfl(gtab_ld(gt + ib_peek(r, IFB)));
             if (en == IVSLOW) {
                 const uint32_t e16 = ientry_slow(r, S.lt);
                 if (e16 == ISLOW) { err = -(int)E_HUFINV; break; }
@@ -694,7 +709,7 @@ __device__ __forceinline__ int iblock(InfLDS<W, typename std::conditional<CELL, 
         }
         if (ex != IX_MATCH) {   // the distance the general way
             ib_refill(r);
-            uint32_t ed = rfl(S.dt.fast[ib_peek(r, IFB)]);
+            uint32_t ed = rfl(gtab_ld(gt + (1u << IFB) + ib_peek(r, IFB)));
             if (ed >= IVBAD) {
                 const uint32_t e16 = ed == IVSLOW ? ientry_slow(r, S.dt) : ISLOW;
                 ed = e16 == ISLOW ? IVBAD : iv_d(e16);
@@ -770,10 +785,13 @@ template <bool CELL>
 __global__ __launch_bounds__(64) void dmx_inflate_index_kernel(const uint8_t* __restrict__ z, uint64_t zbytes,
                                                                const dmx_iblock* __restrict__ index,
                                                                uint8_t* __restrict__ out, uint64_t out_cap,
+                                                               uint32_t* __restrict__ gtab,
                                                                dmx_inflate_status* __restrict__ st) {
-    // bytes: an 8 KiB ring, 18 KiB of LDS, 8 workgroups per CU (a 32 KiB window allowed 4);
-    // cells: 16 KiB of ring, 26 KiB, 6 per CU
-    __shared__ InfLDS<IWX, typename std::conditional<CELL, uint16_t, uint8_t>::type> S;
+    // bytes: an 8 KiB ring, 10 KiB of LDS; cells: 4 096 cells, the same 10 KiB.  12 workgroups
+    // per CU (151 VGPRs: 3 waves per SIMD), so 3 072 blocks decode at once
+    constexpr uint32_t WR = CELL ? IWC : IWX;
+    __shared__ InfLDS<WR, typename std::conditional<CELL, uint16_t, uint8_t>::type> S;
+    uint32_t* gt = gtab + (uint64_t)blockIdx.x * ITAB_WORDS;
     const uint32_t lane = threadIdx.x;
     IBits r;
     ib_init(r, z, zbytes);
@@ -798,7 +816,7 @@ __global__ __launch_bounds__(64) void dmx_inflate_index_kernel(const uint8_t* __
         ib_seek(r, bit);
         bool last = false;
         do {   // one sw block may be several DEFLATE blocks (DMX_F_SPLIT)
-            err = iblock<true, false, IWX, CELL>(S, r, o, lane, last);
+            err = iblock<true, false, WR, CELL>(S, r, o, gt, lane, last);
         } while (!err && o.op < olen && !last);
         if (!err && o.op != olen) err = -(int)E_SZ;
         if (!err) io_flush<false>(S, o, o.op, lane);
@@ -812,6 +830,7 @@ __global__ __launch_bounds__(64) void dmx_inflate_index_kernel(const uint8_t* __
 
 __global__ __launch_bounds__(64) void dmx_inflate_stream_kernel(const uint8_t* __restrict__ z, uint64_t zbytes,
                                                                 uint8_t* __restrict__ out, uint64_t out_cap,
+                                                                uint32_t* __restrict__ gtab,
                                                                 dmx_inflate_status* __restrict__ st) {
     __shared__ InfLDS<IW> S;
     const uint32_t lane = threadIdx.x;
@@ -841,7 +860,7 @@ __global__ __launch_bounds__(64) void dmx_inflate_stream_kernel(const uint8_t* _
     if (!err) {
         ib_seek(r, 16);
         bool last = false;
-        while (!err && !last) err = iblock<true, true, IW>(S, r, o, lane, last);
+        while (!err && !last) err = iblock<true, true, IW>(S, r, o, gtab, lane, last);
     }
     if (!err) {
         io_flush<true>(S, o, o.op, lane);
@@ -867,13 +886,18 @@ extern "C" int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_ibl
     if (zbytes > 0xFFFFFFF0ull) return -(int)E_RANGE;   // reader word indices are 32-bit
     hipStream_t s = (hipStream_t)stream;
     if (hipMemsetAsync(d_status, 0, sizeof(dmx_inflate_status), s) != hipSuccess) return -(int)E_DEVICE;
+    // the workgroups' first-level tables: stream-ordered scratch, freed after the launch
+    uint32_t* gtab = nullptr;
+    const uint64_t tb = (uint64_t)(d_index ? nblk : 1) * ITAB_WORDS * 4;
+    if (hipMallocAsync((void**)&gtab, tb, s) != hipSuccess) return -(int)E_MALLOC;
     if (d_index)
         hipLaunchKernelGGL(dmx_inflate_index_kernel<false>, dim3(nblk), dim3(64), 0, s, (const uint8_t*)d_z, zbytes,
-                           d_index, (uint8_t*)d_out, out_cap, d_status);
+                           d_index, (uint8_t*)d_out, out_cap, gtab, d_status);
     else
         hipLaunchKernelGGL(dmx_inflate_stream_kernel, dim3(1), dim3(64), 0, s, (const uint8_t*)d_z, zbytes,
-                           (uint8_t*)d_out, out_cap, d_status);
-    if (hipGetLastError() != hipSuccess) return -(int)E_DEVICE;
+                           (uint8_t*)d_out, out_cap, gtab, d_status);
+    const bool bad = hipGetLastError() != hipSuccess;
+    if (hipFreeAsync(gtab, s) != hipSuccess || bad) return -(int)E_DEVICE;
     return 0;
 }
 
@@ -1038,11 +1062,12 @@ __global__ __launch_bounds__(256) void dmx_cells_final_kernel(const uint16_t* __
     if (bad) atomicCAS(&st->status, 0, -(int32_t)E_HUFDIS);
 }
 
-// work layout: [list lengths 2 x nblk, 256-aligned][cells 2*cap, 256-aligned][P 4*cap][list A 4*cap][list B 4*cap]
+// work layout: [list lengths 2 x nblk, 256-aligned][tables ITAB_WORDS x nblk][cells 2*cap, 256-aligned]
+// [P 4*cap][list A 4*cap][list B 4*cap]
 static inline uint64_t chain_a256(uint64_t x) { return (x + 255) & ~255ull; }
 
 extern "C" uint64_t dmx_inflate_chained_work(uint64_t out_cap, uint32_t nblk) {
-    return chain_a256(8ull * nblk) + chain_a256(2 * out_cap) + 12 * out_cap;
+    return chain_a256(8ull * nblk) + 4ull * ITAB_WORDS * nblk + chain_a256(2 * out_cap) + 12 * out_cap;
 }
 
 extern "C" int dmx_inflate_chained_async(const void* d_z, uint64_t zbytes, const dmx_iblock* d_index, uint32_t nblk,
@@ -1053,12 +1078,13 @@ extern "C" int dmx_inflate_chained_async(const void* d_z, uint64_t zbytes, const
     if (work_bytes < dmx_inflate_chained_work(out_cap, nblk) || ((uintptr_t)d_work & 255)) return -(int)E_SZ;
     hipStream_t s = (hipStream_t)stream;
     uint32_t* C[2] = {(uint32_t*)d_work, (uint32_t*)d_work + nblk};
-    uint16_t* cells = (uint16_t*)((uint8_t*)d_work + chain_a256(8ull * nblk));
+    uint32_t* gtab = (uint32_t*)((uint8_t*)d_work + chain_a256(8ull * nblk));
+    uint16_t* cells = (uint16_t*)(gtab + (uint64_t)ITAB_WORDS * nblk);
     uint32_t* P = (uint32_t*)((uint8_t*)cells + chain_a256(2 * out_cap));
     uint32_t* L[2] = {P + out_cap, P + 2 * out_cap};
     if (hipMemsetAsync(d_status, 0, sizeof(dmx_inflate_status), s) != hipSuccess) return -(int)E_DEVICE;
     hipLaunchKernelGGL(dmx_inflate_index_kernel<true>, dim3(nblk), dim3(64), 0, s, (const uint8_t*)d_z, zbytes, d_index,
-                       (uint8_t*)cells, out_cap, d_status);
+                       (uint8_t*)cells, out_cap, gtab, d_status);
     hipLaunchKernelGGL(dmx_cells_prep_kernel, dim3(nblk), dim3(CHAIN_WG), 0, s, d_index, cells, P, L[0], C[0], out_cap, d_status);
     uint32_t rounds = 2;   // pointer jumping: a chain through k blocks takes ~log2(k) + 1 rounds
     while ((1ull << (rounds - 2)) < (uint64_t)nblk && rounds < CHAIN_ROUNDS_MAX) rounds++;
