@@ -18,9 +18,11 @@
 // is copied by the whole wave, 64 bytes a round (periodic sources by residue; sources older
 // than the ring from the output already flushed to HBM).  Output is assembled in an LDS ring
 // and written to HBM in 16-byte-per-lane coalesced stores every half ring (indexed mode: an
-// 8 KiB ring, so 8 workgroups fit a CU; stream mode: the 32 KiB window, folding the Adler-32
-// sums into the same pass).  Tables: 10-bit first level, built lane-parallel (ballot counts
-// and ranks); longer codes take a canonical slow path (first code / count / offset per length).
+// 8 KiB ring; stream mode: the 32 KiB window, folding the Adler-32 sums into the same pass).
+// Tables: 10-bit first level, built lane-parallel (ballot counts and ranks) into a per-
+// workgroup area of HBM and loaded into VGPRs by the symbol loop, so that LDS holds only the
+// ring (12 workgroups per CU); longer codes take a canonical slow path (first code / count /
+// offset per length, in LDS).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <type_traits>
@@ -474,8 +476,9 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // The symbol loop's common path, hand-scheduled.  Compiled code for this state machine spent
 // ~100 instructions a token (the structurizer's branch flags, copies of the stream registers
 // that waited for their prefetch); this one spends ~20 on a literal and ~60 on a match.
-// In SGPRs: the 64-bit bit buffer (s[94:95]), bc, wi, op; the two tables come from LDS into
-// v96..v111 (literal/length) and v112..v127 (distance, bases in v128..v143) and are read by
+// In SGPRs: the 64-bit bit buffer (s[94:95]), bc, wi, op; the two tables come from HBM (the
+// workgroup's table area, agent-scope loads) into v96..v111 (literal/length) and v112..v127
+// (distance, bases in v128..v143) and are read by
 // v_readlane under s_set_gpr_idx_on.  A literal is one ds_write_b8 (every lane stores the same
 // byte); a match is 64 bytes a round (lane t: byte src + t, read before the round's writes,
 // when distance >= length or >= 64; byte src + t mod distance for a shorter period; a
