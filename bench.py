@@ -19,6 +19,7 @@ Prints ONE JSON line on rank 0 (see DESIGN.md §5 for the roofline accounting).
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import socket
@@ -617,6 +618,13 @@ def main() -> int:
                                "indexed: one single-wave workgroup per block",
                        "kernel": "dmx_inflate_index_kernel<true> + dmx_cells_*" if chained else
                                  "dmx_inflate_index_kernel"}
+        if chained:   # how fast the chains resolve: reference-list lengths after prep and each jump launch
+            lists = (ctypes.c_uint32 * 41)()
+            if Lib.dmx_inflate_chained_lists(wptr, lists, 41, stream) == 0:
+                ls = list(lists)
+                while len(ls) > 1 and ls[-1] == 0 and ls[-2] == 0:
+                    ls.pop()
+                gpu_inflate["reference_lists"] = ls
     del work
     del dec
     run(args.warmup)

@@ -126,6 +126,7 @@ def lib() -> ctypes.CDLL:
         "dmx_gen_text": ([vp, u64, u64], None),
         "dmx_gen_random": ([vp, u64, u64], None),
         "dmx_inflate_chained_async": ([vp, u64, vp, u32, vp, u64, vp, u64, vp, vp], ctypes.c_int),
+        "dmx_inflate_chained_lists": ([vp, u32p, u32, vp], ctypes.c_int),
         "dmx_inflate_chained_work": ([u64, u32], u64),
         "dmx_refest_create": ([], vp),
         "dmx_refest_destroy": ([vp], None),

@@ -943,8 +943,8 @@ __device__ inline void chain_push(bool want, uint32_t v, uint32_t* __restrict__ 
 
 __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_prep_kernel(const dmx_iblock* __restrict__ index, uint16_t* __restrict__ cells,
                                                             uint32_t* __restrict__ P, uint32_t* __restrict__ list,
-                                                            uint32_t* __restrict__ count, uint64_t cap,
-                                                            dmx_inflate_status* __restrict__ st) {
+                                                            uint32_t* __restrict__ count, uint32_t* __restrict__ total,
+                                                            uint64_t cap, dmx_inflate_status* __restrict__ st) {
     __shared__ uint32_t nl;
     const uint64_t off = index[blockIdx.x].out_off;
     const uint32_t len = index[blockIdx.x].out_len;
@@ -984,14 +984,17 @@ __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_prep_kernel(const dmx_iblo
         chain_push(want, (uint32_t)(off + j), list + off, &nl);
     }
     __syncthreads();
-    if (threadIdx.x == 0) count[blockIdx.x] = nl;
+    if (threadIdx.x == 0) {
+        count[blockIdx.x] = nl;
+        if (nl) atomicAdd(total, nl);
+    }
     if (bad) atomicCAS(&st->status, 0, -(int32_t)E_HUFDIS);
 }
 
 __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_jump_kernel(const dmx_iblock* __restrict__ index, uint16_t* __restrict__ cells,
                                                                  uint32_t* __restrict__ P, const uint32_t* __restrict__ lin,
                                                                  uint32_t* __restrict__ lout, const uint32_t* __restrict__ cin,
-                                                                 uint32_t* __restrict__ cout) {
+                                                                 uint32_t* __restrict__ cout, uint32_t* __restrict__ total) {
     __shared__ uint32_t nl;
     const uint32_t cnt = cin[blockIdx.x];
     if (cnt == 0) {
@@ -1036,7 +1039,10 @@ __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_jump_kernel(const dmx_iblo
         chain_push(want[1], j[1], lout + off, &nl);
     }
     __syncthreads();
-    if (threadIdx.x == 0) cout[blockIdx.x] = nl;
+    if (threadIdx.x == 0) {
+        cout[blockIdx.x] = nl;
+        if (nl) atomicAdd(total, nl);
+    }
 }
 
 __global__ __launch_bounds__(256) void dmx_cells_final_kernel(const uint16_t* __restrict__ cells, uint8_t* __restrict__ out,
@@ -1065,12 +1071,22 @@ __global__ __launch_bounds__(256) void dmx_cells_final_kernel(const uint16_t* __
     if (bad) atomicCAS(&st->status, 0, -(int32_t)E_HUFDIS);
 }
 
-// work layout: [list lengths 2 x nblk, 256-aligned][tables ITAB_WORDS x nblk][cells 2*cap, 256-aligned]
-// [P 4*cap][list A 4*cap][list B 4*cap]
+// work layout: [list totals per round, 256 B][list lengths 2 x nblk, 256-aligned][tables ITAB_WORDS x nblk]
+// [cells 2*cap, 256-aligned][P 4*cap][list A 4*cap][list B 4*cap]
 static inline uint64_t chain_a256(uint64_t x) { return (x + 255) & ~255ull; }
 
 extern "C" uint64_t dmx_inflate_chained_work(uint64_t out_cap, uint32_t nblk) {
-    return chain_a256(8ull * nblk) + 4ull * ITAB_WORDS * nblk + chain_a256(2 * out_cap) + 12 * out_cap;
+    return 256 + chain_a256(8ull * nblk) + 4ull * ITAB_WORDS * nblk + chain_a256(2 * out_cap) + 12 * out_cap;
+}
+
+// The reference lists' total lengths of the last chained decode on this work buffer: [0] after
+// the prep kernel, [r + 1] after jump launch r (a diagnostic: how fast the chains resolve).
+extern "C" int dmx_inflate_chained_lists(const void* d_work, uint32_t* host, uint32_t n, void* stream) {
+    if (!d_work || !host || n > CHAIN_ROUNDS_MAX + 1) return -(int)E_INVAL;
+    if (hipMemcpyAsync(host, d_work, 4ull * n, hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
+        hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
+        return -(int)E_DEVICE;
+    return 0;
 }
 
 extern "C" int dmx_inflate_chained_async(const void* d_z, uint64_t zbytes, const dmx_iblock* d_index, uint32_t nblk,
@@ -1080,20 +1096,22 @@ extern "C" int dmx_inflate_chained_async(const void* d_z, uint64_t zbytes, const
     if (zbytes > 0xFFFFFFF0ull || out_cap > 0xFFFFFFF0ull) return -(int)E_RANGE;   // 32-bit positions
     if (work_bytes < dmx_inflate_chained_work(out_cap, nblk) || ((uintptr_t)d_work & 255)) return -(int)E_SZ;
     hipStream_t s = (hipStream_t)stream;
-    uint32_t* C[2] = {(uint32_t*)d_work, (uint32_t*)d_work + nblk};
-    uint32_t* gtab = (uint32_t*)((uint8_t*)d_work + chain_a256(8ull * nblk));
+    uint32_t* T = (uint32_t*)d_work;   // list totals per round
+    uint32_t* C[2] = {T + 64, T + 64 + nblk};
+    uint32_t* gtab = (uint32_t*)((uint8_t*)d_work + 256 + chain_a256(8ull * nblk));
     uint16_t* cells = (uint16_t*)(gtab + (uint64_t)ITAB_WORDS * nblk);
     uint32_t* P = (uint32_t*)((uint8_t*)cells + chain_a256(2 * out_cap));
     uint32_t* L[2] = {P + out_cap, P + 2 * out_cap};
     if (hipMemsetAsync(d_status, 0, sizeof(dmx_inflate_status), s) != hipSuccess) return -(int)E_DEVICE;
+    if (hipMemsetAsync(T, 0, 256, s) != hipSuccess) return -(int)E_DEVICE;
     hipLaunchKernelGGL(dmx_inflate_index_kernel<true>, dim3(nblk), dim3(64), 0, s, (const uint8_t*)d_z, zbytes, d_index,
                        (uint8_t*)cells, out_cap, gtab, d_status);
-    hipLaunchKernelGGL(dmx_cells_prep_kernel, dim3(nblk), dim3(CHAIN_WG), 0, s, d_index, cells, P, L[0], C[0], out_cap, d_status);
+    hipLaunchKernelGGL(dmx_cells_prep_kernel, dim3(nblk), dim3(CHAIN_WG), 0, s, d_index, cells, P, L[0], C[0], T, out_cap, d_status);
     uint32_t rounds = 2;   // pointer jumping: a chain through k blocks takes ~log2(k) + 1 rounds
     while ((1ull << (rounds - 2)) < (uint64_t)nblk && rounds < CHAIN_ROUNDS_MAX) rounds++;
     for (uint32_t rd = 0; rd < rounds; rd++)
         hipLaunchKernelGGL(dmx_cells_jump_kernel, dim3(nblk), dim3(CHAIN_WG), 0, s, d_index, cells, P, L[rd & 1],
-                           L[(rd + 1) & 1], C[rd & 1], C[(rd + 1) & 1]);
+                           L[(rd + 1) & 1], C[rd & 1], C[(rd + 1) & 1], T + rd + 1);
     const uint64_t gf0 = (out_cap + 4095) / 4096;
     const uint32_t gf = (uint32_t)(gf0 < 4096 ? gf0 : 4096);
     hipLaunchKernelGGL(dmx_cells_final_kernel, dim3(gf ? gf : 1), dim3(256), 0, s, cells, (uint8_t*)d_out, out_cap, d_status);

@@ -267,6 +267,10 @@ uint64_t dmx_inflate_chained_work(uint64_t out_cap, uint32_t nblk);
 int dmx_inflate_chained_async(const void* d_z, uint64_t zbytes, const dmx_iblock* d_index, uint32_t nblk, void* d_out,
                               uint64_t out_cap, void* d_work, uint64_t work_bytes, dmx_inflate_status* d_status,
                               void* stream);
+/* Diagnostic: the total length of the reference lists of the last chained decode that used
+ * d_work -- host[0] after the prep kernel, host[r + 1] after jump launch r (n <= 41 entries;
+ * synchronizes the stream).  Returns 0 or -E_*. */
+int dmx_inflate_chained_lists(const void* d_work, uint32_t* host, uint32_t n, void* stream);
 
 /* Introspection of the last encode of ctx (tests / fd_stats): per-block token
  * counts and the token stream (t = byte | dist << 9 | len),
