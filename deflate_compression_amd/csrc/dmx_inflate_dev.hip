@@ -967,7 +967,7 @@ __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_prep_kernel(const dmx_iblo
 
 // One wave per 2 048 cells (32 bitmap words, lane k < 32 holds word k); dense: the first
 // launch (no bitmap yet).  Words go 8 at a time, their loads in flight together.
-__global__ __launch_bounds__(256) void dmx_cells_jump_kernel(uint32_t* X, unsigned long long* __restrict__ U,
+__global__ __launch_bounds__(256) void dmx_cells_jump_kernel(uint32_t* __restrict__ X, unsigned long long* __restrict__ U,
                                                             uint64_t n, uint32_t* __restrict__ total, uint32_t dense) {
     if (!dense && __hip_atomic_load(total - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
     const uint32_t lane = threadIdx.x & 63;
@@ -998,13 +998,13 @@ __global__ __launch_bounds__(256) void dmx_cells_jump_kernel(uint32_t* X, unsign
                 const uint32_t sp = x[i] & ~XREF;
                 pend[i] = (x[i] & XREF) != 0;
                 ok[i] = pend[i] && sp < j;   // (never otherwise from a well-formed prep: stays unresolved)
-                y[i] = ok[i] ? X[sp] : 0u;   // (plain: a stale copy in this XCD's L2 is an older link of the same chain)
+                y[i] = ok[i] ? __hip_atomic_load(X + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
             }
 #pragma unroll
             for (int i = 0; i < 8; i++) {
                 const uint64_t j = 64 * (w0 + kb + i) + lane;
                 if (ok[i]) {
-                    X[j] = y[i];
+                    __hip_atomic_store(X + j, y[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     pend[i] = (y[i] & XREF) != 0;
                 }
                 const uint64_t nm = __ballot(pend[i]);
