@@ -965,54 +965,37 @@ __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_prep_kernel(const dmx_iblo
     if (bad) atomicCAS(&st->status, 0, -(int32_t)E_HUFDIS);
 }
 
-// One wave per 2 048 cells (32 bitmap words, lane k < 32 holds word k); dense: the first
-// launch (no bitmap yet).  Words go 8 at a time, their loads in flight together.
+// One wave per 2 048 cells (32 bitmap words); dense: the first launch (no bitmap yet).
 __global__ __launch_bounds__(256) void dmx_cells_jump_kernel(uint32_t* __restrict__ X, unsigned long long* __restrict__ U,
                                                             uint64_t n, uint32_t* __restrict__ total, uint32_t dense) {
     if (!dense && __hip_atomic_load(total - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t nch = (n + 2047) / 2048, nw = (n + 63) / 64;
+    const uint64_t nch = (n + 2047) / 2048;
     uint32_t nl = 0;
     for (uint64_t ch = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); ch < nch; ch += (uint64_t)gridDim.x * 4) {
-        const uint64_t w0 = ch * 32;
-        const bool wl = lane < 32 && w0 + lane < nw;   // this lane's bitmap word exists
-        const uint64_t um = wl ? (dense ? ~0ull : U[w0 + lane]) : 0ull;
-        const uint64_t nz = __ballot(um != 0);
-        uint64_t nu = 0;   // lane k: word k's new bitmap
-        for (uint32_t kb = 0; kb < 32; kb += 8) {
-            if (((nz >> kb) & 0xFFull) == 0) continue;
-            uint32_t x[8], y[8];
-            bool ok[8], pend[8];
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const uint32_t k = kb + i;
-                const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(um >> 32), (int)k) << 32) |
-                                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)um, (int)k);
-                const uint64_t j = 64 * (w0 + k) + lane;
-                const bool act = ((m >> lane) & 1) && j < n;
-                x[i] = act ? X[j] : 0u;
-            }
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const uint64_t j = 64 * (w0 + kb + i) + lane;
-                const uint32_t sp = x[i] & ~XREF;
-                pend[i] = (x[i] & XREF) != 0;
-                ok[i] = pend[i] && sp < j;   // (never otherwise from a well-formed prep: stays unresolved)
-                y[i] = ok[i] ? __hip_atomic_load(X + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-            }
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const uint64_t j = 64 * (w0 + kb + i) + lane;
-                if (ok[i]) {
-                    __hip_atomic_store(X + j, y[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    pend[i] = (y[i] & XREF) != 0;
+        for (uint32_t k = 0; k < 32; k++) {
+            const uint64_t w = ch * 32 + k;   // bitmap word: cells 64 w .. 64 w + 63
+            if (64 * w >= n) break;
+            const uint64_t m = dense ? ~0ull : U[w];
+            if (m == 0) continue;
+            const uint64_t j = 64 * w + lane;
+            bool pend = false;
+            if (((m >> lane) & 1) && j < n) {
+                const uint32_t x = X[j];
+                if (x & XREF) {
+                    pend = true;
+                    const uint32_t sp = x & ~XREF;
+                    if (sp < j) {   // (never otherwise from a well-formed prep: stays unresolved)
+                        const uint32_t y = __hip_atomic_load(X + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(X + j, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        pend = (y & XREF) != 0;
+                    }
                 }
-                const uint64_t nm = __ballot(pend[i]);
-                if (lane == kb + i) nu = nm;
-                nl += (uint32_t)__popcll(nm);
             }
+            const uint64_t nm = __ballot(pend);
+            if (lane == 0) U[w] = nm;
+            nl += (uint32_t)__popcll(nm);
         }
-        if (wl) U[w0 + lane] = nu;
     }
     if (lane == 0 && nl) atomicAdd(total, nl);
 }
