@@ -912,128 +912,175 @@ extern "C" int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_ibl
 //      copy of such a cell) becomes a reference cell 0x100 + b - 1 = the byte b positions
 //      before the block's start.  Copies inside the block copy cells, so a reference always
 //      names a byte of an EARLIER block.
-//   2. dmx_cells_prep_kernel (one workgroup per block): every cell becomes a 32-bit word X[j]
-//      -- a byte (resolved), or XREF | s, the absolute position of its source; a reference
-//      whose source is already a byte takes that byte at once.
-//      dmx_cells_jump_kernel, about log2(nblk) + 2 launches: X[j] = X[s] for every unresolved
-//      j (pointer jumping: a resolved source is copied, an unresolved one's pointer is taken,
-//      so chains of references through many blocks -- a phrase copied from block to block
-//      through the whole stream -- halve each launch).  In place: a stale read only delays
-//      resolution, never changes the value.  A wave owns 2 048 cells and their 32 words of an
-//      unresolved-cell bitmap: the first launch reads every X and writes the bitmap, later
-//      ones read only the words whose bitmap bits are set (coalesced, a lane per cell), and a
-//      launch whose predecessor left nothing unresolved returns at once.  (Lists of
-//      unresolved positions instead: 3.84 ms for the 100 MB dict stream, 76 % of whose cells
-//      are references after prep, their chains up to ~500 blocks long.)
-//   3. dmx_cells_final_kernel: X -> bytes; any cell still unresolved is an error.
+//   2. dmx_cells_prep_kernel: each reference becomes an absolute source position s; a source
+//      that is already a byte is copied at once, otherwise P[j] = s, the cell is marked
+//      unresolved (0xFFFF) and j goes on its block's list.  The lists are per block -- block
+//      b's entries sit in [out_off, out_off + count) of a list buffer, so a workgroup appends
+//      with one LDS atomic per wave and no global atomic at all.
+//      dmx_cells_jump_kernel, about log2(nblk) + 2 launches of one workgroup per block, each
+//      over the list the one before it left: an unresolved j looks at s = P[j]: a resolved
+//      cell is copied, otherwise P[j] = P[s] and j goes on the next list (pointer jumping:
+//      chains of references through many blocks -- a run carried across every block, say --
+//      halve each launch).  In place: a stale read only delays resolution, never changes the
+//      value (P moves along the chain, a resolved cell stays).  A block whose list is empty
+//      returns at once.
+//   3. dmx_cells_final_kernel: cells -> bytes; any cell still unresolved is an error.
 // ------------------------------------------------------------------------------------
 #define CHAIN_ROUNDS_MAX 40
-#define CHAIN_WG 1024      // threads per block in prep
-#define XREF 0x80000000u   // X[j]: an unresolved cell, source position in the low 31 bits
+#define CHAIN_WG 1024   // threads per block in prep and jump: a block's list is latency-bound
 
-__global__ __launch_bounds__(CHAIN_WG) void dmx_cells_prep_kernel(const dmx_iblock* __restrict__ index,
-                                                                 const uint16_t* __restrict__ cells,
-                                                                 uint32_t* __restrict__ X, uint32_t* __restrict__ total,
-                                                                 uint64_t cap, dmx_inflate_status* __restrict__ st) {
+// Appends v at list[*lds_cnt ...] for every lane with want set; the whole wave calls it.
+__device__ inline void chain_push(bool want, uint32_t v, uint32_t* __restrict__ list, uint32_t* lds_cnt) {
+    const uint64_t m = __ballot(want);
+    if (!m) return;
+    const int lead = __ffsll((unsigned long long)m) - 1;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t base = 0;
+    if ((int)lane == lead) base = atomicAdd(lds_cnt, (uint32_t)__popcll(m));
+    base = __shfl(base, lead);
+    if (want) list[base + __popcll(m & ((1ull << lane) - 1))] = v;
+}
+
+__global__ __launch_bounds__(CHAIN_WG) void dmx_cells_prep_kernel(const dmx_iblock* __restrict__ index, uint16_t* __restrict__ cells,
+                                                            uint32_t* __restrict__ P, uint32_t* __restrict__ list,
+                                                            uint32_t* __restrict__ count, uint32_t* __restrict__ total,
+                                                            uint64_t cap, dmx_inflate_status* __restrict__ st) {
+    __shared__ uint32_t nl;
     const uint64_t off = index[blockIdx.x].out_off;
     const uint32_t len = index[blockIdx.x].out_len;
     if (off > cap || len > cap - off) {   // the decode already failed this index; read nothing
-        if (threadIdx.x == 0) atomicCAS(&st->status, 0, -(int32_t)E_RANGE);
+        if (threadIdx.x == 0) {
+            count[blockIdx.x] = 0;
+            atomicCAS(&st->status, 0, -(int32_t)E_RANGE);
+        }
         return;
     }
-    uint32_t nl = 0;
+    if (threadIdx.x == 0) nl = 0;
+    __syncthreads();
     bool bad = false;
-    for (uint32_t j = threadIdx.x; j < len; j += CHAIN_WG) {
-        const uint32_t c = cells[off + j];
-        uint32_t x = c;
-        if (c >= 0x100u) {
-            const uint64_t back = (uint64_t)(c - 0xFFu) + j;   // positions before j
-            if (back > off + j) {
-                bad = true;
-                x = XREF;   // stays unresolved (the status already says why)
-            } else {
-                const uint32_t sp = (uint32_t)(off + j - back);
-                const uint32_t cs = cells[sp];   // cells no longer change: a byte, or a reference
-                x = cs < 0x100u ? cs : (XREF | sp);
-            }
-        }
-        nl += x >> 31;
-        X[off + j] = x;
-    }
-    nl = __reduce_add_sync(~0ull, nl);
-    if ((threadIdx.x & 63) == 0 && nl) atomicAdd(total, nl);
-    if (bad) atomicCAS(&st->status, 0, -(int32_t)E_HUFDIS);
-}
-
-// One wave per 2 048 cells (32 bitmap words); dense: the first launch (no bitmap yet).
-__global__ __launch_bounds__(256) void dmx_cells_jump_kernel(uint32_t* __restrict__ X, unsigned long long* __restrict__ U,
-                                                            uint64_t n, uint32_t* __restrict__ total, uint32_t dense) {
-    if (!dense && __hip_atomic_load(total - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t nch = (n + 2047) / 2048;
-    uint32_t nl = 0;
-    for (uint64_t ch = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); ch < nch; ch += (uint64_t)gridDim.x * 4) {
-        for (uint32_t k = 0; k < 32; k++) {
-            const uint64_t w = ch * 32 + k;   // bitmap word: cells 64 w .. 64 w + 63
-            if (64 * w >= n) break;
-            const uint64_t m = dense ? ~0ull : U[w];
-            if (m == 0) continue;
-            const uint64_t j = 64 * w + lane;
-            bool pend = false;
-            if (((m >> lane) & 1) && j < n) {
-                const uint32_t x = X[j];
-                if (x & XREF) {
-                    pend = true;
-                    const uint32_t sp = x & ~XREF;
-                    if (sp < j) {   // (never otherwise from a well-formed prep: stays unresolved)
-                        const uint32_t y = __hip_atomic_load(X + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store(X + j, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        pend = (y & XREF) != 0;
+    for (uint32_t j0 = 0; j0 < len; j0 += CHAIN_WG) {   // uniform trip count: chain_push needs the whole wave
+        const uint32_t j = j0 + threadIdx.x;
+        bool want = false;
+        if (j < len) {
+            const uint32_t c = cells[off + j];
+            if (c >= 0x100u) {
+                const uint64_t back = (uint64_t)(c - 0xFFu) + j;   // positions before j
+                if (back > off + j) {
+                    bad = true;
+                } else {
+                    const uint32_t sp = (uint32_t)(off + j - back);
+                    // a byte cell never changes; a reference (raw or already marked) waits
+                    const uint16_t cs = __hip_atomic_load(cells + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (cs < 0x100u) {
+                        cells[off + j] = cs;
+                    } else {
+                        P[off + j] = sp;
+                        __hip_atomic_store(cells + off + j, (uint16_t)0xFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        want = true;
                     }
                 }
             }
-            const uint64_t nm = __ballot(pend);
-            if (lane == 0) U[w] = nm;
-            nl += (uint32_t)__popcll(nm);
         }
+        chain_push(want, (uint32_t)(off + j), list + off, &nl);
     }
-    if (lane == 0 && nl) atomicAdd(total, nl);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        count[blockIdx.x] = nl;
+        if (nl) atomicAdd(total, nl);
+    }
+    if (bad) atomicCAS(&st->status, 0, -(int32_t)E_HUFDIS);
 }
 
-__global__ __launch_bounds__(256) void dmx_cells_final_kernel(const uint32_t* __restrict__ X, uint8_t* __restrict__ out,
+__global__ __launch_bounds__(CHAIN_WG) void dmx_cells_jump_kernel(const dmx_iblock* __restrict__ index, uint16_t* __restrict__ cells,
+                                                                 uint32_t* __restrict__ P, const uint32_t* __restrict__ lin,
+                                                                 uint32_t* __restrict__ lout, const uint32_t* __restrict__ cin,
+                                                                 uint32_t* __restrict__ cout, uint32_t* __restrict__ total) {
+    __shared__ uint32_t nl;
+    const uint32_t cnt = cin[blockIdx.x];
+    if (cnt == 0) {
+        if (threadIdx.x == 0) cout[blockIdx.x] = 0;
+        return;
+    }
+    const uint64_t off = index[blockIdx.x].out_off;
+    if (threadIdx.x == 0) nl = 0;
+    __syncthreads();
+    // two entries per thread, their dependent loads (list, P, cell, P) interleaved
+    for (uint32_t u0 = 0; u0 < cnt; u0 += 2 * CHAIN_WG) {
+        uint32_t j[2], sp[2];
+        uint16_t cs[2];
+        bool act[2], want[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const uint32_t u = u0 + k * CHAIN_WG + threadIdx.x;
+            act[k] = u < cnt;
+            j[k] = act[k] ? lin[off + u] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            sp[k] = act[k] ? P[j[k]] : 0;
+            act[k] = act[k] && sp[k] < j[k];   // never otherwise from a well-formed prep: stays unresolved
+        }
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+            cs[k] = act[k] ? __hip_atomic_load(cells + sp[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            want[k] = false;
+            if (act[k]) {
+                if (cs[k] != 0xFFFFu) {
+                    cells[j[k]] = cs[k];
+                } else {
+                    P[j[k]] = __hip_atomic_load(P + sp[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    want[k] = true;
+                }
+            }
+        }
+        chain_push(want[0], j[0], lout + off, &nl);
+        chain_push(want[1], j[1], lout + off, &nl);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        cout[blockIdx.x] = nl;
+        if (nl) atomicAdd(total, nl);
+    }
+}
+
+__global__ __launch_bounds__(256) void dmx_cells_final_kernel(const uint16_t* __restrict__ cells, uint8_t* __restrict__ out,
                                                              uint64_t n, dmx_inflate_status* __restrict__ st) {
     const uint64_t stride = (uint64_t)gridDim.x * 256 * 16;
     bool bad = false;
     for (uint64_t j0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16; j0 < n; j0 += stride) {
         if (j0 + 16 <= n && ((uintptr_t)(out + j0) & 15) == 0) {
+            const uint4 a = *reinterpret_cast<const uint4*>(cells + j0), b = *reinterpret_cast<const uint4*>(cells + j0 + 8);
+            const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
             uint32_t o[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const uint4 a = *reinterpret_cast<const uint4*>(X + j0 + 4 * k);
-                bad = bad || ((a.x | a.y | a.z | a.w) & 0xFFFFFF00u) != 0;
-                o[k] = (a.x & 0xFFu) | ((a.y & 0xFFu) << 8) | ((a.z & 0xFFu) << 16) | (a.w << 24);
+                const uint32_t lo = w[2 * k], hi = w[2 * k + 1];
+                bad = bad || ((lo | hi) & 0xFF00FF00u) != 0;
+                o[k] = (lo & 0xFFu) | ((lo >> 8) & 0xFF00u) | ((hi & 0xFFu) << 16) | ((hi << 8) & 0xFF000000u);
             }
             *reinterpret_cast<uint4*>(out + j0) = make_uint4(o[0], o[1], o[2], o[3]);
         } else {
             for (uint64_t j = j0; j < n && j < j0 + 16; j++) {
-                bad = bad || X[j] > 0xFFu;
-                out[j] = (uint8_t)X[j];
+                bad = bad || cells[j] > 0xFFu;
+                out[j] = (uint8_t)cells[j];
             }
         }
     }
     if (bad) atomicCAS(&st->status, 0, -(int32_t)E_HUFDIS);
 }
 
-// work layout: [list totals per round, 256 B][tables ITAB_WORDS x nblk][cells 2*cap, 256-aligned]
-// [X 4*cap, 256-aligned][bitmap cap/8, 8-byte words]
+// work layout: [list totals per round, 256 B][list lengths 2 x nblk, 256-aligned][tables ITAB_WORDS x nblk]
+// [cells 2*cap, 256-aligned][P 4*cap][list A 4*cap][list B 4*cap]
 static inline uint64_t chain_a256(uint64_t x) { return (x + 255) & ~255ull; }
 
 extern "C" uint64_t dmx_inflate_chained_work(uint64_t out_cap, uint32_t nblk) {
-    return 256 + 4ull * ITAB_WORDS * nblk + chain_a256(2 * out_cap) + chain_a256(4 * out_cap) + 8 * ((out_cap + 63) / 64);
+    return 256 + chain_a256(8ull * nblk) + 4ull * ITAB_WORDS * nblk + chain_a256(2 * out_cap) + 12 * out_cap;
 }
 
-// The unresolved-cell totals of the last chained decode on this work buffer: [0] after the
-// prep kernel, [r + 1] after jump launch r (a diagnostic: how fast the chains resolve).
+// The reference lists' total lengths of the last chained decode on this work buffer: [0] after
+// the prep kernel, [r + 1] after jump launch r (a diagnostic: how fast the chains resolve).
 extern "C" int dmx_inflate_chained_lists(const void* d_work, uint32_t* host, uint32_t n, void* stream) {
     if (!d_work || !host || n > CHAIN_ROUNDS_MAX + 1) return -(int)E_INVAL;
     if (hipMemcpyAsync(host, d_work, 4ull * n, hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
@@ -1046,29 +1093,28 @@ extern "C" int dmx_inflate_chained_async(const void* d_z, uint64_t zbytes, const
                                          void* d_out, uint64_t out_cap, void* d_work, uint64_t work_bytes,
                                          dmx_inflate_status* d_status, void* stream) {
     if (!d_z || !d_out || !d_status || !d_index || !nblk || !d_work) return -(int)E_INVAL;
-    if (zbytes > 0xFFFFFFF0ull || out_cap > 0x7FFFFFF0ull) return -(int)E_RANGE;   // 31-bit positions in X
+    if (zbytes > 0xFFFFFFF0ull || out_cap > 0xFFFFFFF0ull) return -(int)E_RANGE;   // 32-bit positions
     if (work_bytes < dmx_inflate_chained_work(out_cap, nblk) || ((uintptr_t)d_work & 255)) return -(int)E_SZ;
     hipStream_t s = (hipStream_t)stream;
-    uint32_t* T = (uint32_t*)d_work;   // unresolved totals per round
-    uint32_t* gtab = T + 64;
+    uint32_t* T = (uint32_t*)d_work;   // list totals per round
+    uint32_t* C[2] = {T + 64, T + 64 + nblk};
+    uint32_t* gtab = (uint32_t*)((uint8_t*)d_work + 256 + chain_a256(8ull * nblk));
     uint16_t* cells = (uint16_t*)(gtab + (uint64_t)ITAB_WORDS * nblk);
-    uint32_t* X = (uint32_t*)((uint8_t*)cells + chain_a256(2 * out_cap));
-    unsigned long long* U = (unsigned long long*)((uint8_t*)X + chain_a256(4 * out_cap));
+    uint32_t* P = (uint32_t*)((uint8_t*)cells + chain_a256(2 * out_cap));
+    uint32_t* L[2] = {P + out_cap, P + 2 * out_cap};
     if (hipMemsetAsync(d_status, 0, sizeof(dmx_inflate_status), s) != hipSuccess) return -(int)E_DEVICE;
     if (hipMemsetAsync(T, 0, 256, s) != hipSuccess) return -(int)E_DEVICE;
     hipLaunchKernelGGL(dmx_inflate_index_kernel<true>, dim3(nblk), dim3(64), 0, s, (const uint8_t*)d_z, zbytes, d_index,
                        (uint8_t*)cells, out_cap, gtab, d_status);
-    hipLaunchKernelGGL(dmx_cells_prep_kernel, dim3(nblk), dim3(CHAIN_WG), 0, s, d_index, cells, X, T, out_cap, d_status);
+    hipLaunchKernelGGL(dmx_cells_prep_kernel, dim3(nblk), dim3(CHAIN_WG), 0, s, d_index, cells, P, L[0], C[0], T, out_cap, d_status);
     uint32_t rounds = 2;   // pointer jumping: a chain through k blocks takes ~log2(k) + 1 rounds
     while ((1ull << (rounds - 2)) < (uint64_t)nblk && rounds < CHAIN_ROUNDS_MAX) rounds++;
-    const uint64_t gj0 = (out_cap + 8191) / 8192;   // 4 waves of 2 048 cells per workgroup
-    const uint32_t gj = (uint32_t)(gj0 < 16384 ? gj0 : 16384);
     for (uint32_t rd = 0; rd < rounds; rd++)
-        hipLaunchKernelGGL(dmx_cells_jump_kernel, dim3(gj ? gj : 1), dim3(256), 0, s, X, U, out_cap, T + rd + 1,
-                           rd == 0 ? 1u : 0u);
+        hipLaunchKernelGGL(dmx_cells_jump_kernel, dim3(nblk), dim3(CHAIN_WG), 0, s, d_index, cells, P, L[rd & 1],
+                           L[(rd + 1) & 1], C[rd & 1], C[(rd + 1) & 1], T + rd + 1);
     const uint64_t gf0 = (out_cap + 4095) / 4096;
     const uint32_t gf = (uint32_t)(gf0 < 4096 ? gf0 : 4096);
-    hipLaunchKernelGGL(dmx_cells_final_kernel, dim3(gf ? gf : 1), dim3(256), 0, s, X, (uint8_t*)d_out, out_cap, d_status);
+    hipLaunchKernelGGL(dmx_cells_final_kernel, dim3(gf ? gf : 1), dim3(256), 0, s, cells, (uint8_t*)d_out, out_cap, d_status);
     if (hipGetLastError() != hipSuccess) return -(int)E_DEVICE;
     return 0;
 }
