@@ -941,8 +941,8 @@ __device__ inline void chain_push(bool want, uint32_t v, uint32_t* __restrict__ 
     if (want) list[base + __popcll(m & ((1ull << lane) - 1))] = v;
 }
 
-__global__ __launch_bounds__(CHAIN_WG) void dmx_cells_prep_kernel(const dmx_iblock* __restrict__ index, uint16_t* __restrict__ cells,
-                                                            uint32_t* __restrict__ P, uint32_t* __restrict__ list,
+__global__ __launch_bounds__(CHAIN_WG) void dmx_cells_prep_kernel(const dmx_iblock* __restrict__ index, uint16_t* cells,
+                                                            uint32_t* P, uint32_t* __restrict__ list,
                                                             uint32_t* __restrict__ count, uint32_t* __restrict__ total,
                                                             uint64_t cap, dmx_inflate_status* __restrict__ st) {
     __shared__ uint32_t nl;
@@ -970,12 +970,12 @@ __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_prep_kernel(const dmx_iblo
                 } else {
                     const uint32_t sp = (uint32_t)(off + j - back);
                     // a byte cell never changes; a reference (raw or already marked) waits
-                    const uint16_t cs = __hip_atomic_load(cells + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint16_t cs = cells[sp];
                     if (cs < 0x100u) {
                         cells[off + j] = cs;
                     } else {
                         P[off + j] = sp;
-                        __hip_atomic_store(cells + off + j, (uint16_t)0xFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        cells[off + j] = 0xFFFFu;
                         want = true;
                     }
                 }
@@ -991,8 +991,8 @@ __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_prep_kernel(const dmx_iblo
     if (bad) atomicCAS(&st->status, 0, -(int32_t)E_HUFDIS);
 }
 
-__global__ __launch_bounds__(CHAIN_WG) void dmx_cells_jump_kernel(const dmx_iblock* __restrict__ index, uint16_t* __restrict__ cells,
-                                                                 uint32_t* __restrict__ P, const uint32_t* __restrict__ lin,
+__global__ __launch_bounds__(CHAIN_WG) void dmx_cells_jump_kernel(const dmx_iblock* __restrict__ index, uint16_t* cells,
+                                                                 uint32_t* P, const uint32_t* __restrict__ lin,
                                                                  uint32_t* __restrict__ lout, const uint32_t* __restrict__ cin,
                                                                  uint32_t* __restrict__ cout, uint32_t* __restrict__ total) {
     __shared__ uint32_t nl;
@@ -1022,7 +1022,7 @@ __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_jump_kernel(const dmx_iblo
         }
 #pragma unroll
         for (int k = 0; k < 2; k++)
-            cs[k] = act[k] ? __hip_atomic_load(cells + sp[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+            cs[k] = act[k] ? cells[sp[k]] : 0;   // (plain loads: a stale copy is an older link of the chain)
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             want[k] = false;
@@ -1030,7 +1030,7 @@ __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_jump_kernel(const dmx_iblo
                 if (cs[k] != 0xFFFFu) {
                     cells[j[k]] = cs[k];
                 } else {
-                    P[j[k]] = __hip_atomic_load(P + sp[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    P[j[k]] = P[sp[k]];
                     want[k] = true;
                 }
             }
