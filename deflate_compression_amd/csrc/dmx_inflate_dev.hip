@@ -928,6 +928,9 @@ extern "C" int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_ibl
 // ------------------------------------------------------------------------------------
 #define CHAIN_ROUNDS_MAX 40
 #define CHAIN_WG 1024   // threads per block in prep and jump: a block's list is latency-bound
+#ifndef CHAIN_ILP
+#define CHAIN_ILP 4     // list entries per jump thread in flight (2: 0.65 ms a full round, `profiles/r03_t`)
+#endif
 
 // Appends v at list[*lds_cnt ...] for every lane with want set; the whole wave calls it.
 __device__ inline void chain_push(bool want, uint32_t v, uint32_t* __restrict__ list, uint32_t* lds_cnt) {
@@ -1004,27 +1007,27 @@ __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_jump_kernel(const dmx_iblo
     const uint64_t off = index[blockIdx.x].out_off;
     if (threadIdx.x == 0) nl = 0;
     __syncthreads();
-    // two entries per thread, their dependent loads (list, P, cell, P) interleaved
-    for (uint32_t u0 = 0; u0 < cnt; u0 += 2 * CHAIN_WG) {
-        uint32_t j[2], sp[2];
-        uint16_t cs[2];
-        bool act[2], want[2];
+    // CHAIN_ILP entries per thread, their dependent loads (list, P, cell, P) interleaved
+    for (uint32_t u0 = 0; u0 < cnt; u0 += CHAIN_ILP * CHAIN_WG) {
+        uint32_t j[CHAIN_ILP], sp[CHAIN_ILP];
+        uint16_t cs[CHAIN_ILP];
+        bool act[CHAIN_ILP], want[CHAIN_ILP];
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < CHAIN_ILP; k++) {
             const uint32_t u = u0 + k * CHAIN_WG + threadIdx.x;
             act[k] = u < cnt;
             j[k] = act[k] ? lin[off + u] : 0;
         }
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < CHAIN_ILP; k++) {
             sp[k] = act[k] ? P[j[k]] : 0;
             act[k] = act[k] && sp[k] < j[k];   // never otherwise from a well-formed prep: stays unresolved
         }
 #pragma unroll
-        for (int k = 0; k < 2; k++)
+        for (int k = 0; k < CHAIN_ILP; k++)
             cs[k] = act[k] ? cells[sp[k]] : 0;   // (plain loads: a stale copy is an older link of the chain)
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < CHAIN_ILP; k++) {
             want[k] = false;
             if (act[k]) {
                 if (cs[k] != 0xFFFFu) {
@@ -1035,8 +1038,8 @@ __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_jump_kernel(const dmx_iblo
                 }
             }
         }
-        chain_push(want[0], j[0], lout + off, &nl);
-        chain_push(want[1], j[1], lout + off, &nl);
+#pragma unroll
+        for (int k = 0; k < CHAIN_ILP; k++) chain_push(want[k], j[k], lout + off, &nl);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
