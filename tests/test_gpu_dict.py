@@ -195,6 +195,31 @@ def test_dict_gpu_inflate_chained_corrupt(enc):
     assert st == -D.E["E_HUFDIS"]
 
 
+def test_dict_gpu_inflate_chained_lists_and_bad_index(enc):
+    """The chained decode's unresolved-reference totals (dmx_inflate_chained_lists) shrink to 0
+    launch by launch, and an index entry past the output capacity ends with -E_RANGE."""
+    import ctypes
+    data = D.gen_text(400000, 5).tobytes()[:32768] * 12
+    z, _ = enc.compress_bytes(data, max_chain=6, flags=D.DMX_ZLIB | D.DMX_F_DICT | D.DMX_F_LAZY)
+    ix, nblk = enc.block_index()
+    L = D.lib()
+    wb = int(L.dmx_inflate_chained_work(len(data), nblk))
+    work = torch.empty(wb + 256, dtype=torch.uint8, device="cuda")
+    dz = torch.frombuffer(bytearray(z), dtype=torch.uint8).cuda()
+    out, st = D.inflate_gpu_chained(dz, len(data), ix, nblk, work=work)
+    assert st == 0 and out.cpu().numpy().tobytes() == data
+    lists = (ctypes.c_uint32 * 41)()
+    wp = (work.data_ptr() + 255) & ~255
+    assert L.dmx_inflate_chained_lists(wp, lists, 41, torch.cuda.current_stream().cuda_stream) == 0
+    ls = list(lists)
+    assert ls[0] > 0                                   # every block after the first copies its predecessor
+    assert all(a >= b for a, b in zip(ls, ls[1:])) and ls[-1] == 0
+    bad = ix.clone()
+    bad[8:16] = torch.tensor(np.frombuffer(np.uint64(len(data)).tobytes(), np.uint8))   # block 0 at out_off = cap
+    out, st = D.inflate_gpu_chained(dz, len(data), bad, nblk)
+    assert st == -D.E["E_RANGE"]
+
+
 def test_dict_max_distance_tokens(enc):
     """A block equal to its predecessor: position 0 matches at distance exactly 32768."""
     text = D.gen_text(40000, 13).tobytes()
