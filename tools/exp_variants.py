@@ -22,6 +22,22 @@ VARIANTS = {
                    "                    else if (jj) dist = jj;")],
     "noperm_st": [("                    L.sorted[(pw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu] = (uint16_t)(dw[e >> 1] >> (16 * (e & 1)));",
                    "                    L.sorted[kk] = (uint16_t)(dw[e >> 1] >> (16 * (e & 1)));")],
+    # P0 rank by a wave-level multisplit: same-digit lane masks from 7 ballots,
+    # the rank by popcount, one LDS add per (wave, distinct digit), the base by ds_bpermute
+    "ms_rank": [("    if (!RUNCHK) return valid ? atomicAdd(&T[v], 1u) : 0u;",
+                 """    if (!RUNCHK) {
+        uint64_t eq = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 7; b++) {
+            const uint64_t bb = __ballot(valid && ((v >> b) & 1u));
+            eq &= ((v >> b) & 1u) ? bb : ~bb;
+        }
+        const uint32_t lead = eq ? (uint32_t)__builtin_ctzll(eq) : 0u;
+        uint32_t base = 0;
+        if (valid && (eq & lt) == 0) base = atomicAdd(&T[v], (uint32_t)__popcll(eq));
+        base = (uint32_t)__shfl((int)base, (int)lead);
+        return valid ? base + (uint32_t)__popcll(eq & lt) : 0u;
+    }""")],
     # K0 (C4 noise): the 4-gram bitmap's LDS atomics, knocked out and compacted
     "k0_nobm": [("                atomicOr(&bm[x >> 20], 1u << ((x >> 15) & 31));\n", "")],
     "k0_compact": [("""#pragma unroll
