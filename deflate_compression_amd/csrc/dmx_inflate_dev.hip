@@ -477,8 +477,8 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // ~100 instructions a token (the structurizer's branch flags, copies of the stream registers
 // that waited for their prefetch); this one spends ~20 on a literal and ~60 on a match.
 // In SGPRs: the 64-bit bit buffer (s[94:95]), bc, wi, op; the two tables come from HBM (the
-// workgroup's table area, agent-scope loads) into v96..v111 (literal/length) and v112..v127
-// (distance, bases in v128..v143) and are read by
+// workgroup's table area, agent-scope loads) into v64..v79 (literal/length) and v80..v95
+// (distance, bases in v96..v111) and are read by
 // v_readlane under s_set_gpr_idx_on.  A literal is one ds_write_b8 (every lane stores the same
 // byte); a match is 64 bytes a round (lane t: byte src + t, read before the round's writes,
 // when distance >= length or >= 64; byte src + t mod distance for a shorter period; a
@@ -506,16 +506,16 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 #else
 #define ICOPY_WAIT "s_waitcnt lgkmcnt(0)\n"
 #endif
-// table lookups: lane s94 & 63 of register v96 + (s94 >> 6 & 15) (v112 + for distances, their
-// bases at v128 +), read by v_readlane under the index mode: the mode indexes the readlane's
+// table lookups: lane s94 & 63 of register v64 + (s94 >> 6 & 15) (v80 + for distances, their
+// bases at v96 +), read by v_readlane under the index mode: the mode indexes the readlane's
 // VGPR source too (tools/gpridx_test.hip checks it on the device), so a lookup is s_bfe,
 // s_set_gpr_idx_on, v_readlane, s_set_gpr_idx_off -- no VGPR copy of the indexed register
-#define ILOOK_LL "s_set_gpr_idx_on s98, gpr_idx(SRC0)\n" "v_readlane_b32 s99, v96, s94\n" "s_set_gpr_idx_off\n"
-#define ILOOK_D "s_set_gpr_idx_on s98, gpr_idx(SRC0)\n" "v_readlane_b32 s99, v112, s94\n" \
-                "v_readlane_b32 s90, v128, s94\n" "s_set_gpr_idx_off\n"
+#define ILOOK_LL "s_set_gpr_idx_on s98, gpr_idx(SRC0)\n" "v_readlane_b32 s99, v64, s94\n" "s_set_gpr_idx_off\n"
+#define ILOOK_D "s_set_gpr_idx_on s98, gpr_idx(SRC0)\n" "v_readlane_b32 s99, v80, s94\n" \
+                "v_readlane_b32 s90, v96, s94\n" "s_set_gpr_idx_off\n"
 // A copy of one round (length <= 64) is left pending: its LDS read (or HBM load, for a source
 // older than the ring) is issued and the wave goes on decoding the next token while it is in
-// flight; the write (lanes in s[84:85], data v148 >> v150, address v149) is issued before
+// flight; the write (lanes in s[84:85], data v116 >> v118, address v117) is issued before
 // the next read of the ring, the next copy, or the return.  Literal stores in between touch
 // other positions.
 #define IFLUSH_PENDING(N) \
@@ -523,8 +523,8 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
     "s_cbranch_scc1 L_nf" #N "%=\n" \
     "s_waitcnt vmcnt(0) lgkmcnt(0)\n" \
     "s_mov_b64 exec, s[84:85]\n" \
-    "v_lshrrev_b32 v148, v150, v148\n" \
-    IWR " v149, v148\n" \
+    "v_lshrrev_b32 v116, v118, v116\n" \
+    IWR " v117, v116\n" \
     "s_mov_b64 exec, s[86:87]\n" \
     "s_mov_b64 s[84:85], 0\n" \
     "L_nf" #N "%=:\n"
