@@ -914,7 +914,7 @@ extern "C" int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_ibl
 //      names a byte of an EARLIER block.
 //   2. dmx_cells_prep_kernel: each reference becomes an absolute source position s; a source
 //      that is already a byte is copied at once, otherwise P[j] = s, the cell is marked
-//      unresolved (0xFFFF) and j goes on its block's list.  The lists are per block -- block
+//      unresolved (0xFFFF) and j goes on its block's list (as a 16-bit offset in the block).  The lists are per block -- block
 //      b's entries sit in [out_off, out_off + count) of a list buffer, so a workgroup appends
 //      with one LDS atomic per wave and no global atomic at all.
 //      dmx_cells_jump_kernel, about log2(nblk) + 2 launches of one workgroup per block, each
@@ -933,7 +933,7 @@ extern "C" int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_ibl
 #endif
 
 // Appends v at list[*lds_cnt ...] for every lane with want set; the whole wave calls it.
-__device__ inline void chain_push(bool want, uint32_t v, uint32_t* __restrict__ list, uint32_t* lds_cnt) {
+__device__ inline void chain_push(bool want, uint32_t v, uint16_t* __restrict__ list, uint32_t* lds_cnt) {
     const uint64_t m = __ballot(want);
     if (!m) return;
     const int lead = __ffsll((unsigned long long)m) - 1;
@@ -941,17 +941,17 @@ __device__ inline void chain_push(bool want, uint32_t v, uint32_t* __restrict__ 
     uint32_t base = 0;
     if ((int)lane == lead) base = atomicAdd(lds_cnt, (uint32_t)__popcll(m));
     base = __shfl(base, lead);
-    if (want) list[base + __popcll(m & ((1ull << lane) - 1))] = v;
+    if (want) list[base + __popcll(m & ((1ull << lane) - 1))] = (uint16_t)v;
 }
 
 __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_prep_kernel(const dmx_iblock* __restrict__ index, uint16_t* cells,
-                                                            uint32_t* P, uint32_t* __restrict__ list,
+                                                            uint32_t* P, uint16_t* __restrict__ list,
                                                             uint32_t* __restrict__ count, uint32_t* __restrict__ total,
                                                             uint64_t cap, dmx_inflate_status* __restrict__ st) {
     __shared__ uint32_t nl;
     const uint64_t off = index[blockIdx.x].out_off;
     const uint32_t len = index[blockIdx.x].out_len;
-    if (off > cap || len > cap - off) {   // the decode already failed this index; read nothing
+    if (off > cap || len > cap - off || len > IW) {   // the decode already failed this index; read nothing
         if (threadIdx.x == 0) {
             count[blockIdx.x] = 0;
             atomicCAS(&st->status, 0, -(int32_t)E_RANGE);
@@ -984,7 +984,7 @@ __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_prep_kernel(const dmx_iblo
                 }
             }
         }
-        chain_push(want, (uint32_t)(off + j), list + off, &nl);
+        chain_push(want, j, list + off, &nl);   // block-relative: 2 bytes an entry
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -995,8 +995,8 @@ __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_prep_kernel(const dmx_iblo
 }
 
 __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_jump_kernel(const dmx_iblock* __restrict__ index, uint16_t* cells,
-                                                                 uint32_t* P, const uint32_t* __restrict__ lin,
-                                                                 uint32_t* __restrict__ lout, const uint32_t* __restrict__ cin,
+                                                                 uint32_t* P, const uint16_t* __restrict__ lin,
+                                                                 uint16_t* __restrict__ lout, const uint32_t* __restrict__ cin,
                                                                  uint32_t* __restrict__ cout, uint32_t* __restrict__ total) {
     __shared__ uint32_t nl;
     const uint32_t cnt = cin[blockIdx.x];
@@ -1016,7 +1016,7 @@ __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_jump_kernel(const dmx_iblo
         for (int k = 0; k < CHAIN_ILP; k++) {
             const uint32_t u = u0 + k * CHAIN_WG + threadIdx.x;
             act[k] = u < cnt;
-            j[k] = act[k] ? lin[off + u] : 0;
+            j[k] = act[k] ? (uint32_t)(off + lin[off + u]) : 0;
         }
 #pragma unroll
         for (int k = 0; k < CHAIN_ILP; k++) {
@@ -1039,7 +1039,7 @@ __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_jump_kernel(const dmx_iblo
             }
         }
 #pragma unroll
-        for (int k = 0; k < CHAIN_ILP; k++) chain_push(want[k], j[k], lout + off, &nl);
+        for (int k = 0; k < CHAIN_ILP; k++) chain_push(want[k], (uint32_t)(j[k] - off), lout + off, &nl);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1079,7 +1079,7 @@ __global__ __launch_bounds__(256) void dmx_cells_final_kernel(const uint16_t* __
 static inline uint64_t chain_a256(uint64_t x) { return (x + 255) & ~255ull; }
 
 extern "C" uint64_t dmx_inflate_chained_work(uint64_t out_cap, uint32_t nblk) {
-    return 256 + chain_a256(8ull * nblk) + 4ull * ITAB_WORDS * nblk + chain_a256(2 * out_cap) + 12 * out_cap;
+    return 256 + chain_a256(8ull * nblk) + 4ull * ITAB_WORDS * nblk + chain_a256(2 * out_cap) + 8 * out_cap;
 }
 
 // The reference lists' total lengths of the last chained decode on this work buffer: [0] after
@@ -1104,7 +1104,7 @@ extern "C" int dmx_inflate_chained_async(const void* d_z, uint64_t zbytes, const
     uint32_t* gtab = (uint32_t*)((uint8_t*)d_work + 256 + chain_a256(8ull * nblk));
     uint16_t* cells = (uint16_t*)(gtab + (uint64_t)ITAB_WORDS * nblk);
     uint32_t* P = (uint32_t*)((uint8_t*)cells + chain_a256(2 * out_cap));
-    uint32_t* L[2] = {P + out_cap, P + 2 * out_cap};
+    uint16_t* L[2] = {(uint16_t*)(P + out_cap), (uint16_t*)(P + out_cap) + out_cap};
     if (hipMemsetAsync(d_status, 0, sizeof(dmx_inflate_status), s) != hipSuccess) return -(int)E_DEVICE;
     if (hipMemsetAsync(T, 0, 256, s) != hipSuccess) return -(int)E_DEVICE;
     hipLaunchKernelGGL(dmx_inflate_index_kernel<true>, dim3(nblk), dim3(64), 0, s, (const uint8_t*)d_z, zbytes, d_index,

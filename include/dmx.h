@@ -261,7 +261,7 @@ int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_iblock* d_inde
  * starts).  Each block decodes into 16-bit cells -- a byte, or a reference to a position
  * before the block -- and pointer jumping over the references, about log2(nblk) + 2 short
  * launches, resolves them; then the cells become bytes in d_out.  d_work: device scratch of
- * dmx_inflate_chained_work(out_cap, nblk) bytes (about 14 per output byte), 256-byte aligned.  Status in d_status (out_len =
+ * dmx_inflate_chained_work(out_cap, nblk) bytes (about 10 per output byte), 256-byte aligned.  Status in d_status (out_len =
  * bytes decoded; a reference before the output start is -E_HUFDIS).  Returns 0 or -E_*. */
 uint64_t dmx_inflate_chained_work(uint64_t out_cap, uint32_t nblk);
 int dmx_inflate_chained_async(const void* d_z, uint64_t zbytes, const dmx_iblock* d_index, uint32_t nblk, void* d_out,
