@@ -199,6 +199,9 @@ __device__ __forceinline__ uint32_t adv_of(const MatchLDS& L, uint32_t p) {
 #endif
 #define CB 12   // bytes compared in registers per candidate step; longer matches extend from LDS
 #define KE 8    // chains up to KE candidates use chunks with the halo embedded (64-K owned entries)
+#ifndef XU
+#define XU 4    // exhaustive later windows: filter steps whose LDS reads are in flight together
+#endif
 #define JR 8    // Jacobi rounds of the walk before the serial fallback
 #define WALK_SERIAL 1024   // fallback: at most this many tokens (approximate path) -> one-lane token walk
 #define TPMAX (DMX_NBUCKET)   // token positions listed in bstart (u16) for the token-major compaction
@@ -730,10 +733,19 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
     // LDS (resolve_full).  Later windows of KD = 32 candidates: the byte-at-best filter below.
     // A lane needs more windows while its chain goes on and its best is short of
     // min(258, bn - i); the wave stops when no lane does.
+    {
+    // H4: the seeds (HBM) of the wave's next chunk are loaded one chunk ahead
+    uint32_t snext = 0;
+    if (H4 && (wave << 6) + lane < nvalid) snext = seeds[L.sorted[(wave << 6) + lane]];
     for (uint32_t k0 = wave << 6; k0 < nvalid; k0 += MT) {
         const uint32_t k = k0 + lane;
         const bool act = k < nvalid;
         uint32_t i = 0, nc = 0, lim = 0;
+        uint32_t seed = 0;
+        if (H4) {
+            seed = snext;
+            if (k + MT < nvalid) snext = seeds[L.sorted[k + MT]];
+        }
         uint64_t iv0 = 0;
         uint32_t i2 = 0;
         if (act) {
@@ -750,7 +762,7 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
         const uint32_t lim_eff = act ? lim : 0;
         const uint8_t* D8 = reinterpret_cast<const uint8_t*>(L.data);
         uint32_t bestkey = 0;
-        if (H4 && act) bestkey = seeds[i];   // the best match shorter than NB (P0', in HBM)
+        if (H4 && act) bestkey = seed;   // the best match shorter than NB (P0', in HBM)
         constexpr uint32_t W0X = H4 ? DMX_W0H4 : W0;
         for (uint32_t jb = 0, wl = K <= KD ? KD : W0X;; jb += wl, wl = KD) {   // (bounded K <= KD: all in registers)
             // lanes that still need candidates jb + 1 ...: wave-uniform window length (window
@@ -817,15 +829,22 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
                 const uint32_t omsk = live ? msk : 0u;   // lanes without work never survive
                 uint32_t xp = (uint32_t)L.sorted[k - min(jb, k)];          // lane l: entry k - jb
                 uint32_t surv = 0;
-                if (guard) {
-                    for (uint32_t j = 1; j <= jmax; j++) {
-                        xp = wshr(xp, __builtin_amdgcn_readlane(hq, (int)j - 1));
-                        surv |= ((ld4(L.data, xp + s0) & omsk) == ob && j <= ncw) ? 1u << (j - 1) : 0u;
+                // XU steps at a time: the positions by XU wave shifts, then all their LDS reads
+                // in flight before the compares (one step at a time waited on every read)
+                const uint32_t jlim = guard ? 0u : 0xFFFFFFFFu;   // guard: j <= ncw
+                for (uint32_t j = 1; j <= jmax; j += XU) {
+                    uint32_t xs[XU], v[XU];
+#pragma unroll
+                    for (uint32_t u = 0; u < XU; u++) {
+                        xp = wshr(xp, __builtin_amdgcn_readlane(hq, (int)min(j + u - 1, (uint32_t)KD - 1)));
+                        xs[u] = xp + s0;
                     }
-                } else {
-                    for (uint32_t j = 1; j <= jmax; j++) {
-                        xp = wshr(xp, __builtin_amdgcn_readlane(hq, (int)j - 1));
-                        surv |= ((ld4(L.data, xp + s0) & omsk) == ob) ? 1u << (j - 1) : 0u;
+#pragma unroll
+                    for (uint32_t u = 0; u < XU; u++) v[u] = ld4(L.data, xs[u]);
+#pragma unroll
+                    for (uint32_t u = 0; u < XU; u++) {
+                        const uint32_t jj = j + u;
+                        surv |= ((v[u] & omsk) == ob && jj <= jmax && jj <= max(ncw, jlim)) ? 1u << (jj - 1) : 0u;
                     }
                 }
                 const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
@@ -843,6 +862,7 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
             }
         }
         if (act) store_result<DICT>(L, pg, k, i, bestkey, hbk);
+    }
     }
     // the last two positions have no trigram: literals
     if (tid < 2 && bn >= 1 + tid) {

@@ -7,7 +7,7 @@ and on the GPU box:
 import os, subprocess, sys, json
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(R, "deflate_compression_amd", "csrc")
-OUT = os.path.join(R, "build", "exp")
+OUT = os.path.join(R, "build", os.environ.get("DMX_EXP_DIR", "exp"))
 
 VARIANTS = {
     "base": [],
@@ -70,6 +70,13 @@ VARIANTS = {
             atomicOr(&bm[x >> 20], 1u << ((x >> 15) & 31));
         }
 """)],
+    # exhaustive later windows: filter steps with their LDS reads in flight together
+    "xu1": [("#define XU 4 ", "#define XU 1 ")],
+    "xu2": [("#define XU 4 ", "#define XU 2 ")],
+    "xu8": [("#define XU 4 ", "#define XU 8 ")],
+    "noseed": [("        if (H4 && act) bestkey = seed;   // the best", "        if (H4 && act) bestkey = 0 * seed;   // the best")],
+    "now1": [("            if (jmax == 0) break;\n            iters += jmax;", "            if (jmax == 0 || jb) break;\n            iters += jmax;")],
+    "nold": [("for (uint32_t u = 0; u < XU; u++) v[u] = ld4(L.data, xs[u]);", "for (uint32_t u = 0; u < XU; u++) v[u] = xs[u];")],
     "k0_nohist": [("            if (((uint32_t)j & smask) == 0 && p + j < bn) atomicAdd(&hist[(lo >> (8 * (j & 3))) & 0xFFu], 1u);\n", "")],
 }
 
@@ -131,14 +138,18 @@ def one(name):
     D.LIB_PATH = os.path.join(OUT, f"libdmx_{name}.so")
     n = 20_000_000
     t = torch.from_numpy(D.gen_text(n, 0xE5818)).cuda()
-    e = D.Encoder(0, n, max_chain=int(os.environ.get("EXP_K", "6")), flags=D.DMX_ZLIB | D.DMX_F_LAZY)
+    lazy = D.DMX_F_LAZY if os.environ.get("EXP_LAZY", "1") == "1" else 0
+    e = D.Encoder(0, n, max_chain=int(os.environ.get("EXP_K", "6")), flags=D.DMX_ZLIB | lazy)
     for _ in range(2):
         out, r = e.compress_tensor(t)
     st = e.stamps(r.nblocks).astype(np.float64)
     e.close()
-    print(json.dumps({"w1": round(st[:, 5].mean() / 1e3, 1), "walk": round(st[:, 2].mean() / 1e3, 1), "p0": round(st[:, 0].mean() / 1e3, 1), "pass1_end": round(st[:, 9].mean() / 1e3, 1),
+    import hashlib
+    sha = hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()[:16]
+    print(json.dumps({"sha": sha, "w1": round(st[:, 5].mean() / 1e3, 1), "walk": round(st[:, 2].mean() / 1e3, 1), "p0": round(st[:, 0].mean() / 1e3, 1), "pass1_end": round(st[:, 9].mean() / 1e3, 1),
                       "pass2_end": round(st[:, 10].mean() / 1e3, 1), "search": round(st[:, 1].mean() / 1e3, 1),
-                      "total": round(st[:, 7].mean() / 1e3, 1)}))
+                      "deferred": round(st[:, 3].mean() / 1e3, 1), "iters": round(st[:, 4].mean() / 16, 1),
+                      "h4_sort_end": round((st[:, 15] % 2**48).mean() / 1e3, 1), "total": round(st[:, 7].mean() / 1e3, 1)}))
 
 if __name__ == "__main__":
     if sys.argv[1] == "one_k0":
