@@ -74,6 +74,9 @@ VARIANTS = {
     "xu1": [("#define XU 4 ", "#define XU 1 ")],
     "xu2": [("#define XU 4 ", "#define XU 2 ")],
     "xu8": [("#define XU 4 ", "#define XU 8 ")],
+    "w0h4_4": [("#define DMX_W0H4 8 ", "#define DMX_W0H4 4 ")],
+    "w0h4_12": [("#define DMX_W0H4 8 ", "#define DMX_W0H4 12 ")],
+    "w0h4_16": [("#define DMX_W0H4 8 ", "#define DMX_W0H4 16 ")],
     "noseed": [("        if (H4 && act) bestkey = seed;   // the best", "        if (H4 && act) bestkey = 0 * seed;   // the best")],
     "now1": [("            if (jmax == 0) break;\n            iters += jmax;", "            if (jmax == 0 || jb) break;\n            iters += jmax;")],
     "nold": [("for (uint32_t u = 0; u < XU; u++) v[u] = ld4(L.data, xs[u]);", "for (uint32_t u = 0; u < XU; u++) v[u] = xs[u];")],
