@@ -2650,14 +2650,20 @@ struct HuffRes {
     uint64_t body, cost;
 };
 
+// The code-length alphabet of a block whose lit/len and distance lengths and HLIT / HDIST
+// are in S: the run-length coding of the lengths, its Huffman lengths, HCLEN.  One wave.
+__device__ void huff_cl(K2LDS& S, uint32_t lane) {
+    rle_lengths(S, lane);
+    huff_lengths<1>(S, S.fcl, 19, 7, S.lcl, lane);
+    const uint64_t nzc = __ballot(lane < 19 && S.lcl[c_clorder[lane < 19 ? lane : 0]] != 0);
+    if (lane == 0) S.hclen = nzc ? max(4, 64 - (int)__builtin_clzll(nzc)) : 4;
+    wsync();
+}
+
 // Plan one DEFLATE block from the frequencies in S.fll / S.fd (EOB included): code
 // lengths, exact stored / fixed / dynamic costs, the type (the cheapest; stored only if
-// allow_stored), canonical codes into codes_out (global) and the header bits (BFINAL/BTYPE + trees)
-// in S.hdr.  One wave.
-__device__ HuffRes huff_block(K2LDS& S, uint32_t bn, uint32_t final_bit, bool allow_stored, uint32_t lane,
-                              uint32_t* __restrict__ codes_out) {
-    for (int k = (int)lane; k < DMX_HDR_WORDS; k += 64) S.hdr[k] = 0;
-    wsync();
+// allow_stored) and the header's bit count.  S keeps the lengths for huff_emit.  One wave.
+__device__ HuffRes huff_plan(K2LDS& S, uint32_t bn, bool allow_stored, uint32_t lane) {
     // lit/len and distance code lengths
     huff_lengths<5>(S, S.fll, 286, 15, S.lll, lane);
     huff_lengths<1>(S, S.fd, 30, 15, S.ld, lane);
@@ -2679,13 +2685,7 @@ __device__ HuffRes huff_block(K2LDS& S, uint32_t bn, uint32_t final_bit, bool al
         }
         wsync();
     }
-    rle_lengths(S, lane);
-    huff_lengths<1>(S, S.fcl, 19, 7, S.lcl, lane);
-    {
-        const uint64_t nzc = __ballot(lane < 19 && S.lcl[c_clorder[lane < 19 ? lane : 0]] != 0);
-        if (lane == 0) S.hclen = nzc ? max(4, 64 - (int)__builtin_clzll(nzc)) : 4;
-        wsync();
-    }
+    huff_cl(S, lane);
 
     // exact costs
     uint64_t dyn_body = 0, fix_body = 0, extra = 0;
@@ -2715,7 +2715,20 @@ __device__ HuffRes huff_block(K2LDS& S, uint32_t bn, uint32_t final_bit, bool al
     uint64_t best = dyn_bits;
     if (fix_bits <= best) { best = fix_bits; bt = 1; }
     if (allow_stored && sto_bits < best) { best = sto_bits; bt = 0; }
+    HuffRes h;
+    h.bt = bt;
+    h.hbits = bt == 2 ? (uint32_t)dyn_hdr : 3u;   // = the header items huff_emit places
+    h.body = (bt == 2 ? dyn_body : fix_body) + extra;
+    h.cost = best;
+    return h;
+}
 
+// The planned block's canonical codes into codes_out (global; fixed codes for BTYPE 1) and its
+// header bits (BFINAL/BTYPE + trees) into S.hdr; returns their count.  S holds huff_plan's
+// (or huff_cl's) state.  One wave.
+__device__ uint32_t huff_emit(K2LDS& S, uint32_t final_bit, uint32_t bt, uint32_t lane, uint32_t* __restrict__ codes_out) {
+    for (int k = (int)lane; k < DMX_HDR_WORDS; k += 64) S.hdr[k] = 0;
+    wsync();
     // code table for the packer (fixed codes for BTYPE 1)
     if (bt == 1) {
         for (int s = (int)lane; s < 288; s += 64) S.lll[s] = (uint8_t)fixed_len((uint32_t)s);
@@ -2762,11 +2775,13 @@ __device__ HuffRes huff_block(K2LDS& S, uint32_t bn, uint32_t final_bit, bool al
         }
     }
     wsync();
-    HuffRes h;
-    h.bt = bt;
-    h.hbits = carry;
-    h.body = (bt == 2 ? dyn_body : fix_body) + extra;
-    h.cost = best;
+    return carry;
+}
+
+__device__ HuffRes huff_block(K2LDS& S, uint32_t bn, uint32_t final_bit, bool allow_stored, uint32_t lane,
+                              uint32_t* __restrict__ codes_out) {
+    HuffRes h = huff_plan(S, bn, allow_stored, lane);
+    h.hbits = huff_emit(S, final_bit, h.bt, lane, codes_out);
     return h;
 }
 
@@ -2821,15 +2836,14 @@ __constant__ uint8_t c_gi[SPW] = {0, 1, 2, 3, 0, 1, 2, 0, 1, 0};
 __constant__ uint8_t c_gj[SPW] = {0, 1, 2, 3, 1, 2, 3, 2, 3, 3};
 
 struct SplitGroup {
-    uint32_t bt, hbits, empty, pad;
+    uint32_t bt, hbits, empty, hl;   // hl: HLIT | HDIST << 16
     uint64_t body, cost;
 };
 struct SplitScratch {   // per block, in HBM (dmx_ctx.split)
     uint32_t qh[4][DMX_HIST];
     uint32_t qt[8];
     SplitGroup g[SPW];
-    uint32_t code[SPW][DMX_HIST];
-    uint32_t hdr[SPW][DMX_HDR_WORDS];
+    uint8_t lens[SPW][320];   // lit/len lengths 0..287, distance lengths 288..319 (huff_plan's)
 };
 
 __device__ __forceinline__ uint32_t grp_of(uint32_t i, uint32_t j) {   // inverse of c_gi / c_gj
@@ -2910,7 +2924,6 @@ __global__ __launch_bounds__(64) void dmx_split_plan_kernel(SplitScratch* __rest
     if (info[b].prestored & 1u) return;
     const uint32_t bn = info[b].n;
     const uint32_t i = c_gi[g], j = c_gj[g];
-    const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1 && j == 3) ? 1u : 0u;
     for (int s = (int)lane; s < 288; s += 64) {
         uint32_t f = 0;
         if (s == 256) f = 1;   // end of block
@@ -2925,14 +2938,17 @@ __global__ __launch_bounds__(64) void dmx_split_plan_kernel(SplitScratch* __rest
         S.fd[s] = f;
     }
     wsync();
-    const HuffRes h = huff_block(S, bn, final_bit, g == SPW - 1, lane, o.code[g]);
-    for (uint32_t k = lane; k < (h.hbits + 31) / 32; k += 64) o.hdr[g][k] = S.hdr[k];
+    // costs only: the codes and header of the (few) chosen groups are built by the choose kernel
+    const HuffRes h = huff_plan(S, bn, g == SPW - 1, lane);
+    for (uint32_t k = lane; k < 80; k += 64)
+        reinterpret_cast<uint32_t*>(o.lens[g])[k] = k < 72 ? reinterpret_cast<const uint32_t*>(S.lll)[k]
+                                                           : reinterpret_cast<const uint32_t*>(S.ld)[k - 72];
     if (lane == 0) {
         SplitGroup r;
         r.bt = h.bt;
         r.hbits = h.hbits;
         r.empty = o.qt[j + 1] == o.qt[i];
-        r.pad = 0;
+        r.hl = (uint32_t)S.hlit | ((uint32_t)S.hdist << 16);
         r.body = h.body;
         r.cost = h.cost;
         o.g[g] = r;
@@ -2943,8 +2959,10 @@ __global__ __launch_bounds__(64) void dmx_split_choose_kernel(const SplitScratch
                                                               dmx_blkinfo* __restrict__ info,
                                                               uint32_t* __restrict__ codes_g,
                                                               uint32_t* __restrict__ hdr_g,
-                                                              dmx_subinfo* __restrict__ sub_g) {
+                                                              dmx_subinfo* __restrict__ sub_g, uint32_t nblk,
+                                                              uint32_t flags) {
     __shared__ uint32_t sg[DMX_NSUB], nsub_s;
+    __shared__ K2LDS S;
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x;
     const SplitScratch& o = sp[b];
@@ -2992,10 +3010,22 @@ __global__ __launch_bounds__(64) void dmx_split_choose_kernel(const SplitScratch
     for (uint32_t s = 0; s < nsub; s++) {
         const uint32_t g = sg[s];
         const uint64_t slot = (uint64_t)b * DMX_NSUB + s;
-        uint32_t* cg = codes_g + slot * DMX_HIST;
-        for (int k = (int)lane; k < 316; k += 64) cg[k] = o.code[g][k];
+        // the group's codes and header from its planned lengths (as huff_block would emit them)
+        for (uint32_t k = lane; k < 80; k += 64) {
+            const uint32_t w = reinterpret_cast<const uint32_t*>(o.lens[g])[k];
+            if (k < 72) reinterpret_cast<uint32_t*>(S.lll)[k] = w;
+            else reinterpret_cast<uint32_t*>(S.ld)[k - 72] = w;
+        }
+        if (lane == 0) {
+            S.hlit = (int32_t)(o.g[g].hl & 0xFFFFu);
+            S.hdist = (int32_t)(o.g[g].hl >> 16);
+        }
+        wsync();
+        if (o.g[g].bt == 2) huff_cl(S, lane);
+        const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1 && c_gj[g] == 3) ? 1u : 0u;
+        const uint32_t hbits = huff_emit(S, final_bit, o.g[g].bt, lane, codes_g + slot * DMX_HIST);
         uint32_t* hg = hdr_g + slot * DMX_HDR_WORDS;
-        for (uint32_t k = lane; k < (o.g[g].hbits + 31) / 32; k += 64) hg[k] = o.hdr[g][k];
+        for (uint32_t k = lane; k < (hbits + 31) / 32; k += 64) hg[k] = S.hdr[k];
         if (lane == 0) {
             dmx_subinfo si;
             si.t0 = o.qt[c_gi[g]];
@@ -3848,7 +3878,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                 hipLaunchKernelGGL(dmx_split_plan_kernel, dim3(nblk * SPW), dim3(64), 0, s, (SplitScratch*)c->split,
                                    c->info, nblk, o.flags);
                 hipLaunchKernelGGL(dmx_split_choose_kernel, dim3(nblk), dim3(64), 0, s, (const SplitScratch*)c->split,
-                                   c->info, c->codes, c->hdr, c->sub);
+                                   c->info, c->codes, c->hdr, c->sub, nblk, o.flags);
             }
         else
             hipLaunchKernelGGL(dmx_huff_kernel, dim3(nblk), dim3(64), 0, s, c->hist, c->info, c->codes, c->hdr, c->sub,
