@@ -2334,21 +2334,30 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
 // K2: Huffman codes + block type (one wave per block)
 // ------------------------------------------------------------------------------------
 
-struct K2LDS {
-    uint32_t fll[288];
-    uint32_t fd[32];
-    uint32_t fcl[20];
+struct K2LDS {   // 16-bit weights (a block has at most 32 769 symbols): 5.6 KB, 28 one-wave workgroups per CU
+    uint16_t fll[288];
+    uint16_t fd[32];
+    uint32_t fcl[20];     // (LDS atomics: 32-bit)
     uint8_t lll[288];
     uint8_t ld[32];
     uint8_t lcl[20];
     // Huffman construction (one alphabet at a time)
-    uint32_t fs[320];     // used symbols' weights sorted by (weight, symbol)
-    uint16_t sym[320];    //   and their symbols
-    uint32_t nodew[320];  // internal node weights, in creation order
-    uint16_t lpar[320];   // sorted leaf -> parent node
-    uint16_t up[320];     // node -> ancestor (pointer jumping)
-    uint16_t dd[320];     // node -> distance to that ancestor (-> depth)
-    int32_t blc[64];      // leaves per code length
+    // (at most 286 used symbols, 285 internal nodes)
+    uint16_t fs[288];     // used symbols' weights sorted by (weight, symbol)
+    uint16_t sym[288];    //   and their symbols
+    union {
+        uint16_t nodew[288];            // internal node weights, in creation order (huff_lengths)
+        uint32_t hdr[DMX_HDR_WORDS];    // the header bits (huff_emit, after every huff_lengths)
+    };
+    uint16_t lpar[288];   // sorted leaf -> parent node
+    union {
+        uint32_t keys[288];   // the used symbols' sort keys (weight << 9 | symbol), before the merge
+        struct {
+            uint16_t up[288];     // node -> ancestor (pointer jumping)
+            uint16_t dd[288];     // node -> distance to that ancestor (-> depth)
+        };
+    };
+    int32_t blc[32];      // leaves per code length (a depth > 31 needs a total weight > 32 769)
     int32_t lstart[16];   // first sorted index that gets length d
     int32_t cnt[16];      // canonical codes: codes handed out per length so far
     uint32_t next[16];    // canonical codes: first code of each length
@@ -2356,7 +2365,6 @@ struct K2LDS {
     // run-length coding of the code lengths (RFC 1951 §3.2.7)
     uint8_t rle_sym[320];
     uint8_t rle_ext[320];
-    uint32_t hdr[DMX_HDR_WORDS];
     int32_t rle_n, hlit, hdist, hclen;
 };
 
@@ -2380,8 +2388,8 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v) { return wave_inc
 // lengths to the least frequent symbols.  One wave; NR = symbol registers (64 each).
 // Sorting, depths and the length assignment are lane-parallel; only the merge is serial
 // (lane 0, one LDS round trip per node: both heads of both queues are read together).
-template <int NR>
-__device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, uint8_t* len, uint32_t lane) {
+template <int NR, typename F>
+__device__ void huff_lengths(K2LDS& S, const F* f, int n, int maxbits, uint8_t* len, uint32_t lane) {
     uint32_t key[NR];
     uint32_t m = 0;
 #pragma unroll
@@ -2405,8 +2413,8 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
         wsync();
         return;
     }
-    // rank among the used symbols: the used keys are compacted first (S.nodew is free until
-    // canon_codes), so the broadcast loop runs over the m used keys only, not all n slots
+    // rank among the used symbols: the used keys are compacted first (into S.keys, free until
+    // the merge), so the broadcast loop runs over the m used keys only, not all n slots
     const uint32_t nru = (m + 63) >> 6;   // registers holding used keys
     {
         uint32_t base = 0;
@@ -2414,7 +2422,7 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
         for (int r = 0; r < NR; r++) {
             const bool u = key[r] != 0xFFFFFFFFu;
             const uint64_t um = __ballot(u);
-            if (u) S.nodew[base + (uint32_t)__popcll(um & ((1ull << lane) - 1ull))] = key[r];
+            if (u) S.keys[base + (uint32_t)__popcll(um & ((1ull << lane) - 1ull))] = key[r];
             base += (uint32_t)__popcll(um);
         }
     }
@@ -2423,7 +2431,7 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
 #pragma unroll
     for (int r = 0; r < NR; r++) {
         const uint32_t i = (uint32_t)r * 64 + lane;
-        ck[r] = i < m ? S.nodew[i] : 0xFFFFFFFFu;
+        ck[r] = i < m ? S.keys[i] : 0xFFFFFFFFu;
         rk[r] = 0;
     }
 #pragma unroll
@@ -2440,10 +2448,10 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
 #pragma unroll
     for (int r = 0; r < NR; r++)
         if (ck[r] != 0xFFFFFFFFu) {
-            S.fs[rk[r]] = ck[r] >> 9;
+            S.fs[rk[r]] = (uint16_t)(ck[r] >> 9);
             S.sym[rk[r]] = (uint16_t)(ck[r] & 511u);
         }
-    for (int k = (int)lane; k < 64; k += 64) S.blc[k] = 0;
+    if (lane < 32) S.blc[lane] = 0;
     wsync();
     const int mm = (int)m, nn = mm - 1, root = nn - 1;
     if (lane == 0) {   // two-queue merge
@@ -2457,7 +2465,7 @@ __device__ void huff_lengths(K2LDS& S, const uint32_t* f, int n, int maxbits, ui
             else { w = b0; S.up[ni++] = (uint16_t)k; A = a0; B = b1; }
             if (li < mm && A <= B) { w += A; S.lpar[li++] = (uint16_t)k; }
             else { w += B; S.up[ni++] = (uint16_t)k; }
-            S.nodew[k] = w;
+            S.nodew[k] = (uint16_t)w;
         }
         S.up[root] = (uint16_t)root;
     }
