@@ -77,6 +77,10 @@ VARIANTS = {
     "w0h4_4": [("#define DMX_W0H4 8 ", "#define DMX_W0H4 4 ")],
     "w0h4_12": [("#define DMX_W0H4 8 ", "#define DMX_W0H4 12 ")],
     "w0h4_16": [("#define DMX_W0H4 8 ", "#define DMX_W0H4 16 ")],
+    # P1 (K <= 8) knockouts: the sort check, the result stores, the queued extension
+    "p1_nochk": [("                    if (__ballot(act && ei >= 1 && pk > sk)) L.sortbad = 1;", "")],
+    "p1_nostore": [("                store_short<DICT>(L, k, i, m >= 3 ? m : 0u, m >= 3 ? 8u - (jkey & 7u) : 0u, hbk);", "                if (m == 0x1234u) L.len8[i] = 1;")],
+    "p1_noq": [("                ext_queue<DICT, RUNS>(L, bn, K, Qw, qn, lane, hbk);", "")],
     "noseed": [("        if (H4 && act) bestkey = seed;   // the best", "        if (H4 && act) bestkey = 0 * seed;   // the best")],
     "now1": [("            if (jmax == 0) break;\n            iters += jmax;", "            if (jmax == 0 || jb) break;\n            iters += jmax;")],
     "nold": [("for (uint32_t u = 0; u < XU; u++) v[u] = ld4(L.data, xs[u]);", "for (uint32_t u = 0; u < XU; u++) v[u] = xs[u];")],
