@@ -173,6 +173,14 @@ __device__ __forceinline__ uint32_t ld4(const uint32_t* W, uint32_t p) {   // by
 }
 template <int NB>
 __device__ __forceinline__ uint64_t ldg(const uint32_t* W, uint32_t p) { return NB > 4 ? ld8(W, p) : (uint64_t)ld4(W, p); }
+// bytes p..p+11 from four aligned dwords (two ds_read2_b32; ld8 + ld4 issued a fifth read)
+__device__ __forceinline__ void ld12(const uint32_t* W, uint32_t p, uint32_t& x0, uint32_t& x1, uint32_t& x2) {
+    const uint32_t a = p >> 2, sh = p & 3;
+    const uint32_t w0 = W[a], w1 = W[a + 1], w2 = W[a + 2], w3 = W[a + 3];
+    x0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    x2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+}
 
 __device__ __forceinline__ uint32_t adv_of(const MatchLDS& L, uint32_t p) {
     return ((L.lit[p >> 5] >> (p & 31)) & 1u) ? 1u : (uint32_t)L.len8[p] + 3u;
@@ -750,8 +758,9 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
         uint32_t i2 = 0;
         if (act) {
             i = L.sorted[k];
-            iv0 = ld8(L.data, i);
-            i2 = ld4(L.data, i + 8);
+            uint32_t a0, a1;
+            ld12(L.data, i, a0, a1, i2);
+            iv0 = (uint64_t)a0 | ((uint64_t)a1 << 32);
             // bounded mode (K <= KD) needs no bucket rank: the K entries below k are examined
             // and those of other buckets never reach 3 equal bytes (cand_steps); only the
             // first K entries of the block lack K predecessors.  Longer chains need the rank.
@@ -783,8 +792,9 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
             if (lane < KD && k0 >= jb + lane + 1) {
                 hq = L.sorted[k0 - 1 - jb - lane];
                 if (jb == 0) {
-                    hv0 = ld8(L.data, hq);
-                    h2 = ld4(L.data, hq + 8);
+                    uint32_t a0, a1;
+                    ld12(L.data, hq, a0, a1, h2);
+                    hv0 = (uint64_t)a0 | ((uint64_t)a1 << 32);
                 }
             }
             // lanes without a candidate j of this window: halo lanes before the block start
@@ -1339,12 +1349,7 @@ __device__ __forceinline__ bool hist_group(const HistLDS& L, int32_t x, uint32_t
 #pragma unroll
     for (int g = 0; g < HG; g++) q[g] = (x - g >= 0 && (!ONE || (uint32_t)g < K)) ? (uint32_t)Sp[x - g] : 0u;
 #pragma unroll
-    for (int g = 0; g < HG; g++) {
-        const uint64_t v = ld8(L.data, q[g]);
-        s0[g] = (uint32_t)v;
-        s1[g] = (uint32_t)(v >> 32);
-        s2[g] = ld4(L.data, q[g] + 8);
-    }
+    for (int g = 0; g < HG; g++) ld12(L.data, q[g], s0[g], s1[g], s2[g]);
     uint32_t key = 0, full = 0;
     bool left = false;
 #pragma unroll
@@ -1458,8 +1463,8 @@ __global__ __launch_bounds__(MT) void dmx_hist_kernel_t(const uint8_t* __restric
         uint32_t best = 0, bq = 0, full = 0;
         int32_t x0 = -1;
         if (act) {
-            const uint64_t tv = ld8(L.cur, i);
-            const uint32_t t0 = (uint32_t)tv, t1 = (uint32_t)(tv >> 32), t2 = ld4(L.cur, i + 8);
+            uint32_t t0, t1, t2;
+            ld12(L.cur, i, t0, t1, t2);
             const uint32_t h = dmx_hash(t0 & 0xFFFFFFu);
             const uint32_t lim = min(bn - i, (uint32_t)MAXLEN);
             const int32_t minq = (int32_t)(hn + i) - 32768;   // distance <= 32768
