@@ -928,8 +928,11 @@ extern "C" int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_ibl
 // ------------------------------------------------------------------------------------
 #define CHAIN_ROUNDS_MAX 40
 #define CHAIN_WG 1024   // threads per block in prep and jump: a block's list is latency-bound
+#ifndef CHAIN_HOPS
+#define CHAIN_HOPS 2    // links followed per list entry and jump launch (1: 16.1, 2: 18.2 GB/s, `profiles/r03_d3`)
+#endif
 #ifndef CHAIN_ILP
-#define CHAIN_ILP 4     // list entries per jump thread in flight (2: 0.65 ms a full round, `profiles/r03_t`)
+#define CHAIN_ILP 2     // list entries per jump thread in flight (two links each: 2 beat 4, `profiles/r03_d3`)
 #endif
 
 // Appends v at list[*lds_cnt ...] for every lane with want set; the whole wave calls it.
@@ -1026,6 +1029,33 @@ __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_jump_kernel(const dmx_iblo
 #pragma unroll
         for (int k = 0; k < CHAIN_ILP; k++)
             cs[k] = act[k] ? cells[sp[k]] : 0;   // (plain loads: a stale copy is an older link of the chain)
+#if CHAIN_HOPS > 1
+        // a second link in the same launch: the unresolved source's own source, s2 = P[s]; a
+        // byte there resolves j now, otherwise j jumps to P[s2] (two links a launch)
+        uint32_t s2[CHAIN_ILP];
+#pragma unroll
+        for (int k = 0; k < CHAIN_ILP; k++) s2[k] = (act[k] && cs[k] == 0xFFFFu) ? P[sp[k]] : 0u;
+        uint16_t c2[CHAIN_ILP];
+#pragma unroll
+        for (int k = 0; k < CHAIN_ILP; k++) c2[k] = (act[k] && cs[k] == 0xFFFFu && s2[k] < sp[k]) ? cells[s2[k]] : 0xFFFFu;
+#pragma unroll
+        for (int k = 0; k < CHAIN_ILP; k++) {
+            want[k] = false;
+            if (act[k]) {
+                if (cs[k] != 0xFFFFu) {
+                    cells[j[k]] = cs[k];
+                } else if (s2[k] >= sp[k]) {   // (a malformed link: stays unresolved)
+                    P[j[k]] = s2[k];
+                    want[k] = true;
+                } else if (c2[k] != 0xFFFFu) {
+                    cells[j[k]] = c2[k];
+                } else {
+                    P[j[k]] = P[s2[k]];
+                    want[k] = true;
+                }
+            }
+        }
+#else
 #pragma unroll
         for (int k = 0; k < CHAIN_ILP; k++) {
             want[k] = false;
@@ -1038,6 +1068,7 @@ __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_jump_kernel(const dmx_iblo
                 }
             }
         }
+#endif
 #pragma unroll
         for (int k = 0; k < CHAIN_ILP; k++) chain_push(want[k], (uint32_t)(j[k] - off), lout + off, &nl);
     }
