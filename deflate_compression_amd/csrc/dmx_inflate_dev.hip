@@ -929,7 +929,7 @@ extern "C" int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_ibl
 #define CHAIN_ROUNDS_MAX 40
 #define CHAIN_WG 1024   // threads per block in prep and jump: a block's list is latency-bound
 #ifndef CHAIN_HOPS
-#define CHAIN_HOPS 2    // links followed per list entry and jump launch (1: 16.1, 2: 18.2 GB/s, `profiles/r03_d3`)
+#define CHAIN_HOPS 3    // links followed per list entry and jump launch (1: 16.1, 2: 18.1, 3: 18.4, 4: 18.2 GB/s, `profiles/r03_h`)
 #endif
 #ifndef CHAIN_ILP
 #define CHAIN_ILP 2     // list entries per jump thread in flight (two links each: 2 beat 4, `profiles/r03_d3`)
@@ -1030,27 +1030,33 @@ __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_jump_kernel(const dmx_iblo
         for (int k = 0; k < CHAIN_ILP; k++)
             cs[k] = act[k] ? cells[sp[k]] : 0;   // (plain loads: a stale copy is an older link of the chain)
 #if CHAIN_HOPS > 1
-        // a second link in the same launch: the unresolved source's own source, s2 = P[s]; a
-        // byte there resolves j now, otherwise j jumps to P[s2] (two links a launch)
-        uint32_t s2[CHAIN_ILP];
+        // more links in the same launch: while the source is unresolved, step to its own source
+        // (P[s] < s on a well-formed chain); a byte found resolves j now, otherwise j jumps to
+        // the last source's P (CHAIN_HOPS links a launch)
+        uint32_t cur[CHAIN_ILP];
+        bool ok[CHAIN_ILP];
 #pragma unroll
-        for (int k = 0; k < CHAIN_ILP; k++) s2[k] = (act[k] && cs[k] == 0xFFFFu) ? P[sp[k]] : 0u;
-        uint16_t c2[CHAIN_ILP];
+        for (int k = 0; k < CHAIN_ILP; k++) { cur[k] = sp[k]; ok[k] = true; }
 #pragma unroll
-        for (int k = 0; k < CHAIN_ILP; k++) c2[k] = (act[k] && cs[k] == 0xFFFFu && s2[k] < sp[k]) ? cells[s2[k]] : 0xFFFFu;
+        for (int h = 1; h < CHAIN_HOPS; h++) {
+            uint32_t nx[CHAIN_ILP];
+#pragma unroll
+            for (int k = 0; k < CHAIN_ILP; k++) {
+                nx[k] = (act[k] && ok[k] && cs[k] == 0xFFFFu) ? P[cur[k]] : 0u;
+                if (act[k] && ok[k] && cs[k] == 0xFFFFu && nx[k] >= cur[k]) ok[k] = false;   // (malformed: stays)
+            }
+#pragma unroll
+            for (int k = 0; k < CHAIN_ILP; k++)
+                if (act[k] && ok[k] && cs[k] == 0xFFFFu) { cs[k] = cells[nx[k]]; cur[k] = nx[k]; }
+        }
 #pragma unroll
         for (int k = 0; k < CHAIN_ILP; k++) {
             want[k] = false;
             if (act[k]) {
                 if (cs[k] != 0xFFFFu) {
                     cells[j[k]] = cs[k];
-                } else if (s2[k] >= sp[k]) {   // (a malformed link: stays unresolved)
-                    P[j[k]] = s2[k];
-                    want[k] = true;
-                } else if (c2[k] != 0xFFFFu) {
-                    cells[j[k]] = c2[k];
                 } else {
-                    P[j[k]] = P[s2[k]];
+                    P[j[k]] = ok[k] ? P[cur[k]] : cur[k];
                     want[k] = true;
                 }
             }
