@@ -919,7 +919,8 @@ extern "C" int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_ibl
 //      with one LDS atomic per wave and no global atomic at all.
 //      dmx_cells_jump_kernel, about log2(nblk) + 2 launches of one workgroup per block, each
 //      over the list the one before it left: an unresolved j looks at s = P[j]: a resolved
-//      cell is copied, otherwise P[j] = P[s] and j goes on the next list (pointer jumping:
+//      cell is copied; otherwise it follows up to CHAIN_HOPS - 1 more links s <- P[s] in the
+//      same launch, and if none reaches a byte, P[j] = P[s] and j goes on the next list (pointer jumping:
 //      chains of references through many blocks -- a run carried across every block, say --
 //      halve each launch).  In place: a stale read only delays resolution, never changes the
 //      value (P moves along the chain, a resolved cell stays).  A block whose list is empty
