@@ -2339,9 +2339,17 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
 // K2: Huffman codes + block type (one wave per block)
 // ------------------------------------------------------------------------------------
 
-struct K2LDS {   // 16-bit weights (a block has at most 32 769 symbols): 5.6 KB, 28 one-wave workgroups per CU
-    uint16_t fll[288];
-    uint16_t fd[32];
+struct K2LDS {   // 16-bit weights (a block has at most 32 769 symbols): 5.0 KB, 32 one-wave workgroups per CU
+    union {
+        struct {   // the frequencies (dead once huff_plan has the body costs)
+            uint16_t fll[288];
+            uint16_t fd[32];
+        };
+        struct {   // run-length coding of the code lengths (RFC 1951 §3.2.7), huff_cl onwards
+            uint8_t rle_sym[320];
+            uint8_t rle_ext[320];
+        };
+    };
     uint32_t fcl[20];     // (LDS atomics: 32-bit)
     uint8_t lll[288];
     uint8_t ld[32];
@@ -2367,9 +2375,6 @@ struct K2LDS {   // 16-bit weights (a block has at most 32 769 symbols): 5.6 KB,
     int32_t cnt[16];      // canonical codes: codes handed out per length so far
     uint32_t next[16];    // canonical codes: first code of each length
     uint32_t ccode[20];   // code-length codes, same packing
-    // run-length coding of the code lengths (RFC 1951 §3.2.7)
-    uint8_t rle_sym[320];
-    uint8_t rle_ext[320];
     int32_t rle_n, hlit, hdist, hclen;
 };
 
@@ -2698,9 +2703,8 @@ __device__ HuffRes huff_plan(K2LDS& S, uint32_t bn, bool allow_stored, uint32_t 
         }
         wsync();
     }
-    huff_cl(S, lane);
-
-    // exact costs
+    // exact costs: the bodies first -- the frequencies share their LDS with
+    // the run-length coding of the lengths (huff_cl)
     uint64_t dyn_body = 0, fix_body = 0, extra = 0;
     for (int s = (int)lane; s < 286; s += 64) {
         const uint64_t f = S.fll[s];
@@ -2714,6 +2718,8 @@ __device__ HuffRes huff_plan(K2LDS& S, uint32_t bn, bool allow_stored, uint32_t 
         fix_body += f * 5;
         extra += f * dist_eb_of_sym(lane);
     }
+    wsync();
+    huff_cl(S, lane);
     uint64_t hdr_rle = 0;
     for (int k = (int)lane; k < S.rle_n; k += 64) hdr_rle += S.lcl[S.rle_sym[k]] + c_cl_eb[S.rle_sym[k]];
     dyn_body = wave_sum_u64(dyn_body);
@@ -2798,7 +2804,7 @@ __device__ HuffRes huff_block(K2LDS& S, uint32_t bn, uint32_t final_bit, bool al
     return h;
 }
 
-__global__ __launch_bounds__(64) void dmx_huff_kernel(const uint32_t* __restrict__ hist_g, dmx_blkinfo* __restrict__ info,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void dmx_huff_kernel(const uint32_t* __restrict__ hist_g, dmx_blkinfo* __restrict__ info,
                                                       uint32_t* __restrict__ codes_g, uint32_t* __restrict__ hdr_g,
                                                       dmx_subinfo* __restrict__ sub_g, uint32_t nblk, uint32_t flags) {
     __shared__ K2LDS S;
@@ -2927,7 +2933,7 @@ __global__ __launch_bounds__(SHT) void dmx_split_hist_kernel(const uint32_t* __r
     if (tid < 5) o.qt[tid] = qt[tid];
 }
 
-__global__ __launch_bounds__(64) void dmx_split_plan_kernel(SplitScratch* __restrict__ sp,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void dmx_split_plan_kernel(SplitScratch* __restrict__ sp,
                                                             const dmx_blkinfo* __restrict__ info, uint32_t nblk,
                                                             uint32_t flags) {
     __shared__ K2LDS S;

@@ -81,6 +81,11 @@ VARIANTS = {
     "p1_nochk": [("                    if (__ballot(act && ei >= 1 && pk > sk)) L.sortbad = 1;", "")],
     "p1_nostore": [("                store_short<DICT>(L, k, i, m >= 3 ? m : 0u, m >= 3 ? 8u - (jkey & 7u) : 0u, hbk);", "                if (m == 0x1234u) L.len8[i] = 1;")],
     "p1_noq": [("                ext_queue<DICT, RUNS>(L, bn, K, Qw, qn, lane, hbk);", "")],
+    # Huffman plans without the 8-waves-per-SIMD request (7 per SIMD, no SGPR spills)
+    "huff7": [("__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void dmx_huff_kernel(",
+               "__global__ __launch_bounds__(64) void dmx_huff_kernel("),
+              ("__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void dmx_split_plan_kernel(",
+               "__global__ __launch_bounds__(64) void dmx_split_plan_kernel(")],
     "noseed": [("        if (H4 && act) bestkey = seed;   // the best", "        if (H4 && act) bestkey = 0 * seed;   // the best")],
     "now1": [("            if (jmax == 0) break;\n            iters += jmax;", "            if (jmax == 0 || jb) break;\n            iters += jmax;")],
     "nold": [("for (uint32_t u = 0; u < XU; u++) v[u] = ld4(L.data, xs[u]);", "for (uint32_t u = 0; u < XU; u++) v[u] = xs[u];")],
@@ -132,6 +137,31 @@ def one_k0(name):
     e.close()
     print(json.dumps({"stage_ms": st, "bytes": int(out.numel()), "sha": h}))
 
+def one_split(name):
+    """C3 text, K=6 lazy: the Huffman stage ('huff', HIP events) unsplit and with DMX_F_SPLIT."""
+    sys.path.insert(0, R)
+    import hashlib, numpy as np, torch
+    import deflate_compression_amd as D
+    D.LIB_PATH = os.path.join(OUT, f"libdmx_{name}.so")
+    n = 100_000_000
+    t = torch.from_numpy(D.gen_text(n, 0xE5818)).cuda()
+    res = {}
+    for tag, fl in (("plain", 0), ("split", D.DMX_F_SPLIT)):
+        e = D.Encoder(0, n, max_chain=6, flags=D.DMX_ZLIB | D.DMX_F_LAZY | fl)
+        out, r = e.compress_tensor(t)
+        e.set_timing(True)
+        for _ in range(10):
+            out, r = e.compress_tensor(t)
+        st, cnt = e.stage_times()
+        res[tag] = {"huff_ms": round(st["huff"] / max(cnt, 1), 4), "sha": hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()[:16]}
+        e.close()
+    print(json.dumps(res))
+
+def run_split():
+    for name in sys.argv[2].split(","):
+        r = subprocess.run([sys.executable, __file__, "one_split", name], capture_output=True, text=True, timeout=300)
+        print(name, r.stdout.strip() or r.stderr[-300:], flush=True)
+
 def run_k0():
     for name in sys.argv[2].split(","):
         r = subprocess.run([sys.executable, __file__, "one_k0", name], capture_output=True, text=True, timeout=300)
@@ -161,5 +191,7 @@ def one(name):
 if __name__ == "__main__":
     if sys.argv[1] == "one_k0":
         one_k0(sys.argv[2])
+    elif sys.argv[1] == "one_split":
+        one_split(sys.argv[2])
     else:
-        {"build": build, "run": run, "run_k0": run_k0}.get(sys.argv[1], lambda: one(sys.argv[2]))()
+        {"build": build, "run": run, "run_k0": run_k0, "run_split": run_split}.get(sys.argv[1], lambda: one(sys.argv[2]))()
