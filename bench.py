@@ -57,9 +57,12 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="text", choices=sorted(WORKLOADS))
     ap.add_argument("--bytes", type=int, default=0, help="override bytes per rank")
-    ap.add_argument("--max-chain", type=int, default=int(os.environ.get("DMX_MAX_CHAIN", "6")),
-                    help="0 = exhaustive (reference parse); K = K newest chain entries (default 6: the "
-                         "fastest setting inside the <= 2 %% size budget on C3 text, +1.32 %% vs S_ref)")
+    ap.add_argument("--max-chain", type=int, default=int(os.environ.get("DMX_MAX_CHAIN", "8")),
+                    help="0 = exhaustive (reference parse); K = K newest chain entries (default 8: inside "
+                         "the <= 2 %% size budget vs S_ref on every reference-held text with --deep, "
+                         "profiles/r04_size/size_table.md)")
+    ap.add_argument("--deep", type=int, default=int(os.environ.get("DMX_DEEP", "1")),
+                    help="1 = adaptive chain depth: small-alphabet blocks search 64 deep (DMX_F_DEEP)")
     ap.add_argument("--lazy", type=int, default=int(os.environ.get("DMX_LAZY", "1")),
                     help="1 = lazy evaluation parse (DMX_F_LAZY, SURVEY §8 f2)")
     ap.add_argument("--split", type=int, default=int(os.environ.get("DMX_SPLIT", "0")),
@@ -69,7 +72,7 @@ def parse_args(argv=None):
     ap.add_argument("--dict", type=int, default=int(os.environ.get("DMX_DICT", "0")),
                     help="1 = cross-block dictionary (DMX_F_DICT, SURVEY §8 f1); N > 1: halo exchange of "
                          "the block before each shard inside the step")
-    ap.add_argument("--tradeoff", default="4,8,16",
+    ap.add_argument("--tradeoff", default="4,6,7,16",
                     help="N = 1: also time these max_chain values (same flags) for the speed/size curve "
                          "(reported under 'tradeoff'; '' = skip)")
     ap.add_argument("--exhaustive-steps", type=int, default=3,
@@ -146,7 +149,8 @@ def make_input(kind: str, n: int, seed: int):
 def parse_str(args) -> str:
     return (("exhaustive" if args.max_chain == 0 else f"max_chain={args.max_chain}")
             + (", lazy" if args.lazy else ", greedy") + (", split" if args.split else "")
-            + (", dict" if args.dict else "") + (", store-check" if args.store_check else ""))
+            + (", dict" if args.dict else "") + (", store-check" if args.store_check else "")
+            + (", deep" if args.deep and 0 < args.max_chain < 64 else ""))
 
 
 def cpu_info():
@@ -199,8 +203,8 @@ def cpu_baselines(data, args, budget_s: float):
     n = int(data.size)
     sw = 32768
 
-    def leg(max_chain, lazy, split, dct, store, budget, name, thr, want_full):
-        kw = dict(lazy=lazy, split=split, dict=dct, store_check=store, threads=thr)
+    def leg(max_chain, lazy, split, dct, store, deep, budget, name, thr, want_full):
+        kw = dict(lazy=lazy, split=split, dict=dct, store_check=store, threads=thr, deep=deep)
         piece = min(n, sw * max(4 * thr, 32))
         t0 = time.perf_counter()
         O.compress_par(data[:piece], sw, max_chain, flags=5, **kw)   # probe: the first piece
@@ -229,7 +233,8 @@ def cpu_baselines(data, args, budget_s: float):
                 "cpu_model": info["cpu_model"], "nproc": info["nproc"]}, done, z
 
     parse = parse_str(args)
-    same = (args.max_chain, bool(args.lazy), bool(args.split), bool(args.dict), bool(args.store_check))
+    same = (args.max_chain, bool(args.lazy), bool(args.split), bool(args.dict), bool(args.store_check),
+            bool(args.deep))
     r, _, z = leg(*same, budget_s, f"compress ({parse}: the GPU line's parse)", info["threads"], True)
     r["parse"] = parse
     out["same_parse_stream"] = z
@@ -244,7 +249,7 @@ def cpu_baselines(data, args, budget_s: float):
         if r2["value"] > r["value"]:   # more threads than the cgroup's CPUs only oversubscribe them
             r, best_thr = r2, info["share_threads"]
     out["same_parse"] = r
-    r, done, z = leg(0, False, False, False, False, budget_s,
+    r, done, z = leg(0, False, False, False, False, False, budget_s,
                      "compress (the reference's exhaustive greedy parse + Huffman/emitter)", best_thr, True)
     r["parse"] = "exhaustive, greedy (reference semantics)"
     out["exhaustive"] = r
@@ -296,7 +301,8 @@ def real_text_leg(enc_flags, args, dev, local, stream):
     finally:
         e.close()
     port = O.compress_par(host, 32768, args.max_chain, lazy=bool(args.lazy), split=bool(args.split),
-                          dict=bool(args.dict), store_check=bool(args.store_check), threads=thr)
+                          dict=bool(args.dict), store_check=bool(args.store_check), threads=thr,
+                          deep=bool(args.deep))
     sref = O.compress_par(host, 32768, 0, threads=thr)
     return {"value": round(n / dt / 1e9, 3), "unit": "GB/s", "ms_per_step": round(dt * 1e3, 4), "steps": 5,
             "input": "tests/golden/bee_movie_script.txt (the reference's corpus) tiled to 100 000 000 B, "
@@ -314,7 +320,7 @@ def end_to_end(host, args):
     import tempfile
     import deflate_compression_amd as D
     env = {"DMX_MAX_CHAIN": str(args.max_chain), "DMX_LAZY": str(args.lazy), "DMX_SPLIT": str(args.split),
-           "DMX_DICT": str(args.dict), "DMX_STORE_CHECK": str(args.store_check)}
+           "DMX_DICT": str(args.dict), "DMX_STORE_CHECK": str(args.store_check), "DMX_DEEP": str(args.deep)}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     td = tempfile.mkdtemp(dir="/tmp")
@@ -452,6 +458,8 @@ def main() -> int:
         flags |= D.DMX_F_DICT
     if args.store_check:
         flags |= D.DMX_F_STORE_CHECK
+    if args.deep:
+        flags |= D.DMX_F_DEEP
     enc = D.Encoder(local, n, 32768, args.max_chain, flags)
     d_in = torch.from_numpy(host).to(dev)
     cap = D.max_compressed(n)
@@ -678,7 +686,8 @@ def main() -> int:
     exh_stream = None
     if world == 1 and args.max_chain != 0 and args.exhaustive_steps > 0:
         # the reference's own parse (every earlier position of the bucket), same input
-        ex = D.Encoder(local, n, 32768, 0, flags & ~(D.DMX_F_LAZY | D.DMX_F_DICT | D.DMX_F_SPLIT | D.DMX_F_STORE_CHECK))
+        ex = D.Encoder(local, n, 32768, 0, flags & ~(D.DMX_F_LAZY | D.DMX_F_DICT | D.DMX_F_SPLIT | D.DMX_F_STORE_CHECK
+                                                    | D.DMX_F_DEEP))
         ex.encode_async(d_in.data_ptr(), n, d_out.data_ptr(), cap, stream)
         ex_len = int(ex.result(stream).out_len)
         torch.cuda.synchronize(dev)

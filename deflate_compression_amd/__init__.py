@@ -23,7 +23,7 @@ import struct
 __all__ = [
     "DeflateError", "Opts", "Result", "Encoder", "lib", "compress", "deflate_compress",
     "deflate_decompress", "max_compressed", "adler32_combine", "gen_text", "gen_random",
-    "COMPRESS_STATS", "E", "DMX_F_HEADER", "DMX_F_TRAILER", "DMX_F_FINAL", "DMX_ZLIB", "DMX_F_LAZY", "DMX_F_EXACT_SORT", "DMX_F_SPLIT", "DMX_F_DICT", "DMX_F_STORE_CHECK", "inflate_gpu", "inflate_gpu_chained", "ref_estimates",
+    "COMPRESS_STATS", "E", "DMX_F_HEADER", "DMX_F_TRAILER", "DMX_F_FINAL", "DMX_ZLIB", "DMX_F_LAZY", "DMX_F_EXACT_SORT", "DMX_F_SPLIT", "DMX_F_DICT", "DMX_F_STORE_CHECK", "DMX_F_DEEP", "inflate_gpu", "inflate_gpu_chained", "ref_estimates",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -38,6 +38,7 @@ DMX_F_EXACT_SORT = 16
 DMX_F_SPLIT = 32
 DMX_F_DICT = 64
 DMX_F_STORE_CHECK = 128
+DMX_F_DEEP = 256
 _M = 1 << 24
 # src/include/global_errors.h:24-35 and src/include/deflate_errors.h:9-22
 E = {
@@ -164,18 +165,20 @@ def max_compressed(n: int, sw: int = 32768) -> int:
 
 
 def compress(data, sw: int = 32768, max_chain: int = 0, flags: int = DMX_ZLIB, lazy: bool = False,
-             split: bool = False, dict: bool = False, pre=None, store_check: bool = False) -> bytes:
+             split: bool = False, dict: bool = False, pre=None, store_check: bool = False,
+             deep: bool = False) -> bytes:
     """Encode a host buffer on the GPU; returns the zlib stream (or raw DEFLATE with flags).
     lazy = f2 lazy parse (DMX_F_LAZY), split = f3 adaptive block splitting (DMX_F_SPLIT),
     dict = f1 cross-block dictionary (DMX_F_DICT; pre = the bytes before `data`),
-    store_check = noise blocks stored without a parse (DMX_F_STORE_CHECK)."""
+    store_check = noise blocks stored without a parse (DMX_F_STORE_CHECK),
+    deep = adaptive chain depth of small-alphabet blocks (DMX_F_DEEP)."""
     L = lib()
     p, n, keep = _buf(data)
     cap = max_compressed(n, sw)
     out = ctypes.create_string_buffer(cap)
     olen = ctypes.c_uint64(0)
     o = Opts(sw, max_chain, flags | (DMX_F_LAZY if lazy else 0) | (DMX_F_SPLIT if split else 0) |
-             (DMX_F_DICT if dict else 0) | (DMX_F_STORE_CHECK if store_check else 0), 0)
+             (DMX_F_DICT if dict else 0) | (DMX_F_STORE_CHECK if store_check else 0) | (DMX_F_DEEP if deep else 0), 0)
     pk = None
     if dict and pre is not None and len(pre):
         pk = ctypes.create_string_buffer(bytes(pre), len(pre))

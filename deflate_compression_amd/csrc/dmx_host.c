@@ -196,6 +196,10 @@ int deflate_compress(int fd_in, int fd_out, int fd_stats, swi sw, int ops) {
     (void)ops; /* unused by the reference's compress too */
     int swv = sw == 0 ? DMX_BLK : (int)sw;
     if (swv > DMX_BLK) return -E_RANGE;
+    if (fd_stats >= 0) {   /* an unknown DMX_STATS mode fails before anything is encoded or written */
+        const char* mode = getenv("DMX_STATS");
+        if (mode && *mode && strcmp(mode, "exact") != 0 && strcmp(mode, "ref") != 0) return -E_INVAL;
+    }
     const char* mc = getenv("DMX_MAX_CHAIN");
     dmx_opts o;
     o.sw = swv;
@@ -210,6 +214,8 @@ int deflate_compress(int fd_in, int fd_out, int fd_stats, swi sw, int ops) {
     const char* sc = getenv("DMX_STORE_CHECK");   /* 1 = noise blocks stored unparsed (§4.7);
                                                    * not with fd_stats: such blocks have no tokens */
     if (sc && atoi(sc) > 0 && fd_stats < 0) o.flags |= DMX_F_STORE_CHECK;
+    const char* dp = getenv("DMX_DEEP");   /* 1 = adaptive chain depth (DMX_F_DEEP, bounded mode) */
+    if (dp && atoi(dp) > 0) o.flags |= DMX_F_DEEP;
     o.reserved = 0;
     o.dict = NULL;
     o.dict_len = 0;

@@ -24,6 +24,7 @@
 // ring (12 workgroups per CU); longer codes take a canonical slow path (first code / count /
 // offset per length, in LDS).
 #include <hip/hip_runtime.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <type_traits>
 #include <stdio.h>
@@ -883,24 +884,55 @@ __global__ __launch_bounds__(64) void dmx_inflate_stream_kernel(const uint8_t* _
 // C ABI
 // ------------------------------------------------------------------------------------
 
+// Table scratch of dmx_inflate_async, one slot per (device, stream): reused by every decode
+// on that stream (stream order keeps the reuse safe); a larger request frees the old buffer
+// and allocates the new one on the same stream.  Never released (a process-lifetime cache).
+#define ITAB_SLOTS 64
+struct ItabSlot { int dev; hipStream_t s; uint32_t* p; uint64_t bytes; };
+static ItabSlot g_itab[ITAB_SLOTS];
+static int g_nitab = 0;
+static pthread_mutex_t g_itab_mu = PTHREAD_MUTEX_INITIALIZER;
+static uint32_t* itab_scratch(hipStream_t s, uint64_t bytes) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    pthread_mutex_lock(&g_itab_mu);
+    ItabSlot* e = nullptr;
+    for (int k = 0; k < g_nitab; k++)
+        if (g_itab[k].dev == dev && g_itab[k].s == s) { e = &g_itab[k]; break; }
+    if (!e && g_nitab < ITAB_SLOTS) { e = &g_itab[g_nitab++]; *e = {dev, s, nullptr, 0}; }
+    uint32_t* r = nullptr;
+    if (e) {
+        if (e->bytes < bytes) {
+            if (e->p) (void)hipFreeAsync(e->p, s);
+            e->p = nullptr;
+            e->bytes = 0;
+            if (hipMallocAsync((void**)&e->p, bytes, s) == hipSuccess) e->bytes = bytes;
+            else e->p = nullptr;
+        }
+        r = e->p;
+    }
+    pthread_mutex_unlock(&g_itab_mu);
+    return r;
+}
+
 extern "C" int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_iblock* d_index, uint32_t nblk,
                                  void* d_out, uint64_t out_cap, dmx_inflate_status* d_status, void* stream) {
     if (!d_z || !d_out || !d_status || (d_index && !nblk)) return -(int)E_INVAL;
     if (zbytes > 0xFFFFFFF0ull) return -(int)E_RANGE;   // reader word indices are 32-bit
     hipStream_t s = (hipStream_t)stream;
     if (hipMemsetAsync(d_status, 0, sizeof(dmx_inflate_status), s) != hipSuccess) return -(int)E_DEVICE;
-    // the workgroups' first-level tables: stream-ordered scratch, freed after the launch
-    uint32_t* gtab = nullptr;
+    // the workgroups' first-level tables: scratch cached per (device, stream) and grown
+    // stream-ordered, so a steady stream of decodes allocates nothing
     const uint64_t tb = (uint64_t)(d_index ? nblk : 1) * ITAB_WORDS * 4;
-    if (hipMallocAsync((void**)&gtab, tb, s) != hipSuccess) return -(int)E_MALLOC;
+    uint32_t* gtab = itab_scratch(s, tb);
+    if (!gtab) return -(int)E_MALLOC;
     if (d_index)
         hipLaunchKernelGGL(dmx_inflate_index_kernel<false>, dim3(nblk), dim3(64), 0, s, (const uint8_t*)d_z, zbytes,
                            d_index, (uint8_t*)d_out, out_cap, gtab, d_status);
     else
         hipLaunchKernelGGL(dmx_inflate_stream_kernel, dim3(1), dim3(64), 0, s, (const uint8_t*)d_z, zbytes,
                            (uint8_t*)d_out, out_cap, gtab, d_status);
-    const bool bad = hipGetLastError() != hipSuccess;
-    if (hipFreeAsync(gtab, s) != hipSuccess || bad) return -(int)E_DEVICE;
+    if (hipGetLastError() != hipSuccess) return -(int)E_DEVICE;
     return 0;
 }
 
@@ -1086,12 +1118,29 @@ __global__ __launch_bounds__(CHAIN_WG) void dmx_cells_jump_kernel(const dmx_iblo
     }
 }
 
-__global__ __launch_bounds__(256) void dmx_cells_final_kernel(const uint16_t* __restrict__ cells, uint8_t* __restrict__ out,
-                                                             uint64_t n, dmx_inflate_status* __restrict__ st) {
-    const uint64_t stride = (uint64_t)gridDim.x * 256 * 16;
+// One workgroup per sw block: its own output range [out_off, out_off + out_len) of the index,
+// cells -> bytes.  Positions of d_out the index does not cover are neither read nor written
+// (out_cap is a capacity: the cell scratch past the decoded bytes was never initialised).
+__global__ __launch_bounds__(256) void dmx_cells_final_kernel(const dmx_iblock* __restrict__ index,
+                                                             const uint16_t* __restrict__ cells, uint8_t* __restrict__ out,
+                                                             uint64_t cap, dmx_inflate_status* __restrict__ st) {
+    const uint64_t off = index[blockIdx.x].out_off;
+    const uint32_t len = index[blockIdx.x].out_len;
+    if (off > cap || len > cap - off || len > IW) return;   // the decode already failed this index
+    const uint64_t n = off + len;
     bool bad = false;
-    for (uint64_t j0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16; j0 < n; j0 += stride) {
-        if (j0 + 16 <= n && ((uintptr_t)(out + j0) & 15) == 0) {
+    // 16 positions per thread and step; the range's unaligned head and tail byte by byte
+    const uint64_t a0 = min((off + 15) & ~15ull, n), a1 = max(a0, n & ~15ull);
+    for (uint64_t j = off + threadIdx.x; j < a0; j += 256) {
+        bad = bad || cells[j] > 0xFFu;
+        out[j] = (uint8_t)cells[j];
+    }
+    for (uint64_t j = a1 + threadIdx.x; j < n; j += 256) {
+        bad = bad || cells[j] > 0xFFu;
+        out[j] = (uint8_t)cells[j];
+    }
+    if (((uintptr_t)out & 15) == 0) {
+        for (uint64_t j0 = a0 + (uint64_t)threadIdx.x * 16; j0 < a1; j0 += 256 * 16) {
             const uint4 a = *reinterpret_cast<const uint4*>(cells + j0), b = *reinterpret_cast<const uint4*>(cells + j0 + 8);
             const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
             uint32_t o[4];
@@ -1102,18 +1151,18 @@ __global__ __launch_bounds__(256) void dmx_cells_final_kernel(const uint16_t* __
                 o[k] = (lo & 0xFFu) | ((lo >> 8) & 0xFF00u) | ((hi & 0xFFu) << 16) | ((hi << 8) & 0xFF000000u);
             }
             *reinterpret_cast<uint4*>(out + j0) = make_uint4(o[0], o[1], o[2], o[3]);
-        } else {
-            for (uint64_t j = j0; j < n && j < j0 + 16; j++) {
-                bad = bad || cells[j] > 0xFFu;
-                out[j] = (uint8_t)cells[j];
-            }
+        }
+    } else {
+        for (uint64_t j = a0 + threadIdx.x; j < a1; j += 256) {
+            bad = bad || cells[j] > 0xFFu;
+            out[j] = (uint8_t)cells[j];
         }
     }
     if (bad) atomicCAS(&st->status, 0, -(int32_t)E_HUFDIS);
 }
 
 // work layout: [list totals per round, 256 B][list lengths 2 x nblk, 256-aligned][tables ITAB_WORDS x nblk]
-// [cells 2*cap, 256-aligned][P 4*cap][list A 4*cap][list B 4*cap]
+// [cells 2*cap, 256-aligned][P 4*cap][list A 2*cap][list B 2*cap] (list entries: 16-bit block-relative)
 static inline uint64_t chain_a256(uint64_t x) { return (x + 255) & ~255ull; }
 
 extern "C" uint64_t dmx_inflate_chained_work(uint64_t out_cap, uint32_t nblk) {
@@ -1153,9 +1202,8 @@ extern "C" int dmx_inflate_chained_async(const void* d_z, uint64_t zbytes, const
     for (uint32_t rd = 0; rd < rounds; rd++)
         hipLaunchKernelGGL(dmx_cells_jump_kernel, dim3(nblk), dim3(CHAIN_WG), 0, s, d_index, cells, P, L[rd & 1],
                            L[(rd + 1) & 1], C[rd & 1], C[(rd + 1) & 1], T + rd + 1);
-    const uint64_t gf0 = (out_cap + 4095) / 4096;
-    const uint32_t gf = (uint32_t)(gf0 < 4096 ? gf0 : 4096);
-    hipLaunchKernelGGL(dmx_cells_final_kernel, dim3(gf ? gf : 1), dim3(256), 0, s, cells, (uint8_t*)d_out, out_cap, d_status);
+    hipLaunchKernelGGL(dmx_cells_final_kernel, dim3(nblk), dim3(256), 0, s, d_index, cells, (uint8_t*)d_out, out_cap,
+                       d_status);
     if (hipGetLastError() != hipSuccess) return -(int)E_DEVICE;
     return 0;
 }

@@ -709,6 +709,7 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
                     else if (__ballot(act && lim_eff < CBS)) cand_steps_emb<false, true>(K, i0, i1, nc, lim_eff, jkey);
                     else if (K == 6) cand_steps_fixed<6>(i0, i1, jkey);
                     else if (K == 8) cand_steps_fixed<8>(i0, i1, jkey);
+                    else if (K == 7) cand_steps_fixed<7>(i0, i1, jkey);
                     else if (K == 4) cand_steps_fixed<4>(i0, i1, jkey);
                     else cand_steps_emb<false, false>(K, i0, i1, nc, lim_eff, jkey);
                 }
@@ -1878,6 +1879,39 @@ __device__ __forceinline__ bool dbg_stop(uint32_t mflags, uint32_t phase, dmx_bl
     return true;
 }
 
+// DMX_F_DEEP (mflags & 8): the block's own chain depth, dmx_oracle_block_chain's rule --
+// DMX_DEEP_CHAIN when 4 D < samples, D = the distinct buckets of the sampled positions
+// p < bn - 2 with p mod 2048 < 256 (4 096 in a full block: 16 runs of 256).  Called by all
+// threads after the staging barrier; L.hist (zero until P3) holds the 8192-bit bucket set
+// and is zeroed again, L.ntok (zero until the walk) the count.  Two barriers.
+__device__ __forceinline__ int32_t block_chain(MatchLDS& L, uint32_t bn, int32_t max_chain, uint32_t mflags,
+                                               uint32_t tid) {
+    if (!(mflags & 8u) || max_chain <= 0 || max_chain >= DMX_DEEP_CHAIN) return max_chain;
+    const uint32_t nvalid = bn > 2 ? bn - 2 : 0;
+    uint32_t* SB = L.hist;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        const uint32_t p = (((tid >> 8) + 4 * j) << 11) | (tid & 255u);
+        if (p < nvalid) {
+            const uint32_t h = dmx_hash(ld4(L.data, p) & 0xFFFFFFu);
+            atomicOr(&SB[h >> 5], 1u << (h & 31));
+        }
+    }
+    __syncthreads();
+    if (tid < DMX_NBUCKET / 32) {
+        const uint32_t c = wave_sum_u32((uint32_t)__popc(SB[tid]));
+        SB[tid] = 0;
+        if ((tid & 63) == 0) atomicAdd(&L.ntok, c);
+    }
+    __syncthreads();
+    uint32_t ns = 0;
+    for (uint32_t s = 0; s < 16; s++) {
+        const uint32_t lo = s << 11;
+        ns += nvalid > lo ? min(nvalid - lo, 256u) : 0u;
+    }
+    return 4 * L.ntok < ns ? (int32_t)DMX_DEEP_CHAIN : max_chain;
+}
+
 // NBX > 3: the exhaustive parse without a dictionary (max_chain = 0) on NBX-byte chains
 // (P0'); a separate instantiation, so the bounded modes' code and registers are untouched
 #ifndef DMX_NBX
@@ -1903,7 +1937,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
 
     // ---- P0: stage the block, the bucket starts and the bucket-sorted positions in LDS ----
     const uint64_t tbeg = dbg ? __builtin_amdgcn_s_memtime() : 0;
-    if (tid == 0) { L.adl_s = 0; L.adl_t = 0; L.sortbad = (mflags & 2u) ? 1u : 0u; }   // 2: test hook
+    if (tid == 0) { L.adl_s = 0; L.adl_t = 0; L.sortbad = (mflags & 2u) ? 1u : 0u; L.ntok = 0; }   // 2: test hook
     if (dbg && tid == 0) { st_search = 0; st_iters = 0; st_def = 0; st_p3a = 0; }
     for (uint32_t k = tid; k < DMX_HIST; k += MT) L.hist[k] = 0;
     for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) L.lit[k] = 0;
@@ -1938,6 +1972,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
     // DMX_F_DICT: the chain kernel already sorted this block; the history kernel's
     // results (bucket order) wait in the block's token slots until P3
     const uint32_t* hbk = DICT ? tok_g + (uint64_t)b * DMX_BLK : nullptr;
+    int32_t kb = max_chain;   // this block's chain depth (DMX_F_DEEP: block_chain)
     if (DICT) {
         const uint32_t nv = bn > 2 ? bn - 2 : 0;
         const uint16_t* Sg = chs + (uint64_t)(b + 1) * DMX_BLK;
@@ -1945,7 +1980,8 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
             reinterpret_cast<uint4*>(L.sorted)[k] = reinterpret_cast<const uint4*>(Sg)[k];
         for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) L.lit[k] = 0;
         __syncthreads();
-        if (max_chain <= 0 || max_chain > KD) {   // bucket starts, as sort_positions finds them
+        kb = block_chain(L, bn, max_chain, mflags, tid);
+        if (kb <= 0 || kb > KD) {   // bucket starts, as sort_positions finds them
             for (uint32_t k = tid; k < nv; k += MT) {
                 const uint32_t h = dmx_hash(ld4(L.data, L.sorted[k]) & 0xFFFFFFu);
                 const uint32_t hp = k ? dmx_hash(ld4(L.data, L.sorted[k - 1]) & 0xFFFFFFu) : 0xFFFFFFFFu;
@@ -1980,7 +2016,8 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         for (int w = 0; w < MW; w++) nrun0 += L.wexit[w];
         // the exhaustive parse's first sort (trigram chains for the gram pass) needs no bucket
         // starts: the 4-byte sort makes the search's (max_chain 1 here only skips them)
-        const int32_t mc0 = (NBX > 3 && !DICT) ? 1 : max_chain;
+        kb = block_chain(L, bn, max_chain, mflags, tid);
+        const int32_t mc0 = (NBX > 3 && !DICT) ? 1 : kb;
         if (nrun0 * 4 >= ((bn + 15) >> 4)) sort_positions<false, true>(L, bn, mc0, tid, dbg != nullptr, tp0);
         else sort_positions<false, false>(L, bn, mc0, tid, dbg != nullptr, tp0);
     }
@@ -2049,14 +2086,14 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         uint32_t nrun = 0;
 #pragma unroll
         for (int w = 0; w < MW; w++) nrun += L.wexit[w];
-        const bool runs = max_chain > 0 && max_chain <= KE && nrun * 4 >= ((bn + 15) >> 4);
-        if (max_chain > 0 && max_chain <= KE) {   // the winners' nibbles (bstart is free after P0)
+        const bool runs = kb > 0 && kb <= KE && nrun * 4 >= ((bn + 15) >> 4);
+        if (kb > 0 && kb <= KE) {   // the winners' nibbles (bstart is free after P0)
             reinterpret_cast<uint4*>(nib_words(L))[tid] = make_uint4(0, 0, 0, 0);
             __syncthreads();
         }
-        const uint32_t its = runs ? search_positions<DICT, true>(L, bn, max_chain, pg, tid, dbg != nullptr, tdef, hbk)
-                             : h4 ? search_positions<DICT, false, (h4 ? NBX : 3)>(L, bn, max_chain, pg, tid, dbg != nullptr, tdef, hbk, seeds)
-                                  : search_positions<DICT, false>(L, bn, max_chain, pg, tid, dbg != nullptr, tdef, hbk);
+        const uint32_t its = runs ? search_positions<DICT, true>(L, bn, kb, pg, tid, dbg != nullptr, tdef, hbk)
+                             : h4 ? search_positions<DICT, false, (h4 ? NBX : 3)>(L, bn, kb, pg, tid, dbg != nullptr, tdef, hbk, seeds)
+                                  : search_positions<DICT, false>(L, bn, kb, pg, tid, dbg != nullptr, tdef, hbk);
         if (dbg && lane == 0 && attempt == 0) {
             atomicAdd((unsigned long long*)&st_iters, (unsigned long long)its);
             atomicMax((unsigned long long*)&st_search, (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
@@ -2067,8 +2104,8 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         // never observed on gfx950: redo the block with the match-any sort (stable by construction);
         // counted (dmx_result.nsortfallback) so that every run shows it did not happen
         if (tid == 0) atomicAdd(nfallback, 1u);
-        if (h4) sort_positions<true, true, (h4 ? NBX : 3)>(L, bn, max_chain, tid, dbg != nullptr, tp0);
-        else sort_positions<true>(L, bn, max_chain, tid, dbg != nullptr, tp0);
+        if (h4) sort_positions<true, true, (h4 ? NBX : 3)>(L, bn, kb, tid, dbg != nullptr, tp0);
+        else sort_positions<true>(L, bn, kb, tid, dbg != nullptr, tp0);
     }
     const uint64_t t1 = dbg ? __builtin_amdgcn_s_memtime() : 0;
     if (dbg_stop(mflags, 2, info, hist_g, b, bn, tid)) return;
@@ -2116,7 +2153,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         __syncthreads();
         const uint32_t nvalid = bn > 2 ? bn - 2 : 0;
         uint4 dv[4], pv[4];
-        if (max_chain > 0 && max_chain <= KE) {
+        if (kb > 0 && kb <= KE) {
             const uint32_t* NW = nib_words(L);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -3879,7 +3916,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         if (ev) (void)hipEventRecord(ev[1], s);
         const char* dstop = getenv("DMX_DEBUG_STOP");   // diagnostic only (dbg_stop)
         const uint32_t mfl = ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u) |
-                             ((o.flags & DMX_F_STORE_CHECK) ? 4u : 0u) | (dstop ? ((uint32_t)atoi(dstop) & 3u) << 8 : 0u);
+                             ((o.flags & DMX_F_STORE_CHECK) ? 4u : 0u) | ((o.flags & DMX_F_DEEP) ? 8u : 0u) | (dstop ? ((uint32_t)atoi(dstop) & 3u) << 8 : 0u);
         if (o.flags & DMX_F_DICT)
             hipLaunchKernelGGL(dmx_match_kernel<true>, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n,
                                (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb);

@@ -68,6 +68,10 @@ int deflate_decompress(struct string_len* decompr_dat, struct string_len* compr_
  *                  ll_bits / d_bits = the adaptive trees' scores after this token
  *                  (aht.c:239-277), running over the whole stream as in the reference.
  *                  Same records as the reference for the same tokens (dmx_refest_*).
+ *                  Parity unpinned past one window: the reference itself is only correct
+ *                  for its first 32 KiB window, so records of later blocks
+ *                  are checked against this host restatement fed the oracle's tokens, not
+ *                  against the reference's own output.
  *   "exact"        exact costs of this stream, running over the whole stream: tree_bits =
  *                  header bits of every DEFLATE block begun so far (its own included),
  *                  ll_bits = lit/len code + length extra bits of every token so far (8 per
@@ -146,6 +150,12 @@ struct compress_stats {
                                  * encoder policy of our own (the reference always parses);
                                  * the oracle applies the same rule.  Such blocks have no
                                  * tokens (no compress_stats records). */
+#define DMX_F_DEEP 256u  /* parse option: adaptive chain depth for bounded
+                            K < 64 -- a block whose trigrams are few (D distinct 13-bit
+                            buckets among its positions p mod 2048 < 256, 4 D < samples:
+                            small alphabets such as binary digits, hex, DNA) searches its
+                            own chains 64 deep instead of K.  Text never qualifies. */
+#define DMX_DEEP_CHAIN 64
 
 typedef struct {
     int32_t sw;        /* block size 1..32768 (0 = 32768) */
@@ -194,7 +204,10 @@ uint64_t dmx_max_compressed(uint64_t n, int32_t sw);
  * out_cap) on `stream` (hipStream_t; NULL = the context's stream).  No host
  * synchronisation, no allocation (graph-capturable).  Returns 0 or -E_* for argument
  * errors: -E_SZ when n needs more blocks than the context holds, or DMX_F_SPLIT /
- * DMX_F_DICT on a context not reserved for them (dmx_ctx_reserve_flags). */
+ * DMX_F_DICT on a context not reserved for them (dmx_ctx_reserve_flags).  With
+ * DMX_F_STORE_CHECK, bytes of d_out past the final out_len (inside out_cap) may be
+ * overwritten: a noise block is copied speculatively to the offset it would have if every
+ * block before it were stored. */
 int dmx_encode_async(dmx_ctx* ctx, const void* d_in, uint64_t n, void* d_out, uint64_t out_cap,
                      const dmx_opts* opts, void* stream);
 /* Wait for the last encode on `stream` and copy its dmx_result to the host. */
@@ -252,7 +265,10 @@ int dmx_block_index(dmx_ctx* ctx, dmx_iblock* d_index, uint32_t cap, void* strea
 /* Inflate on the GPU.  d_index != NULL: decode the nblk listed blocks in parallel (one
  * wave each) into d_out + out_off.  d_index == NULL: decode the whole zlib stream d_z
  * (header, blocks until BFINAL, Adler-32 check) in one workgroup.  Status in the device
- * record d_status.  Returns 0 or -E_* (launch errors). */
+ * record d_status.  The first-level tables live in device scratch cached per (device,
+ * stream) and grown stream-ordered: the first call on a stream (or a larger one) allocates.
+ * Returns 0 or -E_*: -E_MALLOC when that scratch cannot be allocated, -E_DEVICE for
+ * launch errors. */
 int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_iblock* d_index, uint32_t nblk, void* d_out,
                       uint64_t out_cap, dmx_inflate_status* d_status, void* stream);
 
@@ -262,7 +278,8 @@ int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_iblock* d_inde
  * before the block -- and pointer jumping over the references, about log2(nblk) + 2 short
  * launches, resolves them; then the cells become bytes in d_out.  d_work: device scratch of
  * dmx_inflate_chained_work(out_cap, nblk) bytes (about 10 per output byte), 256-byte aligned.  Status in d_status (out_len =
- * bytes decoded; a reference before the output start is -E_HUFDIS).  Returns 0 or -E_*. */
+ * bytes decoded; a reference before the output start is -E_HUFDIS).  out_cap is a capacity:
+ * only the ranges the index lists are written.  Returns 0 or -E_*. */
 uint64_t dmx_inflate_chained_work(uint64_t out_cap, uint32_t nblk);
 int dmx_inflate_chained_async(const void* d_z, uint64_t zbytes, const dmx_iblock* d_index, uint32_t nblk, void* d_out,
                               uint64_t out_cap, void* d_work, uint64_t work_bytes, dmx_inflate_status* d_status,

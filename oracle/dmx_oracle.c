@@ -175,19 +175,44 @@ static int orc_search_hist(const orc_hist* H, const uint8_t* d, int n, int i, in
     return found ? best_len : 0;
 }
 
+/* Adaptive chain depth (DMX_F_DEEP): the block's own chains are searched
+ * ORC_DEEP_K deep instead of K when its trigrams are few -- D distinct 13-bit buckets
+ * among the sampled positions p (p mod 2048 < 256, p < n - 2) with 4 D < samples.  Small
+ * alphabets (binary digits, hex, DNA, the reference's own bit-level pngtest.png.txt)
+ * have long chains of real matches that K = 8 cuts short; text never qualifies
+ * (D / samples >= 0.32 on the reference-held text, profiles/r04_size). */
+#define ORC_DEEP_K 64
+int dmx_oracle_block_chain(const uint8_t* d, int n, int max_chain) {
+    if (max_chain <= 0 || max_chain >= ORC_DEEP_K) return max_chain;
+    uint32_t seen[8192 / 32];
+    memset(seen, 0, sizeof(seen));
+    int ns = 0, nd = 0;
+    for (int p = 0; p + 2 < n; p++) {
+        if ((p & 2047) >= 256) continue;
+        unsigned h = orc_hash_mul(d + p);
+        ns++;
+        if (!((seen[h >> 5] >> (h & 31)) & 1u)) { seen[h >> 5] |= 1u << (h & 31); nd++; }
+    }
+    return 4 * nd < ns ? ORC_DEEP_K : max_chain;
+}
+
 /* Parse one block; returns the number of tokens written to tok (<= n).
- * lazy = 0: the reference's greedy parse.  lazy = 1 (RFC 1951 §4
+ * lazy bit 0 = 0: the reference's greedy parse.  lazy bit 0 = 1 (RFC 1951 §4
  * "lazy evaluation", one position of lookahead): a match at i is deferred -- i becomes
  * a literal -- when the match at i+1 is strictly longer; the same rule then applies at
  * i+1.  Both matches are searched with the same chains (all positions before them).
+ * lazy bit 1 (DMX_F_DEEP): the block's own chain depth is dmx_oracle_block_chain's.
  * hist/hn (f1): the hn bytes before the block as a dictionary (hn = 0: none); a history
- * match is taken only when strictly longer than the block's own best. */
+ * match is taken only when strictly longer than the block's own best;
+ * the history is searched max_chain deep whatever the block's depth. */
 int dmx_oracle_parse_block_hist(const uint8_t* hist, int hn, const uint8_t* d, int n, int max_chain,
                                 int hash_kind, int lazy, uint32_t* tok) {
     int ntok = 0;
     if (n <= 0) return 0;
     const int nb = hash_kind == DMX_HASH_MORTON ? 1024 : 8192;
-    orc_chains C = {d, n, max_chain, hash_kind, 0, (uint32_t*)malloc(sizeof(uint32_t) * nb),
+    const int own_chain = (lazy & 2) && hash_kind == DMX_HASH_MUL ? dmx_oracle_block_chain(d, n, max_chain) : max_chain;
+    lazy &= 1;
+    orc_chains C = {d, n, own_chain, hash_kind, 0, (uint32_t*)malloc(sizeof(uint32_t) * nb),
                     (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n)};
     for (int b = 0; b < nb; b++) C.head[b] = ORC_NONE;
     orc_hist H, *HP = NULL;

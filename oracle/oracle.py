@@ -72,6 +72,8 @@ def lib():
         L.dmx_oracle_store_check.restype = ctypes.c_int
         L.dmx_oracle_plan.argtypes = [u32p, ctypes.c_int, ctypes.c_int, u64p, u8p, u8p]
         L.dmx_oracle_plan.restype = ctypes.c_int
+        L.dmx_oracle_block_chain.argtypes = [u8p, ctypes.c_int, ctypes.c_int]
+        L.dmx_oracle_block_chain.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -80,28 +82,40 @@ def _u8(a: np.ndarray):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
 
 
+def _lz(lazy: bool, deep: bool) -> int:
+    """The oracle's `lazy` argument: bit 0 = lazy evaluation (f2), bit 1 = DMX_F_DEEP."""
+    return int(bool(lazy)) | (2 if deep else 0)
+
+
+def block_chain(block, max_chain: int) -> int:
+    """DMX_F_DEEP: the chain depth the block's own search uses (dmx_oracle_block_chain)."""
+    a = _as_u8(block)
+    return int(lib().dmx_oracle_block_chain(_u8(a), a.size, max_chain))
+
+
 def _as_u8(data) -> np.ndarray:
     return np.ascontiguousarray(np.frombuffer(bytes(data), dtype=np.uint8)) if not isinstance(
         data, np.ndarray) else np.ascontiguousarray(data, dtype=np.uint8)
 
 
 def parse_block(data, max_chain: int = 0, hash_kind: int = HASH_MUL, lazy: bool = False,
-                hist=None) -> np.ndarray:
+                hist=None, deep: bool = False) -> np.ndarray:
     """Token stream (uint32, see dmx_oracle.c header) of one block (<= 32768 bytes).
-    hist: the bytes before the block as a dictionary (f1), or None."""
+    hist: the bytes before the block as a dictionary (f1), or None.
+    deep: the adaptive chain depth (DMX_F_DEEP; dmx_oracle_block_chain)."""
     a = _as_u8(data)
     assert a.size <= 32768
     tok = np.zeros(max(a.size, 1), dtype=np.uint32)
     h = _as_u8(hist if hist is not None else b"")
-    n = lib().dmx_oracle_parse_block_hist(_u8(h), h.size, _u8(a), a.size, max_chain, hash_kind, int(lazy),
+    n = lib().dmx_oracle_parse_block_hist(_u8(h), h.size, _u8(a), a.size, max_chain, hash_kind, _lz(lazy, deep),
                                           tok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
     return tok[:n].copy()
 
 
 def parse(data, sw: int = 32768, max_chain: int = 0, hash_kind: int = HASH_MUL, lazy: bool = False,
-          dict: bool = False) -> list:
+          dict: bool = False, deep: bool = False) -> list:
     a = _as_u8(data)
-    return [parse_block(a[o:o + sw], max_chain, hash_kind, lazy, a[o - sw:o] if dict and o else None)
+    return [parse_block(a[o:o + sw], max_chain, hash_kind, lazy, a[o - sw:o] if dict and o else None, deep)
             for o in range(0, a.size, sw)]
 
 
@@ -123,7 +137,7 @@ F_HEADER, F_TRAILER, F_FINAL = 1, 2, 4   # include/dmx.h framing bits (DMX_ZLIB 
 
 def compress(data, sw: int = 32768, max_chain: int = 0, hash_kind: int = HASH_MUL,
              want_btypes: bool = False, lazy: bool = False, split: bool = False, dict: bool = False,
-             pre=None, store_check: bool = False, flags: int = 7):
+             pre=None, store_check: bool = False, flags: int = 7, deep: bool = False):
     """zlib stream of `data`; lazy = f2 parse, split = f3 adaptive block splitting,
     dict = f1 cross-block dictionary (pre: the bytes before `data`, history of block 0),
     store_check = blocks that pass the DESIGN.md §4.7 noise check are stored unparsed.
@@ -135,7 +149,7 @@ def compress(data, sw: int = 32768, max_chain: int = 0, hash_kind: int = HASH_MU
     out = np.zeros(cap, dtype=np.uint8)
     bt = np.zeros(max(nblk, 1), dtype=np.uint8)
     pa = _as_u8(pre if pre is not None else b"")
-    r = lib().dmx_oracle_compress_framed(_u8(a), a.size, sw, max_chain, hash_kind, int(lazy),
+    r = lib().dmx_oracle_compress_framed(_u8(a), a.size, sw, max_chain, hash_kind, _lz(lazy, deep),
                                          int(split) | (2 if store_check else 0), int(dict), _u8(pa), pa.size,
                                          flags, _u8(out), cap, _u8(bt))
     if r < 0:
@@ -145,14 +159,15 @@ def compress(data, sw: int = 32768, max_chain: int = 0, hash_kind: int = HASH_MU
 
 
 def compress_par(data, sw: int = 32768, max_chain: int = 0, lazy: bool = False, split: bool = False,
-                 dict: bool = False, store_check: bool = False, flags: int = 7, threads: int = 0) -> bytes:
+                 dict: bool = False, store_check: bool = False, flags: int = 7, threads: int = 0,
+                 deep: bool = False) -> bytes:
     """The same stream as compress(), blocks encoded in parallel by `threads` OpenMP threads
     (dmx_oracle_compress_par; the all-cores CPU baseline)."""
     a = _as_u8(data)
     nblk = (a.size + sw - 1) // sw
     cap = a.size + 5 * (nblk + 1) + 64
     out = np.zeros(cap, dtype=np.uint8)
-    r = lib().dmx_oracle_compress_par(_u8(a), a.size, sw, max_chain, HASH_MUL, int(lazy),
+    r = lib().dmx_oracle_compress_par(_u8(a), a.size, sw, max_chain, HASH_MUL, _lz(lazy, deep),
                                       int(split) | (2 if store_check else 0), int(dict), flags, threads, _u8(out), cap)
     if r < 0:
         raise RuntimeError(f"oracle compress_par failed: {r}")

@@ -220,6 +220,32 @@ def test_dict_gpu_inflate_chained_lists_and_bad_index(enc):
     assert st == -D.E["E_RANGE"]
 
 
+def test_dict_gpu_inflate_chained_capacity_larger_than_output(enc):
+    """out_cap is a capacity: a buffer 4 KiB larger than the decoded bytes decodes
+    exactly, and the bytes past the output are left as they were."""
+    data = _inputs()["mixed"]
+    z, _ = enc.compress_bytes(data, max_chain=6, flags=D.DMX_ZLIB | D.DMX_F_DICT | D.DMX_F_LAZY)
+    ix, nblk = enc.block_index()
+    dz = torch.frombuffer(bytearray(z), dtype=torch.uint8).cuda()
+    L = D.lib()
+    cap = len(data) + 4096
+    out = torch.full((cap,), 0xA5, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    wb = int(L.dmx_inflate_chained_work(cap, nblk))
+    work = torch.full((wb + 256,), 0x77, dtype=torch.uint8, device="cuda")   # stale scratch
+    wp = (work.data_ptr() + 255) & ~255
+    s = torch.cuda.current_stream().cuda_stream
+    assert L.dmx_inflate_chained_async(dz.data_ptr(), dz.numel(), ix.data_ptr(), nblk, out.data_ptr(), cap, wp,
+                                       wb, st.data_ptr(), s) == 0
+    torch.cuda.synchronize()
+    h = st.cpu().numpy()
+    assert int(np.frombuffer(h[:4].tobytes(), np.int32)[0]) == 0
+    assert int(np.frombuffer(h[8:16].tobytes(), np.uint64)[0]) == len(data)
+    o = out.cpu().numpy()
+    assert o[:len(data)].tobytes() == data
+    assert (o[len(data):] == 0xA5).all()
+
+
 def test_dict_max_distance_tokens(enc):
     """A block equal to its predecessor: position 0 matches at distance exactly 32768."""
     text = D.gen_text(40000, 13).tobytes()

@@ -143,6 +143,24 @@ def test_no_cpu_fallback_without_gpu():
     os.close(r)
 
 
+def test_bad_stats_mode_fails_before_encoding(tmp_path, monkeypatch):
+    """An unknown DMX_STATS value is rejected with -E_INVAL before anything is read, encoded
+    or written (no GPU needed: the check comes first)."""
+    monkeypatch.setenv("DMX_STATS", "bogus")
+    fi, fo, fs = tmp_path / "in", tmp_path / "out", tmp_path / "st"
+    fi.write_bytes(b"hello hello hello")
+    a = os.open(fi, os.O_RDONLY)
+    b = os.open(fo, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    c = os.open(fs, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    try:
+        assert D.deflate_compress(a, b, c, 32768, 0) == -D.E["E_INVAL"]
+        assert os.lseek(a, 0, os.SEEK_CUR) == 0
+    finally:
+        for x in (a, b, c):
+            os.close(x)
+    assert fo.read_bytes() == b"" and fs.read_bytes() == b""
+
+
 def test_product_does_not_reference_oracle():
     """The shipped package never imports or links the oracle."""
     pkg = os.path.join(REPO, "deflate_compression_amd")
