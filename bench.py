@@ -235,19 +235,12 @@ def cpu_baselines(data, args, budget_s: float):
     parse = parse_str(args)
     same = (args.max_chain, bool(args.lazy), bool(args.split), bool(args.dict), bool(args.store_check),
             bool(args.deep))
-    r, _, z = leg(*same, budget_s, f"compress ({parse}: the GPU line's parse)", info["threads"], True)
+    # the box's CPU share (OMP_NUM_THREADS = the cgroup quota): more threads than that only
+    # oversubscribe the quota
+    best_thr = info["share_threads"]
+    r, _, z = leg(*same, budget_s, f"compress ({parse}: the GPU line's parse)", best_thr, True)
     r["parse"] = parse
     out["same_parse_stream"] = z
-    out["all_cores"] = r
-    best_thr = info["threads"]
-    if info["share_threads"] != info["threads"]:
-        r2, _, z2 = leg(*same, budget_s, f"compress ({parse}: the GPU line's parse)", info["share_threads"], z is None)
-        r2["parse"] = parse
-        out["share"] = r2
-        if z is None:
-            out["same_parse_stream"] = z2
-        if r2["value"] > r["value"]:   # more threads than the cgroup's CPUs only oversubscribe them
-            r, best_thr = r2, info["share_threads"]
     out["same_parse"] = r
     r, done, z = leg(0, False, False, False, False, False, budget_s,
                      "compress (the reference's exhaustive greedy parse + Huffman/emitter)", best_thr, True)
@@ -401,6 +394,9 @@ def main() -> int:
     # JSON line is written to the saved original.
     argv = sys.argv[1:]
     args = parse_args(argv)
+    # OpenMP threads (the oracle's CPU legs) that spin after a parallel region eat the cgroup's
+    # CPU quota and starve the host threads of the GPU legs: passive waiting, before libgomp loads
+    os.environ.setdefault("OMP_WAIT_POLICY", "PASSIVE")
     if args.gpus < 1:
         log("bench: --gpus must be >= 1")
         return 2
@@ -757,17 +753,18 @@ def main() -> int:
         cpu, info = ({}, cpu_info())
         e2e = zl6 = real = None
         if world == 1 and args.cpu_budget > 0:
-            cpu, info = cpu_baselines(host, args, args.cpu_budget)
+            # the GPU-side legs first: the CPU legs' threads must not share the host with them
             try:
                 e2e = end_to_end(host, args)
             except Exception as e:  # pragma: no cover
                 log("end-to-end fd API leg failed:", e)
-            zl6 = len(zlib.compress(host.tobytes(), 6))   # context: zlib -6 on the same input
             if args.real_text and args.workload == "text":
                 real = real_text_leg(flags, args, dev, local, stream)
                 if not (real["parity_vs_port"] and real["inflates"]):
                     log("ERROR: real-text stream differs from the port's or does not inflate")
                     ok = False
+            cpu, info = cpu_baselines(host, args, args.cpu_budget)
+            zl6 = len(zlib.compress(host.tobytes(), 6))   # context: zlib -6 on the same input
         base = cpu.get("same_parse")
         size_pct = s_ref_bytes = None
         # full-size parity witness: the port's stream at the GPU line's exact parse,
@@ -847,8 +844,6 @@ def main() -> int:
             "zlib6": None if zl6 is None else {"ratio": round(zl6 / n, 5), "compressed_bytes": zl6,
                                                  "ours_vs_zlib6_pct": round((out_len / zl6 - 1) * 100, 3)},
             "cpu_baseline": base,
-            "cpu_baseline_all_affinity": cpu.get("all_cores"),
-            "cpu_baseline_share": cpu.get("share"),
             "cpu_baseline_exhaustive": cpu.get("exhaustive"),
             "real_text": real,
             "cpu_baseline_reference": cpu.get("reference"),

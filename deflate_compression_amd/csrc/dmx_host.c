@@ -21,9 +21,8 @@
 #include "dmx_internal.h"
 
 /* from dmx_kernels.hip */
-dmx_ctx* dmx_cached_ctx(int device, uint64_t max_input, int* err);
-void dmx_cached_lock(void);
-void dmx_cached_unlock(void);
+int dmx_encode_fd_cb(int fd_in, int fd_out, const dmx_opts* opts, uint64_t chunk,
+                     int (*cb)(void* user, dmx_ctx* c, uint64_t chunk_bytes, uint64_t chunk_off), void* user);
 
 struct deflate_compr {
     int fd_in, fd_out, fd_stats;
@@ -42,31 +41,6 @@ void deflate_compr_init(deflate_compr_t* com, int fd_in, int fd_out, int fd_stat
 
 void deflate_compr_deinit(deflate_compr_t* com) {
     if (com) memset(com, 0, sizeof(*com));
-}
-
-static int read_all(int fd, uint8_t** buf, uint64_t* n) {
-    uint64_t cap = 1 << 20, len = 0;
-    uint8_t* b = (uint8_t*)malloc(cap);
-    if (!b) return -E_MALLOC;
-    for (;;) {
-        if (len == cap) {
-            uint8_t* nb = (uint8_t*)realloc(b, cap * 2);
-            if (!nb) { free(b); return -E_MALLOC; }
-            b = nb;
-            cap *= 2;
-        }
-        ssize_t r = read(fd, b + len, cap - len);
-        if (r < 0) {
-            if (errno == EINTR) continue;
-            free(b);
-            return -E_NEXIST;
-        }
-        if (r == 0) break;
-        len += (uint64_t)r;
-    }
-    *buf = b;
-    *n = len;
-    return 0;
 }
 
 static int write_all(int fd, const void* p, uint64_t n) {
@@ -115,24 +89,28 @@ static void h_dist_sym(int dist, int* sym, int* eb) {
  *                   blocks: 8 per byte),
  *       d_bits    = distance code bits + distance extra bits of every match so far.
  * The fields are int (deflate_ext.h:19-31).  A record whose bytes or *_bits would exceed
- * INT_MAX is never written: the records before it are, and the call returns -E_RANGE. */
-static int write_stats(dmx_ctx* c, int fd, uint64_t n, int sw) {
+ * INT_MAX is never written: the records before it are, and the call returns -E_RANGE.
+ * The records are written chunk by chunk as the stream is encoded (dmx_encode_fd_cb): the
+ * state (the estimator's trees, the exact running sums) carries over the chunks. */
+typedef struct {
+    int fd, exact, sw, range;   /* range: a record did not fit; none after it */
+    dmx_refest* est;
+    uint32_t* tok;
+    struct compress_stats* rec;
+    long long tree_bits, ll_bits, d_bits;
+} stats_writer;
+
+static int stats_chunk(void* user, dmx_ctx* c, uint64_t n, uint64_t base) {
+    stats_writer* W = (stats_writer*)user;
+    const int sw = W->sw;
     const uint32_t nblk = (uint32_t)((n + (uint64_t)sw - 1) / (uint64_t)sw);
-    if (!nblk) return 0;
-    const char* mode = getenv("DMX_STATS");
-    const int exact = mode && strcmp(mode, "exact") == 0;
-    if (mode && *mode && !exact && strcmp(mode, "ref") != 0) return -E_INVAL;
-    uint32_t* tok = (uint32_t*)malloc(sizeof(uint32_t) * DMX_BLK);
-    struct compress_stats* rec = (struct compress_stats*)malloc(sizeof(struct compress_stats) * DMX_BLK);
-    dmx_refest* est = exact ? NULL : dmx_refest_create();
-    int r = 0;
-    long long tree_bits = 0, ll_bits = 0, d_bits = 0;   /* exact: over the whole stream */
-    if (!tok || !rec || (!exact && !est)) r = -E_MALLOC;
-    for (uint32_t b = 0; !r && b < nblk; b++) {
+    uint32_t* tok = W->tok;
+    struct compress_stats* rec = W->rec;
+    for (uint32_t b = 0; !W->range && b < nblk; b++) {
         int nt = dmx_last_tokens(c, b, tok, DMX_BLK);
-        if (nt < 0) { r = nt; break; }
+        if (nt < 0) return nt;
         uint32_t lim = (uint32_t)nt;   /* records of this block that fit the int fields */
-        uint64_t pos = (uint64_t)b * (uint64_t)sw;
+        uint64_t pos = base + (uint64_t)b * (uint64_t)sw;
         for (uint32_t k = 0; k < (uint32_t)nt; k++) {
             const uint32_t t = tok[k];
             if (pos + 1 > (uint64_t)INT_MAX) { lim = k; break; }
@@ -147,58 +125,58 @@ static int write_stats(dmx_ctx* c, int fd, uint64_t n, int sw) {
                 pos += t & 0x1FF;
             }
         }
-        if (!exact) {
+        if (!W->exact) {
             uint32_t nf = 0;
-            const int e = dmx_refest_feed(est, tok, lim, rec, &nf);
-            if (e && e != -E_RANGE) { r = e; break; }
+            const int e = dmx_refest_feed(W->est, tok, lim, rec, &nf);
+            if (e && e != -E_RANGE) return e;
             lim = nf;
         } else {
             int nsub = 1;
-            for (int sb = 0; !r && sb < nsub; sb++) {
+            for (int sb = 0; sb < nsub; sb++) {
                 uint8_t lens[316];
                 uint32_t range[2], bt = 0, hb = 0;
                 nsub = dmx_last_subblock(c, b, (uint32_t)sb, range, &bt, &hb, lens);
-                if (nsub < 0) { r = nsub; break; }
-                tree_bits += bt == 2 ? (long long)hb : 3;
+                if (nsub < 0) return nsub;
+                W->tree_bits += bt == 2 ? (long long)hb : 3;
                 for (uint32_t k = range[0]; k < range[1] && k < lim; k++) {
                     const uint32_t t = tok[k];
                     if ((t >> 9) == 0) {
-                        ll_bits += bt == 0 ? 8 : (long long)lens[t & 0xFF];
+                        W->ll_bits += bt == 0 ? 8 : (long long)lens[t & 0xFF];
                     } else {
                         const int len = (int)(t & 0x1FF), dist = (int)(t >> 9);
                         int sy, eb;
                         if (bt == 0) {          /* stored block: the bytes themselves */
-                            ll_bits += 8 * len;
+                            W->ll_bits += 8 * len;
                         } else {
                             h_len_sym(len, &sy, &eb);
-                            ll_bits += lens[sy] + eb;
+                            W->ll_bits += lens[sy] + eb;
                             h_dist_sym(dist, &sy, &eb);
-                            d_bits += lens[DMX_DIST0 + sy] + eb;
+                            W->d_bits += lens[DMX_DIST0 + sy] + eb;
                         }
                     }
-                    if (tree_bits > INT_MAX || ll_bits > INT_MAX || d_bits > INT_MAX) { lim = k; break; }
-                    rec[k].tree_bits = (int)tree_bits;
-                    rec[k].ll_bits = (int)ll_bits;
-                    rec[k].d_bits = (int)d_bits;
+                    if (W->tree_bits > INT_MAX || W->ll_bits > INT_MAX || W->d_bits > INT_MAX) { lim = k; break; }
+                    rec[k].tree_bits = (int)W->tree_bits;
+                    rec[k].ll_bits = (int)W->ll_bits;
+                    rec[k].d_bits = (int)W->d_bits;
                 }
             }
-            if (r) break;
         }
-        r = write_all(fd, rec, sizeof(struct compress_stats) * (uint64_t)lim);
-        if (!r && lim < (uint32_t)nt) r = -E_RANGE;
+        const int e = write_all(W->fd, rec, sizeof(struct compress_stats) * (uint64_t)lim);
+        if (e) return e;
+        if (lim < (uint32_t)nt) W->range = 1;   /* the stream goes on; no more records */
     }
-    free(tok); free(rec);
-    dmx_refest_destroy(est);
-    return r;
+    return 0;
 }
 
 int deflate_compress(int fd_in, int fd_out, int fd_stats, swi sw, int ops) {
     (void)ops; /* unused by the reference's compress too */
     int swv = sw == 0 ? DMX_BLK : (int)sw;
     if (swv > DMX_BLK) return -E_RANGE;
+    int exact = 0;
     if (fd_stats >= 0) {   /* an unknown DMX_STATS mode fails before anything is encoded or written */
         const char* mode = getenv("DMX_STATS");
         if (mode && *mode && strcmp(mode, "exact") != 0 && strcmp(mode, "ref") != 0) return -E_INVAL;
+        exact = mode && strcmp(mode, "exact") == 0;
     }
     const char* mc = getenv("DMX_MAX_CHAIN");
     dmx_opts o;
@@ -219,35 +197,32 @@ int deflate_compress(int fd_in, int fd_out, int fd_stats, swi sw, int ops) {
     o.reserved = 0;
     o.dict = NULL;
     o.dict_len = 0;
-    if (fd_stats < 0) {   /* streaming: chunks of DMX_CHUNK_MB MiB (default 16) through pinned buffers */
-        const char* cm = getenv("DMX_CHUNK_MB");
-        const uint64_t mb = cm && atoi(cm) > 0 ? (uint64_t)atoi(cm) : 16u;
+    /* streaming: chunks of DMX_CHUNK_MB MiB (default 16) through pinned buffers; each chunk a
+     * shard of one zlib stream (DESIGN.md §6 framing), so any input size streams */
+    const char* cm = getenv("DMX_CHUNK_MB");
+    const uint64_t mb = cm && atoi(cm) > 0 ? (uint64_t)atoi(cm) : 16u;
+    if (fd_stats < 0) {
         int devs[64];
         const int nd = dmx_devices_from_env(devs, 64);   /* DMX_DEVICES: one host thread per GPU */
         if (nd < 0) return nd;
         if (nd > 0) return dmx_encode_fd_multi(fd_in, fd_out, &o, mb << 20, devs, nd);
         return dmx_encode_fd(fd_in, fd_out, &o, mb << 20);
     }
-    uint8_t* in = NULL;
-    uint64_t n = 0;
-    int r = read_all(fd_in, &in, &n);
-    if (r) return r;
-    uint64_t cap = dmx_max_compressed(n, swv);
-    uint8_t* out = (uint8_t*)malloc(cap);
-    if (!out) { free(in); return -E_MALLOC; }
-    uint64_t out_len = 0;
-    dmx_cached_lock();   /* the stats read this encode's tokens back from the cached context */
-    r = dmx_encode_host(in, n, out, cap, &out_len, &o);
-    if (!r && fd_out >= 0) r = write_all(fd_out, out, out_len);
-    if (!r && fd_stats >= 0) {
-        const char* dev_s = getenv("DMX_DEVICE");
-        int err = 0;
-        dmx_ctx* c = dmx_cached_ctx(dev_s ? atoi(dev_s) : 0, n, &err);
-        r = c ? write_stats(c, fd_stats, n, swv) : err;
-    }
-    dmx_cached_unlock();
-    free(in);
-    free(out);
+    /* with the records: each chunk's tokens become records before the next chunk encodes */
+    stats_writer W;
+    memset(&W, 0, sizeof(W));
+    W.fd = fd_stats;
+    W.exact = exact;
+    W.sw = swv;
+    W.tok = (uint32_t*)malloc(sizeof(uint32_t) * DMX_BLK);
+    W.rec = (struct compress_stats*)malloc(sizeof(struct compress_stats) * DMX_BLK);
+    W.est = exact ? NULL : dmx_refest_create();
+    int r = (!W.tok || !W.rec || (!exact && !W.est)) ? -E_MALLOC : 0;
+    if (!r) r = dmx_encode_fd_cb(fd_in, fd_out, &o, mb << 20, stats_chunk, &W);
+    if (!r && W.range) r = -E_RANGE;
+    free(W.tok);
+    free(W.rec);
+    dmx_refest_destroy(W.est);
     return r;
 }
 

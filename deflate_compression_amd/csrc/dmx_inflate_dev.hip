@@ -488,7 +488,8 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 //   IX_SYM   a long, end-of-block or invalid literal/length code
 //   IX_SEG   a refill at a token start that needs a stream segment it does not rotate into
 //            (the segment after next is not wholly inside the stream)
-//   IX_LIM   op >= lim at a literal or op >= limm at a length (flush, or near the capacity)
+//   IX_LIM   op >= lim at a literal or a length (a flush the run does not do itself, or the
+//            capacity), or a length that does not fit the capacity
 //   IX_DIST  length decoded into len; the distance code is long or invalid
 //   IX_MATCH len and dist decoded: a distance before the output
 // Hazards: a lane select written by SALU is 4+ instructions old at each v_readlane (s_nop 3
@@ -536,7 +537,8 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 #define IX_MATCH 5u
 
 template <uint32_t W, bool CELL>
-__device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t lim, uint32_t limm, uint32_t dfl,
+__device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t& lim, uint32_t& fl, uint32_t capr,
+                                             uint32_t fok, uint64_t gfl, uint32_t dfl,
                                              uint64_t tgl, uint64_t tgd, uint32_t toff, uint32_t lane, uint64_t gpos0,
                                              uint32_t& len, uint32_t& dist) {
     uint32_t ex;
@@ -671,11 +673,14 @@ __device__ __forceinline__ int iblock(InfLDS<W, typename std::conditional<CELL, 
     const uint64_t tgl = (uint64_t)(uintptr_t)gt, tgd = tgl + 4 * (1u << IFB);   // the tables' words, 4 bytes a lane
     const uint32_t dfl = o.ob != 0 ? 0x40000000u : 0u;   // stream mode: sources before ob exist
     const uint64_t gpos0 = (uint64_t)(uintptr_t)(o.out + CS * (o.base + o.ob));
+    // the run flushes half rings itself (no Adler sums; a 16-byte aligned output)
+    const uint32_t fok = (uint32_t)__builtin_amdgcn_readfirstlane((RING && !ADLER && (gpos0 & 15) == 0) ? 1 : 0);
     for (;;) {
-        const uint32_t lim = RING ? min(capr, o.fl + FL) : capr;
-        const uint32_t limm = rfl(min(lim, capr >= 258 ? capr - 258 : 0u));   // below it any length fits
+        uint32_t lim = RING ? min(capr, o.fl + FL) : capr, fl = o.fl;
         uint32_t len, dist;
-        const uint32_t ex = isym_run<W, CELL>(r, op, lim, limm, dfl, tgl, tgd, lane * 4, lane, gpos0, len, dist);
+        const uint32_t ex = isym_run<W, CELL>(r, op, lim, fl, capr, fok, gpos0, dfl, tgl, tgd, lane * 4, lane, gpos0, len,
+                                              dist);
+        o.fl = fl;
         if (ex == IX_SEG) {   // a refill at a token start that the run does not rotate into
             ib_refill(r);
             continue;

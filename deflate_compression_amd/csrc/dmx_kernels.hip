@@ -644,6 +644,165 @@ __device__ __forceinline__ void ext_queue(MatchLDS& L, uint32_t bn, uint32_t K, 
     __builtin_amdgcn_wave_barrier();
 }
 
+// ---- Short chains K = 6..8 (the bench's parse), two entries per lane ----------------------
+// Lane l holds the consecutive entries A = 2l' and B = 2l' + 1 of S (l' = l - HL); lanes below
+// HL = ceil(K/2) are the halo.  Candidate j of A is B of lane l - (j+1)/2 (j odd) or A of lane
+// l - j/2 (j even); of B, A of lane l - (j-1)/2 (j odd) or B of lane l - j/2 (j even).  So the
+// wave shifts SA_s = A shifted down s lanes and SB_s serve both entries: per step pair one
+// shift of each stream and four compares -- one DPP move per compare instead of two, half the
+// halo lanes (HL of 64 instead of K), and the chunk's bookkeeping spread over 2 (64 - HL)
+// entries instead of 64 - K.  Same keys and results as the one-entry-per-lane path.
+#define PSHR(x) ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)(x), 0x138, 0xF, 0xF, true))   // wave_shr:1
+template <int SJ>
+__device__ __forceinline__ uint32_t pkey(uint32_t e0, uint32_t e1, uint32_t c0, uint32_t c1) {
+    const uint32_t mb = min(min(ffbl_hw(e0 ^ c0), __builtin_elementwise_add_sat(ffbl_hw(e1 ^ c1), 32u)), 64u);
+    uint32_t key;
+    asm("v_and_or_b32 %0, %1, -8, %2" : "=v"(key) : "v"(mb), "n"(SJ));
+    return key;
+}
+// the first chunk (GUARD: candidates below entry 0) and chunks holding one of the last CBS - 1
+// positions (CLAMP: lengths capped at the block end), per entry
+template <bool GUARD, bool CLAMP>
+__device__ __forceinline__ uint32_t pkey_g(uint32_t e0, uint32_t e1, uint32_t c0, uint32_t c1, uint32_t j, uint32_t nc,
+                                           uint32_t lim) {
+    const uint32_t mb = min(min(ffbl_hw(e0 ^ c0), __builtin_elementwise_add_sat(ffbl_hw(e1 ^ c1), 32u)), 64u);
+    uint32_t key = CLAMP ? ((min(mb >> 3, lim) << 3) | (8u - j)) : ((mb & ~7u) | (8u - j));
+    if (GUARD) key = j <= nc ? key : 0u;
+    return key;
+}
+// step pair s (template recursion: the keys' 8 - j are inline constants); on entry pa = SA_{s-1},
+// sb = SB_{s-1}
+template <int KK, int S, bool GEN, bool GUARD, bool CLAMP>
+__device__ __forceinline__ void pair_from(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1, uint32_t& pa0,
+                                          uint32_t& pa1, uint32_t& sb0, uint32_t& sb1, uint32_t& ka, uint32_t& kb,
+                                          uint32_t nca, uint32_t ncb, uint32_t lima, uint32_t limb) {
+    if constexpr (2 * S - 1 <= KK) {
+        constexpr int J1 = 2 * S - 1, J2 = 2 * S;
+        sb0 = PSHR(sb0);
+        sb1 = PSHR(sb1);   // SB_S
+        uint32_t ta, tb;
+        if constexpr (GEN) {
+            ta = pkey_g<GUARD, CLAMP>(a0, a1, sb0, sb1, J1, nca, lima);   // A vs B of lane l - S
+            tb = pkey_g<GUARD, CLAMP>(b0, b1, pa0, pa1, J1, ncb, limb);   // B vs A of lane l - S + 1
+        } else {
+            ta = pkey<8 - J1>(a0, a1, sb0, sb1);
+            tb = pkey<8 - J1>(b0, b1, pa0, pa1);
+        }
+        if constexpr (J2 <= KK) {
+            pa0 = PSHR(pa0);
+            pa1 = PSHR(pa1);   // SA_S
+            uint32_t ua, ub;
+            if constexpr (GEN) {
+                ua = pkey_g<GUARD, CLAMP>(a0, a1, pa0, pa1, J2, nca, lima);   // A vs A of lane l - S
+                ub = pkey_g<GUARD, CLAMP>(b0, b1, sb0, sb1, J2, ncb, limb);   // B vs B of lane l - S
+            } else {
+                ua = pkey<8 - J2>(a0, a1, pa0, pa1);
+                ub = pkey<8 - J2>(b0, b1, sb0, sb1);
+            }
+            ka = max(ka, max(ta, ua));
+            kb = max(kb, max(tb, ub));
+        } else {
+            ka = max(ka, ta);
+            kb = max(kb, tb);
+        }
+        pair_from<KK, S + 1, GEN, GUARD, CLAMP>(a0, a1, b0, b1, pa0, pa1, sb0, sb1, ka, kb, nca, ncb, lima, limb);
+    }
+}
+// Result of entry k at position i without a queued extension (store_short's, returning the
+// winner nibble instead of storing it: both entries of a lane share one nibble word).
+template <bool DICT>
+__device__ __forceinline__ uint32_t short_result(MatchLDS& L, uint32_t k, uint32_t i, uint32_t jkey,
+                                                 const uint32_t* __restrict__ hbk) {
+    const uint32_t m = jkey >> 3;
+    uint32_t len = m >= 3 ? m : 0u, j = m >= 3 ? 8u - (jkey & 7u) : 0u;
+    if (DICT) {
+        const uint32_t hw = hbk[k];
+        if ((hw >> 16) > len) { len = hw >> 16; j = NIB_HIST; }
+    }
+    if (len == 0) {
+        atomicOr(&L.lit[i >> 5], 1u << (i & 31));
+        L.len8[i] = 0;
+        return 0;
+    }
+    L.len8[i] = (uint8_t)(len - 3);
+    return j;
+}
+template <bool DICT, int KK>
+__device__ __forceinline__ uint32_t search_pairs(MatchLDS& L, uint32_t bn, uint32_t tid, bool stamp, uint64_t& tdef,
+                                                 const uint32_t* __restrict__ hbk) {
+    constexpr uint32_t HL = (KK + 1) / 2, OWN = 2 * (64 - HL);
+    const uint32_t lane = tid & 63, wave = wave_of(tid);
+    const uint32_t nvalid = bn > 2 ? bn - 2 : 0;
+    uint32_t* Qw = L.tsm + (wave << 6);   // the extension queue (P2 arrays are free during the search)
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t qn = 0, iters = 0;
+    for (uint32_t base = wave * OWN;; base += MW * OWN) {
+        const bool more = base < nvalid;   // wave-uniform
+        const int ea = (int)base + 2 * ((int)lane - (int)HL);
+        const uint32_t ka = (uint32_t)ea, kb = ka + 1;
+        const bool own = lane >= HL;
+        const bool actA = more && own && ka < nvalid, actB = more && own && kb < nvalid;
+        uint32_t jA = 0, jB = 0, limA = 0, limB = 0, iA = 0, iB = 0;
+        if (more) {
+            uint32_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+            if (ea >= 0 && ka < nvalid) {   // both positions in one aligned LDS word
+                const uint32_t pr = reinterpret_cast<const uint32_t*>(L.sorted)[ka >> 1];
+                iA = pr & 0xFFFFu;
+                const uint64_t va = ld8(L.data, iA);
+                a0 = (uint32_t)va;
+                a1 = (uint32_t)(va >> 32);
+                if (kb < nvalid) {
+                    iB = pr >> 16;
+                    const uint64_t vb = ld8(L.data, iB);
+                    b0 = (uint32_t)vb;
+                    b1 = (uint32_t)(vb >> 32);
+                }
+            }
+            if (actA) limA = (bn - iA) < MAXLEN ? (bn - iA) : MAXLEN;
+            if (actB) limB = (bn - iB) < MAXLEN ? (bn - iB) : MAXLEN;
+            iters += 2 * KK;
+            {   // sort check: A after B of the lane below, B after A
+                const uint32_t skA = sort_key(a0, iA), skB = sort_key(b0, iB);
+                const uint32_t pk = PSHR(skB);
+                if (__ballot((actA && ka >= 1 && pk > skA) || (actB && skA > skB))) L.sortbad = 1;
+            }
+            uint32_t pa0 = a0, pa1 = a1, sb0 = b0, sb1 = b1;
+            if (base == 0)
+                pair_from<KK, 1, true, true, true>(a0, a1, b0, b1, pa0, pa1, sb0, sb1, jA, jB, min(ka, (uint32_t)KK),
+                                                   min(kb, (uint32_t)KK), limA, limB);
+            else if (__ballot((actA && limA < CBS) || (actB && limB < CBS)))
+                pair_from<KK, 1, true, false, true>(a0, a1, b0, b1, pa0, pa1, sb0, sb1, jA, jB, KK, KK, limA, limB);
+            else
+                pair_from<KK, 1, false, false, false>(a0, a1, b0, b1, pa0, pa1, sb0, sb1, jA, jB, 0, 0, 0, 0);
+        }
+        // a candidate equal in all CBS bytes (key >= 64): the entry is queued for the LDS
+        // extension (unless the block end caps it there); A's items, then B's
+        const bool pushA = actA && jA >= (CBS << 3) && limA > CBS, pushB = actB && jB >= (CBS << 3) && limB > CBS;
+        const uint64_t pmA = __ballot(pushA), pmB = __ballot(pushB);
+#pragma nounroll
+        for (uint32_t h = 0; h < 2; h++) {   // (one call site of ext_queue)
+            const uint64_t pm = h ? pmB : pmA;
+            const uint32_t npx = (uint32_t)__popcll(pm);
+            if (qn + npx > 64 || (!more && qn)) {
+                const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
+                ext_queue<DICT, false>(L, bn, KK, Qw, qn, lane, hbk);
+                if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
+                qn = 0;
+            }
+            if (!more) break;
+            const bool p = h ? pushB : pushA;
+            if (p) lds_st(&Qw[qn + (uint32_t)__popcll(pm & lt)], (h ? kb : ka) | ((8u - ((h ? jB : jA) & 7u)) << 15));
+            qn += npx;
+        }
+        if (!more) break;
+        uint32_t nib = 0;
+        if (actA && !pushA) nib |= short_result<DICT>(L, ka, iA, jA, hbk) << ((ka & 7u) << 2);
+        if (actB && !pushB) nib |= short_result<DICT>(L, kb, iB, jB, hbk) << ((kb & 7u) << 2);
+        if (nib) atomicOr(&nib_words(L)[ka >> 3], nib);
+    }
+    return iters;
+}
+
 template <bool DICT, bool RUNS, int NB = 3>
 __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint16_t* __restrict__ pg,
                                      uint32_t tid, bool stamp, uint64_t& tdef, const uint32_t* __restrict__ hbk,
@@ -654,6 +813,13 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
     const uint32_t nvalid = bn > 2 ? bn - 2 : 0;   // positions with a full trigram = entries of S
     uint32_t iters = 0;
     if (RUNS) build_chg(L, bn, tid);
+#ifndef DMX_NO_PAIRS
+    if (!RUNS && NB == 3 && K >= 6 && K <= 8) {   // two entries per lane (search_pairs)
+        iters = K == 8 ? search_pairs<DICT, 8>(L, bn, tid, stamp, tdef, hbk)
+              : K == 7 ? search_pairs<DICT, 7>(L, bn, tid, stamp, tdef, hbk)
+                       : search_pairs<DICT, 6>(L, bn, tid, stamp, tdef, hbk);
+    } else
+#endif
     if (K <= KE) {
         // bounded mode with a short chain: chunks of 64-K owned entries, halo embedded.
         // Entries with a candidate equal in all CBS register bytes need the LDS extension; they
@@ -2088,7 +2254,9 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         for (int w = 0; w < MW; w++) nrun += L.wexit[w];
         const bool runs = kb > 0 && kb <= KE && nrun * 4 >= ((bn + 15) >> 4);
         if (kb > 0 && kb <= KE) {   // the winners' nibbles (bstart is free after P0)
-            reinterpret_cast<uint4*>(nib_words(L))[tid] = make_uint4(0, 0, 0, 0);
+            uint32_t z = 0;
+            asm volatile("" : "+v"(z));   // (else the compiler keeps a zero quad in a scratch slot)
+            reinterpret_cast<uint4*>(nib_words(L))[tid] = make_uint4(z, z, z, z);
             __syncthreads();
         }
         const uint32_t its = runs ? search_positions<DICT, true>(L, bn, kb, pg, tid, dbg != nullptr, tdef, hbk)
@@ -3634,6 +3802,7 @@ struct dmx_ctx {
     hipStream_t fd_cs;    // multi-GPU worker: D2H copies beside the next encode
     hipEvent_t fd_ev[2];  // multi-GPU worker: encode i done
     uint64_t fd_chunk, fd_ocap;
+    struct FdPipe* fdp;   // dmx_encode_fd's pipeline buffers (single device)
     uint16_t* chs;        // DMX_F_DICT: (cap_chain) x DMX_BLK bucket-sorted positions per block (+ the dict)
     uint16_t* che;        // DMX_F_DICT: (cap_chain) x DMX_NBUCKET bucket ends
     uint64_t cap_chain;
@@ -3648,6 +3817,9 @@ struct dmx_ctx {
     double stage_ms[6];
     uint32_t stage_n;
 };
+
+struct FdPipe;
+static void fdp_free(FdPipe* P);
 
 // ---- fault injection (tests): DMX_FAULT="malloc:N" makes the N-th device / pinned allocation
 // from now fail, "launch:N" the N-th encode launch check; dmx_fault_set() sets it at run time.
@@ -3842,6 +4014,7 @@ extern "C" void dmx_ctx_destroy(dmx_ctx* c) {
         if (c->fd_ev[k]) (void)hipEventDestroy(c->fd_ev[k]);
     }
     if (c->fd_cs) (void)hipStreamDestroy(c->fd_cs);
+    fdp_free(c->fdp);
     if (c->chs) (void)hipFree(c->chs);
     if (c->che) (void)hipFree(c->che);
     if (c->split) (void)hipFree(c->split);
@@ -4196,7 +4369,7 @@ static int write_full(int fd, const uint8_t* p, uint64_t n) {
 
 // Reader: a regular file of known size is read with FD_READERS parallel preads per chunk;
 // anything else (pipes) with read() and a one-byte lookahead.
-#define FD_READERS 4
+#define FD_READERS 8
 struct FdReader {
     int fd;
     bool seekable;
@@ -4233,7 +4406,7 @@ static int64_t fd_read_chunk(FdReader* R, uint8_t* b, uint64_t chunk) {
         const uint64_t piece = ((len + FD_READERS - 1) / FD_READERS + 4095) & ~4095ull;
         PreadJob jobs[FD_READERS];
         pthread_t th[FD_READERS];
-        bool started[FD_READERS] = {false, false, false, false};
+        bool started[FD_READERS] = {};
         int nj = 0;
         for (uint64_t o = 0; o < len; o += piece, nj++) {
             jobs[nj] = {R->fd, b + o, R->off + o, (len - o) < piece ? (len - o) : piece, 0};
@@ -4314,14 +4487,188 @@ static int fd_buffers(dmx_ctx* c, uint64_t chunk, uint64_t ocap) {
     return 0;
 }
 
-static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts, uint64_t chunk);
+// --- the single-device fd path (dmx_encode_fd): a five-stage pipeline ---
+// reader thread   chunk j of fd_in -> pinned input slot j % FDP_NIN (FD_READERS parallel preads
+//                 on a regular file), running ahead of the device;
+// H2D stream      slot -> device input j % FDP_NDIN;
+// encode stream   the context's stream: encode j (its history, with DMX_F_DICT, is the previous
+//                 device input's tail) -> device output j % 2, result -> pinned record j % 2;
+// D2H stream      device output -> pinned output slot j % FDP_NOUT, as soon as the host has
+//                 read the chunk's length (the next chunk is already encoding);
+// writer thread   slots to fd_out in order.
+// The chunks are shards of one zlib stream (header on the first, a sync flush after every
+// chunk but the last, BFINAL on the last; Adler-32 combined here), so the stream is
+// byte-identical to the sequential loop's.  A chunk callback (the compress_stats writer)
+// makes the loop serial: chunk j's tokens are read from the context before j + 1 encodes.
+#define FDP_NIN 3
+#define FDP_NOUT 3
+#define FDP_NDIN 3
+struct FdPipe {
+    uint64_t chunk, ocap;
+    uint8_t* hin[FDP_NIN];      // pinned input slots
+    uint8_t* hout[FDP_NOUT];    // pinned output slots
+    void* din[FDP_NDIN];        // device input chunks
+    void* dout[2];              // device output chunks
+    dmx_result* hres[2];        // pinned result records
+    hipStream_t sh, sd;         // H2D and D2H streams
+    hipEvent_t evh[FDP_NIN];    // H2D from input slot k done
+    hipEvent_t eve[2];          // encode j (and its result copy) done
+    hipEvent_t evd[2];          // D2H from device output k done
+    hipEvent_t evo[FDP_NOUT];   // D2H into output slot k done
+};
+
+static void fdp_free(FdPipe* P) {
+    if (!P) return;
+    for (int k = 0; k < FDP_NIN; k++) {
+        if (P->hin[k]) (void)hipHostFree(P->hin[k]);
+        if (P->evh[k]) (void)hipEventDestroy(P->evh[k]);
+    }
+    for (int k = 0; k < FDP_NOUT; k++) {
+        if (P->hout[k]) (void)hipHostFree(P->hout[k]);
+        if (P->evo[k]) (void)hipEventDestroy(P->evo[k]);
+    }
+    for (int k = 0; k < FDP_NDIN; k++)
+        if (P->din[k]) (void)hipFree(P->din[k]);
+    for (int k = 0; k < 2; k++) {
+        if (P->dout[k]) (void)hipFree(P->dout[k]);
+        if (P->hres[k]) (void)hipHostFree(P->hres[k]);
+        if (P->eve[k]) (void)hipEventDestroy(P->eve[k]);
+        if (P->evd[k]) (void)hipEventDestroy(P->evd[k]);
+    }
+    if (P->sh) (void)hipStreamDestroy(P->sh);
+    if (P->sd) (void)hipStreamDestroy(P->sd);
+    free(P);
+}
+
+// The context's pipeline buffers for chunks of `chunk` bytes (kept across calls: pinning
+// ~100 MB costs milliseconds).
+static int fdp_get(dmx_ctx* c, uint64_t chunk, uint64_t ocap, FdPipe** out) {
+    if (c->fdp && c->fdp->chunk >= chunk && c->fdp->ocap >= ocap) { *out = c->fdp; return 0; }
+    fdp_free(c->fdp);
+    c->fdp = NULL;
+    FdPipe* P = (FdPipe*)calloc(1, sizeof(FdPipe));
+    if (!P) return -(int)E_MALLOC;
+    int r = 0;
+    for (int k = 0; !r && k < FDP_NIN; k++) {
+        if (hip_fail(dmx_host_malloc((void**)&P->hin[k], chunk + 16), "hipHostMalloc")) r = -(int)E_MALLOC;
+        else if (hip_fail(hipEventCreateWithFlags(&P->evh[k], hipEventDisableTiming), "hipEventCreate")) r = -(int)E_DEVICE;
+    }
+    for (int k = 0; !r && k < FDP_NOUT; k++) {
+        if (hip_fail(dmx_host_malloc((void**)&P->hout[k], ocap), "hipHostMalloc")) r = -(int)E_MALLOC;
+        else if (hip_fail(hipEventCreateWithFlags(&P->evo[k], hipEventDisableTiming), "hipEventCreate")) r = -(int)E_DEVICE;
+    }
+    for (int k = 0; !r && k < FDP_NDIN; k++)
+        if (hip_fail(dmx_malloc(&P->din[k], chunk + 16), "hipMalloc")) r = -(int)E_DEVICE;
+    for (int k = 0; !r && k < 2; k++) {
+        if (hip_fail(dmx_malloc(&P->dout[k], ocap), "hipMalloc")) r = -(int)E_DEVICE;
+        else if (hip_fail(dmx_host_malloc((void**)&P->hres[k], sizeof(dmx_result)), "hipHostMalloc")) r = -(int)E_MALLOC;
+        else if (hip_fail(hipEventCreateWithFlags(&P->eve[k], hipEventDisableTiming), "hipEventCreate") ||
+                 hip_fail(hipEventCreateWithFlags(&P->evd[k], hipEventDisableTiming), "hipEventCreate"))
+            r = -(int)E_DEVICE;
+    }
+    if (!r && (hip_fail(hipStreamCreateWithFlags(&P->sh, hipStreamNonBlocking), "hipStreamCreate") ||
+               hip_fail(hipStreamCreateWithFlags(&P->sd, hipStreamNonBlocking), "hipStreamCreate")))
+        r = -(int)E_DEVICE;
+    if (r) { fdp_free(P); return r; }
+    P->chunk = chunk;
+    P->ocap = ocap;
+    c->fdp = P;
+    *out = P;
+    return 0;
+}
+
+// Host-side hand-off between the main loop and its reader / writer threads.
+struct FdSync {
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    int err;                 // first error (any thread); stops everything
+    uint64_t nread;          // chunks read (slots filled)
+    uint64_t h2d_issued;     // chunks whose H2D was enqueued (evh recorded)
+    uint64_t nposted;        // chunks handed to the writer
+    uint64_t nwritten;       // chunks written
+    int64_t len[FDP_NIN];    // bytes in input slot k
+    bool eof[FDP_NIN];       // nothing after the chunk in slot k
+    uint64_t olen[FDP_NOUT]; // stream bytes in output slot k
+    bool done_reading;
+};
+struct FdReadJob { FdSync* S; FdReader* R; FdPipe* P; uint64_t chunk; };
+struct FdWriteJob { FdSync* S; FdPipe* P; int fd; };
+
+static void fds_fail(FdSync* S, int r) {
+    pthread_mutex_lock(&S->mu);
+    if (!S->err) S->err = r;
+    pthread_cond_broadcast(&S->cv);
+    pthread_mutex_unlock(&S->mu);
+}
+
+static void* fdp_reader(void* a) {
+    FdReadJob* J = (FdReadJob*)a;
+    FdSync* S = J->S;
+    for (uint64_t j = 0;; j++) {
+        const int k = (int)(j % FDP_NIN);
+        pthread_mutex_lock(&S->mu);   // slot k is free once chunk j - FDP_NIN's H2D was enqueued...
+        while (!S->err && j >= FDP_NIN && S->h2d_issued < j - FDP_NIN + 1) pthread_cond_wait(&S->cv, &S->mu);
+        const bool stop = S->err != 0;
+        pthread_mutex_unlock(&S->mu);
+        if (stop) break;
+        // ...and has completed
+        if (j >= FDP_NIN && hip_fail(hipEventSynchronize(J->P->evh[k]), "hipEventSynchronize")) {
+            fds_fail(S, -(int)E_DEVICE);
+            break;
+        }
+        const int64_t len = fd_read_chunk(J->R, J->P->hin[k], J->chunk);
+        if (len < 0) { fds_fail(S, (int)len); break; }
+        pthread_mutex_lock(&S->mu);
+        S->len[k] = len;
+        S->eof[k] = J->R->eof;
+        S->nread = j + 1;
+        pthread_cond_broadcast(&S->cv);
+        pthread_mutex_unlock(&S->mu);
+        if (J->R->eof) break;
+    }
+    return NULL;
+}
+
+static void* fdp_writer(void* a) {
+    FdWriteJob* J = (FdWriteJob*)a;
+    FdSync* S = J->S;
+    for (uint64_t j = 0;; j++) {
+        const int k = (int)(j % FDP_NOUT);
+        pthread_mutex_lock(&S->mu);
+        while (!S->err && S->nposted <= j && !(S->done_reading && S->nposted == j)) pthread_cond_wait(&S->cv, &S->mu);
+        const bool stop = S->err != 0 || S->nposted <= j;   // an error, or every posted chunk written
+        const uint64_t olen = S->olen[k];
+        pthread_mutex_unlock(&S->mu);
+        if (stop) break;
+        if (hip_fail(hipEventSynchronize(J->P->evo[k]), "hipEventSynchronize")) { fds_fail(S, -(int)E_DEVICE); break; }
+        const int r = J->fd >= 0 ? write_full(J->fd, J->P->hout[k], olen) : 0;
+        if (r) { fds_fail(S, r); break; }
+        pthread_mutex_lock(&S->mu);
+        S->nwritten = j + 1;
+        pthread_cond_broadcast(&S->cv);
+        pthread_mutex_unlock(&S->mu);
+    }
+    return NULL;
+}
+
+typedef int (*dmx_fd_chunk_cb)(void* user, dmx_ctx* c, uint64_t chunk_bytes, uint64_t chunk_off);
+static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts, uint64_t chunk,
+                        dmx_fd_chunk_cb cb, void* user);
 
 extern "C" int dmx_encode_fd(int fd_in, int fd_out, const dmx_opts* opts, uint64_t chunk) {
     const char* dev_s = getenv("DMX_DEVICE");
-    return encode_fd_on(dev_s ? atoi(dev_s) : 0, fd_in, fd_out, opts, chunk);
+    return encode_fd_on(dev_s ? atoi(dev_s) : 0, fd_in, fd_out, opts, chunk, NULL, NULL);
+}
+// The same with a callback after every chunk's encode (dmx_host.c: the compress_stats records,
+// from the context's tokens of that chunk); the chunks are then encoded one at a time.
+extern "C" int dmx_encode_fd_cb(int fd_in, int fd_out, const dmx_opts* opts, uint64_t chunk, dmx_fd_chunk_cb cb,
+                                void* user) {
+    const char* dev_s = getenv("DMX_DEVICE");
+    return encode_fd_on(dev_s ? atoi(dev_s) : 0, fd_in, fd_out, opts, chunk, cb, user);
 }
 
-static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts, uint64_t chunk) {
+static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts, uint64_t chunk,
+                        dmx_fd_chunk_cb cb, void* user) {
     dmx_opts o = {0, 0, DMX_ZLIB, 0, NULL, 0};
     if (opts) o = *opts;
     if (o.sw == 0) o.sw = DMX_BLK;
@@ -4329,7 +4676,8 @@ static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts,
     const uint64_t sw = (uint64_t)o.sw;
     if (chunk < sw) chunk = sw;
     chunk -= chunk % sw;
-    const uint32_t pflags = o.flags & (DMX_F_LAZY | DMX_F_SPLIT | DMX_F_DICT | DMX_F_EXACT_SORT | DMX_F_STORE_CHECK);
+    const uint32_t pflags = o.flags & (DMX_F_LAZY | DMX_F_SPLIT | DMX_F_DICT | DMX_F_EXACT_SORT | DMX_F_STORE_CHECK |
+                                       DMX_F_DEEP);
     FdReader R = {fd_in, false, 0, 0, -1, true};
     {   // a regular file of known size from the current offset: parallel preads
         struct stat st;
@@ -4345,74 +4693,123 @@ static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts,
     dmx_ctx* c = dmx_cached_ctx(device, chunk, &err);
     int r = err;
     const uint64_t ocap = dmx_max_compressed(chunk, o.sw);
+    FdPipe* P = NULL;
     if (!r) r = dmx_ctx_reserve_flags(c, chunk, (int32_t)sw, pflags);
     if (!r && hip_fail(hipSetDevice(c->device), "hipSetDevice")) r = -(int)E_DEVICE;
-    if (!r) r = fd_buffers(c, chunk, ocap);
-    hipStream_t s = c ? c->stream : NULL;
-    int64_t len = 0;
-    if (!r) {
-        len = fd_read_chunk(&R, c->fd_hin[0], chunk);
-        if (len < 0) r = (int)len;
+    if (!r) r = fdp_get(c, chunk, ocap, &P);
+    if (r) {
+        pthread_mutex_unlock(&g_mu);
+        return r;
     }
+    hipStream_t s = c->stream;
+    FdSync S;
+    memset(&S, 0, sizeof(S));
+    pthread_mutex_init(&S.mu, NULL);
+    pthread_cond_init(&S.cv, NULL);
+    FdReadJob rj = {&S, &R, P, chunk};
+    FdWriteJob wj = {&S, P, fd_out};
+    pthread_t rt, wt;
+    const bool rstarted = pthread_create(&rt, NULL, fdp_reader, &rj) == 0;
+    if (!rstarted) fds_fail(&S, -(int)E_MALLOC);
+    const bool wstarted = pthread_create(&wt, NULL, fdp_writer, &wj) == 0;
+    if (!wstarted) fds_fail(&S, -(int)E_MALLOC);
     uint32_t adler = 1;
-    WriteJob wj[2];
-    pthread_t wt[2];
-    bool wact[2] = {false, false};
+    uint64_t off = 0;   // offset of the chunk being finished in the bytes read (callback)
+    uint64_t clen[2] = {0, 0};
+    // chunk j - 1's result: its length, Adler-32, the callback; then its D2H and the writer
+    auto finish = [&](uint64_t j) -> int {
+        const int k2 = (int)(j & 1), ko = (int)(j % FDP_NOUT);
+        if (hip_fail(hipEventSynchronize(P->eve[k2]), "hipEventSynchronize")) return -(int)E_DEVICE;
+        if (P->hres[k2]->status) return P->hres[k2]->status;
+        const uint64_t olen = P->hres[k2]->out_len;
+        adler = dmx_adler32_combine(adler, P->hres[k2]->adler, clen[k2]);
+        if (cb) {
+            const int e = cb(user, c, clen[k2], off);
+            if (e) return e;
+        }
+        off += clen[k2];
+        pthread_mutex_lock(&S.mu);   // output slot ko: chunk j - FDP_NOUT written
+        while (!S.err && j >= FDP_NOUT && S.nwritten < j - FDP_NOUT + 1) pthread_cond_wait(&S.cv, &S.mu);
+        const int e = S.err;
+        pthread_mutex_unlock(&S.mu);
+        if (e) return e;
+        if (olen && hip_fail(hipMemcpyAsync(P->hout[ko], P->dout[k2], olen, hipMemcpyDeviceToHost, P->sd), "D2H"))
+            return -(int)E_DEVICE;
+        if (hip_fail(hipEventRecord(P->evd[k2], P->sd), "hipEventRecord") ||
+            hip_fail(hipEventRecord(P->evo[ko], P->sd), "hipEventRecord"))
+            return -(int)E_DEVICE;
+        pthread_mutex_lock(&S.mu);
+        S.olen[ko] = olen;
+        S.nposted = j + 1;
+        pthread_cond_broadcast(&S.cv);
+        pthread_mutex_unlock(&S.mu);
+        return 0;
+    };
+    bool have_prev = false;
     for (uint64_t i = 0; !r; i++) {
-        const int cur = (int)(i & 1);
-        const bool last = R.eof;
+        const int ki = (int)(i % FDP_NIN), kd = (int)(i % FDP_NDIN), k2 = (int)(i & 1);
+        pthread_mutex_lock(&S.mu);
+        while (!S.err && S.nread <= i) pthread_cond_wait(&S.cv, &S.mu);
+        r = S.err;
+        const int64_t len = r ? 0 : S.len[ki];
+        const bool last = r ? true : S.eof[ki];
+        pthread_mutex_unlock(&S.mu);
+        if (r) break;
+        // H2D into device input kd: encode i - FDP_NDIN read it, encode i - FDP_NDIN + 1 its tail
+        // (history); the latter is ordered after the former on the encode stream
+        if (i >= FDP_NDIN - 1 && hip_fail(hipStreamWaitEvent(P->sh, P->eve[(i - (FDP_NDIN - 1)) & 1], 0), "wait"))
+            r = -(int)E_DEVICE;
+        if (!r && len && hip_fail(hipMemcpyAsync(P->din[kd], P->hin[ki], (size_t)len, hipMemcpyHostToDevice, P->sh), "H2D"))
+            r = -(int)E_DEVICE;
+        if (!r && hip_fail(hipEventRecord(P->evh[ki], P->sh), "hipEventRecord")) r = -(int)E_DEVICE;
+        pthread_mutex_lock(&S.mu);
+        S.h2d_issued = i + 1;
+        pthread_cond_broadcast(&S.cv);
+        pthread_mutex_unlock(&S.mu);
+        // the encode: after its H2D, and after the D2H that last read device output k2
+        if (!r && hip_fail(hipStreamWaitEvent(s, P->evh[ki], 0), "wait")) r = -(int)E_DEVICE;
+        if (!r && i >= 2 && hip_fail(hipStreamWaitEvent(s, P->evd[k2], 0), "wait")) r = -(int)E_DEVICE;
         dmx_opts oc = o;
         oc.flags = pflags | (i == 0 ? DMX_F_HEADER : 0u) | (last ? DMX_F_FINAL : 0u);
         oc.dict = NULL;
         oc.dict_len = 0;
-        if ((pflags & DMX_F_DICT) && i > 0) {      // the previous chunk's tail (still on the device)
-            oc.dict = (const uint8_t*)c->fd_din[cur ^ 1] + (chunk - sw);
+        if ((pflags & DMX_F_DICT) && i > 0) {   // the previous chunk's tail, still on the device
+            oc.dict = (const uint8_t*)P->din[(i - 1) % FDP_NDIN] + (chunk - sw);
             oc.dict_len = sw;
         }
-        if (len && hip_fail(hipMemcpyAsync(c->fd_din[cur], c->fd_hin[cur], (size_t)len, hipMemcpyHostToDevice, s), "H2D"))
-            r = -(int)E_DEVICE;
-        if (!r) r = dmx_encode_async(c, c->fd_din[cur], (uint64_t)len, c->fd_dout[0], ocap, &oc, s);
-        if (!r) r = dmx_encode_result_async(c, c->fd_hres[0], s);
-        int64_t nlen = 0;
-        if (!r && !last) {   // the next chunk, read while the device encodes this one
-            nlen = fd_read_chunk(&R, c->fd_hin[cur ^ 1], chunk);
-            if (nlen < 0) r = (int)nlen;
+        if (!r) r = dmx_encode_async(c, P->din[kd], (uint64_t)len, P->dout[k2], ocap, &oc, s);
+        if (!r) r = dmx_encode_result_async(c, P->hres[k2], s);
+        if (!r && hip_fail(hipEventRecord(P->eve[k2], s), "hipEventRecord")) r = -(int)E_DEVICE;
+        clen[k2] = (uint64_t)len;
+        // the previous chunk finishes while this one encodes (a callback needs the context's
+        // tokens of its own chunk: then each chunk finishes before the next encodes)
+        if (!r && cb) r = finish(i);
+        else if (!r && have_prev) r = finish(i - 1);
+        have_prev = !cb;
+        if (!r && last) {
+            if (!cb) r = finish(i);
+            break;
         }
-        if (!r && hip_fail(hipStreamSynchronize(s), "hipStreamSynchronize")) r = -(int)E_DEVICE;
-        if (!r && c->fd_hres[0]->status) r = c->fd_hres[0]->status;
-        const uint64_t olen = r ? 0 : c->fd_hres[0]->out_len;
-        const uint32_t cadl = r ? 0 : c->fd_hres[0]->adler;
-        if (wact[cur]) {   // writer i-2 used this buffer (writer i-1 waited for it already)
-            pthread_join(wt[cur], NULL);
-            wact[cur] = false;
-            if (!r && wj[cur].rc) r = wj[cur].rc;
-        }
-        if (!r && hip_fail(hipMemcpy(c->fd_hout[cur], c->fd_dout[0], olen, hipMemcpyDeviceToHost), "D2H")) r = -(int)E_DEVICE;
-        if (wact[cur ^ 1]) {   // in order: writer i starts after writer i-1
-            pthread_join(wt[cur ^ 1], NULL);
-            wact[cur ^ 1] = false;
-            if (!r && wj[cur ^ 1].rc) r = wj[cur ^ 1].rc;
-        }
-        if (!r && fd_out >= 0) {
-            wj[cur] = {fd_out, c->fd_hout[cur], olen, 0};
-            if (pthread_create(&wt[cur], NULL, write_job, &wj[cur]) == 0) wact[cur] = true;
-            else r = write_full(fd_out, c->fd_hout[cur], olen);
-        }
-        if (!r) adler = dmx_adler32_combine(adler, cadl, (uint64_t)len);
-        if (last) break;
-        len = nlen;
     }
-    for (int k = 0; k < 2; k++)
-        if (wact[k]) {
-            pthread_join(wt[k], NULL);
-            if (!r && wj[k].rc) r = wj[k].rc;
-        }
+    if (r) fds_fail(&S, r);
+    pthread_mutex_lock(&S.mu);
+    S.done_reading = true;
+    pthread_cond_broadcast(&S.cv);
+    pthread_mutex_unlock(&S.mu);
+    if (rstarted) pthread_join(rt, NULL);
+    if (wstarted) pthread_join(wt, NULL);
+    if (!r) r = S.err;
     if (!r && fd_out >= 0) {
         const uint8_t tail[4] = {(uint8_t)(adler >> 24), (uint8_t)(adler >> 16), (uint8_t)(adler >> 8), (uint8_t)adler};
         r = write_full(fd_out, tail, 4);
     }
     if (R.seekable) (void)lseek(fd_in, (off_t)R.off, SEEK_SET);   // consumed, as read() would leave it
-    if (r && c && s) (void)hipStreamSynchronize(s);   // an error left copies in flight from the cached buffers
+    // nothing may still run on the cached buffers when the lock is released
+    (void)hipStreamSynchronize(P->sh);
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamSynchronize(P->sd);
+    pthread_cond_destroy(&S.cv);
+    pthread_mutex_destroy(&S.mu);
     pthread_mutex_unlock(&g_mu);
     return r;
 }
@@ -4575,7 +4972,7 @@ extern "C" int dmx_encode_fd_multi(int fd_in, int fd_out, const dmx_opts* opts, 
         if (devices[w] < 0 || devices[w] >= nd) return -(int)E_RANGE;
     // one device: the single-device streaming path (read-ahead and writer threads overlap
     // the encode), not one worker doing every step in turn
-    if (ndev == 1) return encode_fd_on(devices[0], fd_in, fd_out, opts, chunk);
+    if (ndev == 1) return encode_fd_on(devices[0], fd_in, fd_out, opts, chunk, NULL, NULL);
     dmx_opts o = {0, 0, DMX_ZLIB, 0, NULL, 0};
     if (opts) o = *opts;
     if (o.sw == 0) o.sw = DMX_BLK;
@@ -4586,7 +4983,7 @@ extern "C" int dmx_encode_fd_multi(int fd_in, int fd_out, const dmx_opts* opts, 
     struct stat st;
     const off_t cur = lseek(fd_in, 0, SEEK_CUR);
     if (cur < 0 || fstat(fd_in, &st) != 0 || !S_ISREG(st.st_mode) || (uint64_t)st.st_size < (uint64_t)cur)
-        return encode_fd_on(devices[0], fd_in, fd_out, opts, chunk);   // a pipe: one device, one reader
+        return encode_fd_on(devices[0], fd_in, fd_out, opts, chunk, NULL, NULL);   // a pipe: one device, one reader
     MultiJob J;
     J.fd_in = fd_in;
     J.fd_out = fd_out;
@@ -4597,7 +4994,7 @@ extern "C" int dmx_encode_fd_multi(int fd_in, int fd_out, const dmx_opts* opts, 
     J.nchunks = (J.size - J.off0 + chunk - 1) / chunk;
     if (J.nchunks == 0) J.nchunks = 1;   // an empty input is one empty chunk (header, EOB block, trailer)
     J.o = o;
-    J.pflags = o.flags & (DMX_F_LAZY | DMX_F_SPLIT | DMX_F_DICT | DMX_F_EXACT_SORT | DMX_F_STORE_CHECK);
+    J.pflags = o.flags & (DMX_F_LAZY | DMX_F_SPLIT | DMX_F_DICT | DMX_F_EXACT_SORT | DMX_F_STORE_CHECK | DMX_F_DEEP);
     J.ndev = ndev < (int)J.nchunks ? ndev : (int)J.nchunks;
     pthread_mutex_init(&J.mu, NULL);
     pthread_cond_init(&J.cv, NULL);

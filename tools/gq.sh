@@ -1,7 +1,41 @@
 #!/bin/bash
-# quick GPU check: parity suite, bench (no cpu legs), stamps
-T=$1; shift
-mkdir -p gpurun_out/$T
-timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/$T/pytest.log 2>&1; tail -3 gpurun_out/$T/pytest.log
-timeout -k 10 300 python3 bench.py --cpu-budget 0 --exhaustive-steps 0 --long-run 0 "$@" > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err || exit 1
-timeout -k 10 120 python3 tools/stamps.py text:6 text:8 > gpurun_out/$T/stamps.txt 2>&1; cat gpurun_out/$T/stamps.txt
+# One GPU-box probe (diagnostic): a -m gpu subset, then optional steps, each under its own
+# time limit; the first failure (other than failed tests) ends the script.
+# usage (on the box): bash tools/gq.sh TAG PYTEST_K [step ...]
+#   steps: bench[:ARGS]  stamps[:CFGS]  sq[:ARGS]  inflate[:ARGS]  infpmc[:ARGS]  deep  trace[:ARGS]
+set -uo pipefail
+TAG=$1; K=$2; shift 2
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+if [ "$K" != "-" ]; then
+  timeout -k 10 600 python3 -u -m pytest "$R/tests" -m gpu -x -q -p no:cacheprovider --timeout 240 \
+      --timeout-method thread -k "$K" > "$OUT/pytest.log" 2>&1
+  rc=$?; tail -3 "$OUT/pytest.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ] && [ $rc -ne 5 ]; then echo "pytest status $rc: stopping"; exit $rc; fi
+fi
+for st in "$@"; do
+  name=${st%%:*}; arg=""; [ "$name" != "$st" ] && arg=${st#*:}
+  case $name in
+    bench) timeout -k 10 600 python3 "$R/bench.py" ${arg//,/ } > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 3
+           python3 - "$OUT/bench.json" <<'PY'
+import json, sys; d = json.load(open(sys.argv[1]))
+print('value', d['value'], 'size', d.get('size_vs_ref_pct'), 'parity', d.get('parity_vs_port'), 'stage', d['stage_ms'])
+for k in ('exhaustive', 'real_text', 'gpu_inflate', 'end_to_end_fd_api'):
+    v = d.get(k); print(k, {x: v.get(x) for x in ('value', 'GBps_out', 'size_vs_ref_pct', 'parity_vs_port', 'bit_exact')} if v else None)
+print('tradeoff', [(t['max_chain'], t['value'], t.get('size_vs_ref_pct')) for t in (d.get('tradeoff') or [])])
+PY
+           ;;
+    stamps) timeout -k 10 300 python3 "$R/tools/stamps.py" ${arg//,/ } > "$OUT/stamps.txt" 2>&1 || exit 3; cat "$OUT/stamps.txt" ;;
+    sq) bash "$R/tools/sq_profile.sh" "$TAG/sq" ${arg//,/ } > /dev/null 2>&1 || exit 3; cat "$OUT/sq/sq_summary.txt" ;;
+    inflate) timeout -k 10 300 python3 "$R/tools/inflate_bench.py" ${arg//,/ } > "$OUT/inflate.json" 2>&1 || exit 3; cat "$OUT/inflate.json" ;;
+    infpmc) cd /tmp; for set in "FETCH_SIZE" "WRITE_SIZE"; do
+              timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d "$OUT/ipmc_$set" -o p -- python3 "$R/tools/inflate_bench.py" --steps 2 --stream-mb 1 $arg > /dev/null 2> "$OUT/ipmc_$set.err" || exit 3
+            done; python3 "$R/tools/pmc.py" "$OUT/ipmc_FETCH_SIZE,$OUT/ipmc_WRITE_SIZE" | tee "$OUT/inf_pmc.txt"; cd "$R" ;;
+    deep) timeout -k 10 300 python3 "$R/tools/deep_bench.py" 32 > "$OUT/deep.txt" 2>&1 || exit 3; cat "$OUT/deep.txt" ;;
+    trace) cd /tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --cpu-budget 0 --exhaustive-steps 0 --tradeoff= --long-run 0 $arg > "$OUT/bench_trace.json" 2> "$OUT/trace.err" || exit 3
+           find "$OUT/trace" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \; ; cut -d, -f1-8 "$OUT/kernel_stats.csv" | head -20; cd "$R" ;;
+    *) echo "unknown step $name"; exit 2 ;;
+  esac
+done
