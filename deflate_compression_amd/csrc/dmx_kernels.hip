@@ -736,8 +736,14 @@ __device__ __forceinline__ uint32_t search_pairs(MatchLDS& L, uint32_t bn, uint3
     uint32_t* Qw = L.tsm + (wave << 6);   // the extension queue (P2 arrays are free during the search)
     const uint64_t lt = (1ull << lane) - 1ull;
     uint32_t qn = 0, iters = 0;
-    for (uint32_t base = wave * OWN;; base += MW * OWN) {
+    // chunks are taken from a workgroup counter (L.ntok, zeroed before the search), the next
+    // one fetched a chunk ahead: the waves finish together whatever their queues cost
+    uint32_t cnext = 0;
+    if (lane == 0) cnext = atomicAdd(&L.ntok, 1u);
+    for (;;) {
+        const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnext) * OWN;
         const bool more = base < nvalid;   // wave-uniform
+        if (more && lane == 0) cnext = atomicAdd(&L.ntok, 1u);
         const int ea = (int)base + 2 * ((int)lane - (int)HL);
         const uint32_t ka = (uint32_t)ea, kb = ka + 1;
         const bool own = lane >= HL;
@@ -2257,6 +2263,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
             uint32_t z = 0;
             asm volatile("" : "+v"(z));   // (else the compiler keeps a zero quad in a scratch slot)
             reinterpret_cast<uint4*>(nib_words(L))[tid] = make_uint4(z, z, z, z);
+            if (tid == 0) L.ntok = 0;   // search_pairs' chunk counter
             __syncthreads();
         }
         const uint32_t its = runs ? search_positions<DICT, true>(L, bn, kb, pg, tid, dbg != nullptr, tdef, hbk)
@@ -3533,6 +3540,12 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply_kernel(dmx_blkinfo* 
 #define TPT 8   // tokens per thread per packing round
 #define PK_RING 4096   // pack ring words: > 1 + max(160 header words, 2048 tokens x 48 bits / 32) + 1
 
+// A workgroup barrier that orders LDS only: global loads in flight (the next round's tokens)
+// stay in flight across it (__syncthreads() also waits for every outstanding global access).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __device__ __forceinline__ void st_or64(uint32_t* st, uint32_t pos, uint64_t v, uint32_t nb) {
     if (!nb) return;
     const uint32_t w = pos >> 5, sh = pos & 31;
@@ -3654,21 +3667,27 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
     };
     // write the ring's complete words below block bit `pos`; the partial word moves to stage[0]
     auto flush = [&](uint32_t pos) {
-        __syncthreads();
+        lds_barrier();
         const uint32_t done = (pos >> 5) - base;
         for (uint32_t k = tid; k < done; k += PT) out_word(base + k, stage[k]);
         const uint32_t part = stage[done];
-        __syncthreads();
+        lds_barrier();
         for (uint32_t k = tid; k <= done; k += PT) stage[k] = k == 0 ? part : 0u;
         base += done;
-        __syncthreads();
+        lds_barrier();
     };
+    const uint32_t* tb = tok_g + (uint64_t)b * DMX_BLK;
+    // the first round's tokens, loaded before anything else (each round prefetches the next):
+    // the rounds of a block no longer wait on a global load each
+    uint32_t nxt[TPT];
+    const uint32_t si0_t0 = bi.nsub > 1 ? sub_g[(uint64_t)b * DMX_NSUB].t0 : 0u;
+#pragma unroll
+    for (int t = 0; t < TPT; t++) nxt[t] = tb[min(si0_t0 + tid * TPT + (uint32_t)t, (uint32_t)DMX_BLK - 1)];
     for (uint32_t k = tid; k < PK_RING; k += PT) stage[k] = 0;
     for (uint32_t k = tid; k < 316; k += PT) code[k] = codes_g[(uint64_t)b * DMX_NSUB * DMX_HIST + k];
     __syncthreads();
     {   // (stored blocks left above)
         // one or more DEFLATE blocks (f3 split): header, tokens [t0, t1), end of block
-        const uint32_t* tb = tok_g + (uint64_t)b * DMX_BLK;
         uint32_t pos = s0;   // block bit position
         for (uint32_t sb = 0; sb < bi.nsub; sb++) {
             const uint64_t slot = (uint64_t)b * DMX_NSUB + sb;
@@ -3676,6 +3695,8 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
             if (sb) {   // this block's codes (every thread is done with the previous ones)
                 __syncthreads();
                 for (uint32_t k = tid; k < 316; k += PT) code[k] = codes_g[slot * DMX_HIST + k];
+#pragma unroll
+                for (int t = 0; t < TPT; t++) nxt[t] = tb[min(si.t0 + tid * TPT + (uint32_t)t, (uint32_t)DMX_BLK - 1)];
                 __syncthreads();
             }
             flush(pos);
@@ -3692,13 +3713,20 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
             for (uint32_t c = si.t0; c < si.t1; c += PT * TPT) {
                 flush(pos);
                 const uint32_t j0 = c + tid * TPT;
+                uint32_t cur[TPT];
+    #pragma unroll
+                for (int t = 0; t < TPT; t++) cur[t] = nxt[t];
+                if (c + PT * TPT < si.t1) {   // the next round's tokens, in flight during this one
+    #pragma unroll
+                    for (int t = 0; t < TPT; t++) nxt[t] = tb[min(j0 + PT * TPT + (uint32_t)t, (uint32_t)DMX_BLK - 1)];
+                }
                 uint32_t pv[2 * TPT], pb[2 * TPT];   // up to two pieces per token, <= 28 bits each
                 uint32_t mybits = 0;
     #pragma unroll
                 for (int t = 0; t < TPT; t++) {
                     pv[2 * t] = pb[2 * t] = pv[2 * t + 1] = pb[2 * t + 1] = 0;
                     if (j0 + t < si.t1) {
-                        const uint32_t tk = tb[j0 + t];
+                        const uint32_t tk = cur[t];
                         if ((tk >> 9) == 0) {
                             const uint32_t cw = code[tk];
                             pv[2 * t] = cw & 0xFFFFu;
@@ -3720,7 +3748,7 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
                 // exclusive scan of the threads' bit counts over the workgroup
                 const uint32_t incl = wave_incl_scan(mybits);
                 if (lane == 63) wsum[wave] = incl;
-                __syncthreads();
+                lds_barrier();
                 uint32_t wbase = 0, tot = 0;
     #pragma unroll
                 for (int w = 0; w < PT / 64; w++) {
@@ -3749,7 +3777,7 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
                     if (ab) atomicOr(&stage[w], (uint32_t)acc);   // shared with the next thread
                 }
                 pos += tot;
-                __syncthreads();
+                lds_barrier();
             }
             const uint32_t cw = code[256];
             if (tid == 0) st_or64(stage, pos - 32 * base, cw & 0xFFFFu, cw >> 16);

@@ -68,6 +68,49 @@ def main():
         dt = par(wr, m, T)
         os.close(fdo)
         res[f"pwrite_T{T}"] = round(m / dt / 1e9, 2)
+    # the output through a shared mapping of the file (ftruncate + mmap), T threads copying
+    import ctypes
+    import mmap
+    src = torch.from_numpy(pin.numpy()[:m])
+    for T in (1, 4, 8, 16):
+        fdo = os.open(fo, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o644)
+        t0 = time.perf_counter()
+        os.ftruncate(fdo, m)
+        mm = mmap.mmap(fdo, m, mmap.MAP_SHARED, mmap.PROT_WRITE | mmap.PROT_READ)
+        dst = torch.from_numpy(np.frombuffer(mm, dtype=np.uint8))
+
+        def cp(lo, hi):
+            dst[lo:hi].copy_(src[lo:hi])
+        par(cp, m, T)
+        del dst
+        mm.close()
+        os.close(fdo)
+        res[f"mmap_write_T{T}"] = round(m / (time.perf_counter() - t0) / 1e9, 2)
+    # D2H straight into the mapped file pages (hipHostRegister of the mapping)
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        fdo = os.open(fo, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o644)
+        t0 = time.perf_counter()
+        os.ftruncate(fdo, m)
+        mm = mmap.mmap(fdo, m, mmap.MAP_SHARED, mmap.PROT_WRITE | mmap.PROT_READ)
+        buf = (ctypes.c_char * m).from_buffer(mm)
+        ptr = ctypes.addressof(buf)
+        t1 = time.perf_counter()
+        rc = hip.hipHostRegister(ctypes.c_void_p(ptr), ctypes.c_size_t(m), 0)
+        t2 = time.perf_counter()
+        rc2 = hip.hipMemcpy(ctypes.c_void_p(ptr), ctypes.c_void_p(d.data_ptr()), ctypes.c_size_t(m), 2)
+        t3 = time.perf_counter()
+        hip.hipHostUnregister(ctypes.c_void_p(ptr))
+        t4 = time.perf_counter()
+        del buf
+        mm.close()
+        os.close(fdo)
+        res["reg_d2h"] = {"rc": (rc, rc2), "map_ms": round((t1 - t0) * 1e3, 2), "register_ms": round((t2 - t1) * 1e3, 2),
+                          "d2h_ms": round((t3 - t2) * 1e3, 2), "unregister_ms": round((t4 - t3) * 1e3, 2),
+                          "GBps_total": round(m / (t4 - t0) / 1e9, 2)}
+    except Exception as e:  # pragma: no cover
+        res["reg_d2h"] = repr(e)
+    print("fs of /tmp:", os.popen("stat -f -c %T /tmp").read().strip())
     os.remove(fi)
     os.remove(fo)
     os.rmdir(td)
