@@ -837,8 +837,13 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
         const uint32_t own = 64 - K;
         // one call site of ext_queue (code size, registers): the pass after the last chunk
         // only flushes the queue
-        for (uint32_t base = wave * own;; base += MW * own) {
+        // chunks from the workgroup counter (L.ntok, zeroed before the search), as search_pairs
+        uint32_t cnext = 0;
+        if (lane == 0) cnext = atomicAdd(&L.ntok, 1u);
+        for (;;) {
+            const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnext) * own;
             const bool more = base < nvalid;   // wave-uniform
+            if (more && lane == 0) cnext = atomicAdd(&L.ntok, 1u);
             const int ei = (int)(base + lane) - (int)K;   // entry of this lane
             const uint32_t k = (uint32_t)ei;
             const bool act = more && lane >= K && k < nvalid;
@@ -916,16 +921,27 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
     // min(258, bn - i); the wave stops when no lane does.
     {
     // H4: the seeds (HBM) of the wave's next chunk are loaded one chunk ahead
+    // chunks of 64 entries from the workgroup counter (L.ntok, zeroed before the search): a
+    // chunk's chains cost anything from one window to hundreds, so a fixed share per wave left
+    // the waves idling at the end of the phase; the next chunk (and its seeds) is fetched a
+    // chunk ahead
+    uint32_t cnx = 0;
+    if (lane == 0) cnx = atomicAdd(&L.ntok, 1u);
+    uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnx);
     uint32_t snext = 0;
-    if (H4 && (wave << 6) + lane < nvalid) snext = seeds[L.sorted[(wave << 6) + lane]];
-    for (uint32_t k0 = wave << 6; k0 < nvalid; k0 += MT) {
+    if (H4 && (c0 << 6) + lane < nvalid) snext = seeds[L.sorted[(c0 << 6) + lane]];
+    for (;;) {
+        const uint32_t k0 = c0 << 6;
+        if (k0 >= nvalid) break;
+        if (lane == 0) cnx = atomicAdd(&L.ntok, 1u);
+        const uint32_t c1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnx);
         const uint32_t k = k0 + lane;
         const bool act = k < nvalid;
         uint32_t i = 0, nc = 0, lim = 0;
         uint32_t seed = 0;
         if (H4) {
             seed = snext;
-            if (k + MT < nvalid) snext = seeds[L.sorted[k + MT]];
+            if ((c1 << 6) + lane < nvalid) snext = seeds[L.sorted[(c1 << 6) + lane]];
         }
         uint64_t iv0 = 0;
         uint32_t i2 = 0;
@@ -1045,6 +1061,7 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
             }
         }
         if (act) store_result<DICT>(L, pg, k, i, bestkey, hbk);
+        c0 = c1;
     }
     }
     // the last two positions have no trigram: literals
@@ -2263,9 +2280,9 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
             uint32_t z = 0;
             asm volatile("" : "+v"(z));   // (else the compiler keeps a zero quad in a scratch slot)
             reinterpret_cast<uint4*>(nib_words(L))[tid] = make_uint4(z, z, z, z);
-            if (tid == 0) L.ntok = 0;   // search_pairs' chunk counter
-            __syncthreads();
         }
+        if (tid == 0) L.ntok = 0;   // the search's chunk counter
+        __syncthreads();
         const uint32_t its = runs ? search_positions<DICT, true>(L, bn, kb, pg, tid, dbg != nullptr, tdef, hbk)
                              : h4 ? search_positions<DICT, false, (h4 ? NBX : 3)>(L, bn, kb, pg, tid, dbg != nullptr, tdef, hbk, seeds)
                                   : search_positions<DICT, false>(L, bn, kb, pg, tid, dbg != nullptr, tdef, hbk);
