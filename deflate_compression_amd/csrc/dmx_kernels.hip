@@ -1333,12 +1333,17 @@ __device__ __forceinline__ uint32_t gram_pass(MatchLDS& L, uint32_t nv, uint32_t
     constexpr uint32_t PW = DMX_GRAM_PW;   // (diagnostic builds)
 #endif
     constexpr uint32_t GM = NG == 3 ? 0xFFFFFFu : 0xFFFFFFFFu;
-    const uint32_t lane = tid & 63, wave = wave_of(tid);
+    const uint32_t lane = tid & 63;
     uint32_t* UL = L.tsm;   // tsm + exitp: 2048 slots, free until the next sort
     uint32_t bad = 0;
-    if (tid == 0) L.ntok = 0;
+    if (tid == 0) { L.ntok = 0; L.wsum[0] = 0; L.wsum[1] = 0; }   // list length, chunk and walk counters
     __syncthreads();
-    for (uint32_t kb = wave << 6; kb < nv; kb += MT) {
+    uint32_t cnx = 0;
+    if (lane == 0) cnx = atomicAdd(&L.wsum[0], 1u);
+    for (;;) {   // chunks of 64 entries from the workgroup counter, the next fetched a chunk ahead
+        const uint32_t kb = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnx) << 6;
+        if (kb >= nv) break;
+        if (lane == 0) cnx = atomicAdd(&L.wsum[0], 1u);
         const uint32_t k = kb + lane;
         const bool act = k < nv;
         const uint32_t i = act ? (uint32_t)L.sorted[k] : 0u, w = act ? ld4(L.data, i) : 0u;
@@ -1382,7 +1387,11 @@ __device__ __forceinline__ uint32_t gram_pass(MatchLDS& L, uint32_t nv, uint32_t
     tsweep += __builtin_amdgcn_s_memtime();   // (diagnostic stamps: the sweep's end)
     const uint32_t nul = min(L.ntok, 2u * (DMX_BLK / 32));
     ndefer += L.ntok;
-    for (uint32_t u = wave; u < nul; u += MW) {
+    for (;;) {   // listed entries from the workgroup counter (their walks differ in length)
+        uint32_t un = 0;
+        if (lane == 0) un = atomicAdd(&L.wsum[1], 1u);
+        const uint32_t u = (uint32_t)__builtin_amdgcn_readfirstlane((int)un);
+        if (u >= nul) break;
         const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)UL[u]);
         const uint32_t k = e & 0xFFFFu, i = L.sorted[k], t = ld4(L.data, i) & GM;
         const uint32_t hb = bucket_of<NG>(t);
