@@ -121,6 +121,15 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
     return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32);
 }
+// A wave's next work item from a workgroup counter in LDS, called by all 64 lanes: each adds 1
+// (one LDS add of 64 after the atomic optimizer) and (old value) / 64 is the item, the same in
+// every lane.  Not `if (lane == 0) x = atomicAdd(..)`: the compiler threaded that branch into
+// the previous iteration's lane-0 branches and made gram_pass's walk loop exit lane by lane --
+// lanes 1..63 then spun on item 0, a GPU hang (round 4); a lane-0-only add value (1 : 0) takes
+// the optimizer's 64-step iterative scan instead.
+__device__ __forceinline__ uint32_t wave_claim(uint32_t* ctr) {
+    return atomicAdd(ctr, 1u) >> 6;
+}
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
     v += dpp_shr64(v, 1);
     v += dpp_shr64(v, 2);
@@ -738,12 +747,11 @@ __device__ __forceinline__ uint32_t search_pairs(MatchLDS& L, uint32_t bn, uint3
     uint32_t qn = 0, iters = 0;
     // chunks are taken from a workgroup counter (L.ntok, zeroed before the search), the next
     // one fetched a chunk ahead: the waves finish together whatever their queues cost
-    uint32_t cnext = 0;
-    if (lane == 0) cnext = atomicAdd(&L.ntok, 1u);
+    uint32_t cnext = wave_claim(&L.ntok);
     for (;;) {
         const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnext) * OWN;
         const bool more = base < nvalid;   // wave-uniform
-        if (more && lane == 0) cnext = atomicAdd(&L.ntok, 1u);
+        if (more) cnext = wave_claim(&L.ntok);
         const int ea = (int)base + 2 * ((int)lane - (int)HL);
         const uint32_t ka = (uint32_t)ea, kb = ka + 1;
         const bool own = lane >= HL;
@@ -838,12 +846,11 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
         // one call site of ext_queue (code size, registers): the pass after the last chunk
         // only flushes the queue
         // chunks from the workgroup counter (L.ntok, zeroed before the search), as search_pairs
-        uint32_t cnext = 0;
-        if (lane == 0) cnext = atomicAdd(&L.ntok, 1u);
+        uint32_t cnext = wave_claim(&L.ntok);
         for (;;) {
             const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnext) * own;
             const bool more = base < nvalid;   // wave-uniform
-            if (more && lane == 0) cnext = atomicAdd(&L.ntok, 1u);
+            if (more) cnext = wave_claim(&L.ntok);
             const int ei = (int)(base + lane) - (int)K;   // entry of this lane
             const uint32_t k = (uint32_t)ei;
             const bool act = more && lane >= K && k < nvalid;
@@ -925,15 +932,14 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
     // chunk's chains cost anything from one window to hundreds, so a fixed share per wave left
     // the waves idling at the end of the phase; the next chunk (and its seeds) is fetched a
     // chunk ahead
-    uint32_t cnx = 0;
-    if (lane == 0) cnx = atomicAdd(&L.ntok, 1u);
+    uint32_t cnx = wave_claim(&L.ntok);
     uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnx);
     uint32_t snext = 0;
     if (H4 && (c0 << 6) + lane < nvalid) snext = seeds[L.sorted[(c0 << 6) + lane]];
     for (;;) {
         const uint32_t k0 = c0 << 6;
         if (k0 >= nvalid) break;
-        if (lane == 0) cnx = atomicAdd(&L.ntok, 1u);
+        cnx = wave_claim(&L.ntok);
         const uint32_t c1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnx);
         const uint32_t k = k0 + lane;
         const bool act = k < nvalid;
@@ -1338,12 +1344,11 @@ __device__ __forceinline__ uint32_t gram_pass(MatchLDS& L, uint32_t nv, uint32_t
     uint32_t bad = 0;
     if (tid == 0) { L.ntok = 0; L.wsum[0] = 0; L.wsum[1] = 0; }   // list length, chunk and walk counters
     __syncthreads();
-    uint32_t cnx = 0;
-    if (lane == 0) cnx = atomicAdd(&L.wsum[0], 1u);
+    uint32_t cnx = wave_claim(&L.wsum[0]);
     for (;;) {   // chunks of 64 entries from the workgroup counter, the next fetched a chunk ahead
         const uint32_t kb = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnx) << 6;
         if (kb >= nv) break;
-        if (lane == 0) cnx = atomicAdd(&L.wsum[0], 1u);
+        cnx = wave_claim(&L.wsum[0]);
         const uint32_t k = kb + lane;
         const bool act = k < nv;
         const uint32_t i = act ? (uint32_t)L.sorted[k] : 0u, w = act ? ld4(L.data, i) : 0u;
@@ -1388,8 +1393,7 @@ __device__ __forceinline__ uint32_t gram_pass(MatchLDS& L, uint32_t nv, uint32_t
     const uint32_t nul = min(L.ntok, 2u * (DMX_BLK / 32));
     ndefer += L.ntok;
     for (;;) {   // listed entries from the workgroup counter (their walks differ in length)
-        uint32_t un = 0;
-        if (lane == 0) un = atomicAdd(&L.wsum[1], 1u);
+        const uint32_t un = wave_claim(&L.wsum[1]);
         const uint32_t u = (uint32_t)__builtin_amdgcn_readfirstlane((int)un);
         if (u >= nul) break;
         const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)UL[u]);
@@ -2625,6 +2629,26 @@ __device__ __forceinline__ void wsync() {
 }
 
 __constant__ uint8_t c_clorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// Diagnostic builds (-DDMX_K2_STAMPS): cycles per K2 phase summed over the launch's blocks
+// (dmx_k2_stamps): 0 rank sort, 1 two-queue merge, 2 depths + lengths, 3 canonical codes,
+// 4 run-length coding, 5 header emission, 6 the rest, 7 blocks.
+#ifdef DMX_K2_STAMPS
+__device__ unsigned long long dmx_k2_st[8];
+#define K2T() __builtin_amdgcn_s_memtime()
+#define K2ST(k, t0) do { const uint64_t t1_ = K2T(); if ((threadIdx.x & 63) == 0) atomicAdd(&dmx_k2_st[k], (unsigned long long)(t1_ - (t0))); t0 = t1_; } while (0)
+extern "C" int dmx_k2_stamps(unsigned long long* host, int reset) {
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(dmx_k2_st), sizeof(unsigned long long) * 8, 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(dmx_k2_st), z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#else
+#define K2T() 0ull
+#define K2ST(k, t0) ((void)(t0))
+#endif
 __constant__ uint8_t c_cl_eb[19] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 3, 7};
 
 // Exclusive prefix sum over one wave (64 lanes).
@@ -2638,6 +2662,7 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v) { return wave_inc
 // (lane 0, one LDS round trip per node: both heads of both queues are read together).
 template <int NR, typename F>
 __device__ void huff_lengths(K2LDS& S, const F* f, int n, int maxbits, uint8_t* len, uint32_t lane) {
+    [[maybe_unused]] uint64_t kt = K2T();
     uint32_t key[NR];
     uint32_t m = 0;
 #pragma unroll
@@ -2701,6 +2726,7 @@ __device__ void huff_lengths(K2LDS& S, const F* f, int n, int maxbits, uint8_t* 
         }
     if (lane < 32) S.blc[lane] = 0;
     wsync();
+    K2ST(0, kt);
     const int mm = (int)m, nn = mm - 1, root = nn - 1;
     if (lane == 0) {   // two-queue merge
         int li = 0, ni = 0;
@@ -2718,6 +2744,7 @@ __device__ void huff_lengths(K2LDS& S, const F* f, int n, int maxbits, uint8_t* 
         S.up[root] = (uint16_t)root;
     }
     wsync();
+    K2ST(1, kt);
     // node depths by pointer jumping: dd = distance to up, up = an ancestor, doubling
     uint32_t u[5], d[5];
 #pragma unroll
@@ -2787,6 +2814,7 @@ __device__ void huff_lengths(K2LDS& S, const F* f, int n, int maxbits, uint8_t* 
         }
     }
     wsync();
+    K2ST(2, kt);
 }
 
 // Canonical codes (RFC 1951 §3.2.2), bit-reversed, packed code | len << 16.  Lane-parallel:
@@ -2909,7 +2937,9 @@ struct HuffRes {
 // The code-length alphabet of a block whose lit/len and distance lengths and HLIT / HDIST
 // are in S: the run-length coding of the lengths, its Huffman lengths, HCLEN.  One wave.
 __device__ void huff_cl(K2LDS& S, uint32_t lane) {
+    [[maybe_unused]] uint64_t kt = K2T();
     rle_lengths(S, lane);
+    K2ST(4, kt);
     huff_lengths<1>(S, S.fcl, 19, 7, S.lcl, lane);
     const uint64_t nzc = __ballot(lane < 19 && S.lcl[c_clorder[lane < 19 ? lane : 0]] != 0);
     if (lane == 0) S.hclen = nzc ? max(4, 64 - (int)__builtin_clzll(nzc)) : 4;
@@ -2995,9 +3025,11 @@ __device__ uint32_t huff_emit(K2LDS& S, uint32_t final_bit, uint32_t bt, uint32_
     // fixed codes: the canonical assignment counts all 288 lit/len lengths (RFC 1951
     // 3.2.6: 280..287 are 8-bit codes, so the 9-bit codes of 144..255 start after them);
     // slots 286/287 are overwritten by the distance codes next (never emitted)
+    [[maybe_unused]] uint64_t kt = K2T();
     canon_codes<5>(S, S.lll, bt == 1 ? 288 : 286, codes_out, lane);
     canon_codes<1>(S, S.ld, 30, codes_out + DMX_DIST0, lane);
     wsync();
+    K2ST(3, kt);
 
     // header bits: items (value, bits) placed by a prefix sum over their bit counts
     uint32_t nitems = 1;
@@ -3032,6 +3064,7 @@ __device__ uint32_t huff_emit(K2LDS& S, uint32_t final_bit, uint32_t bt, uint32_
         }
     }
     wsync();
+    K2ST(5, kt);
     return carry;
 }
 
@@ -3053,11 +3086,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void dm
     const uint32_t bn = info[b].n;
     const uint32_t final_bit = ((flags & DMX_F_FINAL) && b == nblk - 1) ? 1u : 0u;
 
+    [[maybe_unused]] uint64_t kt0 = K2T();
     for (int s = (int)lane; s < 288; s += 64) S.fll[s] = s < 286 ? (s == 256 ? 1u : hg[s]) : 0u;   // + end of block
     for (int s = (int)lane; s < 32; s += 64) S.fd[s] = s < 30 ? hg[DMX_DIST0 + s] : 0u;
     wsync();
     uint32_t* cg = codes_g + (uint64_t)b * DMX_NSUB * DMX_HIST;
     const HuffRes h = huff_block(S, bn, final_bit, true, lane, cg);
+#ifdef DMX_K2_STAMPS
+    if (lane == 0) { atomicAdd(&dmx_k2_st[6], (unsigned long long)(K2T() - kt0)); atomicAdd(&dmx_k2_st[7], 1ull); }
+#endif
     uint32_t* hgout = hdr_g + (uint64_t)b * DMX_NSUB * DMX_HDR_WORDS;
     for (uint32_t k = lane; k < (h.hbits + 31) / 32; k += 64) hgout[k] = S.hdr[k];
     if (lane == 0) {

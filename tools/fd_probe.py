@@ -24,8 +24,9 @@ def par(fn, n, T):
 
 def main():
     mb = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+    where = sys.argv[2] if len(sys.argv) > 2 else "/tmp"
     n = mb * 1_000_000
-    td = tempfile.mkdtemp(dir="/tmp")
+    td = tempfile.mkdtemp(dir=where)
     fi = os.path.join(td, "in")
     np.random.default_rng(1).integers(0, 256, n, dtype=np.uint8).tofile(fi)
     pin = torch.empty(n, dtype=torch.uint8).pin_memory()
@@ -110,7 +111,7 @@ def main():
                           "GBps_total": round(m / (t4 - t0) / 1e9, 2)}
     except Exception as e:  # pragma: no cover
         res["reg_d2h"] = repr(e)
-    print("fs of /tmp:", os.popen("stat -f -c %T /tmp").read().strip())
+    print("fs of", where, ":", os.popen("stat -f -c %T " + where).read().strip())
     os.remove(fi)
     os.remove(fo)
     os.rmdir(td)

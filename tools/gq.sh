@@ -15,11 +15,13 @@ if [ "$K" != "-" ]; then
   rc=$?; tail -3 "$OUT/pytest.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ] && [ $rc -ne 5 ]; then echo "pytest status $rc: stopping"; exit $rc; fi
 fi
+nb=0
 for st in "$@"; do
   name=${st%%:*}; arg=""; [ "$name" != "$st" ] && arg=${st#*:}
   case $name in
-    bench) timeout -k 10 600 python3 "$R/bench.py" ${arg//,/ } > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 3
-           python3 - "$OUT/bench.json" <<'PY'
+    bench) nb=$((nb + 1)); bj=$OUT/bench$([ $nb -gt 1 ] && echo $nb).json
+           timeout -k 10 600 python3 "$R/bench.py" ${arg//,/ } > "$bj" 2> "${bj%.json}.err" || exit 3
+           python3 - "$bj" <<'PY'
 import json, sys; d = json.load(open(sys.argv[1]))
 print('value', d['value'], 'size', d.get('size_vs_ref_pct'), 'parity', d.get('parity_vs_port'), 'stage', d['stage_ms'])
 for k in ('exhaustive', 'real_text', 'gpu_inflate', 'end_to_end_fd_api'):
