@@ -2127,7 +2127,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
                                                        dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg,
                                                        uint32_t* __restrict__ nfallback) {
     __shared__ MatchLDS L;
-    __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def, tp0[3], st_rounds, st_p3a, st_h4[3];
+    __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def, tp0[3], st_rounds, st_p3a, st_h4[3], st_lz, st_w1w;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = wave_of(tid);
     const uint32_t b = blockIdx.x;
     if ((mflags & 4u) && info[b].prestored) return;   // stored by the noise check (K0)
@@ -2339,6 +2339,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         L.lit[tid] = lw | (~lw & ~litn & longer);
         __syncthreads();
     }
+    if (dbg && tid == 0) st_lz = __builtin_amdgcn_s_memtime() - t1;
 
     // ---- P2: greedy path ----
     {   // W1: speculative walk of every 32-position segment from its start
@@ -2356,6 +2357,7 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         // chains (K <= KE): distance = S[k] - S[k - j] from the winner nibble j of entry k (the
         // history's from its result); longer chains staged the distances in pg (HBM).
         __syncthreads();
+        if (dbg && tid == 0) st_w1w = __builtin_amdgcn_s_memtime() - t1;
         const uint32_t nvalid = bn > 2 ? bn - 2 : 0;
         uint4 dv[4], pv[4];
         if (kb > 0 && kb <= KE) {
@@ -2564,8 +2566,8 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         if (!DICT) {   // (12, 13 are the history kernel's with DMX_F_DICT)
             dbg[(uint64_t)b * DMX_STAMPS + 12] = h4 ? st_h4[2] : st_p3a;   // P3: token list built (exhaustive: sweep end)
             dbg[(uint64_t)b * DMX_STAMPS + 13] = p3b;        // P3: tokens and histograms done
-            dbg[(uint64_t)b * DMX_STAMPS + 14] = h4 ? st_h4[0] : 0;   // exhaustive: nearest-trigram pass done
-            dbg[(uint64_t)b * DMX_STAMPS + 15] = h4 ? st_h4[1] : 0;   //   4-byte sort done
+            dbg[(uint64_t)b * DMX_STAMPS + 14] = h4 ? st_h4[0] : st_lz;    // exhaustive: nearest-trigram pass done; else P1b done
+            dbg[(uint64_t)b * DMX_STAMPS + 15] = h4 ? st_h4[1] : st_w1w;   //   4-byte sort done; else W1's walk done
         }
     }
     if (tid == 0) {

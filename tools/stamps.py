@@ -25,6 +25,8 @@ def run(kind, n, mc, flags=D.DMX_ZLIB | D.DMX_F_LAZY):
                       **({} if flags & D.DMX_F_DICT else {"p3_list_kcyc": round(st[:, 12].mean() / 1e3, 1), "p3_done_kcyc": round(st[:, 13].mean() / 1e3, 1)}), "walk_fallback_frac": round(float((st[:, 11] >= 8).mean()), 3),
                       **({"h4_trigram_pass_end_kcyc": round((st[:, 14] % 2**48).mean() / 1e3, 1), "h4_passes": round((st[:, 14] // 2**48).mean(), 3), "h4_sort_end_kcyc": round((st[:, 15] % 2**48).mean() / 1e3, 1), "h4_deferred_walks": round((st[:, 15] // 2**48).mean(), 1)}
                          if mc == 0 and not flags & D.DMX_F_DICT else {}),
+                      **({"p1b_end_kcyc": round(st[:, 14].mean() / 1e3, 1), "w1_walk_end_kcyc": round(st[:, 15].mean() / 1e3, 1)}
+                         if mc != 0 and not flags & D.DMX_F_DICT else {}),
                       **({"hist_staged_kcyc": round(st[1:, 12].mean() / 1e3, 1), "hist_total_kcyc": round(st[1:, 13].mean() / 1e3, 1)}
                          if flags & D.DMX_F_DICT else {})}))
 
