@@ -57,10 +57,10 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="text", choices=sorted(WORKLOADS))
     ap.add_argument("--bytes", type=int, default=0, help="override bytes per rank")
-    ap.add_argument("--max-chain", type=int, default=int(os.environ.get("DMX_MAX_CHAIN", "8")),
-                    help="0 = exhaustive (reference parse); K = K newest chain entries (default 8: inside "
-                         "the <= 2 %% size budget vs S_ref on every reference-held text with --deep, "
-                         "profiles/r04_size/size_table.md)")
+    ap.add_argument("--max-chain", type=int, default=int(os.environ.get("DMX_MAX_CHAIN", "7")),
+                    help="0 = exhaustive (reference parse); K = K newest chain entries (default 7: the "
+                         "fastest K inside the <= 2 %% size budget vs S_ref on every reference-held text "
+                         "with --deep, profiles/r04_size/size_table.md)")
     ap.add_argument("--deep", type=int, default=int(os.environ.get("DMX_DEEP", "1")),
                     help="1 = adaptive chain depth: small-alphabet blocks search 64 deep (DMX_F_DEEP)")
     ap.add_argument("--lazy", type=int, default=int(os.environ.get("DMX_LAZY", "1")),
@@ -72,7 +72,7 @@ def parse_args(argv=None):
     ap.add_argument("--dict", type=int, default=int(os.environ.get("DMX_DICT", "0")),
                     help="1 = cross-block dictionary (DMX_F_DICT, SURVEY §8 f1); N > 1: halo exchange of "
                          "the block before each shard inside the step")
-    ap.add_argument("--tradeoff", default="4,6,7,16",
+    ap.add_argument("--tradeoff", default="4,6,8,16",
                     help="N = 1: also time these max_chain values (same flags) for the speed/size curve "
                          "(reported under 'tradeoff'; '' = skip)")
     ap.add_argument("--exhaustive-steps", type=int, default=3,

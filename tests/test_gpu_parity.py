@@ -108,7 +108,7 @@ def test_bounded_chain_parity(enc, k):
     check_stream(z, data)
 
 
-@pytest.mark.parametrize("k", [0, 1, 4, 6, 8, 16])
+@pytest.mark.parametrize("k", [0, 1, 4, 6, 7, 8, 16])
 def test_lazy_parity(enc, golden_cases, k):
     """DMX_F_LAZY: byte-identical to the oracle's sequential lazy parse."""
     data = (golden_cases["bee0"] + D.gen_text(200000, 12).tobytes() + bytes(5000)
@@ -118,7 +118,7 @@ def test_lazy_parity(enc, golden_cases, k):
     check_stream(z, data)
 
 
-@pytest.mark.parametrize("k", [0, 6, 8, 16])
+@pytest.mark.parametrize("k", [0, 6, 7, 8, 16])
 def test_exact_sort_fallback_parity(enc, golden_cases, k):
     """The match-any sort (the fallback if lane-ordered LDS atomics ever misorder) gives the
     same stream as the fast sort and the oracle.  dmx_result.nsortfallback counts the
@@ -305,7 +305,7 @@ def _run_heavy(seed=7):
     return b"".join(parts)
 
 
-@pytest.mark.parametrize("k", [1, 2, 4, 6, 8])
+@pytest.mark.parametrize("k", [1, 2, 4, 6, 7, 8])
 @pytest.mark.parametrize("lazy", [False, True])
 def test_run_dominated_blocks(enc, k, lazy):
     """Run-dominated blocks search with the change bitmap (run_len, bounded mode K <= 8):
@@ -407,7 +407,7 @@ def test_fd_api_streaming_pipes_and_offsets(tmp_path, n):
 
 
 @pytest.mark.parametrize("check", [False, True])
-@pytest.mark.parametrize("k,lazy", [(0, False), (6, True), (8, False), (16, True)])
+@pytest.mark.parametrize("k,lazy", [(0, False), (6, True), (7, True), (8, False), (16, True)])
 def test_uniform_blocks_closed_form(enc, check, k, lazy):
     """Blocks of one repeated byte take a closed-form parse (K1's uniform path, or K0's with
     DMX_F_STORE_CHECK): byte-identical to the oracle's search for every remainder of
