@@ -320,7 +320,7 @@ __constant__ uint8_t c_iclorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 
 // ---------------------------------------------------------------------------------------
 // DMX_INF_STAMPS (diagnostic builds only): per-workgroup cycle totals of the decode phases
 #ifdef DMX_INF_STAMPS
-#define INF_NST 12
+#define INF_NST 16
 __device__ unsigned long long dmx_inf_st[1 << 16][INF_NST];
 #define IST_NOW() __builtin_amdgcn_s_memtime()
 #define IST_ADD(o, k, v) ((o).st[k] += (v))
@@ -331,8 +331,9 @@ __device__ unsigned long long dmx_inf_st[1 << 16][INF_NST];
 
 struct IOut {
 #ifdef DMX_INF_STAMPS
-    unsigned long long st[INF_NST];   // 0 header + tables, 1 symbol loop, 2 flushes, 3 matches, 4 far matches, 5 -, 6 blocks,
-                                      // 7 code length table, 8 code lengths, 9 literal/length table, 10 distance table
+    unsigned long long st[INF_NST];   // 0 header + tables, 1 symbol loop, 2 flushes, 3 matches, 4 far matches, 5 asm runs,
+                                      // 6 blocks, 7 code length table, 8 code lengths, 9 literal/length table,
+                                      // 10 distance table, 11..15 asm-run exits IX_SYM .. IX_MATCH
 #endif
     uint8_t* out;     // + base + ob = position 0
     uint64_t base, ob, cap;   // cap: absolute output capacity
@@ -538,7 +539,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 
 template <uint32_t W, bool CELL>
 __device__ __forceinline__ uint32_t isym_run(IBits& r, uint32_t& op, uint32_t& lim, uint32_t& fl, uint32_t capr,
-                                             uint32_t fok, uint64_t gfl, uint32_t dfl,
+                                             uint32_t fok, uint64_t gfl, uint32_t dfl, uint32_t lta,
                                              uint64_t tgl, uint64_t tgd, uint32_t toff, uint32_t lane, uint64_t gpos0,
                                              uint32_t& len, uint32_t& dist) {
     uint32_t ex;
@@ -675,12 +676,22 @@ __device__ __forceinline__ int iblock(InfLDS<W, typename std::conditional<CELL, 
     const uint64_t gpos0 = (uint64_t)(uintptr_t)(o.out + CS * (o.base + o.ob));
     // the run flushes half rings itself (no Adler sums; a 16-byte aligned output)
     const uint32_t fok = (uint32_t)__builtin_amdgcn_readfirstlane((RING && !ADLER && (gpos0 & 15) == 0) ? 1 : 0);
+    // the literal/length table's canonical arrays (long codes inside the run; 16-byte aligned:
+    // the ring before them is W positions)
+    const uint32_t lta = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_addr(&S.lt));
+    static_assert((W * CS) % 16 == 0 && sizeof(ITable) == 672, "the run's ITable offsets (dmx_isym.inc)");
     for (;;) {
         uint32_t lim = RING ? min(capr, o.fl + FL) : capr, fl = o.fl;
         uint32_t len, dist;
-        const uint32_t ex = isym_run<W, CELL>(r, op, lim, fl, capr, fok, gpos0, dfl, tgl, tgd, lane * 4, lane, gpos0, len,
-                                              dist);
+        const uint32_t ex = isym_run<W, CELL>(r, op, lim, fl, capr, fok, gpos0, dfl, lta, tgl, tgd, lane * 4, lane, gpos0,
+                                              len, dist);
         o.fl = fl;
+        IST_ADD(o, 5, 1);
+        IST_ADD(o, 11, ex == IX_SYM ? 1 : 0);
+        IST_ADD(o, 12, ex == IX_SEG ? 1 : 0);
+        IST_ADD(o, 13, ex == IX_LIM ? 1 : 0);
+        IST_ADD(o, 14, ex == IX_DIST ? 1 : 0);
+        IST_ADD(o, 15, ex == IX_MATCH ? 1 : 0);
         if (ex == IX_SEG) {   // a refill at a token start that the run does not rotate into
             ib_refill(r);
             continue;

@@ -42,3 +42,35 @@ def test_exhaustive_tokens_collisions_and_ends(golden_cases, lazy):
     data = golden_cases["bee0"] + grams + D.gen_text(30000, 3).tobytes() + b"abcabcabx" * 500
     _check(data, 32768, lazy)
     _check(data[:70001], 7000, lazy)
+
+
+def _colliding_trigram(a: bytes) -> bytes:
+    """A trigram of printable bytes in the same 13-bit bucket as `a` (dmx_hash), a != it."""
+    ta = a[0] | a[1] << 8 | a[2] << 16
+    h = ((ta * 0x9E3779B1) & 0xFFFFFFFF) >> 19
+    for x in range(65, 123):
+        for y in range(65, 123):
+            for z in range(65, 123):
+                t = x | y << 8 | z << 16
+                if t != ta and ((t * 0x9E3779B1) & 0xFFFFFFFF) >> 19 == h:
+                    return bytes([x, y, z])
+    raise AssertionError("no collision")
+
+
+@pytest.mark.parametrize("lazy", [False, True])
+def test_exhaustive_deferred_walks(lazy):
+    """A rare trigram in the bucket of a common one: the nearest earlier entry with the same
+    trigram lies hundreds of bucket entries down, so the gram pass lists the walk and walks it
+    a wave per entry (the path that hung in round 4 when its work counter was claimed by lane 0
+    only).  Tokens equal the oracle's."""
+    rng = np.random.default_rng(9)
+    a = b"qzv"
+    b = _colliding_trigram(a)
+    parts = []
+    for n in range(3000):
+        parts.append(a + bytes([int(rng.integers(48, 58))]))
+        if n % 150 == 75:
+            parts.append(b + bytes([int(rng.integers(97, 123))]))
+    data = b"".join(parts)
+    _check(data, 32768, lazy)
+    _check(data, 4096, lazy)

@@ -15,7 +15,7 @@ D.LIB_PATH = os.environ["DMX_LIBV"]
 mb = int(sys.argv[1]) if len(sys.argv) > 1 else 100
 n = mb * 1_000_000
 data = torch.from_numpy(D.gen_text(n, 0xE5818)).cuda()
-enc = D.Encoder(0, n, max_chain=8, flags=D.DMX_ZLIB | D.DMX_F_LAZY)
+enc = D.Encoder(0, n, max_chain=7, flags=D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_DEEP)
 out, r = enc.compress_tensor(data)
 ix, nb = enc.block_index()
 L = D.lib()
@@ -32,7 +32,7 @@ assert L.dmx_inflate_async(out.data_ptr(), out.numel(), ix.data_ptr(), nb, dec.d
                            s.cuda_stream) == 0
 e1.record(s)
 torch.cuda.synchronize()
-a = np.zeros((nb, 12), np.uint64)
+a = np.zeros((nb, 16), np.uint64)
 assert L.dmx_inflate_stamps(a.ctypes.data, a.nbytes) == 0
 a = a.astype(np.float64)
 tot = a[:, 0] + a[:, 1]
@@ -44,5 +44,7 @@ print(json.dumps({"lib": os.path.basename(D.LIB_PATH), "ms": round(e0.elapsed_ti
                   "cl_table_kcyc": round(a[:, 7].mean() / 1e3, 1),
                   "header_to_ll_table_kcyc": round(a[:, 8].mean() / 1e3, 1),
                   "ll_table_kcyc": round(a[:, 9].mean() / 1e3, 1), "dist_table_kcyc": round(a[:, 10].mean() / 1e3, 1),
+                  "asm_runs": round(a[:, 5].mean(), 1),
+                  "exits": {k: round(a[:, 11 + j].mean(), 1) for j, k in enumerate(["sym", "seg", "lim", "dist", "match"])},
                   "total_kcyc_max": round(tot.max() / 1e3, 1)}))
 enc.close()
