@@ -33,10 +33,10 @@ PY
     sq) bash "$R/tools/sq_profile.sh" "$TAG/sq" ${arg//,/ } > /dev/null 2>&1 || exit 3; cat "$OUT/sq/sq_summary.txt" ;;
     inflate) timeout -k 10 300 python3 "$R/tools/inflate_bench.py" ${arg//,/ } > "$OUT/inflate.json" 2>&1 || exit 3; cat "$OUT/inflate.json" ;;
     infpmc) cd /tmp; for set in "FETCH_SIZE" "WRITE_SIZE"; do
-              timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d "$OUT/ipmc_$set" -o p -- python3 "$R/tools/inflate_bench.py" --steps 2 --stream-mb 1 $arg > /dev/null 2> "$OUT/ipmc_$set.err" || exit 3
+              timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d "$OUT/ipmc_$set" -o p -- python3 "$R/tools/inflate_bench.py" --steps 2 --stream-mb 1 ${arg//,/ } > /dev/null 2> "$OUT/ipmc_$set.err" || exit 3
             done; python3 "$R/tools/pmc.py" "$OUT/ipmc_FETCH_SIZE,$OUT/ipmc_WRITE_SIZE" | tee "$OUT/inf_pmc.txt"; cd "$R" ;;
     deep) timeout -k 10 300 python3 "$R/tools/deep_bench.py" 32 > "$OUT/deep.txt" 2>&1 || exit 3; cat "$OUT/deep.txt" ;;
-    trace) cd /tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --cpu-budget 0 --exhaustive-steps 0 --tradeoff= --long-run 0 $arg > "$OUT/bench_trace.json" 2> "$OUT/trace.err" || exit 3
+    trace) cd /tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --cpu-budget 0 --exhaustive-steps 0 --tradeoff= --long-run 0 ${arg//,/ } > "$OUT/bench_trace.json" 2> "$OUT/trace.err" || exit 3
            find "$OUT/trace" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \; ; cut -d, -f1-8 "$OUT/kernel_stats.csv" | head -20; cd "$R" ;;
     *) echo "unknown step $name"; exit 2 ;;
   esac
