@@ -167,3 +167,90 @@ def test_stream_ring_edges(level):
         dec, st = D.inflate_gpu(_dev(z), len(data) + 16)
         assert st == 0, (name, level, st)
         assert dec.cpu().numpy().tobytes() == data, (name, level)
+
+
+def _max_code_lengths(z: bytes, raw_offset: int = 2):
+    """(longest literal/length code, longest distance code) of the first DEFLATE block of a
+    zlib stream (RFC 1951 §3.2.7 header), or None if that block is not dynamic."""
+    pos = raw_offset * 8
+
+    def bits(n):
+        nonlocal pos
+        v = 0
+        for i in range(n):
+            v |= ((z[(pos + i) >> 3] >> ((pos + i) & 7)) & 1) << i
+        pos += n
+        return v
+
+    bits(1)
+    if bits(2) != 2:
+        return None
+    hlit, hdist, hclen = bits(5) + 257, bits(5) + 1, bits(4) + 4
+    order = [16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15]
+    cl = [0] * 19
+    for k in range(hclen):
+        cl[order[k]] = bits(3)
+    # canonical decode of the code-length code (codes read MSB first)
+    codes, code, nxt = {}, 0, {}
+    for L in range(1, 8):
+        code = (code + sum(1 for x in cl if x == L - 1 and L > 1)) << 1 if L > 1 else 0
+        nxt[L] = code
+    for s in range(19):
+        if cl[s]:
+            codes[(cl[s], nxt[cl[s]])] = s
+            nxt[cl[s]] += 1
+    lens = []
+    while len(lens) < hlit + hdist:
+        c, L = 0, 0
+        while (L, c) not in codes or L == 0:
+            c = (c << 1) | bits(1)
+            L += 1
+        s = codes[(L, c)]
+        if s < 16:
+            lens.append(s)
+        elif s == 16:
+            lens += [lens[-1]] * (3 + bits(2))
+        elif s == 17:
+            lens += [0] * (3 + bits(3))
+        else:
+            lens += [0] * (11 + bits(7))
+    return max(lens[:hlit]), max(lens[hlit:])
+
+
+def _long_code_input() -> bytes:
+    """Text with rare literals (each once: long literal codes), one long repeat (a rare length
+    symbol) and a few far repeats (rare distance codes)."""
+    rng = np.random.default_rng(77)
+    t = bytearray(D.gen_text(30000, 41).tobytes())
+    for k, p in enumerate(rng.choice(len(t), 60, replace=False)):
+        t[int(p)] = 128 + k
+    t[20000:20230] = t[3000:3230]                          # a 230-byte match
+    for d, p in ((5, 9000), (6, 9100), (9, 9200), (13, 9300)):
+        t[p:p + 5] = t[p - d:p - d + 5]                     # short-distance matches: distance codes 4..7
+    return bytes(t)
+
+
+def test_long_codes_inside_the_run():
+    """Literal/length and distance codes longer than the 10-bit first-level tables: decoded
+    inside the asm run from the canonical arrays.  Checked on our
+    streams (indexed, one block) and zlib's (stream mode); the headers are parsed to show the
+    codes really are longer than 10 bits."""
+    data = _long_code_input()
+    enc = D.Encoder(0, 1 << 20)
+    try:
+        for k, lazy in ((0, False), (8, True)):
+            z = D.compress(data, max_chain=k, lazy=lazy)
+            ll, dl = _max_code_lengths(z)
+            assert ll > 10 and dl > 10, (k, ll, dl)
+            out, r = enc.compress_tensor(_dev(data), opts=D.Opts(32768, k, D.DMX_ZLIB | (D.DMX_F_LAZY if lazy else 0), 0))
+            ix, n = enc.block_index()
+            dec, st = D.inflate_gpu(out, len(data), ix, n)
+            assert st == 0 and dec.cpu().numpy().tobytes() == data, (k, st)
+            dec, st = D.inflate_gpu(_dev(z), len(data) + 16)
+            assert st == 0 and dec.cpu().numpy().tobytes() == data, (k, st)
+    finally:
+        enc.close()
+    for level in (6, 9):
+        z = zlib.compress(data, level)
+        dec, st = D.inflate_gpu(_dev(z), len(data) + 16)
+        assert st == 0 and dec.cpu().numpy().tobytes() == data, (level, st)
