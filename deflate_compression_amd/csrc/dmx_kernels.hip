@@ -182,6 +182,16 @@ __device__ __forceinline__ uint32_t ld4(const uint32_t* W, uint32_t p) {   // by
 }
 template <int NB>
 __device__ __forceinline__ uint64_t ldg(const uint32_t* W, uint32_t p) { return NB > 4 ? ld8(W, p) : (uint64_t)ld4(W, p); }
+// A seed in 16 bits: the nearest earlier position q with the same first NG bytes (NG = 3 or
+// 4, bit 15 = NG == 4), 0xFFFF = none (q <= bn - 3 < 0x7FFF); decoded into the search's key
+// form NG << 15 | q, 0 = none.
+template <int NG>
+__device__ __forceinline__ uint16_t seed_enc(uint32_t q) {
+    return q != 0xFFFFu ? (uint16_t)((NG == 4 ? 0x8000u : 0u) | q) : (uint16_t)0xFFFFu;
+}
+__device__ __forceinline__ uint32_t seed_dec(uint32_t s) {
+    return s == 0xFFFFu ? 0u : ((3u + (s >> 15)) << 15) | (s & 0x7FFFu);
+}
 // bytes p..p+11 from four aligned dwords (two ds_read2_b32; ld8 + ld4 issued a fifth read)
 __device__ __forceinline__ void ld12(const uint32_t* W, uint32_t p, uint32_t& x0, uint32_t& x1, uint32_t& x2) {
     const uint32_t a = p >> 2, sh = p & 3;
@@ -820,7 +830,7 @@ __device__ __forceinline__ uint32_t search_pairs(MatchLDS& L, uint32_t bn, uint3
 template <bool DICT, bool RUNS, int NB = 3>
 __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint16_t* __restrict__ pg,
                                      uint32_t tid, bool stamp, uint64_t& tdef, const uint32_t* __restrict__ hbk,
-                                     const uint32_t* __restrict__ seeds = nullptr) {
+                                     const uint16_t* __restrict__ seeds = nullptr) {
     constexpr bool H4 = NB > 3;   // NB-byte chains seeded with the shorter matches (P0')
     const uint32_t lane = tid & 63, wave = wave_of(tid);
     const uint32_t K = max_chain > 0 ? (uint32_t)max_chain : 0xFFFFFFFFu;
@@ -934,8 +944,8 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
     // chunk ahead
     uint32_t cnx = wave_claim(&L.ntok);
     uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnx);
-    uint32_t snext = 0;
-    if (H4 && (c0 << 6) + lane < nvalid) snext = seeds[L.sorted[(c0 << 6) + lane]];
+    uint32_t snext = 0xFFFFu;   // (a 16-bit seed: none)
+    if (H4 && (c0 << 6) + lane < nvalid) snext = seeds[L.sorted[(c0 << 6) + lane]];   // (raw: decoded at use)
     for (;;) {
         const uint32_t k0 = c0 << 6;
         if (k0 >= nvalid) break;
@@ -946,7 +956,7 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
         uint32_t i = 0, nc = 0, lim = 0;
         uint32_t seed = 0;
         if (H4) {
-            seed = snext;
+            seed = seed_dec(snext);
             if ((c1 << 6) + lane < nvalid) snext = seeds[L.sorted[(c1 << 6) + lane]];
         }
         uint64_t iv0 = 0;
@@ -1331,7 +1341,7 @@ __device__ __forceinline__ void sort_positions(MatchLDS& L, uint32_t bn, int32_t
 // and walked afterwards a wave per entry, 64 entries a step.  Returns this thread's
 // sort-order check (an entry before its predecessor).
 template <int NG>
-__device__ __forceinline__ uint32_t gram_pass(MatchLDS& L, uint32_t nv, uint32_t tid, uint32_t* __restrict__ seeds,
+__device__ __forceinline__ uint32_t gram_pass(MatchLDS& L, uint32_t nv, uint32_t tid, uint16_t* __restrict__ seeds,
                                               uint32_t& ndefer, uint64_t& tsweep) {
 #ifndef DMX_GRAM_PW
     constexpr uint32_t PW = 9;
@@ -1383,9 +1393,9 @@ __device__ __forceinline__ uint32_t gram_pass(MatchLDS& L, uint32_t nv, uint32_t
         }
         // (a gram that runs past the block's end is a match of fewer bytes: the 3-byte seed stays)
 #ifndef DMX_H4_NOSTORE
-        if (act && (NG == 3 || (q != 0xFFFFu && i + NG <= nv + 2))) seeds[i] = q != 0xFFFFu ? ((uint32_t)NG << 15) | q : 0u;
+        if (act && (NG == 3 || (q != 0xFFFFu && i + NG <= nv + 2))) seeds[i] = seed_enc<NG>(q);
 #else
-        if (act && q == 0x1234u) seeds[i] = q;   // (diagnostic timing builds: the output is wrong)
+        if (act && q == 0x1234u) seeds[i] = (uint16_t)q;   // (diagnostic timing builds: the output is wrong)
 #endif
     }
     __syncthreads();
@@ -1414,7 +1424,7 @@ __device__ __forceinline__ uint32_t gram_pass(MatchLDS& L, uint32_t nv, uint32_t
             }
             if (x) break;
         }
-        if (lane == 0 && (NG == 3 || (q != 0xFFFFu && i + NG <= nv + 2))) seeds[i] = q != 0xFFFFu ? ((uint32_t)NG << 15) | q : 0u;
+        if (lane == 0 && (NG == 3 || (q != 0xFFFFu && i + NG <= nv + 2))) seeds[i] = seed_enc<NG>(q);
     }
     // every store complete (in L2) before the caller's barrier: the search's loads of the
     // seeds come from other waves, and a workgroup barrier alone does not wait for stores
@@ -2250,7 +2260,9 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
     // the trigram's bucket with equal bytes; hash collisions are skipped) and kept in HBM,
     // in this block's token slots, until the search merges it (longest, then nearest).
     constexpr bool h4 = NBX > 3 && !DICT;   // launched only with max_chain == 0
-    uint32_t* seeds = tok_g + (uint64_t)b * DMX_BLK;   // this block's token slots, free until P3
+    // this block's token slots (free until P3), as 16-bit seeds: 64 KB per block, so the seeds of
+    // the 32 blocks of an XCD (2 MB) stay in its 4 MB L2 between the gram pass and the search
+    uint16_t* seeds = reinterpret_cast<uint16_t*>(tok_g + (uint64_t)b * DMX_BLK);
     if constexpr (h4) {
         const uint32_t nv = bn > 2 ? bn - 2 : 0;
         const uint32_t hook = L.sortbad;   // the exact-sort test hook (mflags & 2)
