@@ -1628,8 +1628,8 @@ __device__ __forceinline__ void hist_flush(const HistLDS& L, uint32_t wave, uint
     __builtin_amdgcn_wave_barrier();
 }
 
-// HG = history candidates per group: 6 for K <= 6 (the bench default), 8 otherwise (K > 6 in
-// fewer groups).
+// HG = history candidates per group: 6 for K <= 6, 7 for K = 7 (the bench default), 8 otherwise
+// (K > 8 in groups of 8).
 template <int HG>
 __global__ __launch_bounds__(MT) void dmx_hist_kernel_t(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
                                                       int32_t max_chain, const uint8_t* __restrict__ pre, uint32_t npre,
@@ -4182,7 +4182,8 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         if (o.flags & DMX_F_DICT) {
             hipLaunchKernelGGL(dmx_chain_kernel, dim3(nblk + 1), dim3(MT), 0, s, (const uint8_t*)d_in, n,
                                (uint32_t)o.sw, (const uint8_t*)o.dict, dict_len, c->chs, c->che, c->nfb);
-            hipLaunchKernelGGL((o.max_chain >= 1 && o.max_chain <= 6) ? dmx_hist_kernel_t<6> : dmx_hist_kernel_t<8>,
+            hipLaunchKernelGGL((o.max_chain >= 1 && o.max_chain <= 6) ? dmx_hist_kernel_t<6>
+                               : o.max_chain == 7 ? dmx_hist_kernel_t<7> : dmx_hist_kernel_t<8>,
                                dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n, (uint32_t)o.sw,
                                o.max_chain, (const uint8_t*)o.dict, dict_len, c->chs, c->che, c->tok, dbg);
         }

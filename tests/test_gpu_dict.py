@@ -43,7 +43,7 @@ def gpu_inflate_stream(z: bytes, n: int) -> bytes:
     return out.cpu().numpy().tobytes(), st
 
 
-@pytest.mark.parametrize("K", [0, 1, 4, 6, 8, 16, 64])
+@pytest.mark.parametrize("K", [0, 1, 4, 6, 7, 8, 16, 64])
 @pytest.mark.parametrize("lazy", [False, True])
 def test_dict_streams_match_oracle(enc, K, lazy):
     flags = D.DMX_ZLIB | D.DMX_F_DICT | (D.DMX_F_LAZY if lazy else 0)
