@@ -1689,7 +1689,7 @@ __global__ __launch_bounds__(MT) void dmx_hist_kernel_t(const uint8_t* __restric
             // is another trigram), so it is masked, and the walk ends after its group; the
             // exhaustive walk also ends where the bucket does.
             x0 = (int32_t)Ep[h] - 1;
-            if (K <= (uint32_t)HG) {   // bounded (the bench's K = 6): one group, extensions queued
+            if (K <= (uint32_t)HG) {   // bounded (the bench's K = 7): one group, extensions queued
                 hist_group<HG, true, true>(L, x0, 0, K, h, t0, t1, t2, i, lim, minq, best, bq, &full);
             } else {
                 uint32_t cnt = 0;
