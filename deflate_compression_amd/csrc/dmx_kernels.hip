@@ -3613,9 +3613,16 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply_kernel(dmx_blkinfo* 
 // K4: bit packing
 // ------------------------------------------------------------------------------------
 
+#ifndef PT
 #define PT 256
+#endif
+#ifndef TPT
 #define TPT 8   // tokens per thread per packing round
-#define PK_RING 4096   // pack ring words: > 1 + max(160 header words, 2048 tokens x 48 bits / 32) + 1
+#endif
+#ifndef PK_RING
+#define PK_RING 4096   // pack ring words: > 1 + max(160 header words, PT x TPT tokens x 48 bits / 32) + 1
+#endif
+static_assert(PK_RING > 2 + (PT * TPT * 48) / 32 && PK_RING > 162, "pack ring too small for a round");
 
 // A workgroup barrier that orders LDS only: global loads in flight (the next round's tokens)
 // stay in flight across it (__syncthreads() also waits for every outstanding global access).

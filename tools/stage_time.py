@@ -1,6 +1,6 @@
 """Diagnostic: HIP-event stage times (ms) of one encode configuration on cuda:0, averaged
 over a few encodes (no verification -- for experiments on a kernel variant).
-usage: stage_time.py [MB] [K] [flags: any of l(azy) s(plit) d(ict) c(store check)]"""
+usage: stage_time.py [MB] [K] [flags: any of l(azy) s(plit) d(ict) c(store check) e (deep)]"""
 import os
 import sys
 
@@ -16,7 +16,8 @@ mb = float(sys.argv[1]) if len(sys.argv) > 1 else 100
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 6
 fs = sys.argv[3] if len(sys.argv) > 3 else "lc"
 flags = D.DMX_ZLIB | (D.DMX_F_LAZY if "l" in fs else 0) | (D.DMX_F_SPLIT if "s" in fs else 0) | \
-    (D.DMX_F_DICT if "d" in fs else 0) | (D.DMX_F_STORE_CHECK if "c" in fs else 0)
+    (D.DMX_F_DICT if "d" in fs else 0) | (D.DMX_F_STORE_CHECK if "c" in fs else 0) | \
+    (D.DMX_F_DEEP if "e" in fs else 0)
 n = int(mb * 1e6)
 t = torch.from_numpy(D.gen_text(n, 0xE5818)).cuda()
 e = D.Encoder(0, n, max_chain=k, flags=flags)
@@ -28,5 +29,9 @@ for _ in range(5):
     e.compress_tensor(t)
 torch.cuda.synchronize()
 st, cnt = e.stage_times()
-print({"config": f"{mb} MB K={k} {fs}", "encodes": cnt, "stage_ms": {a: round(b, 4) for a, b in st.items()}})
+import hashlib
+o, r = e.compress_tensor(t)
+h = hashlib.sha1(o.cpu().numpy().tobytes()).hexdigest()[:16]
+print({"config": f"{mb} MB K={k} {fs}", "encodes": cnt, "stage_ms": {a: round(b, 4) for a, b in st.items()},
+       "out_len": int(r.out_len), "sha1": h})
 e.close()
