@@ -3660,10 +3660,10 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
     __shared__ uint32_t stage[PK_RING];
     __shared__ uint32_t code[DMX_HIST];
     __shared__ uint32_t wsum[PT / 64];
-    if (res->status) return;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t b = blockIdx.x;
-    const dmx_blkinfo bi = info[b];
+    const dmx_blkinfo bi = info[b];   // in flight with the status load (a stored block's WG is
+    if (res->status) return;          // a chain of dependent loads: C4 launches 32 768 of them)
     const uint64_t O = bi.off_bits, Lb = bi.len_bits;
     const uint32_t s0 = (uint32_t)(O & 31);
     const uint32_t nwords = (uint32_t)((s0 + Lb + 31) >> 5);
