@@ -249,20 +249,23 @@ __device__ __forceinline__ uint32_t match_bytes(uint64_t x) {   // equal leading
 __device__ __forceinline__ uint32_t wshr(uint32_t v, uint32_t lane0) {   // lane l <- lane l-1; lane 0 <- lane0
     return (uint32_t)__builtin_amdgcn_update_dpp((int)lane0, (int)v, 0x138, 0xF, 0xF, false);
 }
-// Length of a candidate known to match bytes [0, kk): 16 bytes in the first LDS round trip
+// Length of a candidate known to match bytes [0, kk): 24 bytes in the first LDS round trip
 // (most extensions end there), then 32 per round trip.
 // Each side is read as 9 aligned words and realigned with v_alignbyte (one VALU per 4
 // bytes); the first differing word comes from a mask of non-zero xors.
+#ifndef EXT_W1
+#define EXT_W1 6   // words compared in the first round (24 bytes; 16 took 1.202 ms of K1 on C3, 24 1.185)
+#endif
 __device__ __forceinline__ uint32_t ext_len2(const uint32_t* A, uint32_t i, const uint32_t* B, uint32_t q, uint32_t kk,
                                              uint32_t lim) {
-    {   // first round: 16 bytes (5 aligned words per side) -- most extensions end there
+    {   // first round: 4 EXT_W1 bytes (EXT_W1 + 1 aligned words per side)
         const uint32_t a = (i + kk) >> 2, sa = (i + kk) & 3, c = (q + kk) >> 2, sc = (q + kk) & 3;
-        uint32_t wa[5], wc[5];
+        uint32_t wa[EXT_W1 + 1], wc[EXT_W1 + 1];
 #pragma unroll
-        for (int t = 0; t < 5; t++) { wa[t] = A[a + t]; wc[t] = B[c + t]; }
-        uint32_t x[4], nz = 0;
+        for (int t = 0; t < EXT_W1 + 1; t++) { wa[t] = A[a + t]; wc[t] = B[c + t]; }
+        uint32_t x[EXT_W1], nz = 0;
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
+        for (int t = 0; t < EXT_W1; t++) {
             x[t] = __builtin_amdgcn_alignbyte(wa[t + 1], wa[t], sa) ^ __builtin_amdgcn_alignbyte(wc[t + 1], wc[t], sc);
             nz |= (x[t] != 0 ? 1u : 0u) << t;
         }
@@ -270,10 +273,10 @@ __device__ __forceinline__ uint32_t ext_len2(const uint32_t* A, uint32_t i, cons
             const uint32_t t0 = (uint32_t)__builtin_ctz(nz);
             uint32_t xv = x[0];
 #pragma unroll
-            for (int t = 1; t < 4; t++) xv = (t0 == (uint32_t)t) ? x[t] : xv;
+            for (int t = 1; t < EXT_W1; t++) xv = (t0 == (uint32_t)t) ? x[t] : xv;
             return kk + 4 * t0 + ((uint32_t)__builtin_ctz(xv) >> 3);
         }
-        kk += 16;
+        kk += 4 * EXT_W1;
         if (kk >= lim) return kk;
     }
     for (;;) {
