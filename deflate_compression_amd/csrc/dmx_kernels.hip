@@ -253,6 +253,9 @@ __device__ __forceinline__ uint32_t wshr(uint32_t v, uint32_t lane0) {   // lane
 // (most extensions end there), then 32 per round trip.
 // Each side is read as 9 aligned words and realigned with v_alignbyte (one VALU per 4
 // bytes); the first differing word comes from a mask of non-zero xors.
+#ifndef EXT_W2
+#define EXT_W2 8   // words compared in each later round (reads reach 4 EXT_W2 + 4 bytes past kk)
+#endif
 #ifndef EXT_W1
 #define EXT_W1 6   // words compared in the first round (24 bytes; 16 took 1.202 ms of K1 on C3, 24 1.185)
 #endif
@@ -281,12 +284,12 @@ __device__ __forceinline__ uint32_t ext_len2(const uint32_t* A, uint32_t i, cons
     }
     for (;;) {
         const uint32_t a = (i + kk) >> 2, sa = (i + kk) & 3, c = (q + kk) >> 2, sc = (q + kk) & 3;
-        uint32_t wa[9], wc[9];
+        uint32_t wa[EXT_W2 + 1], wc[EXT_W2 + 1];
 #pragma unroll
-        for (int t = 0; t < 9; t++) { wa[t] = A[a + t]; wc[t] = B[c + t]; }
-        uint32_t x[8], nz = 0;
+        for (int t = 0; t < EXT_W2 + 1; t++) { wa[t] = A[a + t]; wc[t] = B[c + t]; }
+        uint32_t x[EXT_W2], nz = 0;
 #pragma unroll
-        for (int t = 0; t < 8; t++) {
+        for (int t = 0; t < EXT_W2; t++) {
             x[t] = __builtin_amdgcn_alignbyte(wa[t + 1], wa[t], sa) ^ __builtin_amdgcn_alignbyte(wc[t + 1], wc[t], sc);
             nz |= (x[t] != 0 ? 1u : 0u) << t;
         }
@@ -294,10 +297,10 @@ __device__ __forceinline__ uint32_t ext_len2(const uint32_t* A, uint32_t i, cons
             const uint32_t t0 = (uint32_t)__builtin_ctz(nz);
             uint32_t xv = x[0];
 #pragma unroll
-            for (int t = 1; t < 8; t++) xv = (t0 == (uint32_t)t) ? x[t] : xv;
+            for (int t = 1; t < EXT_W2; t++) xv = (t0 == (uint32_t)t) ? x[t] : xv;
             return kk + 4 * t0 + ((uint32_t)__builtin_ctz(xv) >> 3);
         }
-        kk += 32;
+        kk += 4 * EXT_W2;
         if (kk >= lim) return kk;
     }
 }
