@@ -28,6 +28,7 @@
 #include <stdint.h>
 #include <type_traits>
 #include <stdio.h>
+#include <string.h>
 
 #include "../../include/dmx.h"
 
@@ -900,35 +901,45 @@ __global__ __launch_bounds__(64) void dmx_inflate_stream_kernel(const uint8_t* _
 // C ABI
 // ------------------------------------------------------------------------------------
 
-// Table scratch of dmx_inflate_async, one slot per (device, stream): reused by every decode
-// on that stream (stream order keeps the reuse safe); a larger request frees the old buffer
-// and allocates the new one on the same stream.  Never released (a process-lifetime cache).
-#define ITAB_SLOTS 64
-struct ItabSlot { int dev; hipStream_t s; uint32_t* p; uint64_t bytes; };
-static ItabSlot g_itab[ITAB_SLOTS];
-static int g_nitab = 0;
+// Table scratch of dmx_inflate_async: a stream-ordered allocation from a private memory pool
+// per device, freed on the same stream after the launch.  The pool keeps what it was given
+// (release threshold = no limit), so a steady stream of decodes allocates from the pool's
+// reserve, not from the driver, and any number of streams (created and destroyed per
+// request, or the per-thread default stream) is safe: no buffer is shared between calls.
+// (Round 4 cached one buffer per (device, stream handle): it failed past 64 streams, never
+// released a slot, and a reused handle shared a buffer with a destroyed stream's work.)
+#define ITAB_DEVS 64
+static hipMemPool_t g_itab_pool[ITAB_DEVS];
 static pthread_mutex_t g_itab_mu = PTHREAD_MUTEX_INITIALIZER;
+static hipMemPool_t itab_pool(int dev) {
+    if (dev < 0 || dev >= ITAB_DEVS) return nullptr;
+    pthread_mutex_lock(&g_itab_mu);
+    if (!g_itab_pool[dev]) {
+        hipMemPoolProps pp;
+        memset(&pp, 0, sizeof(pp));
+        pp.allocType = hipMemAllocationTypePinned;
+        pp.handleTypes = hipMemHandleTypeNone;
+        pp.location.type = hipMemLocationTypeDevice;
+        pp.location.id = dev;
+        hipMemPool_t p = nullptr;
+        if (hipMemPoolCreate(&p, &pp) == hipSuccess) {
+            uint64_t keep = ~0ull;
+            (void)hipMemPoolSetAttribute(p, hipMemPoolAttrReleaseThreshold, &keep);
+            g_itab_pool[dev] = p;
+        }
+    }
+    hipMemPool_t r = g_itab_pool[dev];
+    pthread_mutex_unlock(&g_itab_mu);
+    return r;
+}
 static uint32_t* itab_scratch(hipStream_t s, uint64_t bytes) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    pthread_mutex_lock(&g_itab_mu);
-    ItabSlot* e = nullptr;
-    for (int k = 0; k < g_nitab; k++)
-        if (g_itab[k].dev == dev && g_itab[k].s == s) { e = &g_itab[k]; break; }
-    if (!e && g_nitab < ITAB_SLOTS) { e = &g_itab[g_nitab++]; *e = {dev, s, nullptr, 0}; }
-    uint32_t* r = nullptr;
-    if (e) {
-        if (e->bytes < bytes) {
-            if (e->p) (void)hipFreeAsync(e->p, s);
-            e->p = nullptr;
-            e->bytes = 0;
-            if (hipMallocAsync((void**)&e->p, bytes, s) == hipSuccess) e->bytes = bytes;
-            else e->p = nullptr;
-        }
-        r = e->p;
-    }
-    pthread_mutex_unlock(&g_itab_mu);
-    return r;
+    void* p = nullptr;
+    hipMemPool_t pool = itab_pool(dev);
+    if (pool ? hipMallocFromPoolAsync(&p, bytes, pool, s) != hipSuccess : hipMallocAsync(&p, bytes, s) != hipSuccess)
+        return nullptr;
+    return (uint32_t*)p;
 }
 
 extern "C" int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_iblock* d_index, uint32_t nblk,
@@ -948,7 +959,9 @@ extern "C" int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_ibl
     else
         hipLaunchKernelGGL(dmx_inflate_stream_kernel, dim3(1), dim3(64), 0, s, (const uint8_t*)d_z, zbytes,
                            (uint8_t*)d_out, out_cap, gtab, d_status);
-    if (hipGetLastError() != hipSuccess) return -(int)E_DEVICE;
+    const hipError_t le = hipGetLastError();
+    (void)hipFreeAsync(gtab, s);   // stream-ordered: after the decode
+    if (le != hipSuccess) return -(int)E_DEVICE;
     return 0;
 }
 

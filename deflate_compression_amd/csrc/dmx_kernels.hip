@@ -127,7 +127,12 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
 // the previous iteration's lane-0 branches and made gram_pass's walk loop exit lane by lane --
 // lanes 1..63 then spun on item 0, a GPU hang (round 4); a lane-0-only add value (1 : 0) takes
 // the optimizer's 64-step iterative scan instead.
+// Every caller runs it with all 64 lanes active (the counter then moves by 64 a claim);
+// DMX_CHECK_CLAIM builds trap on a partial exec mask instead of handing out a wrong item.
 __device__ __forceinline__ uint32_t wave_claim(uint32_t* ctr) {
+#ifdef DMX_CHECK_CLAIM
+    if (__builtin_amdgcn_read_exec() != ~0ull) __builtin_trap();
+#endif
     return atomicAdd(ctr, 1u) >> 6;
 }
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
@@ -1188,6 +1193,120 @@ __device__ __forceinline__ uint32_t block_excl_scan(MatchLDS& L, uint32_t v, uin
     return base + incl - v;
 }
 
+// Rank in the 16-bit field at bit sh of T[v] (a pair of counters per word): the old field of
+// an LDS atomicAdd of 1 << sh, which same-address lanes of one instruction get in lane order
+// (checked at run time, see count_sort_positions).  A step whose valid lanes share v (runs)
+// takes one add of the group size instead of a 64-way same-address atomic.
+template <bool RUNCHK>
+__device__ __forceinline__ uint32_t atomic_rank16(uint32_t* T, uint32_t v, bool valid, uint64_t lt, uint32_t sh) {
+    if (RUNCHK) {
+        const uint64_t vm = __ballot(valid);
+        if (vm == 0) return 0;
+        const uint32_t first = (uint32_t)__builtin_ctzll(vm);
+        const uint32_t v0 = __builtin_amdgcn_readlane(v, (int)first);
+        if (__ballot(valid && v != v0) == 0) {
+            uint32_t base = 0;
+            if ((threadIdx.x & 63) == first) base = atomicAdd(&T[v0], (uint32_t)__popcll(vm) << sh);
+            return ((__builtin_amdgcn_readlane(base, (int)first) >> sh) & 0xFFFFu) + (uint32_t)__popcll(vm & lt);
+        }
+    }
+    return valid ? (atomicAdd(&T[v], 1u << sh) >> sh) & 0xFFFFu : 0u;
+}
+
+// Bucket-sorted positions S (stable by position inside a bucket) by ONE counting pass over
+// the 13-bit bucket (round 5; the two-pass LSD sort below stays as the checked fallback).
+// The block's positions form two groups (g = 0: [0, 16384), g = 1: the rest); T[h] holds
+// group 0's count of bucket h in its low 16 bits and group 1's in its high 16 bits.
+//  1. every wave hashes its 2048 positions [2048w, 2048w + 2048) into registers;
+//  2. eight rounds, one wave of each group per round (wave w in round w & 7, its group
+//     w >> 3), separated by barriers: the wave adds 1 << 16g to T[h] for its 32 steps of
+//     64 positions and keeps the old field as the entry's rank.  Inside a round a wave's LDS
+//     instructions execute in order and same-address lanes of one instruction in lane
+//     order; the rounds run in position order, so the rank of every entry is the number of
+//     earlier positions of its bucket in its group -- the stable order;
+//  3. one scan over the 8192 buckets: T[h] := start(h) | (start(h) + count0(h)) << 16, the
+//     first slot of each group's run (and start(h) is the bucket start the long chains need);
+//  4. every wave stores its entries at T[h]'s field + rank, no atomics.
+// One rank atomic per entry instead of the LSD sort's two (plus its second count), and the
+// scatter is plain stores.  The search checks every adjacent pair of S (sortbad), so a lane
+// order violation can never go unnoticed: the block then re-sorts with the match-any path.
+template <bool RUNCHK, int NB>
+__device__ __forceinline__ void count_sort_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint32_t tid,
+                                                     bool stamp, uint64_t* tp0) {
+    const uint32_t lane = tid & 63, wave = wave_of(tid);
+    const uint32_t nvalid = bn > 2 ? bn - 2 : 0;   // positions with a full trigram
+    const bool need_starts = max_chain <= 0 || max_chain > KD;
+    uint32_t* T = reinterpret_cast<uint32_t*>(L.len8);   // 8192 counter pairs (len8 is free in P0)
+    const uint4 z4 = make_uint4(0, 0, 0, 0);
+    reinterpret_cast<uint4*>(T)[tid] = z4;
+    reinterpret_cast<uint4*>(T)[tid + MT] = z4;
+    __syncthreads();   // (also: the staged block, for callers without a barrier after staging)
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t x0l = (wave << 11) + lane, nvl = nvalid;
+    uint32_t hh[16];   // bucket of each of this lane's 32 entries, two per register
+    asm volatile("" : "+v"(x0l), "+v"(nvl));
+#pragma unroll
+    for (int st = 0; st < 32; st += 2) {
+        const uint32_t xa = x0l + ((uint32_t)st << 6), xb = xa + 64;
+        const uint32_t ha = xa < nvl ? bucket_of<NB>(ldg<NB>(L.data, xa)) : 0u;
+        const uint32_t hb = xb < nvl ? bucket_of<NB>(ldg<NB>(L.data, xb)) : 0u;
+        hh[st >> 1] = ha | (hb << 16);
+        if ((st & 7) == 6) __builtin_amdgcn_sched_barrier(0);   // 8 loads in flight per group
+    }
+    if (stamp && tid == 0) tp0[0] = __builtin_amdgcn_s_memtime();
+    const uint32_t sh = (wave >> 3) << 4;   // this wave's group field
+    uint32_t rk[16];                        // rank of each entry, two per register
+#pragma unroll
+    for (int j = 0; j < 16; j++) rk[j] = 0;
+    for (uint32_t r = 0; r < 8; r++) {
+        if (r == (wave & 7)) {
+            asm volatile("" : "+v"(x0l), "+v"(nvl));
+#pragma unroll
+            for (int st = 0; st < 32; st++) {
+                const uint32_t x = x0l + ((uint32_t)st << 6);
+                const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
+                const uint32_t rr = atomic_rank16<RUNCHK>(T, h, x < nvl, lt, sh);
+                rk[st >> 1] |= rr << (16 * (st & 1));
+            }
+        }
+        __syncthreads();
+    }
+    if (stamp && tid == 0) tp0[1] = __builtin_amdgcn_s_memtime();
+    {   // bucket starts: thread t scans buckets 8t .. 8t + 7
+        const uint4 a = reinterpret_cast<const uint4*>(T)[2 * tid], c = reinterpret_cast<const uint4*>(T)[2 * tid + 1];
+        uint32_t w[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w}, pre[8], s = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            pre[j] = s;
+            s += (w[j] & 0xFFFFu) + (w[j] >> 16);
+        }
+        const uint32_t base = block_excl_scan(L, s, tid);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t st0 = base + pre[j];
+            pre[j] = st0;
+            w[j] = st0 | ((st0 + (w[j] & 0xFFFFu)) << 16);
+        }
+        reinterpret_cast<uint4*>(T)[2 * tid] = make_uint4(w[0], w[1], w[2], w[3]);
+        reinterpret_cast<uint4*>(T)[2 * tid + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+        if (need_starts)
+            reinterpret_cast<uint4*>(L.bstart)[tid] = make_uint4(pre[0] | (pre[1] << 16), pre[2] | (pre[3] << 16),
+                                                                 pre[4] | (pre[5] << 16), pre[6] | (pre[7] << 16));
+    }
+    __syncthreads();
+    asm volatile("" : "+v"(x0l), "+v"(nvl));
+#pragma unroll
+    for (int st = 0; st < 32; st++) {
+        const uint32_t x = x0l + ((uint32_t)st << 6);
+        const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
+        const uint32_t rr = (rk[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
+        if (x < nvl) L.sorted[((T[h] >> sh) & 0xFFFFu) + rr] = (uint16_t)x;
+        if ((st & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    if (stamp && tid == 0) tp0[2] = __builtin_amdgcn_s_memtime();
+}
+
 // Bucket-sorted positions S (stable by position inside a bucket), built here instead of
 // by a separate chain pass: a two-pass LSD radix sort of the positions by bucket,
 // digit 1 = bucket & 127, digit 2 = bucket >> 7.  Wave w owns the 2048 entries
@@ -1210,6 +1329,12 @@ __device__ __forceinline__ uint32_t block_excl_scan(MatchLDS& L, uint32_t v, uin
 template <bool EXACT, bool RUNCHK = true, int NB = 3>
 __device__ __forceinline__ void sort_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint32_t tid, bool stamp,
                                                uint64_t* tp0) {
+#ifndef DMX_OLD_SORT
+    if constexpr (!EXACT) {
+        count_sort_positions<RUNCHK, NB>(L, bn, max_chain, tid, stamp, tp0);
+        return;
+    }
+#endif
     const uint32_t lane = tid & 63, wave = wave_of(tid);
     const uint32_t nvalid = bn > 2 ? bn - 2 : 0;   // positions with a full trigram
     const bool need_starts = max_chain <= 0 || max_chain > KD;
@@ -4605,12 +4730,12 @@ static int fd_buffers(dmx_ctx* c, uint64_t chunk, uint64_t ocap) {
 }
 
 // --- the single-device fd path (dmx_encode_fd): a five-stage pipeline ---
-// reader thread   chunk j of fd_in -> pinned input slot j % FDP_NIN (FD_READERS parallel preads
+// reader thread   chunk j of fd_in -> pinned input slot j % nin (FD_READERS parallel preads
 //                 on a regular file), running ahead of the device;
 // H2D stream      slot -> device input j % FDP_NDIN;
 // encode stream   the context's stream: encode j (its history, with DMX_F_DICT, is the previous
 //                 device input's tail) -> device output j % 2, result -> pinned record j % 2;
-// D2H stream      device output -> pinned output slot j % FDP_NOUT, as soon as the host has
+// D2H stream      device output -> pinned output slot j % nout, as soon as the host has
 //                 read the chunk's length (the next chunk is already encoding);
 // writer thread   slots to fd_out in order.
 // The chunks are shards of one zlib stream (header on the first, a sync flush after every
@@ -4620,8 +4745,13 @@ static int fd_buffers(dmx_ctx* c, uint64_t chunk, uint64_t ocap) {
 #define FDP_NIN 3
 #define FDP_NOUT 3
 #define FDP_NDIN 3
+// Pinned host memory: (nin + nout) x chunk, 6 x DMX_CHUNK_MB at most.  Chunks above
+// FDP_BIG_CHUNK take 2 + 2 slots, and when pinning 3 + 3 fails the pipeline retries with
+// 2 + 2 (the round-3 footprint) before reporting -E_MALLOC.
+#define FDP_BIG_CHUNK (256ull << 20)
 struct FdPipe {
     uint64_t chunk, ocap;
+    int nin, nout;              // pinned slots in use (FDP_NIN / FDP_NOUT, or 2 each, fdp_get)
     uint8_t* hin[FDP_NIN];      // pinned input slots
     uint8_t* hout[FDP_NOUT];    // pinned output slots
     void* din[FDP_NDIN];        // device input chunks
@@ -4659,18 +4789,16 @@ static void fdp_free(FdPipe* P) {
 
 // The context's pipeline buffers for chunks of `chunk` bytes (kept across calls: pinning
 // ~100 MB costs milliseconds).
-static int fdp_get(dmx_ctx* c, uint64_t chunk, uint64_t ocap, FdPipe** out) {
-    if (c->fdp && c->fdp->chunk >= chunk && c->fdp->ocap >= ocap) { *out = c->fdp; return 0; }
-    fdp_free(c->fdp);
-    c->fdp = NULL;
+static int fdp_try(uint64_t chunk, uint64_t ocap, int nslot, FdPipe** out) {
     FdPipe* P = (FdPipe*)calloc(1, sizeof(FdPipe));
     if (!P) return -(int)E_MALLOC;
+    P->nin = P->nout = nslot;
     int r = 0;
-    for (int k = 0; !r && k < FDP_NIN; k++) {
+    for (int k = 0; !r && k < P->nin; k++) {
         if (hip_fail(dmx_host_malloc((void**)&P->hin[k], chunk + 16), "hipHostMalloc")) r = -(int)E_MALLOC;
         else if (hip_fail(hipEventCreateWithFlags(&P->evh[k], hipEventDisableTiming), "hipEventCreate")) r = -(int)E_DEVICE;
     }
-    for (int k = 0; !r && k < FDP_NOUT; k++) {
+    for (int k = 0; !r && k < P->nout; k++) {
         if (hip_fail(dmx_host_malloc((void**)&P->hout[k], ocap), "hipHostMalloc")) r = -(int)E_MALLOC;
         else if (hip_fail(hipEventCreateWithFlags(&P->evo[k], hipEventDisableTiming), "hipEventCreate")) r = -(int)E_DEVICE;
     }
@@ -4689,6 +4817,20 @@ static int fdp_get(dmx_ctx* c, uint64_t chunk, uint64_t ocap, FdPipe** out) {
     if (r) { fdp_free(P); return r; }
     P->chunk = chunk;
     P->ocap = ocap;
+    *out = P;
+    return 0;
+}
+
+// The context's pipeline buffers for chunks of `chunk` bytes (kept across calls: pinning
+// ~100 MB costs milliseconds).
+static int fdp_get(dmx_ctx* c, uint64_t chunk, uint64_t ocap, FdPipe** out) {
+    if (c->fdp && c->fdp->chunk >= chunk && c->fdp->ocap >= ocap) { *out = c->fdp; return 0; }
+    fdp_free(c->fdp);
+    c->fdp = NULL;
+    FdPipe* P = NULL;
+    int r = fdp_try(chunk, ocap, chunk > FDP_BIG_CHUNK ? 2 : FDP_NIN, &P);
+    if (r == -(int)E_MALLOC && chunk <= FDP_BIG_CHUNK) r = fdp_try(chunk, ocap, 2, &P);   // less pinned memory
+    if (r) return r;
     c->fdp = P;
     *out = P;
     return 0;
@@ -4722,14 +4864,15 @@ static void* fdp_reader(void* a) {
     FdReadJob* J = (FdReadJob*)a;
     FdSync* S = J->S;
     for (uint64_t j = 0;; j++) {
-        const int k = (int)(j % FDP_NIN);
-        pthread_mutex_lock(&S->mu);   // slot k is free once chunk j - FDP_NIN's H2D was enqueued...
-        while (!S->err && j >= FDP_NIN && S->h2d_issued < j - FDP_NIN + 1) pthread_cond_wait(&S->cv, &S->mu);
+        const uint64_t nin = (uint64_t)J->P->nin;
+        const int k = (int)(j % nin);
+        pthread_mutex_lock(&S->mu);   // slot k is free once chunk j - nin's H2D was enqueued...
+        while (!S->err && j >= nin && S->h2d_issued < j - nin + 1) pthread_cond_wait(&S->cv, &S->mu);
         const bool stop = S->err != 0;
         pthread_mutex_unlock(&S->mu);
         if (stop) break;
         // ...and has completed
-        if (j >= FDP_NIN && hip_fail(hipEventSynchronize(J->P->evh[k]), "hipEventSynchronize")) {
+        if (j >= nin && hip_fail(hipEventSynchronize(J->P->evh[k]), "hipEventSynchronize")) {
             fds_fail(S, -(int)E_DEVICE);
             break;
         }
@@ -4750,7 +4893,7 @@ static void* fdp_writer(void* a) {
     FdWriteJob* J = (FdWriteJob*)a;
     FdSync* S = J->S;
     for (uint64_t j = 0;; j++) {
-        const int k = (int)(j % FDP_NOUT);
+        const int k = (int)(j % (uint64_t)J->P->nout);
         pthread_mutex_lock(&S->mu);
         while (!S->err && S->nposted <= j && !(S->done_reading && S->nposted == j)) pthread_cond_wait(&S->cv, &S->mu);
         const bool stop = S->err != 0 || S->nposted <= j;   // an error, or every posted chunk written
@@ -4835,7 +4978,7 @@ static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts,
     uint64_t clen[2] = {0, 0};
     // chunk j - 1's result: its length, Adler-32, the callback; then its D2H and the writer
     auto finish = [&](uint64_t j) -> int {
-        const int k2 = (int)(j & 1), ko = (int)(j % FDP_NOUT);
+        const int k2 = (int)(j & 1), ko = (int)(j % (uint64_t)P->nout);
         if (hip_fail(hipEventSynchronize(P->eve[k2]), "hipEventSynchronize")) return -(int)E_DEVICE;
         if (P->hres[k2]->status) return P->hres[k2]->status;
         const uint64_t olen = P->hres[k2]->out_len;
@@ -4845,8 +4988,8 @@ static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts,
             if (e) return e;
         }
         off += clen[k2];
-        pthread_mutex_lock(&S.mu);   // output slot ko: chunk j - FDP_NOUT written
-        while (!S.err && j >= FDP_NOUT && S.nwritten < j - FDP_NOUT + 1) pthread_cond_wait(&S.cv, &S.mu);
+        pthread_mutex_lock(&S.mu);   // output slot ko: chunk j - nout written
+        while (!S.err && j >= (uint64_t)P->nout && S.nwritten < j - (uint64_t)P->nout + 1) pthread_cond_wait(&S.cv, &S.mu);
         const int e = S.err;
         pthread_mutex_unlock(&S.mu);
         if (e) return e;
@@ -4864,7 +5007,7 @@ static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts,
     };
     bool have_prev = false;
     for (uint64_t i = 0; !r; i++) {
-        const int ki = (int)(i % FDP_NIN), kd = (int)(i % FDP_NDIN), k2 = (int)(i & 1);
+        const int ki = (int)(i % (uint64_t)P->nin), kd = (int)(i % FDP_NDIN), k2 = (int)(i & 1);
         pthread_mutex_lock(&S.mu);
         while (!S.err && S.nread <= i) pthread_cond_wait(&S.cv, &S.mu);
         r = S.err;

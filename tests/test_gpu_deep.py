@@ -35,6 +35,16 @@ def test_deep_streams_match_oracle(enc, name, k, lazy):
     assert zlib.decompress(z) == data
 
 
+@pytest.mark.parametrize("name", sorted(inputs()))
+def test_deep_headline_parse(enc, name):
+    """The bench's parse: K=7, lazy, adaptive depth and the noise check together."""
+    data = inputs()[name]
+    fl = D.DMX_ZLIB | D.DMX_F_DEEP | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK
+    z, r = enc.compress_bytes(data, max_chain=7, flags=fl)
+    assert z == O.compress(data, max_chain=7, lazy=True, deep=True, store_check=True), name
+    assert zlib.decompress(z) == data
+
+
 def test_deep_tokens_per_block(enc):
     data = inputs()["mixed"]
     enc.compress_bytes(data, max_chain=8, flags=D.DMX_ZLIB | D.DMX_F_DEEP | D.DMX_F_LAZY)

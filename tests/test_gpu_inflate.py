@@ -254,3 +254,39 @@ def test_long_codes_inside_the_run():
         z = zlib.compress(data, level)
         dec, st = D.inflate_gpu(_dev(z), len(data) + 16)
         assert st == 0 and dec.cpu().numpy().tobytes() == data, (level, st)
+
+
+def test_many_short_lived_streams(golden_cases):
+    """dmx_inflate_async on more than 64 short-lived streams (created and dropped
+    per call) and on two threads' default streams returns 0 every time and decodes bit-exact:
+    the table scratch is a stream-ordered pool allocation per call, not a per-stream cache."""
+    import threading
+    data = golden_cases["bee0"] + D.gen_text(50_000, 3).tobytes()
+    enc = D.Encoder(0, 1 << 20)
+    try:
+        out, r = enc.compress_tensor(_dev(data)[:len(data)], opts=D.Opts(32768, 8, D.DMX_ZLIB | D.DMX_F_LAZY, 0))
+        ix, n = enc.block_index()
+        torch.cuda.synchronize()
+        for k in range(80):
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                dec, st = D.inflate_gpu(out, len(data), ix, n, stream=s.cuda_stream)
+            s.synchronize()
+            assert st == 0, (k, st)
+            assert dec.cpu().numpy().tobytes() == data, k
+            del s
+        res = [None, None]
+
+        def run(j):
+            d2, st2 = D.inflate_gpu(out, len(data), ix, n)
+            torch.cuda.synchronize()
+            res[j] = st2 == 0 and d2.cpu().numpy().tobytes() == data
+
+        th = [threading.Thread(target=run, args=(j,)) for j in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert res == [True, True]
+    finally:
+        enc.close()

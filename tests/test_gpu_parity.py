@@ -275,7 +275,9 @@ def test_fd_api_errors(tmp_path):
 
 
 def test_c3_scale_roundtrip(enc):
-    """C3 size (100 000 000 B of enwik-style text): size-independent properties."""
+    """C3 size (100 000 000 B of enwik-style text): the whole stream equals the oracle's
+    (its OpenMP form) at the reference parse (exhaustive) and at the bench's headline parse
+    (K=7, lazy, adaptive depth, noise check), and both inflate."""
     n = 100_000_000
     a = D.gen_text(n, 0xE5818)
     t = torch.from_numpy(a).cuda()
@@ -283,12 +285,17 @@ def test_c3_scale_roundtrip(enc):
     out, r = enc.compress_tensor(t)
     z = out.cpu().numpy().tobytes()
     assert r.nblocks == 3052 and r.adler == zlib.adler32(a)
-    assert zlib.decompress(z) == a.tobytes()
-    # bytes of a few blocks equal the oracle's block encoding (first, middle, last)
     assert 0.3 < len(z) / n < 0.5
+    assert z == O.compress_par(a, max_chain=0, threads=16)
+    assert zlib.decompress(z) == a.tobytes()
     for b in (0, 1526, 3051):
         blk = a[b * 32768:(b + 1) * 32768].tobytes()
         assert np.array_equal(enc.tokens(b), O.parse_block(blk))
+    o = D.Opts(32768, 7, D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_DEEP | D.DMX_F_STORE_CHECK, 0)
+    out, r = enc.compress_tensor(t, opts=o)
+    z = out.cpu().numpy().tobytes()
+    assert z == O.compress_par(a, max_chain=7, lazy=True, deep=True, store_check=True, threads=16)
+    assert zlib.decompress(z) == a.tobytes()
 
 
 def _run_heavy(seed=7):

@@ -44,10 +44,11 @@ def _stitch(parts):
 def test_c5_shape_8_shards_vs_oracle(cfg):
     n = 8 * 3 * 32768 + 12345   # 25 blocks: shards of 3 or 4 blocks, a short tail
     host = D.gen_text(n, 0xE5819)
-    kw = {"bench": dict(max_chain=6, lazy=True, store_check=True), "exhaustive": dict(max_chain=0),
+    kw = {"bench": dict(max_chain=7, lazy=True, store_check=True, deep=True), "exhaustive": dict(max_chain=0),
           "dict": dict(max_chain=6, lazy=True, dict=True), "split": dict(max_chain=8, lazy=True, split=True)}[cfg]
     flags = (D.DMX_F_LAZY if kw.get("lazy") else 0) | (D.DMX_F_STORE_CHECK if kw.get("store_check") else 0) | \
-            (D.DMX_F_DICT if kw.get("dict") else 0) | (D.DMX_F_SPLIT if kw.get("split") else 0)
+            (D.DMX_F_DICT if kw.get("dict") else 0) | (D.DMX_F_SPLIT if kw.get("split") else 0) | \
+            (D.DMX_F_DEEP if kw.get("deep") else 0)
     e = D.Encoder(0, n)
     try:
         parts = _encode_shards(host, kw["max_chain"], flags, bool(kw.get("dict")), e)
@@ -67,19 +68,20 @@ def test_c5_shape_8_shards_vs_oracle(cfg):
 
 def test_c5_full_size_8_shards():
     """C5 at its stated size: 1 000 000 000 B of enwik9-style text, 8 shards (3 815 blocks
-    each, the last 3 814 with the 18 944 B tail), K=6 lazy + store check (the bench parse);
-    every shard byte-equal to the oracle's (its OpenMP form), the stitched stream inflates."""
+    each, the last 3 814 with the 18 944 B tail) at the bench parse: K=7 lazy + adaptive
+    depth + store check; every shard byte-equal to the oracle's (its OpenMP form), the
+    stitched stream inflates."""
     n = 1_000_000_000
     host = D.gen_text(n, 0xE5819)
-    flags = D.DMX_F_LAZY | D.DMX_F_STORE_CHECK
+    flags = D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | D.DMX_F_DEEP
     e = D.Encoder(0, n // WORLD + 32768)
     try:
-        parts = _encode_shards(host, 6, flags, False, e)
+        parts = _encode_shards(host, 7, flags, False, e)
     finally:
         e.close()
     for r, (z, _, _) in enumerate(parts):
         lo, hi = S.shard_range(n, r, WORLD)
-        assert z == O.compress_par(host[lo:hi], max_chain=6, lazy=True, store_check=True,
+        assert z == O.compress_par(host[lo:hi], max_chain=7, lazy=True, store_check=True, deep=True,
                                    flags=S.shard_flags(r, WORLD), threads=16), r
     d = zlib.decompressobj()
     out = d.decompress(_stitch(parts)) + d.flush()
