@@ -74,6 +74,12 @@ class Result(ctypes.Structure):
                 ("nsortfallback_total", ctypes.c_uint32)]
 
 
+class FdStats(ctypes.Structure):
+    _fields_ = [("chunks", ctypes.c_uint64), ("bytes_in", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64),
+                ("wall_ms", ctypes.c_double), ("read_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double),
+                ("encode_ms", ctypes.c_double), ("d2h_ms", ctypes.c_double), ("write_ms", ctypes.c_double)]
+
+
 class _StringLen(ctypes.Structure):
     _fields_ = [("str", ctypes.POINTER(ctypes.c_ubyte)), ("len", ctypes.c_size_t)]
 
@@ -110,6 +116,7 @@ def lib() -> ctypes.CDLL:
         "dmx_encode_fd_multi": ([ctypes.c_int, ctypes.c_int, ctypes.POINTER(Opts), u64,
                                  ctypes.POINTER(ctypes.c_int), ctypes.c_int], ctypes.c_int),
         "dmx_max_compressed": ([u64, i32], u64),
+        "dmx_fd_last_stats": ([ctypes.POINTER(FdStats)], ctypes.c_int),
         "dmx_encode_async": ([vp, vp, u64, vp, u64, ctypes.POINTER(Opts), vp], ctypes.c_int),
         "dmx_encode_result": ([vp, ctypes.POINTER(Result), vp], ctypes.c_int),
         "dmx_encode_result_async": ([vp, vp, vp], ctypes.c_int),
@@ -158,6 +165,16 @@ def _buf(data):
     b = bytes(data)
     cb = ctypes.create_string_buffer(b, len(b) or 1)
     return ctypes.cast(cb, ctypes.c_void_p), len(b), cb
+
+
+def fd_last_stats() -> dict | None:
+    """Per-stage busy time of the last single-device fd-path call (dmx_fd_last_stats):
+    wall, read, h2d, encode, d2h, write in ms, plus chunks and bytes; None before any."""
+    st = FdStats()
+    if lib().dmx_fd_last_stats(ctypes.byref(st)) != 0:
+        return None
+    return {k: (round(getattr(st, k), 3) if isinstance(getattr(st, k), float) else int(getattr(st, k)))
+            for k, _ in FdStats._fields_}
 
 
 def max_compressed(n: int, sw: int = 32768) -> int:

@@ -40,6 +40,14 @@
 // small device helpers
 // ------------------------------------------------------------------------------------
 
+// The thread index through an empty volatile asm: values derived from it cannot be hoisted
+// out of the match kernel's work-list loop (LICM would keep dozens of them live across the
+// whole per-block body, i.e. in scratch).
+__device__ __forceinline__ uint32_t tidx() {
+    uint32_t t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
 __device__ __forceinline__ uint32_t dmx_hash(uint32_t tri) { return (tri * 0x9E3779B1u) >> DMX_HASH_SHIFT; }
 // The order of the bucket-sorted array S: (bucket of the trigram in the low 3 bytes of w,
 // position p < 32768) as one integer, so that adjacent entries are checked with one compare.
@@ -396,7 +404,7 @@ __device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
 
 // Inclusive prefix sum over the wave: DPP row shifts inside each row of 16, row totals by readlane.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-    const uint32_t r = threadIdx.x & 15, row = (threadIdx.x & 63) >> 4;
+    const uint32_t r = tidx() & 15, row = (tidx() & 63) >> 4;
     uint32_t y;
     y = dpp_shr(x, 1); if (r >= 1) x += y;
     y = dpp_shr(x, 2); if (r >= 2) x += y;
@@ -1129,7 +1137,7 @@ __device__ __forceinline__ uint64_t group_of(unsigned long long* G, uint32_t v, 
     if (__ballot(valid && v != v0) == 0) return valid ? vm : 0;   // one group (runs): no LDS traffic
     uint64_t eq = 0;
     if (valid) {
-        __hip_atomic_fetch_or(&G[v], 1ull << (threadIdx.x & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_or(&G[v], 1ull << (tidx() & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         eq = __hip_atomic_load(&G[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_store(&G[v], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
@@ -1152,7 +1160,7 @@ __device__ __forceinline__ void count_add(uint32_t* T, uint32_t v, bool valid, b
     const uint32_t first = (uint32_t)__builtin_ctzll(vm);
     const uint32_t v0 = __builtin_amdgcn_readlane(v, (int)first);
     if (__ballot(valid && v != v0) == 0) {
-        if ((threadIdx.x & 63) == first) {
+        if ((tidx() & 63) == first) {
             const uint32_t c = (uint32_t)__popcll(vm);
             if (pair16) atomicAdd(&T[v0 >> 1], c << (16 * (v0 & 1)));
             else atomicAdd(&T[v0], c);
@@ -1176,7 +1184,7 @@ __device__ __forceinline__ uint32_t atomic_rank(uint32_t* T, uint32_t v, bool va
     const uint32_t v0 = __builtin_amdgcn_readlane(v, (int)first);
     if (__ballot(valid && v != v0) == 0) {
         uint32_t base = 0;
-        if ((threadIdx.x & 63) == first) base = atomicAdd(&T[v0], (uint32_t)__popcll(vm));
+        if ((tidx() & 63) == first) base = atomicAdd(&T[v0], (uint32_t)__popcll(vm));
         return __builtin_amdgcn_readlane(base, (int)first) + (uint32_t)__popcll(vm & lt);
     }
     return valid ? atomicAdd(&T[v], 1u) : 0u;
@@ -1206,7 +1214,7 @@ __device__ __forceinline__ uint32_t atomic_rank16(uint32_t* T, uint32_t v, bool 
         const uint32_t v0 = __builtin_amdgcn_readlane(v, (int)first);
         if (__ballot(valid && v != v0) == 0) {
             uint32_t base = 0;
-            if ((threadIdx.x & 63) == first) base = atomicAdd(&T[v0], (uint32_t)__popcll(vm) << sh);
+            if ((tidx() & 63) == first) base = atomicAdd(&T[v0], (uint32_t)__popcll(vm) << sh);
             return ((__builtin_amdgcn_readlane(base, (int)first) >> sh) & 0xFFFFu) + (uint32_t)__popcll(vm & lt);
         }
     }
@@ -1919,6 +1927,35 @@ __device__ __forceinline__ uint32_t uniform_parse(uint32_t bn, uint32_t c, uint3
     return ntok;
 }
 
+// Work lists (DMX_F_STORE_CHECK, round 5): K0 lists the blocks each later kernel has work
+// for, so that a stored block costs no workgroup in K1, K2 or K4 (C4: 32 768 stored blocks).
+// Layout of dmx_ctx::wl (u32): counters, then three lists of cap_blocks entries each:
+//   L1 = wl + WL_HDR             blocks K1 parses (prestored 0), appended by K0
+//   L2 = L1 + cap                blocks K2 codes (prestored 0 and 2), appended by K0
+//   L4 = L2 + cap                blocks K4 packs, appended by the scan's apply launch
+// WL_MX = max over the blocks that K0 did NOT store and copy whole (prestored != 3) of
+// nblk - b, so M = the first such block = nblk - WL_MX.  Blocks 1 <= b < min(M, nblk - 1)
+// form a prefix of stored blocks at their speculative offsets (every block before them is
+// stored too): K0 writes every byte of them and K4 never sees them.  The scan kernel copies
+// M to WL_M and zeroes the counters for the next encode (before the apply launch appends L4).
+#define WL_N1 0
+#define WL_C1 1
+#define WL_N2 2
+#define WL_N4 3
+#define WL_MX 4
+#define WL_M 5
+#define WL_HDR 16
+__device__ __forceinline__ void wl_note(uint32_t* __restrict__ wl, uint64_t cap, uint32_t b, uint32_t nblk, uint32_t ps) {
+    if (!wl) return;
+    if (ps != 3) atomicMax(&wl[WL_MX], nblk - b);
+    if (ps == 0) wl[WL_HDR + atomicAdd(&wl[WL_N1], 1u)] = b;
+    if (ps == 0 || ps == 2) wl[WL_HDR + cap + atomicAdd(&wl[WL_N2], 1u)] = b;
+}
+// K4 never sees block x: a stored block of the whole-copy prefix (above)
+__device__ __forceinline__ bool wl_skip(uint32_t x, uint32_t M, uint32_t nblk) {
+    return x >= 1 && x < M && x + 1 < nblk;
+}
+
 // prestored: 0 = parse in K1; 1 = stored by the noise check; 2 = a block of one repeated
 // byte, parsed here in closed form (K1 skips it, the Huffman kernels code it); 3 = stored,
 // and its interior already written to the stream at the offset it has when every block
@@ -1955,18 +1992,20 @@ __device__ __forceinline__ void stored_quads(uint64_t O, uint32_t bn, bool dal, 
 __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
                                                               dmx_blkinfo* __restrict__ info, uint32_t* __restrict__ tok_g,
                                                               uint32_t* __restrict__ hist_g, uint32_t uni_ok, uint32_t flags,
-                                                              uint32_t* __restrict__ out32, uint64_t out_cap) {
+                                                              uint32_t* __restrict__ out32, uint64_t out_cap,
+                                                              uint32_t* __restrict__ wl, uint64_t wl_cap) {
     __shared__ uint32_t bm[1u << 12];   // the 17-bit presence bitmap (16 KB: 8 workgroups per CU)
     __shared__ uint32_t hist[256];
     __shared__ uint64_t red[10][SCT / 64];
     __shared__ uint32_t pass_s;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t tid = tidx(), lane = tid & 63, wave = tid >> 6;
     const uint32_t b = blockIdx.x;
     const uint64_t off = (uint64_t)b * sw;
     const uint32_t bn = (uint32_t)((n - off) < sw ? (n - off) : sw);
     const uint8_t* d = in + off;
+    const uint32_t nblk = gridDim.x;
     if (bn < 4096) {
-        if (tid == 0) info[b].prestored = 0;
+        if (tid == 0) { info[b].prestored = 0; wl_note(wl, wl_cap, b, nblk, 0); }
         return;
     }
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
@@ -2003,7 +2042,10 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
         }
         __syncthreads();
         if (!pass_s) {
-            if (!uni_ok || !uni4k) return;
+            if (!uni_ok || !uni4k) {
+                if (tid == 0) wl_note(wl, wl_cap, b, nblk, 0);
+                return;
+            }
             // the first 4 KiB are one repeated byte: is the whole block?  Then its parse has
             // a closed form (as in K1's uniform path; no dictionary): a literal, distance-1
             // matches of min(258, bytes left) while >= 3 bytes are left, then literals.
@@ -2018,7 +2060,10 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
                     u = u && ((x[q] ^ c4) & m) == 0;
                 }
             }
-            if (!__syncthreads_and(u)) return;
+            if (!__syncthreads_and(u)) {
+                if (tid == 0) wl_note(wl, wl_cap, b, nblk, 0);
+                return;
+            }
             uint32_t* H = bm;   // the 320-entry histogram (bm is free here)
             for (uint32_t k = tid; k < DMX_HIST; k += SCT) H[k] = 0;
             __syncthreads();
@@ -2031,6 +2076,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
                 info[b].adl_s = S;
                 info[b].adl_w = (uint64_t)bn * S - T;
                 info[b].prestored = 2;
+                wl_note(wl, wl_cap, b, nblk, 2);
             }
             __syncthreads();
             for (uint32_t k = tid; k < DMX_HIST; k += SCT) hist_g[(uint64_t)b * DMX_HIST + k] = H[k];
@@ -2135,6 +2181,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
         // the speculative copy (above) when the whole block fits the output at that offset
         const bool spec = sto && (spec_stored_bit(b, sw, flags) >> 3) + (uint64_t)bn + 16 <= out_cap;
         info[b].prestored = sto ? (spec ? 3u : 1u) : 0u;
+        wl_note(wl, wl_cap, b, nblk, sto ? (spec ? 3u : 1u) : 0u);
         pass_s = spec ? 1u : 0u;
         if (sto) {
             info[b].ntok = 0;
@@ -2202,6 +2249,55 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
             *reinterpret_cast<uint4*>(&out32[(O >> 5) + k]) = v;
         });
     }
+    if (pass_s && wl && b >= 1 && b + 1 < nblk) {
+        // the whole copy (work-list mode): every other byte of the block at its speculative
+        // offset too -- the header byte (BFINAL 0, BTYPE 00), LEN / NLEN, the words before and
+        // after the quads, any of the first two and last two quads that did not take the
+        // 20-byte fast path (as the pack kernel's stored path builds them); its two edge words
+        // by byte stores of its own bytes only (the neighbours' bytes share those words)
+        const uint64_t O = spec_stored_bit(b, sw, flags);
+        const uint32_t s0 = (uint32_t)(O & 31), P = (s0 + 3 + 7) & ~7u, B0 = (P + 32) >> 3;
+        const uint32_t nwords = (uint32_t)(((uint64_t)P + 32 + 8ull * bn + 31) >> 5);
+        const uint32_t ebyte = B0 + bn;   // the block's end, in bytes from word O >> 5
+        const uint64_t gw0 = O >> 5;
+        const bool dal = (reinterpret_cast<uintptr_t>(d) & 3) == 0;
+        const uint32_t ks = 4 - (uint32_t)(gw0 & 3);
+        const uint32_t nq = ((full || dal) && nwords > ks + 1) ? (nwords - 1 - ks) >> 2 : 0;
+        const uint32_t lenw = (bn & 0xFFFFu) | ((~bn & 0xFFFFu) << 16);
+        auto gen_byte = [&](uint32_t q) -> uint32_t {
+            if (q >= B0) return (q - B0) < bn ? (uint32_t)d[q - B0] : 0u;
+            if (q >= (P >> 3)) return (lenw >> (8 * (q - (P >> 3)))) & 0xFFu;
+            return 0u;   // the header byte (and the previous block's bytes below it: not written)
+        };
+        uint8_t* out8 = reinterpret_cast<uint8_t*>(out32 + gw0);
+        auto put_word = [&](uint32_t k) {
+            if (k == 0 || k == nwords - 1) {
+                for (uint32_t q = 4 * k; q < 4 * k + 4; q++)
+                    if (q >= (s0 >> 3) && q < ebyte) out8[q] = (uint8_t)gen_byte(q);
+            } else {
+                uint32_t v = 0;
+                for (uint32_t i = 0; i < 4; i++) v |= gen_byte(4 * k + i) << (8 * i);
+                out32[gw0 + k] = v;
+            }
+        };
+        auto fast = [&](uint32_t j) {
+            const int64_t o0 = (int64_t)(4 * (ks + 4 * j)) - (int64_t)B0;
+            return o0 >= 0 && (uint64_t)((o0 & ~3ll) + 20) <= bn;
+        };
+        const uint32_t kq = nq ? ks + 4 * nq : 0;
+        const uint32_t nrest = nq ? ks + (nwords - kq) : nwords;   // words outside the quads
+        for (uint32_t r = tid; r < nrest + 16; r += SCT) {
+            if (r < nrest) {
+                put_word(nq ? (r < ks ? r : kq + (r - ks)) : r);
+            } else {   // quads 0, 1, nq - 2, nq - 1 (each once) that are not fast
+                const uint32_t t = r - nrest, qi = t >> 2;
+                if (qi >= nq || (nq >= 4 ? false : qi >= nq)) continue;
+                const uint32_t j = qi < 2 ? qi : nq - 4 + qi;
+                if ((qi >= 2 && (nq < 4 || j < 2)) || fast(j)) continue;
+                put_word(ks + 4 * j + (t & 3));
+            }
+        }
+    }
 }
 
 // Diagnostic (DMX_DEBUG_STOP=1|2|3, never in a product run): end the block after P0 (sort),
@@ -2260,17 +2356,20 @@ __device__ __forceinline__ int32_t block_chain(MatchLDS& L, uint32_t bn, int32_t
 #ifndef DMX_NBX
 #define DMX_NBX 4   // the exhaustive parse's chain length in bytes (4; 5 measured slower: a second gram pass and sort)
 #endif
-template <bool DICT, int NBX = 3>
-__global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
-                                                       int32_t max_chain, uint32_t mflags, uint16_t* __restrict__ dist_g,
-                                                       const uint16_t* __restrict__ chs, uint32_t* __restrict__ tok_g,
-                                                       uint32_t* __restrict__ hist_g,
-                                                       dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg,
-                                                       uint32_t* __restrict__ nfallback) {
+template <bool DICT, int NBX>
+__device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
+                                            int32_t max_chain, uint32_t mflags, uint16_t* __restrict__ dist_g,
+                                            const uint16_t* __restrict__ chs, uint32_t* __restrict__ tok_g,
+                                            uint32_t* __restrict__ hist_g,
+                                            dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg,
+                                            uint32_t* __restrict__ nfallback) {
     __shared__ MatchLDS L;
     __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def, tp0[3], st_rounds, st_p3a, st_h4[3], st_lz, st_w1w;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = wave_of(tid);
-    const uint32_t b = blockIdx.x;
+    const uint32_t tid = tidx();
+    // (the arguments too: see tidx)
+    asm volatile("" : "+s"(in), "+s"(n), "+s"(sw), "+s"(max_chain), "+s"(mflags), "+s"(dist_g), "+s"(chs),
+                 "+s"(tok_g), "+s"(hist_g), "+s"(info), "+s"(dbg), "+s"(nfallback));
+    const uint32_t lane = tid & 63, wave = wave_of(tid);
     if ((mflags & 4u) && info[b].prestored) return;   // stored by the noise check (K0)
     const uint64_t off = (uint64_t)b * sw;
     const uint32_t bn = (uint32_t)((n - off) < sw ? (n - off) : sw);
@@ -2719,6 +2818,49 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
         info[b].adl_s = L.adl_s;
         info[b].adl_w = (uint64_t)bn * L.adl_s - L.adl_t;
         info[b].prestored = 0;
+    }
+}
+
+// K1.  wl == nullptr: one workgroup per block (blockIdx.x).  Otherwise (DMX_F_STORE_CHECK:
+// K0 listed the blocks that need a parse, dmx_worklist) a persistent grid of about one
+// workgroup per CU takes the listed blocks from a device counter, the next one claimed while
+// the current one runs; the index goes through LDS, so every wave leaves the loop together.
+// Stored blocks then cost nothing here (round 4: 32 768 workgroups that returned at once
+// took 0.07 ms of C4's 0.70).
+template <bool DICT, int NBX = 3>
+__global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
+                                                       int32_t max_chain, uint32_t mflags, uint16_t* __restrict__ dist_g,
+                                                       const uint16_t* __restrict__ chs, uint32_t* __restrict__ tok_g,
+                                                       uint32_t* __restrict__ hist_g,
+                                                       dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg,
+                                                       uint32_t* __restrict__ nfallback, uint32_t* __restrict__ wl) {
+#ifdef DMX_NO_WL_LOOP   // (A/B builds: the round-4 kernel shape, one workgroup per block always)
+    match_block<DICT, NBX>(blockIdx.x, in, n, sw, max_chain, mflags, dist_g, chs, tok_g, hist_g, info, dbg, nfallback);
+    return;
+#endif
+    __shared__ uint32_t nb_s;
+    uint32_t nx = 0;   // thread 0: the list index claimed for the next block
+    if (wl && threadIdx.x == 0) nx = atomicAdd(&wl[WL_C1], 1u);
+    for (uint32_t it = 0;; it++) {
+        uint32_t b;
+        if (!wl) {
+            if (it) break;
+            b = blockIdx.x;
+        } else {
+            if (threadIdx.x == 0) {
+                uint32_t v = 0xFFFFFFFFu;
+                if (nx < wl[WL_N1]) {
+                    v = wl[WL_HDR + nx];
+                    nx = atomicAdd(&wl[WL_C1], 1u);
+                }
+                nb_s = v;
+            }
+            __syncthreads();
+            b = nb_s;
+            __syncthreads();   // every thread has the index before thread 0 may write the next
+            if (b == 0xFFFFFFFFu) break;
+        }
+        match_block<DICT, NBX>(b, in, n, sw, max_chain, mflags, dist_g, chs, tok_g, hist_g, info, dbg, nfallback);
     }
 }
 
@@ -3220,12 +3362,11 @@ __device__ HuffRes huff_block(K2LDS& S, uint32_t bn, uint32_t final_bit, bool al
     return h;
 }
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void dmx_huff_kernel(const uint32_t* __restrict__ hist_g, dmx_blkinfo* __restrict__ info,
-                                                      uint32_t* __restrict__ codes_g, uint32_t* __restrict__ hdr_g,
-                                                      dmx_subinfo* __restrict__ sub_g, uint32_t nblk, uint32_t flags) {
+__device__ __forceinline__ void huff_one(const uint32_t b, const uint32_t* __restrict__ hist_g, dmx_blkinfo* __restrict__ info,
+                                         uint32_t* __restrict__ codes_g, uint32_t* __restrict__ hdr_g,
+                                         dmx_subinfo* __restrict__ sub_g, uint32_t nblk, uint32_t flags) {
     __shared__ K2LDS S;
     const uint32_t lane = threadIdx.x;
-    const uint32_t b = blockIdx.x;
     const uint32_t* hg = hist_g + (uint64_t)b * DMX_HIST;
     if (info[b].prestored & 1u) return;   // K0 wrote the stored record (1, 3)
     const uint32_t bn = info[b].n;
@@ -3254,6 +3395,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void dm
         si.hdr_bits = h.hbits;
         si.body_bits = h.body;
         sub_g[(uint64_t)b * DMX_NSUB] = si;
+    }
+}
+
+// K2: one wave per block (wl == nullptr), or a grid that strides over K0's list L2
+// (DMX_F_STORE_CHECK: the blocks parsed by K1 or in closed form by K0).
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void dmx_huff_kernel(const uint32_t* __restrict__ hist_g, dmx_blkinfo* __restrict__ info,
+                                                      uint32_t* __restrict__ codes_g, uint32_t* __restrict__ hdr_g,
+                                                      dmx_subinfo* __restrict__ sub_g, uint32_t nblk, uint32_t flags,
+                                                      const uint32_t* __restrict__ wl, const uint32_t* __restrict__ L2) {
+    if (!wl) {
+        huff_one(blockIdx.x, hist_g, info, codes_g, hdr_g, sub_g, nblk, flags);
+        return;
+    }
+    const uint32_t cnt = wl[WL_N2];
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+        wsync();   // the previous block's LDS reads are done
+        huff_one(L2[i], hist_g, info, codes_g, hdr_g, sub_g, nblk, flags);
     }
 }
 
@@ -3612,7 +3770,7 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_tile_kernel(dmx_blkinfo* _
 __global__ __launch_bounds__(ST) void dmx_scan_kernel(ScanTile* __restrict__ tiles, uint32_t nblk, uint64_t n,
                                                       uint32_t flags, uint64_t out_cap,
                                                       uint32_t* __restrict__ out32, dmx_result* __restrict__ res,
-                                                      uint32_t* __restrict__ nfallback) {
+                                                      uint32_t* __restrict__ nfallback, uint32_t* __restrict__ wl) {
     __shared__ Mono wtot[ST / 64];
     __shared__ Mono carry_s;
     __shared__ uint64_t red[ST / 64][5];
@@ -3700,6 +3858,14 @@ __global__ __launch_bounds__(ST) void dmx_scan_kernel(ScanTile* __restrict__ til
         nfallback[1] += nfallback[0];       // and the context's running total
         res->nsortfallback_total = nfallback[1];
         nfallback[0] = 0;
+        if (wl) {   // work lists: M for the apply launch; K0's / K1's counters zero for the next encode
+            wl[WL_M] = nblk - wl[WL_MX];
+            wl[WL_MX] = 0;
+            wl[WL_N1] = 0;
+            wl[WL_C1] = 0;
+            wl[WL_N2] = 0;
+            wl[WL_N4] = 0;
+        }
         s_end = end;
         s_T = T;
         s_adler = adler;
@@ -3721,7 +3887,8 @@ __global__ __launch_bounds__(ST) void dmx_scan_kernel(ScanTile* __restrict__ til
 __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply_kernel(dmx_blkinfo* __restrict__ info, uint32_t nblk,
                                                                   uint32_t flags, const ScanTile* __restrict__ tiles,
                                                                   uint32_t* __restrict__ out32,
-                                                                  const dmx_result* __restrict__ res) {
+                                                                  const dmx_result* __restrict__ res,
+                                                                  uint32_t* __restrict__ wl, uint32_t* __restrict__ L4) {
     if (res->status) return;
     const uint32_t b = blockIdx.x * SCAN_TILE + threadIdx.x;
     if (b >= nblk) return;
@@ -3736,8 +3903,30 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply_kernel(dmx_blkinfo* 
     const uint64_t l = mapply(blk_elem(bi), o) - o;
     info[b].off_bits = o;
     info[b].len_bits = l;
-    out32[o >> 5] = 0;            // shared with the block before (or the zlib header)
-    out32[(o + l - 1) >> 5] = 0;  // shared with the block after (or the framing)
+    if (!wl) {
+        out32[o >> 5] = 0;            // shared with the block before (or the zlib header)
+        out32[(o + l - 1) >> 5] = 0;  // shared with the block after (or the framing)
+        return;
+    }
+    // work lists: a block of the whole-copy prefix is complete already (K0) and K4 skips it;
+    // every other block zeroes its edge words -- only its own bytes where the neighbour is a
+    // whole-copy block (that boundary is a byte boundary: both sides are stored blocks at their
+    // speculative offsets) -- and goes on K4's list
+    const uint32_t M = wl[WL_M];
+    if (wl_skip(b, M, nblk)) return;
+    uint8_t* o8 = reinterpret_cast<uint8_t*>(out32);
+    const uint64_t e = o + l, w0 = o >> 5, w1 = (e - 1) >> 5;
+    if (b >= 1 && wl_skip(b - 1, M, nblk)) {
+        for (uint64_t q = o >> 3; q < 4 * w0 + 4 && q < ((e + 7) >> 3); q++) o8[q] = 0;
+    } else {
+        out32[w0] = 0;
+    }
+    if (wl_skip(b + 1, M, nblk)) {
+        for (uint64_t q = 4 * w1 > (o >> 3) ? 4 * w1 : (o >> 3); q < (e >> 3); q++) o8[q] = 0;
+    } else {
+        out32[w1] = 0;
+    }
+    L4[atomicAdd(&wl[WL_N4], 1u)] = b;
 }
 
 // ------------------------------------------------------------------------------------
@@ -3782,17 +3971,16 @@ __device__ __forceinline__ void pack_framing(uint32_t* out32, uint32_t flags, ui
     }
 }
 
-__global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict__ in, uint32_t sw,
-                                                      const uint32_t* __restrict__ tok_g, const uint32_t* __restrict__ codes_g,
-                                                      const uint32_t* __restrict__ hdr_g, const dmx_blkinfo* __restrict__ info,
-                                                      const dmx_subinfo* __restrict__ sub_g,
-                                                      uint32_t nblk, uint32_t flags, uint32_t* __restrict__ out32,
-                                                      dmx_result* __restrict__ res) {
+__device__ __forceinline__ void pack_one(const uint32_t b, const uint8_t* __restrict__ in, uint32_t sw,
+                                         const uint32_t* __restrict__ tok_g, const uint32_t* __restrict__ codes_g,
+                                         const uint32_t* __restrict__ hdr_g, const dmx_blkinfo* __restrict__ info,
+                                         const dmx_subinfo* __restrict__ sub_g,
+                                         uint32_t nblk, uint32_t flags, uint32_t* __restrict__ out32,
+                                         dmx_result* __restrict__ res) {
     __shared__ uint32_t stage[PK_RING];
     __shared__ uint32_t code[DMX_HIST];
     __shared__ uint32_t wsum[PT / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t b = blockIdx.x;
     const dmx_blkinfo bi = info[b];   // in flight with the status load (a stored block's WG is
     if (res->status) return;          // a chain of dependent loads: C4 launches 32 768 of them)
     const uint64_t O = bi.off_bits, Lb = bi.len_bits;
@@ -4002,6 +4190,26 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
     if (tid == 0 && (b == 0 || b == nblk - 1)) pack_framing(out32, flags, nblk, b, res);
 }
 
+// K4: one workgroup per block (wl == nullptr), or a grid that strides over the apply
+// launch's list L4 (DMX_F_STORE_CHECK: every block but the whole-copy prefix).
+__global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict__ in, uint32_t sw,
+                                                      const uint32_t* __restrict__ tok_g, const uint32_t* __restrict__ codes_g,
+                                                      const uint32_t* __restrict__ hdr_g, const dmx_blkinfo* __restrict__ info,
+                                                      const dmx_subinfo* __restrict__ sub_g,
+                                                      uint32_t nblk, uint32_t flags, uint32_t* __restrict__ out32,
+                                                      dmx_result* __restrict__ res,
+                                                      const uint32_t* __restrict__ wl, const uint32_t* __restrict__ L4) {
+    if (!wl) {
+        pack_one(blockIdx.x, in, sw, tok_g, codes_g, hdr_g, info, sub_g, nblk, flags, out32, res);
+        return;
+    }
+    const uint32_t cnt = wl[WL_N4];
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+        __syncthreads();   // the previous block's LDS reads are done
+        pack_one(L4[i], in, sw, tok_g, codes_g, hdr_g, info, sub_g, nblk, flags, out32, res);
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // host side of the HIP layer (C ABI)
 // ------------------------------------------------------------------------------------
@@ -4020,6 +4228,8 @@ struct dmx_ctx {
     dmx_subinfo* sub; // cap_blocks * DMX_NSUB
     dmx_blkinfo* info;
     ScanTile* tiles;  // cap_blocks / SCAN_TILE + 1: per-tile aggregates and prefixes (scan)
+    uint32_t* wl;     // WL_HDR + 3 cap_blocks: the work lists of DMX_F_STORE_CHECK (K0's comment)
+    uint32_t ncu;     // compute units (the persistent K1 grid of the work-list mode)
     dmx_result* res;
     uint32_t* nfb;        // [0] sort fallbacks of the encode in flight (kernels add, K3's scan reads and zeroes), [1] total
     uint64_t* dbg;        // optional per-block phase stamps (DMX_STAMPS=1)
@@ -4134,8 +4344,10 @@ static void ctx_free_ws(dmx_ctx* c) {
     if (c->sub) (void)hipFree(c->sub);
     if (c->info) (void)hipFree(c->info);
     if (c->tiles) (void)hipFree(c->tiles);
+    if (c->wl) (void)hipFree(c->wl);
     c->dist = NULL; c->tok = NULL; c->hist = NULL; c->codes = NULL; c->hdr = NULL; c->sub = NULL; c->info = NULL;
     c->tiles = NULL;
+    c->wl = NULL;
     c->cap_blocks = 0;
 }
 
@@ -4182,6 +4394,8 @@ static int ctx_reserve(dmx_ctx* c, uint64_t nblk) {
     HIPCHK(dmx_malloc(&c->sub, cb * DMX_NSUB * sizeof(dmx_subinfo)));
     HIPCHK(dmx_malloc(&c->info, cb * sizeof(dmx_blkinfo)));
     HIPCHK(dmx_malloc(&c->tiles, (cb / SCAN_TILE + 1) * sizeof(ScanTile)));
+    HIPCHK(dmx_malloc(&c->wl, (WL_HDR + 3 * cb) * sizeof(uint32_t)));
+    HIPCHK(hipMemset(c->wl, 0, WL_HDR * sizeof(uint32_t)));   // counters (the scan kernel re-zeroes them)
     c->cap_blocks = cb;
     return ctx_reserve_scratch(c);
 }
@@ -4198,6 +4412,9 @@ extern "C" int dmx_ctx_create(int device, uint64_t max_input, dmx_ctx** out) {
     dmx_ctx* c = (dmx_ctx*)calloc(1, sizeof(dmx_ctx));
     if (!c) return -(int)E_MALLOC;
     c->device = device;
+    int ncu = 0;
+    c->ncu = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0
+                 ? (uint32_t)ncu : 256u;
     if (hip_fail(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate")) { c->stream = NULL; dmx_ctx_destroy(c); return -(int)E_DEVICE; }
     if (hip_fail(dmx_malloc(&c->res, sizeof(dmx_result)), "hipMalloc(res)")) { dmx_ctx_destroy(c); return -(int)E_DEVICE; }
     if (hip_fail(dmx_malloc(&c->nfb, 16), "hipMalloc(nfb)") || hip_fail(hipMemset(c->nfb, 0, 16), "hipMemset(nfb)")) {
@@ -4302,6 +4519,9 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
     if ((o.flags & DMX_F_SPLIT) && c->cap_split < nblk) return -(int)E_SZ;
     if ((o.flags & DMX_F_DICT) && c->cap_chain < (uint64_t)nblk + 1) return -(int)E_SZ;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    // DMX_F_STORE_CHECK: K0 lists the blocks K1 / K2 / K4 have work for (WL_* above);
+    // DMX_NO_WORKLIST=1 keeps one workgroup per block (A/B measurements)
+    uint32_t* wl = ((o.flags & DMX_F_STORE_CHECK) && !getenv("DMX_NO_WORKLIST")) ? c->wl : NULL;
     hipEvent_t* ev = NULL;
     if (c->timing) {
         const int j = (int)(c->ev_next++ % DMX_EV_RING);
@@ -4327,20 +4547,27 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         if (o.flags & DMX_F_STORE_CHECK)
             hipLaunchKernelGGL(dmx_store_check_kernel, dim3(nblk), dim3(SCT), 0, s, (const uint8_t*)d_in, n,
                                (uint32_t)o.sw, c->info, c->tok, c->hist, (o.flags & DMX_F_DICT) ? 0u : 1u, o.flags,
-                               (uint32_t*)d_out, out_cap);
+                               (uint32_t*)d_out, out_cap, wl, (uint64_t)c->cap_blocks);
         if (ev) (void)hipEventRecord(ev[1], s);
         const char* dstop = getenv("DMX_DEBUG_STOP");   // diagnostic only (dbg_stop)
         const uint32_t mfl = ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u) |
                              ((o.flags & DMX_F_STORE_CHECK) ? 4u : 0u) | ((o.flags & DMX_F_DEEP) ? 8u : 0u) | (dstop ? ((uint32_t)atoi(dstop) & 3u) << 8 : 0u);
+        // work-list mode: a persistent K1 of one workgroup per CU over K0's list
+#ifdef DMX_NO_WL_LOOP
+        uint32_t* wl1 = NULL;
+#else
+        uint32_t* wl1 = wl;
+#endif
+        const dim3 g1(wl1 ? (nblk < c->ncu ? nblk : c->ncu) : nblk);
         if (o.flags & DMX_F_DICT)
-            hipLaunchKernelGGL(dmx_match_kernel<true>, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n,
-                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb);
+            hipLaunchKernelGGL(dmx_match_kernel<true>, g1, dim3(MT), 0, s, (const uint8_t*)d_in, n,
+                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb, wl1);
         else if (o.max_chain == 0)
-            hipLaunchKernelGGL((dmx_match_kernel<false, DMX_NBX>), dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n,
-                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb);
+            hipLaunchKernelGGL((dmx_match_kernel<false, DMX_NBX>), g1, dim3(MT), 0, s, (const uint8_t*)d_in, n,
+                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb, wl1);
         else
-            hipLaunchKernelGGL(dmx_match_kernel<false>, dim3(nblk), dim3(MT), 0, s, (const uint8_t*)d_in, n,
-                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb);
+            hipLaunchKernelGGL(dmx_match_kernel<false>, g1, dim3(MT), 0, s, (const uint8_t*)d_in, n,
+                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb, wl1);
         if (ev) (void)hipEventRecord(ev[2], s);
         if (o.flags & DMX_F_SPLIT)
             {
@@ -4352,8 +4579,9 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                                    c->info, c->codes, c->hdr, c->sub, nblk, o.flags);
             }
         else
-            hipLaunchKernelGGL(dmx_huff_kernel, dim3(nblk), dim3(64), 0, s, c->hist, c->info, c->codes, c->hdr, c->sub,
-                               nblk, o.flags);
+            hipLaunchKernelGGL(dmx_huff_kernel, dim3(wl ? (nblk < 32 * c->ncu ? nblk : 32 * c->ncu) : nblk), dim3(64), 0,
+                               s, c->hist, c->info, c->codes, c->hdr, c->sub, nblk, o.flags, wl,
+                               wl ? wl + WL_HDR + c->cap_blocks : NULL);
         if (ev) (void)hipEventRecord(ev[3], s);
     } else if (ev) {
         (void)hipEventRecord(ev[1], s);
@@ -4364,15 +4592,17 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
     if (nblk)
         hipLaunchKernelGGL(dmx_scan_tile_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, n, (uint32_t)o.sw,
                            c->tiles);
+    uint32_t* L4 = wl ? wl + WL_HDR + 2 * c->cap_blocks : NULL;
     hipLaunchKernelGGL(dmx_scan_kernel, dim3(1), dim3(ST), 0, s, c->tiles, nblk, n, o.flags, out_cap,
-                       (uint32_t*)d_out, c->res, c->nfb);
+                       (uint32_t*)d_out, c->res, c->nfb, c->wl);
     if (nblk)
         hipLaunchKernelGGL(dmx_scan_apply_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, o.flags, c->tiles,
-                           (uint32_t*)d_out, (const dmx_result*)c->res);
+                           (uint32_t*)d_out, (const dmx_result*)c->res, wl, L4);
     if (ev) (void)hipEventRecord(ev[4], s);
     if (nblk)
-        hipLaunchKernelGGL(dmx_pack_kernel, dim3(nblk), dim3(PT), 0, s, (const uint8_t*)d_in, (uint32_t)o.sw, c->tok,
-                           c->codes, c->hdr, c->info, c->sub, nblk, o.flags, (uint32_t*)d_out, c->res);
+        hipLaunchKernelGGL(dmx_pack_kernel, dim3(wl ? (nblk < 4 * c->ncu ? nblk : 4 * c->ncu) : nblk), dim3(PT), 0, s,
+                           (const uint8_t*)d_in, (uint32_t)o.sw, c->tok, c->codes, c->hdr, c->info, c->sub, nblk, o.flags,
+                           (uint32_t*)d_out, c->res, wl, L4);
     if (ev) (void)hipEventRecord(ev[5], s);
     HIPCHK(fault_hit(2) ? hipErrorLaunchFailure : hipGetLastError());
     c->last_nblk = nblk;
@@ -4583,6 +4813,7 @@ extern "C" int dmx_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint
 #include <unistd.h>
 #include <errno.h>
 #include <sys/stat.h>
+#include <time.h>
 static int64_t read_full(int fd, uint8_t* b, uint64_t cap) {
     uint64_t len = 0;
     while (len < cap) {
@@ -4762,6 +4993,7 @@ struct FdPipe {
     hipEvent_t eve[2];          // encode j (and its result copy) done
     hipEvent_t evd[2];          // D2H from device output k done
     hipEvent_t evo[FDP_NOUT];   // D2H into output slot k done
+    hipEvent_t th[FDP_NIN], te[2], td[FDP_NOUT];   // stage timing: H2D / encode / D2H begins
 };
 
 static void fdp_free(FdPipe* P) {
@@ -4769,10 +5001,12 @@ static void fdp_free(FdPipe* P) {
     for (int k = 0; k < FDP_NIN; k++) {
         if (P->hin[k]) (void)hipHostFree(P->hin[k]);
         if (P->evh[k]) (void)hipEventDestroy(P->evh[k]);
+        if (P->th[k]) (void)hipEventDestroy(P->th[k]);
     }
     for (int k = 0; k < FDP_NOUT; k++) {
         if (P->hout[k]) (void)hipHostFree(P->hout[k]);
         if (P->evo[k]) (void)hipEventDestroy(P->evo[k]);
+        if (P->td[k]) (void)hipEventDestroy(P->td[k]);
     }
     for (int k = 0; k < FDP_NDIN; k++)
         if (P->din[k]) (void)hipFree(P->din[k]);
@@ -4781,6 +5015,7 @@ static void fdp_free(FdPipe* P) {
         if (P->hres[k]) (void)hipHostFree(P->hres[k]);
         if (P->eve[k]) (void)hipEventDestroy(P->eve[k]);
         if (P->evd[k]) (void)hipEventDestroy(P->evd[k]);
+        if (P->te[k]) (void)hipEventDestroy(P->te[k]);
     }
     if (P->sh) (void)hipStreamDestroy(P->sh);
     if (P->sd) (void)hipStreamDestroy(P->sd);
@@ -4796,18 +5031,20 @@ static int fdp_try(uint64_t chunk, uint64_t ocap, int nslot, FdPipe** out) {
     int r = 0;
     for (int k = 0; !r && k < P->nin; k++) {
         if (hip_fail(dmx_host_malloc((void**)&P->hin[k], chunk + 16), "hipHostMalloc")) r = -(int)E_MALLOC;
-        else if (hip_fail(hipEventCreateWithFlags(&P->evh[k], hipEventDisableTiming), "hipEventCreate")) r = -(int)E_DEVICE;
+        else if (hip_fail(hipEventCreate(&P->evh[k]), "hipEventCreate") || hip_fail(hipEventCreate(&P->th[k]), "hipEventCreate"))
+            r = -(int)E_DEVICE;
     }
     for (int k = 0; !r && k < P->nout; k++) {
         if (hip_fail(dmx_host_malloc((void**)&P->hout[k], ocap), "hipHostMalloc")) r = -(int)E_MALLOC;
-        else if (hip_fail(hipEventCreateWithFlags(&P->evo[k], hipEventDisableTiming), "hipEventCreate")) r = -(int)E_DEVICE;
+        else if (hip_fail(hipEventCreate(&P->evo[k]), "hipEventCreate") || hip_fail(hipEventCreate(&P->td[k]), "hipEventCreate"))
+            r = -(int)E_DEVICE;
     }
     for (int k = 0; !r && k < FDP_NDIN; k++)
         if (hip_fail(dmx_malloc(&P->din[k], chunk + 16), "hipMalloc")) r = -(int)E_DEVICE;
     for (int k = 0; !r && k < 2; k++) {
         if (hip_fail(dmx_malloc(&P->dout[k], ocap), "hipMalloc")) r = -(int)E_DEVICE;
         else if (hip_fail(dmx_host_malloc((void**)&P->hres[k], sizeof(dmx_result)), "hipHostMalloc")) r = -(int)E_MALLOC;
-        else if (hip_fail(hipEventCreateWithFlags(&P->eve[k], hipEventDisableTiming), "hipEventCreate") ||
+        else if (hip_fail(hipEventCreate(&P->eve[k]), "hipEventCreate") || hip_fail(hipEventCreate(&P->te[k]), "hipEventCreate") ||
                  hip_fail(hipEventCreateWithFlags(&P->evd[k], hipEventDisableTiming), "hipEventCreate"))
             r = -(int)E_DEVICE;
     }
@@ -4849,7 +5086,24 @@ struct FdSync {
     bool eof[FDP_NIN];       // nothing after the chunk in slot k
     uint64_t olen[FDP_NOUT]; // stream bytes in output slot k
     bool done_reading;
+    double read_ms, write_ms, d2h_ms;   // reader / writer thread busy time, D2H event time
 };
+static double fd_now_ms() {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+static dmx_fd_stats g_fd_last;
+static bool g_fd_last_ok = false;
+static pthread_mutex_t g_fd_last_mu = PTHREAD_MUTEX_INITIALIZER;
+extern "C" int dmx_fd_last_stats(dmx_fd_stats* out) {
+    if (!out) return -(int)E_INVAL;
+    pthread_mutex_lock(&g_fd_last_mu);
+    const bool ok = g_fd_last_ok;
+    if (ok) *out = g_fd_last;
+    pthread_mutex_unlock(&g_fd_last_mu);
+    return ok ? 0 : -(int)E_INVAL;
+}
 struct FdReadJob { FdSync* S; FdReader* R; FdPipe* P; uint64_t chunk; };
 struct FdWriteJob { FdSync* S; FdPipe* P; int fd; };
 
@@ -4876,9 +5130,12 @@ static void* fdp_reader(void* a) {
             fds_fail(S, -(int)E_DEVICE);
             break;
         }
+        const double t0 = fd_now_ms();
         const int64_t len = fd_read_chunk(J->R, J->P->hin[k], J->chunk);
+        const double t1 = fd_now_ms();
         if (len < 0) { fds_fail(S, (int)len); break; }
         pthread_mutex_lock(&S->mu);
+        S->read_ms += t1 - t0;
         S->len[k] = len;
         S->eof[k] = J->R->eof;
         S->nread = j + 1;
@@ -4901,9 +5158,15 @@ static void* fdp_writer(void* a) {
         pthread_mutex_unlock(&S->mu);
         if (stop) break;
         if (hip_fail(hipEventSynchronize(J->P->evo[k]), "hipEventSynchronize")) { fds_fail(S, -(int)E_DEVICE); break; }
+        float dms = 0.f;
+        if (olen && hipEventElapsedTime(&dms, J->P->td[k], J->P->evo[k]) != hipSuccess) dms = 0.f;
+        const double t0 = fd_now_ms();
         const int r = J->fd >= 0 ? write_full(J->fd, J->P->hout[k], olen) : 0;
+        const double t1 = fd_now_ms();
         if (r) { fds_fail(S, r); break; }
         pthread_mutex_lock(&S->mu);
+        S->write_ms += t1 - t0;
+        S->d2h_ms += dms;
         S->nwritten = j + 1;
         pthread_cond_broadcast(&S->cv);
         pthread_mutex_unlock(&S->mu);
@@ -4976,12 +5239,20 @@ static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts,
     uint32_t adler = 1;
     uint64_t off = 0;   // offset of the chunk being finished in the bytes read (callback)
     uint64_t clen[2] = {0, 0};
+    int cin[2] = {0, 0};   // the input slot of the chunk in device output k2 (its H2D events)
+    double enc_ms = 0, h2d_ms = 0;
+    uint64_t nchunks = 0, nin_total = 0, nout_total = 0;
+    const double t_begin = fd_now_ms();
     // chunk j - 1's result: its length, Adler-32, the callback; then its D2H and the writer
     auto finish = [&](uint64_t j) -> int {
         const int k2 = (int)(j & 1), ko = (int)(j % (uint64_t)P->nout);
         if (hip_fail(hipEventSynchronize(P->eve[k2]), "hipEventSynchronize")) return -(int)E_DEVICE;
         if (P->hres[k2]->status) return P->hres[k2]->status;
         const uint64_t olen = P->hres[k2]->out_len;
+        float ems = 0.f, hms = 0.f;   // this chunk's encode and H2D (done before its encode began)
+        if (hipEventElapsedTime(&ems, P->te[k2], P->eve[k2]) == hipSuccess) enc_ms += ems;
+        if (clen[k2] && hipEventElapsedTime(&hms, P->th[cin[k2]], P->evh[cin[k2]]) == hipSuccess) h2d_ms += hms;
+        nout_total += olen;
         adler = dmx_adler32_combine(adler, P->hres[k2]->adler, clen[k2]);
         if (cb) {
             const int e = cb(user, c, clen[k2], off);
@@ -4993,6 +5264,7 @@ static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts,
         const int e = S.err;
         pthread_mutex_unlock(&S.mu);
         if (e) return e;
+        if (hip_fail(hipEventRecord(P->td[ko], P->sd), "hipEventRecord")) return -(int)E_DEVICE;
         if (olen && hip_fail(hipMemcpyAsync(P->hout[ko], P->dout[k2], olen, hipMemcpyDeviceToHost, P->sd), "D2H"))
             return -(int)E_DEVICE;
         if (hip_fail(hipEventRecord(P->evd[k2], P->sd), "hipEventRecord") ||
@@ -5019,6 +5291,7 @@ static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts,
         // (history); the latter is ordered after the former on the encode stream
         if (i >= FDP_NDIN - 1 && hip_fail(hipStreamWaitEvent(P->sh, P->eve[(i - (FDP_NDIN - 1)) & 1], 0), "wait"))
             r = -(int)E_DEVICE;
+        if (!r && hip_fail(hipEventRecord(P->th[ki], P->sh), "hipEventRecord")) r = -(int)E_DEVICE;
         if (!r && len && hip_fail(hipMemcpyAsync(P->din[kd], P->hin[ki], (size_t)len, hipMemcpyHostToDevice, P->sh), "H2D"))
             r = -(int)E_DEVICE;
         if (!r && hip_fail(hipEventRecord(P->evh[ki], P->sh), "hipEventRecord")) r = -(int)E_DEVICE;
@@ -5037,10 +5310,14 @@ static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts,
             oc.dict = (const uint8_t*)P->din[(i - 1) % FDP_NDIN] + (chunk - sw);
             oc.dict_len = sw;
         }
+        if (!r && hip_fail(hipEventRecord(P->te[k2], s), "hipEventRecord")) r = -(int)E_DEVICE;
         if (!r) r = dmx_encode_async(c, P->din[kd], (uint64_t)len, P->dout[k2], ocap, &oc, s);
         if (!r) r = dmx_encode_result_async(c, P->hres[k2], s);
         if (!r && hip_fail(hipEventRecord(P->eve[k2], s), "hipEventRecord")) r = -(int)E_DEVICE;
         clen[k2] = (uint64_t)len;
+        cin[k2] = ki;
+        nchunks++;
+        nin_total += (uint64_t)len;
         // the previous chunk finishes while this one encodes (a callback needs the context's
         // tokens of its own chunk: then each chunk finishes before the next encodes)
         if (!r && cb) r = finish(i);
@@ -5068,6 +5345,20 @@ static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts,
     (void)hipStreamSynchronize(P->sh);
     (void)hipStreamSynchronize(s);
     (void)hipStreamSynchronize(P->sd);
+    if (!r) {
+        pthread_mutex_lock(&g_fd_last_mu);
+        g_fd_last.chunks = nchunks;
+        g_fd_last.bytes_in = nin_total;
+        g_fd_last.bytes_out = nout_total + 4;
+        g_fd_last.wall_ms = fd_now_ms() - t_begin;
+        g_fd_last.read_ms = S.read_ms;
+        g_fd_last.h2d_ms = h2d_ms;
+        g_fd_last.encode_ms = enc_ms;
+        g_fd_last.d2h_ms = S.d2h_ms;
+        g_fd_last.write_ms = S.write_ms;
+        g_fd_last_ok = true;
+        pthread_mutex_unlock(&g_fd_last_mu);
+    }
     pthread_cond_destroy(&S.cv);
     pthread_mutex_destroy(&S.mu);
     pthread_mutex_unlock(&g_mu);

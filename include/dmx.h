@@ -73,7 +73,9 @@ int deflate_decompress(struct string_len* decompr_dat, struct string_len* compr_
  *                  are checked against this host restatement fed the oracle's tokens, not
  *                  against the reference's own output.
  *   "exact"        exact costs of this stream, running over the whole stream: tree_bits =
- *                  header bits of every DEFLATE block begun so far (its own included),
+ *                  header bits of every DEFLATE block begun so far (its own included;
+ *                  the empty stored blocks that end each DMX_CHUNK_MB chunk but the last
+ *                  are framing, not coding, and are not counted),
  *                  ll_bits = lit/len code + length extra bits of every token so far (8 per
  *                  byte in stored blocks), d_bits = distance code + extra bits so far.
  * The fields are int, as in the reference: deflate_compress returns -E_RANGE, after the
@@ -230,6 +232,18 @@ int dmx_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t out_ca
  * history across chunks).  opts->flags: the parse/block options (DMX_F_LAZY, _SPLIT, _DICT);
  * the framing is its own.  Returns 0 or -E_*. */
 int dmx_encode_fd(int fd_in, int fd_out, const dmx_opts* opts, uint64_t chunk);
+
+/* Where the last single-device dmx_encode_fd call (or deflate_compress without fd_stats)
+ * spent its time, per stage of its pipeline: wall time of the call; the
+ * reader thread's time in read()/pread(); the H2D copies, encodes and D2H copies on the
+ * device (HIP event times, summed over chunks); the writer thread's time in write().  The
+ * stages overlap, so the largest of them bounds the call.  Returns 0, or -E_INVAL when no
+ * such call has finished in this process. */
+typedef struct {
+    uint64_t chunks, bytes_in, bytes_out;
+    double wall_ms, read_ms, h2d_ms, encode_ms, d2h_ms, write_ms;
+} dmx_fd_stats;
+int dmx_fd_last_stats(dmx_fd_stats* out);
 
 /* The same stream as dmx_encode_fd with the chunks spread over several GPUs: chunk i is
  * read (pread), encoded and copied back by the host thread of devices[i % ndev], and the

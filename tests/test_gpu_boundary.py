@@ -154,6 +154,35 @@ def test_stats_ref_mode_multi_block_equals_host_restatement(tmp_path):
     assert O.replay(np.where(st[:, 5] == 0, st[:, 4], (st[:, 5] << 9) | st[:, 4]).astype(np.uint32)) == data
 
 
+@pytest.mark.parametrize("mode", ["exact", "ref"])
+def test_stats_across_chunks(tmp_path, mode):
+    """fd_stats over several DMX_CHUNK_MB chunks (1 MiB chunks, a 3.2 MB input:
+    four chunks, three sync flushes).  The records equal the one-stream records: exact mode
+    the oracle's running sums (the chunk flushes are framing and not counted, dmx.h), ref
+    mode the host restatement fed every token in stream order (its trees carry across the
+    chunks), and bytes counts from the start of the input, not of the chunk."""
+    data = D.gen_text(3_200_000, 41).tobytes()
+    old = os.environ.get("DMX_CHUNK_MB")
+    os.environ["DMX_CHUNK_MB"] = "1"
+    try:
+        z, st = _stats(tmp_path, data, mode=mode)
+    finally:
+        if old is None:
+            os.environ.pop("DMX_CHUNK_MB", None)
+        else:
+            os.environ["DMX_CHUNK_MB"] = old
+    assert zlib.decompress(z) == data
+    toks = np.concatenate([O.parse_block(data[o:o + 32768]) for o in range(0, len(data), 32768)])
+    assert st.shape[0] == toks.size
+    assert O.replay(np.where(st[:, 5] == 0, st[:, 4], (st[:, 5] << 9) | st[:, 4]).astype(np.uint32)) == data
+    if mode == "exact":
+        assert np.array_equal(st, oracle_records(data))
+    else:
+        assert np.array_equal(st[:, 1:4], D.ref_estimates(toks))
+    starts = np.concatenate([[0], np.cumsum(np.where(st[:-1, 5] == 0, 1, st[:-1, 4]))])
+    assert np.array_equal(st[:, 0], starts + 1)
+
+
 def test_stats_overflow_returns_range(tmp_path):
     """compress_stats fields are int (deflate_ext.h:19-31).  300 MB of splitmix64 bytes go out
     stored (8 bits per byte of ll_bits in the exact mode), so the running ll_bits passes

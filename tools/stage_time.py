@@ -1,6 +1,6 @@
 """Diagnostic: HIP-event stage times (ms) of one encode configuration on cuda:0, averaged
 over a few encodes (no verification -- for experiments on a kernel variant).
-usage: stage_time.py [MB] [K] [flags: any of l(azy) s(plit) d(ict) c(store check) e (deep)]"""
+usage: stage_time.py [MB] [K] [flags: any of l(azy) s(plit) d(ict) c(store check) e (deep)] [text|random|zeros]"""
 import os
 import sys
 
@@ -19,19 +19,26 @@ flags = D.DMX_ZLIB | (D.DMX_F_LAZY if "l" in fs else 0) | (D.DMX_F_SPLIT if "s" 
     (D.DMX_F_DICT if "d" in fs else 0) | (D.DMX_F_STORE_CHECK if "c" in fs else 0) | \
     (D.DMX_F_DEEP if "e" in fs else 0)
 n = int(mb * 1e6)
-t = torch.from_numpy(D.gen_text(n, 0xE5818)).cuda()
+kind = sys.argv[4] if len(sys.argv) > 4 else "text"
+host = {"text": lambda: D.gen_text(n, 0xE5818), "random": lambda: D.gen_random(n, 0x5EED),
+        "zeros": lambda: __import__("numpy").zeros(n, __import__("numpy").uint8)}[kind]()
+t = torch.from_numpy(host).cuda()
 e = D.Encoder(0, n, max_chain=k, flags=flags)
 for _ in range(2):
     e.compress_tensor(t)
 torch.cuda.synchronize()
 e.set_timing(True)   # mean ms per launch of each stage over the timed encodes
+import time
+torch.cuda.synchronize()
+t0 = time.perf_counter()
 for _ in range(5):
     e.compress_tensor(t)
 torch.cuda.synchronize()
+wall = (time.perf_counter() - t0) / 5
 st, cnt = e.stage_times()
 import hashlib
 o, r = e.compress_tensor(t)
 h = hashlib.sha1(o.cpu().numpy().tobytes()).hexdigest()[:16]
-print({"config": f"{mb} MB K={k} {fs}", "encodes": cnt, "stage_ms": {a: round(b, 4) for a, b in st.items()},
+print({"config": f"{mb} MB K={k} {fs} {kind}", "encodes": cnt, "GBps_wall": round(n / wall / 1e9, 2), "stage_ms": {a: round(b, 4) for a, b in st.items()},
        "out_len": int(r.out_len), "sha1": h})
 e.close()
