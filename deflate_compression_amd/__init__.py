@@ -63,7 +63,7 @@ class DeflateError(RuntimeError):
 
 class Opts(ctypes.Structure):
     _fields_ = [("sw", ctypes.c_int32), ("max_chain", ctypes.c_int32), ("flags", ctypes.c_uint32),
-                ("reserved", ctypes.c_int32), ("dict", ctypes.c_void_p), ("dict_len", ctypes.c_uint64)]
+                ("deep_chain", ctypes.c_int32), ("dict", ctypes.c_void_p), ("dict_len", ctypes.c_uint64)]
 
 
 class Result(ctypes.Structure):

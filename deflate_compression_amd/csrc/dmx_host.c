@@ -194,7 +194,8 @@ int deflate_compress(int fd_in, int fd_out, int fd_stats, swi sw, int ops) {
     if (sc && atoi(sc) > 0 && fd_stats < 0) o.flags |= DMX_F_STORE_CHECK;
     const char* dp = getenv("DMX_DEEP");   /* 1 = adaptive chain depth (DMX_F_DEEP, bounded mode) */
     if (dp && atoi(dp) > 0) o.flags |= DMX_F_DEEP;
-    o.reserved = 0;
+    const char* dd = getenv("DMX_DEEP_CHAIN");   /* DMX_F_DEEP depth (0 / unset = 64) */
+    o.deep_chain = dd ? atoi(dd) : 0;
     o.dict = NULL;
     o.dict_len = 0;
     /* streaming: chunks of DMX_CHUNK_MB MiB (default 16) through pinned buffers; each chunk a

@@ -1218,7 +1218,9 @@ __device__ __forceinline__ uint32_t atomic_rank16(uint32_t* T, uint32_t v, bool 
             return ((__builtin_amdgcn_readlane(base, (int)first) >> sh) & 0xFFFFu) + (uint32_t)__popcll(vm & lt);
         }
     }
-    return valid ? (atomicAdd(&T[v], 1u << sh) >> sh) & 0xFFFFu : 0u;
+    // every lane adds (0 when invalid; v = 0 then): no exec-masked branch per step, so the
+    // 32 steps of a round issue their atomics back to back instead of one round trip each
+    return (atomicAdd(&T[v], valid ? 1u << sh : 0u) >> sh) & 0xFFFFu;
 }
 
 // Bucket-sorted positions S (stable by position inside a bucket) by ONE counting pass over
@@ -1269,12 +1271,33 @@ __device__ __forceinline__ void count_sort_positions(MatchLDS& L, uint32_t bn, i
     for (uint32_t r = 0; r < 8; r++) {
         if (r == (wave & 7)) {
             asm volatile("" : "+v"(x0l), "+v"(nvl));
+            if (RUNCHK) {
 #pragma unroll
-            for (int st = 0; st < 32; st++) {
-                const uint32_t x = x0l + ((uint32_t)st << 6);
-                const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
-                const uint32_t rr = atomic_rank16<RUNCHK>(T, h, x < nvl, lt, sh);
-                rk[st >> 1] |= rr << (16 * (st & 1));
+                for (int st = 0; st < 32; st++) {
+                    const uint32_t x = x0l + ((uint32_t)st << 6);
+                    const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
+                    const uint32_t rr = atomic_rank16<true>(T, h, x < nvl, lt, sh);
+                    rk[st >> 1] |= rr << (16 * (st & 1));
+                }
+            } else {
+                // 16 atomics in flight, then their ranks: the compiler keeps an atomic's use
+                // next to it (one LDS round trip per step) unless the uses come after the batch
+#pragma unroll
+                for (int hb = 0; hb < 32; hb += 16) {
+                    uint32_t old[16];
+#pragma unroll
+                    for (int q = 0; q < 16; q++) {
+                        const int st = hb + q;
+                        const uint32_t x = x0l + ((uint32_t)st << 6);
+                        const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
+                        old[q] = atomicAdd(&T[h], x < nvl ? 1u << sh : 0u);
+                    }
+#pragma unroll
+                    for (int q = 0; q < 16; q++) {
+                        const int st = hb + q;
+                        rk[st >> 1] |= ((old[q] >> sh) & 0xFFFFu) << (16 * (st & 1));
+                    }
+                }
             }
         }
         __syncthreads();
@@ -1927,30 +1950,25 @@ __device__ __forceinline__ uint32_t uniform_parse(uint32_t bn, uint32_t c, uint3
     return ntok;
 }
 
-// Work lists (DMX_F_STORE_CHECK, round 5): K0 lists the blocks each later kernel has work
-// for, so that a stored block costs no workgroup in K1, K2 or K4 (C4: 32 768 stored blocks).
-// Layout of dmx_ctx::wl (u32): counters, then three lists of cap_blocks entries each:
-//   L1 = wl + WL_HDR             blocks K1 parses (prestored 0), appended by K0
-//   L2 = L1 + cap                blocks K2 codes (prestored 0 and 2), appended by K0
+// Work lists (DMX_F_STORE_CHECK, round 5), so that a stored block costs no workgroup in K1,
+// K2 or K4 (C4: 32 768 stored blocks).  dmx_worklist_kernel (one workgroup, after K0) builds
+// them from K0's prestored values; dmx_ctx::wl (u32) holds counters, then three lists of
+// cap_blocks entries each:
+//   L1 = wl + WL_HDR             blocks K1 parses (prestored 0)
+//   L2 = L1 + cap                blocks K2 codes (prestored 0 and 2)
 //   L4 = L2 + cap                blocks K4 packs, appended by the scan's apply launch
-// WL_MX = max over the blocks that K0 did NOT store and copy whole (prestored != 3) of
-// nblk - b, so M = the first such block = nblk - WL_MX.  Blocks 1 <= b < min(M, nblk - 1)
-// form a prefix of stored blocks at their speculative offsets (every block before them is
-// stored too): K0 writes every byte of them and K4 never sees them.  The scan kernel copies
-// M to WL_M and zeroes the counters for the next encode (before the apply launch appends L4).
+// WL_M = the first block that K0 did not store and copy whole (prestored != 3).  Blocks
+// 1 <= b < min(M, nblk - 1) form a prefix of stored blocks at their speculative offsets
+// (every block before them is stored too): K0 wrote every byte of them and K4 never sees
+// them.  (A first version appended to the lists from K0 with device atomics: 3 052 text
+// blocks took 0.11 ms, 32 768 blocks of zeros 0.79 ms -- same-address atomics from every
+// XCD serialise.)
 #define WL_N1 0
 #define WL_C1 1
 #define WL_N2 2
 #define WL_N4 3
-#define WL_MX 4
 #define WL_M 5
 #define WL_HDR 16
-__device__ __forceinline__ void wl_note(uint32_t* __restrict__ wl, uint64_t cap, uint32_t b, uint32_t nblk, uint32_t ps) {
-    if (!wl) return;
-    if (ps != 3) atomicMax(&wl[WL_MX], nblk - b);
-    if (ps == 0) wl[WL_HDR + atomicAdd(&wl[WL_N1], 1u)] = b;
-    if (ps == 0 || ps == 2) wl[WL_HDR + cap + atomicAdd(&wl[WL_N2], 1u)] = b;
-}
 // K4 never sees block x: a stored block of the whole-copy prefix (above)
 __device__ __forceinline__ bool wl_skip(uint32_t x, uint32_t M, uint32_t nblk) {
     return x >= 1 && x < M && x + 1 < nblk;
@@ -1993,19 +2011,19 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
                                                               dmx_blkinfo* __restrict__ info, uint32_t* __restrict__ tok_g,
                                                               uint32_t* __restrict__ hist_g, uint32_t uni_ok, uint32_t flags,
                                                               uint32_t* __restrict__ out32, uint64_t out_cap,
-                                                              uint32_t* __restrict__ wl, uint64_t wl_cap) {
+                                                              uint32_t whole) {
     __shared__ uint32_t bm[1u << 12];   // the 17-bit presence bitmap (16 KB: 8 workgroups per CU)
     __shared__ uint32_t hist[256];
     __shared__ uint64_t red[10][SCT / 64];
     __shared__ uint32_t pass_s;
-    const uint32_t tid = tidx(), lane = tid & 63, wave = tid >> 6;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t b = blockIdx.x;
     const uint64_t off = (uint64_t)b * sw;
     const uint32_t bn = (uint32_t)((n - off) < sw ? (n - off) : sw);
     const uint8_t* d = in + off;
     const uint32_t nblk = gridDim.x;
     if (bn < 4096) {
-        if (tid == 0) { info[b].prestored = 0; wl_note(wl, wl_cap, b, nblk, 0); }
+        if (tid == 0) info[b].prestored = 0;
         return;
     }
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
@@ -2042,10 +2060,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
         }
         __syncthreads();
         if (!pass_s) {
-            if (!uni_ok || !uni4k) {
-                if (tid == 0) wl_note(wl, wl_cap, b, nblk, 0);
-                return;
-            }
+            if (!uni_ok || !uni4k) return;
             // the first 4 KiB are one repeated byte: is the whole block?  Then its parse has
             // a closed form (as in K1's uniform path; no dictionary): a literal, distance-1
             // matches of min(258, bytes left) while >= 3 bytes are left, then literals.
@@ -2060,10 +2075,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
                     u = u && ((x[q] ^ c4) & m) == 0;
                 }
             }
-            if (!__syncthreads_and(u)) {
-                if (tid == 0) wl_note(wl, wl_cap, b, nblk, 0);
-                return;
-            }
+            if (!__syncthreads_and(u)) return;
             uint32_t* H = bm;   // the 320-entry histogram (bm is free here)
             for (uint32_t k = tid; k < DMX_HIST; k += SCT) H[k] = 0;
             __syncthreads();
@@ -2076,7 +2088,6 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
                 info[b].adl_s = S;
                 info[b].adl_w = (uint64_t)bn * S - T;
                 info[b].prestored = 2;
-                wl_note(wl, wl_cap, b, nblk, 2);
             }
             __syncthreads();
             for (uint32_t k = tid; k < DMX_HIST; k += SCT) hist_g[(uint64_t)b * DMX_HIST + k] = H[k];
@@ -2181,7 +2192,6 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
         // the speculative copy (above) when the whole block fits the output at that offset
         const bool spec = sto && (spec_stored_bit(b, sw, flags) >> 3) + (uint64_t)bn + 16 <= out_cap;
         info[b].prestored = sto ? (spec ? 3u : 1u) : 0u;
-        wl_note(wl, wl_cap, b, nblk, sto ? (spec ? 3u : 1u) : 0u);
         pass_s = spec ? 1u : 0u;
         if (sto) {
             info[b].ntok = 0;
@@ -2249,7 +2259,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
             *reinterpret_cast<uint4*>(&out32[(O >> 5) + k]) = v;
         });
     }
-    if (pass_s && wl && b >= 1 && b + 1 < nblk) {
+    if (pass_s && whole && b >= 1 && b + 1 < nblk) {
         // the whole copy (work-list mode): every other byte of the block at its speculative
         // offset too -- the header byte (BFINAL 0, BTYPE 00), LEN / NLEN, the words before and
         // after the quads, any of the first two and last two quads that did not take the
@@ -2300,6 +2310,61 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
     }
 }
 
+// The work lists from K0's prestored values (one workgroup; thread t takes blocks t, t + WLT,
+// ...: every load of a round in flight).  Deterministic order: list position = the thread's
+// offset from a block scan + its count so far.  Also zeroes K1's claim counter and K4's list.
+#define WLT 1024
+__global__ __launch_bounds__(WLT) void dmx_worklist_kernel(const dmx_blkinfo* __restrict__ info, uint32_t nblk,
+                                                           uint32_t* __restrict__ wl, uint64_t cap) {
+    __shared__ uint32_t w1[WLT / 64], w2[WLT / 64], wm[WLT / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t c1 = 0, c2 = 0, m = nblk;
+    for (uint32_t b0 = 0; b0 < nblk; b0 += 16 * WLT) {   // 16 loads in flight per thread
+        uint32_t ps[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const uint32_t b = b0 + (uint32_t)j * WLT + tid;
+            ps[j] = b < nblk ? info[b].prestored : 3u;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const uint32_t b = b0 + (uint32_t)j * WLT + tid;
+            c1 += ps[j] == 0 ? 1u : 0u;
+            c2 += (ps[j] == 0 || ps[j] == 2) ? 1u : 0u;
+            if (ps[j] != 3 && b < m) m = b;
+        }
+    }
+    // exclusive block scans of c1 and c2, min of m
+    const uint32_t i1 = wave_incl_scan(c1), i2 = wave_incl_scan(c2);
+    uint32_t mm = m;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mm = min(mm, (uint32_t)__shfl_xor((int)mm, o));
+    if (lane == 63) { w1[wave] = i1; w2[wave] = i2; }
+    if (lane == 0) wm[wave] = mm;
+    __syncthreads();
+    uint32_t o1 = i1 - c1, o2 = i2 - c2, t1 = 0, t2 = 0, M = nblk;
+    for (uint32_t w = 0; w < WLT / 64; w++) {
+        if (w < wave) { o1 += w1[w]; o2 += w2[w]; }
+        t1 += w1[w];
+        t2 += w2[w];
+        M = min(M, wm[w]);
+    }
+    uint32_t* L1 = wl + WL_HDR;
+    uint32_t* L2 = L1 + cap;
+    for (uint32_t b = tid; b < nblk; b += WLT) {   // (the second read of the records: L2 hits)
+        const uint32_t ps = info[b].prestored;
+        if (ps == 0) L1[o1++] = b;
+        if (ps == 0 || ps == 2) L2[o2++] = b;
+    }
+    if (tid == 0) {
+        wl[WL_N1] = t1;
+        wl[WL_C1] = 0;
+        wl[WL_N2] = t2;
+        wl[WL_N4] = 0;
+        wl[WL_M] = M;
+    }
+}
+
 // Diagnostic (DMX_DEBUG_STOP=1|2|3, never in a product run): end the block after P0 (sort),
 // P1 (search) or P2 (walk), recording it as an empty block, so that SQ counters of the
 // truncated kernel give the instruction count of each phase by difference.  The stream
@@ -2325,7 +2390,8 @@ __device__ __forceinline__ bool dbg_stop(uint32_t mflags, uint32_t phase, dmx_bl
 // and is zeroed again, L.ntok (zero until the walk) the count.  Two barriers.
 __device__ __forceinline__ int32_t block_chain(MatchLDS& L, uint32_t bn, int32_t max_chain, uint32_t mflags,
                                                uint32_t tid) {
-    if (!(mflags & 8u) || max_chain <= 0 || max_chain >= DMX_DEEP_CHAIN) return max_chain;
+    const int32_t dk = (mflags >> 16) & 0xFFu ? (int32_t)((mflags >> 16) & 0xFFu) : (int32_t)DMX_DEEP_CHAIN;
+    if (!(mflags & 8u) || max_chain <= 0 || max_chain >= dk) return max_chain;
     const uint32_t nvalid = bn > 2 ? bn - 2 : 0;
     uint32_t* SB = L.hist;
 #pragma unroll
@@ -2348,7 +2414,7 @@ __device__ __forceinline__ int32_t block_chain(MatchLDS& L, uint32_t bn, int32_t
         const uint32_t lo = s << 11;
         ns += nvalid > lo ? min(nvalid - lo, 256u) : 0u;
     }
-    return 4 * L.ntok < ns ? (int32_t)DMX_DEEP_CHAIN : max_chain;
+    return 4 * L.ntok < ns ? dk : max_chain;
 }
 
 // NBX > 3: the exhaustive parse without a dictionary (max_chain = 0) on NBX-byte chains
@@ -2366,9 +2432,6 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
     __shared__ MatchLDS L;
     __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def, tp0[3], st_rounds, st_p3a, st_h4[3], st_lz, st_w1w;
     const uint32_t tid = tidx();
-    // (the arguments too: see tidx)
-    asm volatile("" : "+s"(in), "+s"(n), "+s"(sw), "+s"(max_chain), "+s"(mflags), "+s"(dist_g), "+s"(chs),
-                 "+s"(tok_g), "+s"(hist_g), "+s"(info), "+s"(dbg), "+s"(nfallback));
     const uint32_t lane = tid & 63, wave = wave_of(tid);
     if ((mflags & 4u) && info[b].prestored) return;   // stored by the noise check (K0)
     const uint64_t off = (uint64_t)b * sw;
@@ -2827,17 +2890,29 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
 // the current one runs; the index goes through LDS, so every wave leaves the loop together.
 // Stored blocks then cost nothing here (round 4: 32 768 workgroups that returned at once
 // took 0.07 ms of C4's 0.70).
+struct MatchArgs {   // dmx_match_kernel's arguments, one struct (read back per block in the loop)
+    const uint8_t* in;
+    uint64_t n;
+    uint32_t sw;
+    int32_t max_chain;
+    uint32_t mflags;
+    uint16_t* dist_g;
+    const uint16_t* chs;
+    uint32_t* tok_g;
+    uint32_t* hist_g;
+    dmx_blkinfo* info;
+    uint64_t* dbg;
+    uint32_t* nfallback;
+    uint32_t* wl;
+};
 template <bool DICT, int NBX = 3>
-__global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
-                                                       int32_t max_chain, uint32_t mflags, uint16_t* __restrict__ dist_g,
-                                                       const uint16_t* __restrict__ chs, uint32_t* __restrict__ tok_g,
-                                                       uint32_t* __restrict__ hist_g,
-                                                       dmx_blkinfo* __restrict__ info, uint64_t* __restrict__ dbg,
-                                                       uint32_t* __restrict__ nfallback, uint32_t* __restrict__ wl) {
+__global__ __launch_bounds__(MT) void dmx_match_kernel(const MatchArgs args) {
 #ifdef DMX_NO_WL_LOOP   // (A/B builds: the round-4 kernel shape, one workgroup per block always)
-    match_block<DICT, NBX>(blockIdx.x, in, n, sw, max_chain, mflags, dist_g, chs, tok_g, hist_g, info, dbg, nfallback);
+    match_block<DICT, NBX>(blockIdx.x, args.in, args.n, args.sw, args.max_chain, args.mflags, args.dist_g, args.chs,
+                           args.tok_g, args.hist_g, args.info, args.dbg, args.nfallback);
     return;
 #endif
+    uint32_t* const wl = args.wl;
     __shared__ uint32_t nb_s;
     uint32_t nx = 0;   // thread 0: the list index claimed for the next block
     if (wl && threadIdx.x == 0) nx = atomicAdd(&wl[WL_C1], 1u);
@@ -2860,7 +2935,14 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const uint8_t* __restrict
             __syncthreads();   // every thread has the index before thread 0 may write the next
             if (b == 0xFFFFFFFFu) break;
         }
-        match_block<DICT, NBX>(b, in, n, sw, max_chain, mflags, dist_g, chs, tok_g, hist_g, info, dbg, nfallback);
+        // the arguments through a pointer the compiler cannot follow across iterations: loaded
+        // where the block needs them, as in a kernel without the loop, instead of hoisted and
+        // kept live (spilled) through the whole block
+        typedef const __attribute__((address_space(4))) MatchArgs* KArgs;   // constant memory: rematerialisable loads
+        KArgs A = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(A));
+        match_block<DICT, NBX>(b, A->in, A->n, A->sw, A->max_chain, A->mflags, A->dist_g, A->chs, A->tok_g, A->hist_g,
+                               A->info, A->dbg, A->nfallback);
     }
 }
 
@@ -3770,7 +3852,7 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_tile_kernel(dmx_blkinfo* _
 __global__ __launch_bounds__(ST) void dmx_scan_kernel(ScanTile* __restrict__ tiles, uint32_t nblk, uint64_t n,
                                                       uint32_t flags, uint64_t out_cap,
                                                       uint32_t* __restrict__ out32, dmx_result* __restrict__ res,
-                                                      uint32_t* __restrict__ nfallback, uint32_t* __restrict__ wl) {
+                                                      uint32_t* __restrict__ nfallback) {
     __shared__ Mono wtot[ST / 64];
     __shared__ Mono carry_s;
     __shared__ uint64_t red[ST / 64][5];
@@ -3858,14 +3940,6 @@ __global__ __launch_bounds__(ST) void dmx_scan_kernel(ScanTile* __restrict__ til
         nfallback[1] += nfallback[0];       // and the context's running total
         res->nsortfallback_total = nfallback[1];
         nfallback[0] = 0;
-        if (wl) {   // work lists: M for the apply launch; K0's / K1's counters zero for the next encode
-            wl[WL_M] = nblk - wl[WL_MX];
-            wl[WL_MX] = 0;
-            wl[WL_N1] = 0;
-            wl[WL_C1] = 0;
-            wl[WL_N2] = 0;
-            wl[WL_N4] = 0;
-        }
         s_end = end;
         s_T = T;
         s_adler = adler;
@@ -4395,7 +4469,6 @@ static int ctx_reserve(dmx_ctx* c, uint64_t nblk) {
     HIPCHK(dmx_malloc(&c->info, cb * sizeof(dmx_blkinfo)));
     HIPCHK(dmx_malloc(&c->tiles, (cb / SCAN_TILE + 1) * sizeof(ScanTile)));
     HIPCHK(dmx_malloc(&c->wl, (WL_HDR + 3 * cb) * sizeof(uint32_t)));
-    HIPCHK(hipMemset(c->wl, 0, WL_HDR * sizeof(uint32_t)));   // counters (the scan kernel re-zeroes them)
     c->cap_blocks = cb;
     return ctx_reserve_scratch(c);
 }
@@ -4504,6 +4577,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
     if (o.sw == 0) o.sw = DMX_BLK;
     if (o.sw < 1 || o.sw > DMX_BLK) return -(int)E_RANGE;
     if (o.max_chain < 0) return -(int)E_RANGE;
+    if (o.deep_chain < 0 || o.deep_chain > 255) return -(int)E_RANGE;
     if ((reinterpret_cast<uintptr_t>(d_out) & 3) != 0) return -(int)E_INVAL;
     uint32_t dict_len = 0;   // DMX_F_DICT: history of block 0 (the last sw bytes are used)
     if ((o.flags & DMX_F_DICT) && o.dict && o.dict_len) {
@@ -4547,11 +4621,15 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         if (o.flags & DMX_F_STORE_CHECK)
             hipLaunchKernelGGL(dmx_store_check_kernel, dim3(nblk), dim3(SCT), 0, s, (const uint8_t*)d_in, n,
                                (uint32_t)o.sw, c->info, c->tok, c->hist, (o.flags & DMX_F_DICT) ? 0u : 1u, o.flags,
-                               (uint32_t*)d_out, out_cap, wl, (uint64_t)c->cap_blocks);
+                               (uint32_t*)d_out, out_cap, wl ? 1u : 0u);
+        if (wl)
+            hipLaunchKernelGGL(dmx_worklist_kernel, dim3(1), dim3(WLT), 0, s, (const dmx_blkinfo*)c->info, nblk, wl,
+                               (uint64_t)c->cap_blocks);
         if (ev) (void)hipEventRecord(ev[1], s);
         const char* dstop = getenv("DMX_DEBUG_STOP");   // diagnostic only (dbg_stop)
         const uint32_t mfl = ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u) |
-                             ((o.flags & DMX_F_STORE_CHECK) ? 4u : 0u) | ((o.flags & DMX_F_DEEP) ? 8u : 0u) | (dstop ? ((uint32_t)atoi(dstop) & 3u) << 8 : 0u);
+                             ((o.flags & DMX_F_STORE_CHECK) ? 4u : 0u) | ((o.flags & DMX_F_DEEP) ? 8u : 0u) | (dstop ? ((uint32_t)atoi(dstop) & 3u) << 8 : 0u) |
+                             ((uint32_t)o.deep_chain << 16);   // DMX_F_DEEP depth (0 = DMX_DEEP_CHAIN)
         // work-list mode: a persistent K1 of one workgroup per CU over K0's list
 #ifdef DMX_NO_WL_LOOP
         uint32_t* wl1 = NULL;
@@ -4559,15 +4637,14 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         uint32_t* wl1 = wl;
 #endif
         const dim3 g1(wl1 ? (nblk < c->ncu ? nblk : c->ncu) : nblk);
+        const MatchArgs ma = {(const uint8_t*)d_in, n, (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok,
+                              c->hist, c->info, dbg, c->nfb, wl1};
         if (o.flags & DMX_F_DICT)
-            hipLaunchKernelGGL(dmx_match_kernel<true>, g1, dim3(MT), 0, s, (const uint8_t*)d_in, n,
-                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb, wl1);
+            hipLaunchKernelGGL(dmx_match_kernel<true>, g1, dim3(MT), 0, s, ma);
         else if (o.max_chain == 0)
-            hipLaunchKernelGGL((dmx_match_kernel<false, DMX_NBX>), g1, dim3(MT), 0, s, (const uint8_t*)d_in, n,
-                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb, wl1);
+            hipLaunchKernelGGL((dmx_match_kernel<false, DMX_NBX>), g1, dim3(MT), 0, s, ma);
         else
-            hipLaunchKernelGGL(dmx_match_kernel<false>, g1, dim3(MT), 0, s, (const uint8_t*)d_in, n,
-                               (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok, c->hist, c->info, dbg, c->nfb, wl1);
+            hipLaunchKernelGGL(dmx_match_kernel<false>, g1, dim3(MT), 0, s, ma);
         if (ev) (void)hipEventRecord(ev[2], s);
         if (o.flags & DMX_F_SPLIT)
             {
@@ -4594,7 +4671,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                            c->tiles);
     uint32_t* L4 = wl ? wl + WL_HDR + 2 * c->cap_blocks : NULL;
     hipLaunchKernelGGL(dmx_scan_kernel, dim3(1), dim3(ST), 0, s, c->tiles, nblk, n, o.flags, out_cap,
-                       (uint32_t*)d_out, c->res, c->nfb, c->wl);
+                       (uint32_t*)d_out, c->res, c->nfb);
     if (nblk)
         hipLaunchKernelGGL(dmx_scan_apply_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, o.flags, c->tiles,
                            (uint32_t*)d_out, (const dmx_result*)c->res, wl, L4);

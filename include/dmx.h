@@ -156,14 +156,17 @@ struct compress_stats {
                             K < 64 -- a block whose trigrams are few (D distinct 13-bit
                             buckets among its positions p mod 2048 < 256, 4 D < samples:
                             small alphabets such as binary digits, hex, DNA) searches its
-                            own chains 64 deep instead of K.  Text never qualifies. */
+                            own chains 64 deep instead of K (dmx_opts.deep_chain sets
+                            another depth).  Text never qualifies. */
 #define DMX_DEEP_CHAIN 64
 
 typedef struct {
     int32_t sw;        /* block size 1..32768 (0 = 32768) */
     int32_t max_chain; /* 0 = exhaustive (reference semantics); K > 0 = the K newest chain entries */
     uint32_t flags;    /* DMX_F_* */
-    int32_t reserved;
+    int32_t deep_chain; /* DMX_F_DEEP: the chain depth of a small-alphabet block, K < depth <=
+                           255 (0 = DMX_DEEP_CHAIN); other values return -E_RANGE.  (This
+                           field was `reserved`, always 0, before round 5.) */
     const void* dict;  /* DMX_F_DICT: the bytes just before the input (device memory for
                           dmx_encode_async, host memory for dmx_encode_host), history of
                           block 0; the last min(dict_len, sw) bytes are used.  NULL: none */

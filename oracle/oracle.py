@@ -72,6 +72,8 @@ def lib():
         L.dmx_oracle_store_check.restype = ctypes.c_int
         L.dmx_oracle_plan.argtypes = [u32p, ctypes.c_int, ctypes.c_int, u64p, u8p, u8p]
         L.dmx_oracle_plan.restype = ctypes.c_int
+        L.dmx_oracle_set_deep_chain.argtypes = [ctypes.c_int]
+        L.dmx_oracle_set_deep_chain.restype = None
         L.dmx_oracle_block_chain.argtypes = [u8p, ctypes.c_int, ctypes.c_int]
         L.dmx_oracle_block_chain.restype = ctypes.c_int
         _lib = L
@@ -85,6 +87,11 @@ def _u8(a: np.ndarray):
 def _lz(lazy: bool, deep: bool) -> int:
     """The oracle's `lazy` argument: bit 0 = lazy evaluation (f2), bit 1 = DMX_F_DEEP."""
     return int(bool(lazy)) | (2 if deep else 0)
+
+
+def set_deep_chain(k: int) -> None:
+    """The depth DMX_F_DEEP gives small-alphabet blocks (0 = 64), as dmx_opts.deep_chain."""
+    lib().dmx_oracle_set_deep_chain(int(k))
 
 
 def block_chain(block, max_chain: int) -> int:

@@ -79,3 +79,18 @@ def test_deep_streams_inflate_and_shrink():
         z = O.compress(data, max_chain=8, lazy=True, deep=True, **kw)
         assert zlib.decompress(z) == data
         assert z == O.compress_par(data, max_chain=8, lazy=True, deep=True, threads=4, **kw)
+
+
+def test_oracle_deep_chain_setting():
+    """dmx_oracle_set_deep_chain (the GPU's dmx_opts.deep_chain): a deep block gets that depth,
+    0 restores 64; K >= the depth is left alone."""
+    from tests.deep_inputs import inputs
+    blk = inputs()["bitdump"][:32768]
+    try:
+        assert O.block_chain(blk, 7) == 64
+        O.set_deep_chain(24)
+        assert O.block_chain(blk, 7) == 24
+        assert O.block_chain(blk, 30) == 30
+    finally:
+        O.set_deep_chain(0)
+    assert O.block_chain(blk, 7) == 64

@@ -91,3 +91,18 @@ def test_deep_off_for_exhaustive_and_long_chains(enc):
     for k in (0, 64, 100):
         z, _ = enc.compress_bytes(data, max_chain=k, flags=D.DMX_ZLIB | D.DMX_F_DEEP)
         assert z == O.compress(data, max_chain=k), k
+
+
+@pytest.mark.parametrize("depth", [16, 24, 32])
+def test_deep_chain_depths(enc, depth):
+    """dmx_opts.deep_chain: small-alphabet blocks search `depth` deep (the oracle at the same
+    depth, dmx_oracle_set_deep_chain), at the headline parse."""
+    data = inputs()["mixed"]
+    fl = D.DMX_ZLIB | D.DMX_F_DEEP | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK
+    t = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).cuda()
+    O.set_deep_chain(depth)
+    try:
+        z, _ = enc.compress_tensor(t, opts=D.Opts(32768, 7, fl, depth))
+        assert z.cpu().numpy().tobytes() == O.compress(data, max_chain=7, lazy=True, deep=True, store_check=True)
+    finally:
+        O.set_deep_chain(0)

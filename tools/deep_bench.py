@@ -29,8 +29,12 @@ def main():
         cap = D.max_compressed(a.size)
         d_out = torch.empty(cap, dtype=torch.uint8, device="cuda")
         row = []
-        for k, fl in ((8, 0), (8, D.DMX_F_DEEP), (64, 0), (128, 0), (256, 0)):
+        # (K, DMX_F_DEEP, deep_chain): the bench's K=7 alone, and with the adaptive depth at
+        # the depths VERDICT r4 #6 asks for
+        cfgs = [(7, 0, 0)] + [(7, D.DMX_F_DEEP, dk) for dk in (16, 24, 32, 64)]
+        for k, fl, dk in cfgs:
             e = D.Encoder(0, a.size, 32768, k, D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | fl)
+            e.opts.deep_chain = dk
             e.encode_async(d_in.data_ptr(), a.size, d_out.data_ptr(), cap, stream)
             ln = int(e.result(stream).out_len)
             torch.cuda.synchronize()
@@ -40,7 +44,7 @@ def main():
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / 3
             e.close()
-            row.append(f"K={k}{'+deep' if fl else ''}: {a.size / dt / 1e9:7.2f} GB/s ratio {ln / a.size:.4f}")
+            row.append(f"K={k}{f'+deep{dk}' if fl else ''}: {a.size / dt / 1e9:7.2f} GB/s ratio {ln / a.size:.4f}")
         print(f"{name:8s} " + " | ".join(row), flush=True)
 
 

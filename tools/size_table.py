@@ -42,7 +42,9 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r04_size", "size_table.md"))
     ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--deep-chain", type=int, default=0, help="DMX_F_DEEP depth (dmx_opts.deep_chain; 0 = 64)")
     a = ap.parse_args()
+    O.set_deep_chain(a.deep_chain)
     rows = []
     tot = {c: 0 for c in ["ref"] + COLS}
     for name, b in inputs():
