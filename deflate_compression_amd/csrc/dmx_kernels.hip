@@ -40,14 +40,6 @@
 // small device helpers
 // ------------------------------------------------------------------------------------
 
-// The thread index through an empty volatile asm: values derived from it cannot be hoisted
-// out of the match kernel's work-list loop (LICM would keep dozens of them live across the
-// whole per-block body, i.e. in scratch).
-__device__ __forceinline__ uint32_t tidx() {
-    uint32_t t = threadIdx.x;
-    asm volatile("" : "+v"(t));
-    return t;
-}
 __device__ __forceinline__ uint32_t dmx_hash(uint32_t tri) { return (tri * 0x9E3779B1u) >> DMX_HASH_SHIFT; }
 // The order of the bucket-sorted array S: (bucket of the trigram in the low 3 bytes of w,
 // position p < 32768) as one integer, so that adjacent entries are checked with one compare.
@@ -404,7 +396,7 @@ __device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
 
 // Inclusive prefix sum over the wave: DPP row shifts inside each row of 16, row totals by readlane.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-    const uint32_t r = tidx() & 15, row = (tidx() & 63) >> 4;
+    const uint32_t r = threadIdx.x & 15, row = (threadIdx.x & 63) >> 4;
     uint32_t y;
     y = dpp_shr(x, 1); if (r >= 1) x += y;
     y = dpp_shr(x, 2); if (r >= 2) x += y;
@@ -1137,7 +1129,7 @@ __device__ __forceinline__ uint64_t group_of(unsigned long long* G, uint32_t v, 
     if (__ballot(valid && v != v0) == 0) return valid ? vm : 0;   // one group (runs): no LDS traffic
     uint64_t eq = 0;
     if (valid) {
-        __hip_atomic_fetch_or(&G[v], 1ull << (tidx() & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_or(&G[v], 1ull << (threadIdx.x & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         eq = __hip_atomic_load(&G[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_store(&G[v], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
@@ -1160,7 +1152,7 @@ __device__ __forceinline__ void count_add(uint32_t* T, uint32_t v, bool valid, b
     const uint32_t first = (uint32_t)__builtin_ctzll(vm);
     const uint32_t v0 = __builtin_amdgcn_readlane(v, (int)first);
     if (__ballot(valid && v != v0) == 0) {
-        if ((tidx() & 63) == first) {
+        if ((threadIdx.x & 63) == first) {
             const uint32_t c = (uint32_t)__popcll(vm);
             if (pair16) atomicAdd(&T[v0 >> 1], c << (16 * (v0 & 1)));
             else atomicAdd(&T[v0], c);
@@ -1184,7 +1176,7 @@ __device__ __forceinline__ uint32_t atomic_rank(uint32_t* T, uint32_t v, bool va
     const uint32_t v0 = __builtin_amdgcn_readlane(v, (int)first);
     if (__ballot(valid && v != v0) == 0) {
         uint32_t base = 0;
-        if ((tidx() & 63) == first) base = atomicAdd(&T[v0], (uint32_t)__popcll(vm));
+        if ((threadIdx.x & 63) == first) base = atomicAdd(&T[v0], (uint32_t)__popcll(vm));
         return __builtin_amdgcn_readlane(base, (int)first) + (uint32_t)__popcll(vm & lt);
     }
     return valid ? atomicAdd(&T[v], 1u) : 0u;
@@ -1214,7 +1206,7 @@ __device__ __forceinline__ uint32_t atomic_rank16(uint32_t* T, uint32_t v, bool 
         const uint32_t v0 = __builtin_amdgcn_readlane(v, (int)first);
         if (__ballot(valid && v != v0) == 0) {
             uint32_t base = 0;
-            if ((tidx() & 63) == first) base = atomicAdd(&T[v0], (uint32_t)__popcll(vm) << sh);
+            if ((threadIdx.x & 63) == first) base = atomicAdd(&T[v0], (uint32_t)__popcll(vm) << sh);
             return ((__builtin_amdgcn_readlane(base, (int)first) >> sh) & 0xFFFFu) + (uint32_t)__popcll(vm & lt);
         }
     }
@@ -1963,12 +1955,21 @@ __device__ __forceinline__ uint32_t uniform_parse(uint32_t bn, uint32_t c, uint3
 // them.  (A first version appended to the lists from K0 with device atomics: 3 052 text
 // blocks took 0.11 ms, 32 768 blocks of zeros 0.79 ms -- same-address atomics from every
 // XCD serialise.)
+// The hint (words WL_HINT, WL_HINT + 1: a host-mapped pinned address, set at allocation):
+// {nblk, |L1|, |L2|, |L4|} of the latest encode, written by the list builder and K4, read
+// by the host at the next encode to choose the launch shapes (wl_shape).  Only the shape
+// depends on it -- every shape writes the same stream.
 #define WL_N1 0
 #define WL_C1 1
 #define WL_N2 2
 #define WL_N4 3
 #define WL_M 5
+#define WL_HINT 8
 #define WL_HDR 16
+__device__ __forceinline__ void wl_hint_put(const uint32_t* __restrict__ wl, int k, uint32_t v) {
+    uint32_t* h = reinterpret_cast<uint32_t*>((uint64_t)wl[WL_HINT] | ((uint64_t)wl[WL_HINT + 1] << 32));
+    if (h) __hip_atomic_store(&h[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 // K4 never sees block x: a stored block of the whole-copy prefix (above)
 __device__ __forceinline__ bool wl_skip(uint32_t x, uint32_t M, uint32_t nblk) {
     return x >= 1 && x < M && x + 1 < nblk;
@@ -2016,6 +2017,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
     __shared__ uint32_t hist[256];
     __shared__ uint64_t red[10][SCT / 64];
     __shared__ uint32_t pass_s;
+    __shared__ uint32_t edge[32];   // the whole copy: the block's first and last 64 bytes (full blocks)
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t b = blockIdx.x;
     const uint64_t off = (uint64_t)b * sw;
@@ -2123,6 +2125,9 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
             const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
             chunk1((tid + i * SCT) << 4, w);
         }
+        // the first 4 and the last 4 chunks for the whole copy (published by pass 2's barrier)
+        if (whole && tid < 4) reinterpret_cast<uint4*>(edge)[tid] = v[0];
+        if (whole && tid >= SCT - 4) reinterpret_cast<uint4*>(edge)[4 + tid - (SCT - 4)] = v[7];
     } else {
         for (uint32_t p = tid << 4; p < bn; p += SCT << 4) {
             uint32_t w[5];
@@ -2274,8 +2279,15 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
         const uint32_t ks = 4 - (uint32_t)(gw0 & 3);
         const uint32_t nq = ((full || dal) && nwords > ks + 1) ? (nwords - 1 - ks) >> 2 : 0;
         const uint32_t lenw = (bn & 0xFFFFu) | ((~bn & 0xFFFFu) << 16);
+        const uint8_t* e8 = reinterpret_cast<const uint8_t*>(edge);
         auto gen_byte = [&](uint32_t q) -> uint32_t {
-            if (q >= B0) return (q - B0) < bn ? (uint32_t)d[q - B0] : 0u;
+            if (q >= B0) {   // (every byte the copy needs here is within 64 of an end)
+                const uint32_t i = q - B0;
+                if (i >= bn) return 0u;
+                if (full && i < 64) return e8[i];
+                if (full && i >= bn - 64) return e8[64 + i - (bn - 64)];
+                return (uint32_t)d[i];
+            }
             if (q >= (P >> 3)) return (lenw >> (8 * (q - (P >> 3)))) & 0xFFu;
             return 0u;   // the header byte (and the previous block's bytes below it: not written)
         };
@@ -2362,6 +2374,9 @@ __global__ __launch_bounds__(WLT) void dmx_worklist_kernel(const dmx_blkinfo* __
         wl[WL_N2] = t2;
         wl[WL_N4] = 0;
         wl[WL_M] = M;
+        wl_hint_put(wl, 0, nblk);
+        wl_hint_put(wl, 1, t1);
+        wl_hint_put(wl, 2, t2);
     }
 }
 
@@ -2422,7 +2437,7 @@ __device__ __forceinline__ int32_t block_chain(MatchLDS& L, uint32_t bn, int32_t
 #ifndef DMX_NBX
 #define DMX_NBX 4   // the exhaustive parse's chain length in bytes (4; 5 measured slower: a second gram pass and sort)
 #endif
-template <bool DICT, int NBX>
+template <bool DICT, int NBX, bool LOOP = false>
 __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
                                             int32_t max_chain, uint32_t mflags, uint16_t* __restrict__ dist_g,
                                             const uint16_t* __restrict__ chs, uint32_t* __restrict__ tok_g,
@@ -2431,7 +2446,11 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
                                             uint32_t* __restrict__ nfallback) {
     __shared__ MatchLDS L;
     __shared__ uint64_t st_search, st_iters, st_w1, st_w23, st_def, tp0[3], st_rounds, st_p3a, st_h4[3], st_lz, st_w1w;
-    const uint32_t tid = tidx();
+    uint32_t tid = threadIdx.x;
+    // in the work-list loop the thread index goes through an empty asm: everything derived
+    // from it is then computed per block, not hoisted out of the loop and kept live (spilled)
+    // across the whole block
+    if (LOOP) asm volatile("" : "+v"(tid));
     const uint32_t lane = tid & 63, wave = wave_of(tid);
     if ((mflags & 4u) && info[b].prestored) return;   // stored by the noise check (K0)
     const uint64_t off = (uint64_t)b * sw;
@@ -2884,12 +2903,13 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
     }
 }
 
-// K1.  wl == nullptr: one workgroup per block (blockIdx.x).  Otherwise (DMX_F_STORE_CHECK:
-// K0 listed the blocks that need a parse, dmx_worklist) a persistent grid of about one
-// workgroup per CU takes the listed blocks from a device counter, the next one claimed while
-// the current one runs; the index goes through LDS, so every wave leaves the loop together.
-// Stored blocks then cost nothing here (round 4: 32 768 workgroups that returned at once
-// took 0.07 ms of C4's 0.70).
+// K1.  LOOP = false: one workgroup per block (blockIdx.x).  LOOP = true (DMX_F_STORE_CHECK,
+// when most blocks were stored in the context's previous encode: dmx_encode_async's hint) a
+// persistent grid of one workgroup per CU takes the blocks of the work list L1 from a device
+// counter, the next one claimed while the current one runs; the index goes through LDS, so
+// every wave leaves the loop together.  Stored blocks then cost nothing here (a workgroup per
+// block: 32 768 workgroups of 161 KB that return at once, 0.07-0.16 ms for 1 GiB of noise);
+// the loop's code is 2.5-4 % slower on text (its register allocation), hence the choice.
 struct MatchArgs {   // dmx_match_kernel's arguments, one struct (read back per block in the loop)
     const uint8_t* in;
     uint64_t n;
@@ -2905,13 +2925,13 @@ struct MatchArgs {   // dmx_match_kernel's arguments, one struct (read back per 
     uint32_t* nfallback;
     uint32_t* wl;
 };
-template <bool DICT, int NBX = 3>
+template <bool DICT, int NBX = 3, bool LOOP = false>
 __global__ __launch_bounds__(MT) void dmx_match_kernel(const MatchArgs args) {
-#ifdef DMX_NO_WL_LOOP   // (A/B builds: the round-4 kernel shape, one workgroup per block always)
-    match_block<DICT, NBX>(blockIdx.x, args.in, args.n, args.sw, args.max_chain, args.mflags, args.dist_g, args.chs,
-                           args.tok_g, args.hist_g, args.info, args.dbg, args.nfallback);
-    return;
-#endif
+    if constexpr (!LOOP) {   // one workgroup per block (stored blocks return at once)
+        match_block<DICT, NBX>(blockIdx.x, args.in, args.n, args.sw, args.max_chain, args.mflags, args.dist_g, args.chs,
+                               args.tok_g, args.hist_g, args.info, args.dbg, args.nfallback);
+        return;
+    }
     uint32_t* const wl = args.wl;
     __shared__ uint32_t nb_s;
     uint32_t nx = 0;   // thread 0: the list index claimed for the next block
@@ -2941,8 +2961,8 @@ __global__ __launch_bounds__(MT) void dmx_match_kernel(const MatchArgs args) {
         typedef const __attribute__((address_space(4))) MatchArgs* KArgs;   // constant memory: rematerialisable loads
         KArgs A = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
         asm volatile("" : "+s"(A));
-        match_block<DICT, NBX>(b, A->in, A->n, A->sw, A->max_chain, A->mflags, A->dist_g, A->chs, A->tok_g, A->hist_g,
-                               A->info, A->dbg, A->nfallback);
+        match_block<DICT, NBX, true>(b, A->in, A->n, A->sw, A->max_chain, A->mflags, A->dist_g, A->chs, A->tok_g,
+                                     A->hist_g, A->info, A->dbg, A->nfallback);
     }
 }
 
@@ -4273,11 +4293,14 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
                                                       uint32_t nblk, uint32_t flags, uint32_t* __restrict__ out32,
                                                       dmx_result* __restrict__ res,
                                                       const uint32_t* __restrict__ wl, const uint32_t* __restrict__ L4) {
-    if (!wl) {
+    if (!L4) {   // a workgroup per block; with work lists, the whole-copy prefix returns at once
+        if (wl && wl_skip(blockIdx.x, wl[WL_M], nblk)) return;
         pack_one(blockIdx.x, in, sw, tok_g, codes_g, hdr_g, info, sub_g, nblk, flags, out32, res);
+        if (wl && blockIdx.x == 0 && threadIdx.x == 0) wl_hint_put(wl, 3, wl[WL_N4]);
         return;
     }
     const uint32_t cnt = wl[WL_N4];
+    if (blockIdx.x == 0 && threadIdx.x == 0) wl_hint_put(wl, 3, cnt);
     for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
         __syncthreads();   // the previous block's LDS reads are done
         pack_one(L4[i], in, sw, tok_g, codes_g, hdr_g, info, sub_g, nblk, flags, out32, res);
@@ -4302,7 +4325,8 @@ struct dmx_ctx {
     dmx_subinfo* sub; // cap_blocks * DMX_NSUB
     dmx_blkinfo* info;
     ScanTile* tiles;  // cap_blocks / SCAN_TILE + 1: per-tile aggregates and prefixes (scan)
-    uint32_t* wl;     // WL_HDR + 3 cap_blocks: the work lists of DMX_F_STORE_CHECK (K0's comment)
+    uint32_t* wl;     // WL_HDR + 3 cap_blocks: the work lists of DMX_F_STORE_CHECK (WL_* comment)
+    volatile uint32_t* whint;   // host-mapped pinned {nblk, |L1|, |L2|, |L4|} of the latest encode (WL_HINT)
     uint32_t ncu;     // compute units (the persistent K1 grid of the work-list mode)
     dmx_result* res;
     uint32_t* nfb;        // [0] sort fallbacks of the encode in flight (kernels add, K3's scan reads and zeroes), [1] total
@@ -4469,6 +4493,13 @@ static int ctx_reserve(dmx_ctx* c, uint64_t nblk) {
     HIPCHK(dmx_malloc(&c->info, cb * sizeof(dmx_blkinfo)));
     HIPCHK(dmx_malloc(&c->tiles, (cb / SCAN_TILE + 1) * sizeof(ScanTile)));
     HIPCHK(dmx_malloc(&c->wl, (WL_HDR + 3 * cb) * sizeof(uint32_t)));
+    {   // the hint's device address in the list header
+        uint64_t hp = 0;
+        void* dp = NULL;
+        if (c->whint && hipHostGetDevicePointer(&dp, (void*)c->whint, 0) == hipSuccess) hp = (uint64_t)(uintptr_t)dp;
+        const uint32_t hw[2] = {(uint32_t)hp, (uint32_t)(hp >> 32)};
+        HIPCHK(hipMemcpy(c->wl + WL_HINT, hw, sizeof(hw), hipMemcpyHostToDevice));
+    }
     c->cap_blocks = cb;
     return ctx_reserve_scratch(c);
 }
@@ -4488,6 +4519,13 @@ extern "C" int dmx_ctx_create(int device, uint64_t max_input, dmx_ctx** out) {
     int ncu = 0;
     c->ncu = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0
                  ? (uint32_t)ncu : 256u;
+    {   // the launch-shape hint (WL_HINT): zero = no encode yet; without it every shape is per block
+        void* hp = NULL;
+        if (hipHostMalloc(&hp, 16, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+            memset(hp, 0, 16);
+            c->whint = (volatile uint32_t*)hp;
+        }
+    }
     if (hip_fail(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate")) { c->stream = NULL; dmx_ctx_destroy(c); return -(int)E_DEVICE; }
     if (hip_fail(dmx_malloc(&c->res, sizeof(dmx_result)), "hipMalloc(res)")) { dmx_ctx_destroy(c); return -(int)E_DEVICE; }
     if (hip_fail(dmx_malloc(&c->nfb, 16), "hipMalloc(nfb)") || hip_fail(hipMemset(c->nfb, 0, 16), "hipMemset(nfb)")) {
@@ -4546,6 +4584,7 @@ extern "C" void dmx_ctx_destroy(dmx_ctx* c) {
     }
     if (c->fd_cs) (void)hipStreamDestroy(c->fd_cs);
     fdp_free(c->fdp);
+    if (c->whint) (void)hipHostFree((void*)c->whint);
     if (c->chs) (void)hipFree(c->chs);
     if (c->che) (void)hipFree(c->che);
     if (c->split) (void)hipFree(c->split);
@@ -4567,6 +4606,24 @@ static void ctx_collect_set(dmx_ctx* c, int j) {
     float tot = 0.f;
     if (hipEventElapsedTime(&tot, c->ev[j][0], c->ev[j][5]) == hipSuccess) c->stage_ms[5] += tot;
     c->stage_n++;
+}
+
+// Launch shapes of the work-list mode: the persistent K1 over L1, K2 over L2, K4 over L4 when
+// the context's previous encode (WL_HINT) listed fewer than half of its blocks there, else a
+// workgroup per block.  DMX_WORKLIST=list / plain forces one shape (tests), =0 turns the
+// work lists off (one workgroup per block, no list builder, no whole copies in K0).
+struct WlShape { bool loop1, list2, list4; };
+static WlShape wl_shape(const dmx_ctx* c) {
+    WlShape w = {false, false, false};
+    const char* e = getenv("DMX_WORKLIST");
+    if (e && !strcmp(e, "list")) return WlShape{true, true, true};
+    if ((e && !strcmp(e, "plain")) || !c->whint) return w;
+    const uint32_t nb = c->whint[0];
+    if (!nb) return w;
+    w.loop1 = 2 * c->whint[1] < nb;
+    w.list2 = 2 * c->whint[2] < nb;
+    w.list4 = 2 * c->whint[3] < nb;
+    return w;
 }
 
 extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* d_out, uint64_t out_cap,
@@ -4593,9 +4650,10 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
     if ((o.flags & DMX_F_SPLIT) && c->cap_split < nblk) return -(int)E_SZ;
     if ((o.flags & DMX_F_DICT) && c->cap_chain < (uint64_t)nblk + 1) return -(int)E_SZ;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    // DMX_F_STORE_CHECK: K0 lists the blocks K1 / K2 / K4 have work for (WL_* above);
-    // DMX_NO_WORKLIST=1 keeps one workgroup per block (A/B measurements)
-    uint32_t* wl = ((o.flags & DMX_F_STORE_CHECK) && !getenv("DMX_NO_WORKLIST")) ? c->wl : NULL;
+    // DMX_F_STORE_CHECK: the work lists (WL_* above) and their launch shapes (wl_shape)
+    const char* wle = getenv("DMX_WORKLIST");
+    uint32_t* wl = ((o.flags & DMX_F_STORE_CHECK) && !(wle && !strcmp(wle, "0"))) ? c->wl : NULL;
+    const WlShape wsh = wl_shape(c);
     hipEvent_t* ev = NULL;
     if (c->timing) {
         const int j = (int)(c->ev_next++ % DMX_EV_RING);
@@ -4630,21 +4688,22 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         const uint32_t mfl = ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u) |
                              ((o.flags & DMX_F_STORE_CHECK) ? 4u : 0u) | ((o.flags & DMX_F_DEEP) ? 8u : 0u) | (dstop ? ((uint32_t)atoi(dstop) & 3u) << 8 : 0u) |
                              ((uint32_t)o.deep_chain << 16);   // DMX_F_DEEP depth (0 = DMX_DEEP_CHAIN)
-        // work-list mode: a persistent K1 of one workgroup per CU over K0's list
-#ifdef DMX_NO_WL_LOOP
-        uint32_t* wl1 = NULL;
-#else
-        uint32_t* wl1 = wl;
-#endif
-        const dim3 g1(wl1 ? (nblk < c->ncu ? nblk : c->ncu) : nblk);
+        // work lists: the persistent K1 over L1 when the previous encode left most blocks
+        // stored (wl_shape), else a workgroup per block
+        const bool loop1 = wl && wsh.loop1;
+        const dim3 g1(loop1 ? (nblk < c->ncu ? nblk : c->ncu) : nblk);
         const MatchArgs ma = {(const uint8_t*)d_in, n, (uint32_t)o.sw, o.max_chain, mfl, c->dist, c->chs, c->tok,
-                              c->hist, c->info, dbg, c->nfb, wl1};
-        if (o.flags & DMX_F_DICT)
-            hipLaunchKernelGGL(dmx_match_kernel<true>, g1, dim3(MT), 0, s, ma);
-        else if (o.max_chain == 0)
-            hipLaunchKernelGGL((dmx_match_kernel<false, DMX_NBX>), g1, dim3(MT), 0, s, ma);
-        else
-            hipLaunchKernelGGL(dmx_match_kernel<false>, g1, dim3(MT), 0, s, ma);
+                              c->hist, c->info, dbg, c->nfb, loop1 ? wl : NULL};
+        if (o.flags & DMX_F_DICT) {
+            if (loop1) hipLaunchKernelGGL((dmx_match_kernel<true, 3, true>), g1, dim3(MT), 0, s, ma);
+            else hipLaunchKernelGGL((dmx_match_kernel<true, 3, false>), g1, dim3(MT), 0, s, ma);
+        } else if (o.max_chain == 0) {
+            if (loop1) hipLaunchKernelGGL((dmx_match_kernel<false, DMX_NBX, true>), g1, dim3(MT), 0, s, ma);
+            else hipLaunchKernelGGL((dmx_match_kernel<false, DMX_NBX, false>), g1, dim3(MT), 0, s, ma);
+        } else {
+            if (loop1) hipLaunchKernelGGL((dmx_match_kernel<false, 3, true>), g1, dim3(MT), 0, s, ma);
+            else hipLaunchKernelGGL((dmx_match_kernel<false, 3, false>), g1, dim3(MT), 0, s, ma);
+        }
         if (ev) (void)hipEventRecord(ev[2], s);
         if (o.flags & DMX_F_SPLIT)
             {
@@ -4656,9 +4715,9 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                                    c->info, c->codes, c->hdr, c->sub, nblk, o.flags);
             }
         else
-            hipLaunchKernelGGL(dmx_huff_kernel, dim3(wl ? (nblk < 32 * c->ncu ? nblk : 32 * c->ncu) : nblk), dim3(64), 0,
-                               s, c->hist, c->info, c->codes, c->hdr, c->sub, nblk, o.flags, wl,
-                               wl ? wl + WL_HDR + c->cap_blocks : NULL);
+            hipLaunchKernelGGL(dmx_huff_kernel, dim3(wl && wsh.list2 ? (nblk < 32 * c->ncu ? nblk : 32 * c->ncu) : nblk),
+                               dim3(64), 0, s, c->hist, c->info, c->codes, c->hdr, c->sub, nblk, o.flags,
+                               wl && wsh.list2 ? wl : NULL, wl && wsh.list2 ? wl + WL_HDR + c->cap_blocks : NULL);
         if (ev) (void)hipEventRecord(ev[3], s);
     } else if (ev) {
         (void)hipEventRecord(ev[1], s);
@@ -4677,9 +4736,9 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                            (uint32_t*)d_out, (const dmx_result*)c->res, wl, L4);
     if (ev) (void)hipEventRecord(ev[4], s);
     if (nblk)
-        hipLaunchKernelGGL(dmx_pack_kernel, dim3(wl ? (nblk < 4 * c->ncu ? nblk : 4 * c->ncu) : nblk), dim3(PT), 0, s,
-                           (const uint8_t*)d_in, (uint32_t)o.sw, c->tok, c->codes, c->hdr, c->info, c->sub, nblk, o.flags,
-                           (uint32_t*)d_out, c->res, wl, L4);
+        hipLaunchKernelGGL(dmx_pack_kernel, dim3(wl && wsh.list4 ? (nblk < 16 * c->ncu ? nblk : 16 * c->ncu) : nblk),
+                           dim3(PT), 0, s, (const uint8_t*)d_in, (uint32_t)o.sw, c->tok, c->codes, c->hdr, c->info, c->sub,
+                           nblk, o.flags, (uint32_t*)d_out, c->res, wl, wl && wsh.list4 ? L4 : NULL);
     if (ev) (void)hipEventRecord(ev[5], s);
     HIPCHK(fault_hit(2) ? hipErrorLaunchFailure : hipGetLastError());
     c->last_nblk = nblk;

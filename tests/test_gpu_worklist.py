@@ -1,0 +1,129 @@
+"""Work lists of DMX_F_STORE_CHECK (dmx_worklist_kernel): K1 / K2 / K4 take only
+the blocks they have work for, the prefix of noise blocks at their speculative offsets is
+written whole by K0 and skipped by K4.  Every launch shape (DMX_WORKLIST=list: the persistent
+K1 and the list-striding K2 / K4; =plain: a workgroup per block with the skip; =0: no work
+lists) must write the oracle's stream byte for byte, and the adaptive choice (the previous
+encode's hint) too, whatever it picks.
+
+Bar: bit-exact against the oracle (store_check=True), zlib inflates."""
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import deflate_compression_amd as D  # noqa: E402
+from deflate_compression_amd import shard as S  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+B = 32768
+
+
+def _noise(n, seed):
+    return D.gen_random(n, seed).tobytes()
+
+
+def _cases():
+    text = D.gen_text(6 * B, 77).tobytes()
+    z = bytes(3 * B)
+    return {
+        "all_noise": _noise(9 * B, 1),
+        "noise_prefix_then_text": _noise(5 * B, 2) + text[:3 * B] + _noise(2 * B + 777, 3),
+        "text_in_noise": _noise(3 * B, 4) + text[:B] + _noise(4 * B, 5),
+        "noise_zeros_text": _noise(2 * B, 6) + z + text[:2 * B] + _noise(B + 100, 7),
+        "text_only": text,
+        "noise_short_tail": _noise(4 * B + 5000, 8),
+        "one_block_noise": _noise(B, 9),
+        "two_blocks_noise": _noise(2 * B, 10),
+    }
+
+
+@pytest.fixture(scope="module")
+def enc():
+    e = D.Encoder(0, 16 << 20)
+    yield e
+    e.close()
+
+
+def _with_env(val, fn):
+    old = os.environ.get("DMX_WORKLIST")
+    if val is None:
+        os.environ.pop("DMX_WORKLIST", None)
+    else:
+        os.environ["DMX_WORKLIST"] = val
+    try:
+        return fn()
+    finally:
+        if old is None:
+            os.environ.pop("DMX_WORKLIST", None)
+        else:
+            os.environ["DMX_WORKLIST"] = old
+
+
+@pytest.mark.parametrize("shape", ["list", "plain", "0", None])
+@pytest.mark.parametrize("name", sorted(_cases()))
+def test_worklist_shapes_match_oracle(enc, shape, name):
+    data = _cases()[name]
+    fl = D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | D.DMX_F_DEEP
+    want = O.compress(data, max_chain=7, lazy=True, store_check=True, deep=True)
+    for rep in range(2):   # the second encode on the context follows the first one's hint
+        z, r = _with_env(shape, lambda: enc.compress_bytes(data, max_chain=7, flags=fl))
+        assert r.status == 0
+        assert z == want, (name, shape, rep, len(z), len(want))
+    assert zlib.decompress(z) == data
+
+
+@pytest.mark.parametrize("shape", ["list", "plain"])
+@pytest.mark.parametrize("k", [0, 8])
+def test_worklist_exhaustive_and_greedy(enc, shape, k):
+    data = _cases()["noise_prefix_then_text"]
+    z, _ = _with_env(shape, lambda: enc.compress_bytes(data, max_chain=k, flags=D.DMX_ZLIB | D.DMX_F_STORE_CHECK))
+    assert z == O.compress(data, max_chain=k, store_check=True)
+
+
+@pytest.mark.parametrize("shape", ["list", "plain"])
+@pytest.mark.parametrize("sw", [8192, 20000])
+def test_worklist_small_windows(enc, shape, sw):
+    data = _noise(6 * sw, 11) + D.gen_text(3 * sw, 12).tobytes() + _noise(2 * sw + 9, 13)
+    fl = D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK
+    z, _ = _with_env(shape, lambda: enc.compress_bytes(data, sw=sw, max_chain=6, flags=fl))
+    assert z == O.compress(data, sw=sw, max_chain=6, lazy=True, store_check=True)
+
+
+@pytest.mark.parametrize("shape", ["list", "plain"])
+def test_worklist_shard_framing(enc, shape):
+    """Shards without the zlib header (speculative offsets from bit 0) and without BFINAL."""
+    data = np.frombuffer(_noise(6 * B, 14) + D.gen_text(2 * B, 15).tobytes(), dtype=np.uint8)
+    for r in range(3):
+        lo, hi = S.shard_range(data.size, r, 3)
+        fl = D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | S.shard_flags(r, 3)
+        piece = data[lo:hi]
+        t = torch.from_numpy(piece.copy()).cuda()
+        z, _ = _with_env(shape, lambda: enc.compress_tensor(t, opts=D.Opts(B, 7, fl, 0)))
+        assert z.cpu().numpy().tobytes() == O.compress(piece, max_chain=7, lazy=True, store_check=True,
+                                                        flags=S.shard_flags(r, 3)), (shape, r)
+
+
+def test_worklist_with_dict_and_split(enc):
+    data = _cases()["noise_prefix_then_text"]
+    for shape in ("list", "plain"):
+        z, _ = _with_env(shape, lambda: enc.compress_bytes(
+            data, max_chain=7, flags=D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | D.DMX_F_DICT))
+        assert z == O.compress(data, max_chain=7, lazy=True, store_check=True, dict=True), shape
+        z, _ = _with_env(shape, lambda: enc.compress_bytes(
+            data, max_chain=7, flags=D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | D.DMX_F_SPLIT))
+        assert z == O.compress(data, max_chain=7, lazy=True, store_check=True, split=True), shape
+
+
+def test_worklist_inflate_gpu(enc):
+    """The indexed GPU inflate of a stream whose noise prefix K0 wrote whole."""
+    data = _cases()["noise_prefix_then_text"]
+    t = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).cuda()
+    out, r = _with_env("list", lambda: enc.compress_tensor(
+        t, opts=D.Opts(B, 7, D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK, 0)))
+    ix, n = enc.block_index()
+    dec, st = D.inflate_gpu(out, len(data), ix, n)
+    assert st == 0 and dec.cpu().numpy().tobytes() == data

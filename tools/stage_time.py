@@ -1,6 +1,6 @@
 """Diagnostic: HIP-event stage times (ms) of one encode configuration on cuda:0, averaged
 over a few encodes (no verification -- for experiments on a kernel variant).
-usage: stage_time.py [MB] [K] [flags: any of l(azy) s(plit) d(ict) c(store check) e (deep)] [text|random|zeros]"""
+usage: stage_time.py [MB] [K] [flags: any of l(azy) s(plit) d(ict) c(store check) e (deep)] [text|random|zeros] [nowl|list|plain]"""
 import os
 import sys
 
@@ -20,6 +20,8 @@ flags = D.DMX_ZLIB | (D.DMX_F_LAZY if "l" in fs else 0) | (D.DMX_F_SPLIT if "s" 
     (D.DMX_F_DEEP if "e" in fs else 0)
 n = int(mb * 1e6)
 kind = sys.argv[4] if len(sys.argv) > 4 else "text"
+if len(sys.argv) > 5:   # DMX_WORKLIST: 0 = no work lists, list / plain = that launch shape
+    os.environ["DMX_WORKLIST"] = {"nowl": "0"}.get(sys.argv[5], sys.argv[5])
 host = {"text": lambda: D.gen_text(n, 0xE5818), "random": lambda: D.gen_random(n, 0x5EED),
         "zeros": lambda: __import__("numpy").zeros(n, __import__("numpy").uint8)}[kind]()
 t = torch.from_numpy(host).cuda()
@@ -39,6 +41,6 @@ st, cnt = e.stage_times()
 import hashlib
 o, r = e.compress_tensor(t)
 h = hashlib.sha1(o.cpu().numpy().tobytes()).hexdigest()[:16]
-print({"config": f"{mb} MB K={k} {fs} {kind}", "encodes": cnt, "GBps_wall": round(n / wall / 1e9, 2), "stage_ms": {a: round(b, 4) for a, b in st.items()},
+print({"config": f"{mb} MB K={k} {fs} {kind}{' wl=' + os.environ['DMX_WORKLIST'] if os.environ.get('DMX_WORKLIST') else ''}", "encodes": cnt, "GBps_wall": round(n / wall / 1e9, 2), "stage_ms": {a: round(b, 4) for a, b in st.items()},
        "out_len": int(r.out_len), "sha1": h})
 e.close()
