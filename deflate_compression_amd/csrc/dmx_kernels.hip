@@ -1964,8 +1964,16 @@ __device__ __forceinline__ uint32_t uniform_parse(uint32_t bn, uint32_t c, uint3
 #define WL_N2 2
 #define WL_N4 3
 #define WL_M 5
+#define WL_N5 6
 #define WL_HINT 8
 #define WL_HDR 16
+// Uniform-block dedupe (round 5, the worklist kernel's `dedupe`): full blocks of one repeated
+// byte c (prestored 2, 1 <= b <= nblk - 2) all encode to the same bit string, so only the
+// first of them per byte value (its representative) is coded by K2 and packed by K4; the
+// others (the dups, list L5 = L4 + cap, rep index per block in D = L5 + cap, ~0 = not a dup)
+// take the representative's block record in the scan's tile pass and have its bits copied
+// to their offsets by dmx_dup_copy_kernel after K4.
+__host__ __device__ __forceinline__ const uint32_t* wl_dup(const uint32_t* wl, uint64_t cap) { return wl + WL_HDR + 4 * cap; }
 __device__ __forceinline__ void wl_hint_put(const uint32_t* __restrict__ wl, int k, uint32_t v) {
     uint32_t* h = reinterpret_cast<uint32_t*>((uint64_t)wl[WL_HINT] | ((uint64_t)wl[WL_HINT + 1] << 32));
     if (h) __hip_atomic_store(&h[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2324,13 +2332,21 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
 
 // The work lists from K0's prestored values (one workgroup; thread t takes blocks t, t + WLT,
 // ...: every load of a round in flight).  Deterministic order: list position = the thread's
-// offset from a block scan + its count so far.  Also zeroes K1's claim counter and K4's list.
+// offset from a block scan + its count so far.  Also zeroes K1's claim counter and K4's list,
+// and (dedupe) picks each byte value's representative among the full uniform blocks.
 #define WLT 1024
+__device__ __forceinline__ bool wl_uniform_full(const dmx_blkinfo& bi, uint32_t b, uint32_t nblk, uint32_t sw) {
+    return bi.prestored == 2 && bi.n == sw && b >= 1 && b + 2 <= nblk;
+}
 __global__ __launch_bounds__(WLT) void dmx_worklist_kernel(const dmx_blkinfo* __restrict__ info, uint32_t nblk,
-                                                           uint32_t* __restrict__ wl, uint64_t cap) {
-    __shared__ uint32_t w1[WLT / 64], w2[WLT / 64], wm[WLT / 64];
+                                                           uint32_t* __restrict__ wl, uint64_t cap, uint32_t sw,
+                                                           uint32_t dedupe) {
+    __shared__ uint32_t w1[WLT / 64], w2[WLT / 64], w5[WLT / 64], wm[WLT / 64], rep[256], nuni;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t c1 = 0, c2 = 0, m = nblk;
+    if (tid < 256) rep[tid] = 0xFFFFFFFFu;
+    if (tid == 0) nuni = 0;
+    __syncthreads();
+    uint32_t m = nblk;
     for (uint32_t b0 = 0; b0 < nblk; b0 += 16 * WLT) {   // 16 loads in flight per thread
         uint32_t ps[16];
 #pragma unroll
@@ -2341,32 +2357,67 @@ __global__ __launch_bounds__(WLT) void dmx_worklist_kernel(const dmx_blkinfo* __
 #pragma unroll
         for (int j = 0; j < 16; j++) {
             const uint32_t b = b0 + (uint32_t)j * WLT + tid;
-            c1 += ps[j] == 0 ? 1u : 0u;
-            c2 += (ps[j] == 0 || ps[j] == 2) ? 1u : 0u;
             if (ps[j] != 3 && b < m) m = b;
+            if (dedupe && ps[j] == 2 && b < nblk) {   // the representative: the first block per byte value
+                const dmx_blkinfo bi = info[b];
+                if (wl_uniform_full(bi, b, nblk, sw)) {
+                    atomicMin(&rep[(uint32_t)(bi.adl_s / bi.n) & 0xFFu], b);
+                    atomicAdd(&nuni, 1u);
+                }
+            }
         }
     }
-    // exclusive block scans of c1 and c2, min of m
-    const uint32_t i1 = wave_incl_scan(c1), i2 = wave_incl_scan(c2);
+    __syncthreads();
+    uint32_t* L1 = wl + WL_HDR;
+    uint32_t* L2 = L1 + cap;
+    uint32_t* L5 = L1 + 3 * cap;
+    uint32_t* Dp = L1 + 4 * cap;
+    // per block: 1 = K1 parses it, 2 = K2 codes it, 4 = a dup (of D[b])
+    auto kind = [&](uint32_t b, uint32_t& r) -> uint32_t {
+        const uint32_t ps = info[b].prestored;
+        r = 0xFFFFFFFFu;
+        if (ps == 0) return 3u;
+        if (ps != 2) return 0u;
+        if (dedupe) {
+            const dmx_blkinfo bi = info[b];
+            if (wl_uniform_full(bi, b, nblk, sw)) {
+                const uint32_t rr = rep[(uint32_t)(bi.adl_s / bi.n) & 0xFFu];
+                if (rr != b) { r = rr; return 4u; }
+            }
+        }
+        return 2u;
+    };
+    uint32_t c1 = 0, c2 = 0, c5 = 0;
+    for (uint32_t b = tid; b < nblk; b += WLT) {
+        uint32_t r;
+        const uint32_t k = kind(b, r);
+        c1 += k & 1u;
+        c2 += (k >> 1) & 1u;
+        c5 += (k >> 2) & 1u;
+    }
+    // exclusive block scans of the three counts, min of m
+    const uint32_t i1 = wave_incl_scan(c1), i2 = wave_incl_scan(c2), i5 = wave_incl_scan(c5);
     uint32_t mm = m;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) mm = min(mm, (uint32_t)__shfl_xor((int)mm, o));
-    if (lane == 63) { w1[wave] = i1; w2[wave] = i2; }
+    if (lane == 63) { w1[wave] = i1; w2[wave] = i2; w5[wave] = i5; }
     if (lane == 0) wm[wave] = mm;
     __syncthreads();
-    uint32_t o1 = i1 - c1, o2 = i2 - c2, t1 = 0, t2 = 0, M = nblk;
+    uint32_t o1 = i1 - c1, o2 = i2 - c2, o5 = i5 - c5, t1 = 0, t2 = 0, t5 = 0, M = nblk;
     for (uint32_t w = 0; w < WLT / 64; w++) {
-        if (w < wave) { o1 += w1[w]; o2 += w2[w]; }
+        if (w < wave) { o1 += w1[w]; o2 += w2[w]; o5 += w5[w]; }
         t1 += w1[w];
         t2 += w2[w];
+        t5 += w5[w];
         M = min(M, wm[w]);
     }
-    uint32_t* L1 = wl + WL_HDR;
-    uint32_t* L2 = L1 + cap;
     for (uint32_t b = tid; b < nblk; b += WLT) {   // (the second read of the records: L2 hits)
-        const uint32_t ps = info[b].prestored;
-        if (ps == 0) L1[o1++] = b;
-        if (ps == 0 || ps == 2) L2[o2++] = b;
+        uint32_t r;
+        const uint32_t k = kind(b, r);
+        if (k & 1u) L1[o1++] = b;
+        if (k & 2u) L2[o2++] = b;
+        if (k & 4u) L5[o5++] = b;
+        Dp[b] = r;
     }
     if (tid == 0) {
         wl[WL_N1] = t1;
@@ -2374,9 +2425,46 @@ __global__ __launch_bounds__(WLT) void dmx_worklist_kernel(const dmx_blkinfo* __
         wl[WL_N2] = t2;
         wl[WL_N4] = 0;
         wl[WL_M] = M;
+        wl[WL_N5] = t5;
         wl_hint_put(wl, 0, nblk);
         wl_hint_put(wl, 1, t1);
         wl_hint_put(wl, 2, t2);
+        wl_hint_put(wl, 4, nuni);
+    }
+}
+
+// After K4 (dedupe): every dup block gets its representative's bit string at its own offset,
+// one wave per dup: output word k of the dup holds the representative's bits shifted by the
+// two offsets' difference, masked to the dup's own bits (its two edge words, shared with its
+// neighbours and zeroed by the apply launch, by atomicOr).  The representative is complete:
+// K4 packed it in the previous launch.
+__global__ __launch_bounds__(256) void dmx_dup_copy_kernel(const dmx_blkinfo* __restrict__ info,
+                                                           const uint32_t* __restrict__ wl, uint64_t cap,
+                                                           uint32_t* __restrict__ out32, const dmx_result* __restrict__ res) {
+    if (res->status) return;
+    const uint32_t* L5 = wl + WL_HDR + 3 * cap;
+    const uint32_t* Dp = wl_dup(wl, cap);
+    const uint32_t cnt = wl[WL_N5];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < cnt; i += nw) {
+        const uint32_t b = L5[i], r = Dp[b];
+        const uint64_t Ob = info[b].off_bits, Or = info[r].off_bits, Lb = info[b].len_bits;
+        const uint64_t gw0 = Ob >> 5;
+        const uint32_t nwords = (uint32_t)(((Ob & 31) + Lb + 31) >> 5);
+        for (uint32_t k = lane; k < nwords; k += 64) {
+            const uint64_t lo = 32 * (gw0 + k), hi = lo + 32;               // the word's bits
+            const uint64_t a = lo > Ob ? lo : Ob, e = hi < Ob + Lb ? hi : Ob + Lb;   // its bits of the dup
+            const uint64_t q = a - Ob + Or;                                  // their source bit
+            const uint64_t qw = q >> 5;
+            const uint32_t sh = (uint32_t)(q & 31);
+            const uint64_t src = (uint64_t)out32[qw] | ((uint64_t)out32[qw + 1] << 32);
+            const uint32_t nb = (uint32_t)(e - a);
+            const uint64_t bits = (src >> sh) & (nb >= 64 ? ~0ull : ((1ull << nb) - 1ull));
+            const uint32_t v = (uint32_t)(bits << (a - lo));
+            if (nb == 32) out32[gw0 + k] = v;
+            else atomicOr(&out32[gw0 + k], v);
+        }
     }
 }
 
@@ -2597,8 +2685,12 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
         }
         if (dbg && tid == 0) st_h4[0] = (__builtin_amdgcn_s_memtime() - tbeg) | ((uint64_t)npass << 48);
         if (dbg && tid == 0) st_h4[2] = tsw - tbeg;   // the 3-byte sweep's end (before its listed walks)
+        uint32_t nr4 = 0;   // run-dominated blocks (counted while staging) take the run-aware ranks
+#pragma unroll
+        for (int w = 0; w < MW; w++) nr4 += L.wexit[w];
         if (hook) sort_positions<true, true, NBX>(L, bn, max_chain, tid, false, tp0);
-        else sort_positions<false, true, NBX>(L, bn, max_chain, tid, false, tp0);
+        else if (nr4 * 4 >= ((bn + 15) >> 4)) sort_positions<false, true, NBX>(L, bn, max_chain, tid, false, tp0);
+        else sort_positions<false, false, NBX>(L, bn, max_chain, tid, false, tp0);
         if (dbg && tid == 0) st_h4[1] = (__builtin_amdgcn_s_memtime() - tbeg) | ((uint64_t)min(ndefer, 65535u) << 48);
     }
 
@@ -3505,8 +3597,10 @@ __device__ __forceinline__ void huff_one(const uint32_t b, const uint32_t* __res
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void dmx_huff_kernel(const uint32_t* __restrict__ hist_g, dmx_blkinfo* __restrict__ info,
                                                       uint32_t* __restrict__ codes_g, uint32_t* __restrict__ hdr_g,
                                                       dmx_subinfo* __restrict__ sub_g, uint32_t nblk, uint32_t flags,
-                                                      const uint32_t* __restrict__ wl, const uint32_t* __restrict__ L2) {
-    if (!wl) {
+                                                      const uint32_t* __restrict__ wl, const uint32_t* __restrict__ L2,
+                                                      const uint32_t* __restrict__ dup) {
+    if (!L2) {   // a workgroup per block; dups (uniform-block dedupe) take their representative's coding
+        if (dup && dup[blockIdx.x] != 0xFFFFFFFFu) return;
         huff_one(blockIdx.x, hist_g, info, codes_g, hdr_g, sub_g, nblk, flags);
         return;
     }
@@ -3817,7 +3911,9 @@ __device__ __forceinline__ Mono blk_elem(const dmx_blkinfo& bi) {
 }
 
 __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_tile_kernel(dmx_blkinfo* __restrict__ info, uint32_t nblk,
-                                                                 uint64_t n, uint32_t sw, ScanTile* __restrict__ tiles) {
+                                                                 uint64_t n, uint32_t sw, ScanTile* __restrict__ tiles,
+                                                                 const uint32_t* __restrict__ dup,
+                                                                 dmx_subinfo* __restrict__ sub_g) {
     __shared__ Mono wtot[SCAN_TILE / 64];
     __shared__ uint64_t red[SCAN_TILE / 64][5];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -3825,7 +3921,20 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_tile_kernel(dmx_blkinfo* _
     Mono e = {0, 0, 0};
     uint64_t s1 = 0, s2 = 0, nt = 0, ns = 0, nf = 0;
     if (b < nblk) {
-        const dmx_blkinfo bi = info[b];
+        dmx_blkinfo bi = info[b];
+        const uint32_t r = dup ? dup[b] : 0xFFFFFFFFu;
+        if (r != 0xFFFFFFFFu) {   // a dup (uniform-block dedupe): the representative's coding
+            const dmx_blkinfo ri = info[r];
+            bi.btype = ri.btype;
+            bi.hdr_bits = ri.hdr_bits;
+            bi.body_bits = ri.body_bits;
+            bi.nsub = ri.nsub;
+            info[b].btype = ri.btype;
+            info[b].hdr_bits = ri.hdr_bits;
+            info[b].body_bits = ri.body_bits;
+            info[b].nsub = ri.nsub;
+            sub_g[(uint64_t)b * DMX_NSUB] = sub_g[(uint64_t)r * DMX_NSUB];
+        }
         e = blk_elem(bi);
         const uint64_t end_b = (uint64_t)b * sw + bi.n;
         s1 = bi.adl_s % ADL_MOD;
@@ -3982,7 +4091,8 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply_kernel(dmx_blkinfo* 
                                                                   uint32_t flags, const ScanTile* __restrict__ tiles,
                                                                   uint32_t* __restrict__ out32,
                                                                   const dmx_result* __restrict__ res,
-                                                                  uint32_t* __restrict__ wl, uint32_t* __restrict__ L4) {
+                                                                  uint32_t* __restrict__ wl, uint32_t* __restrict__ L4,
+                                                                  const uint32_t* __restrict__ dup) {
     if (res->status) return;
     const uint32_t b = blockIdx.x * SCAN_TILE + threadIdx.x;
     if (b >= nblk) return;
@@ -4020,6 +4130,7 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply_kernel(dmx_blkinfo* 
     } else {
         out32[w1] = 0;
     }
+    if (dup && dup[b] != 0xFFFFFFFFu) return;   // packed by dmx_dup_copy_kernel
     L4[atomicAdd(&wl[WL_N4], 1u)] = b;
 }
 
@@ -4292,9 +4403,11 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
                                                       const dmx_subinfo* __restrict__ sub_g,
                                                       uint32_t nblk, uint32_t flags, uint32_t* __restrict__ out32,
                                                       dmx_result* __restrict__ res,
-                                                      const uint32_t* __restrict__ wl, const uint32_t* __restrict__ L4) {
+                                                      const uint32_t* __restrict__ wl, const uint32_t* __restrict__ L4,
+                                                      const uint32_t* __restrict__ dup) {
     if (!L4) {   // a workgroup per block; with work lists, the whole-copy prefix returns at once
         if (wl && wl_skip(blockIdx.x, wl[WL_M], nblk)) return;
+        if (dup && dup[blockIdx.x] != 0xFFFFFFFFu) return;   // dmx_dup_copy_kernel's
         pack_one(blockIdx.x, in, sw, tok_g, codes_g, hdr_g, info, sub_g, nblk, flags, out32, res);
         if (wl && blockIdx.x == 0 && threadIdx.x == 0) wl_hint_put(wl, 3, wl[WL_N4]);
         return;
@@ -4326,7 +4439,7 @@ struct dmx_ctx {
     dmx_blkinfo* info;
     ScanTile* tiles;  // cap_blocks / SCAN_TILE + 1: per-tile aggregates and prefixes (scan)
     uint32_t* wl;     // WL_HDR + 3 cap_blocks: the work lists of DMX_F_STORE_CHECK (WL_* comment)
-    volatile uint32_t* whint;   // host-mapped pinned {nblk, |L1|, |L2|, |L4|} of the latest encode (WL_HINT)
+    volatile uint32_t* whint;   // host-mapped pinned {nblk, |L1|, |L2|, |L4|, uniform full blocks} of the latest encode (WL_HINT)
     uint32_t ncu;     // compute units (the persistent K1 grid of the work-list mode)
     dmx_result* res;
     uint32_t* nfb;        // [0] sort fallbacks of the encode in flight (kernels add, K3's scan reads and zeroes), [1] total
@@ -4492,7 +4605,7 @@ static int ctx_reserve(dmx_ctx* c, uint64_t nblk) {
     HIPCHK(dmx_malloc(&c->sub, cb * DMX_NSUB * sizeof(dmx_subinfo)));
     HIPCHK(dmx_malloc(&c->info, cb * sizeof(dmx_blkinfo)));
     HIPCHK(dmx_malloc(&c->tiles, (cb / SCAN_TILE + 1) * sizeof(ScanTile)));
-    HIPCHK(dmx_malloc(&c->wl, (WL_HDR + 3 * cb) * sizeof(uint32_t)));
+    HIPCHK(dmx_malloc(&c->wl, (WL_HDR + 5 * cb) * sizeof(uint32_t)));
     {   // the hint's device address in the list header
         uint64_t hp = 0;
         void* dp = NULL;
@@ -4521,8 +4634,8 @@ extern "C" int dmx_ctx_create(int device, uint64_t max_input, dmx_ctx** out) {
                  ? (uint32_t)ncu : 256u;
     {   // the launch-shape hint (WL_HINT): zero = no encode yet; without it every shape is per block
         void* hp = NULL;
-        if (hipHostMalloc(&hp, 16, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
-            memset(hp, 0, 16);
+        if (hipHostMalloc(&hp, 32, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+            memset(hp, 0, 32);
             c->whint = (volatile uint32_t*)hp;
         }
     }
@@ -4612,17 +4725,20 @@ static void ctx_collect_set(dmx_ctx* c, int j) {
 // the context's previous encode (WL_HINT) listed fewer than half of its blocks there, else a
 // workgroup per block.  DMX_WORKLIST=list / plain forces one shape (tests), =0 turns the
 // work lists off (one workgroup per block, no list builder, no whole copies in K0).
-struct WlShape { bool loop1, list2, list4; };
+struct WlShape { bool loop1, list2, list4, dedupe; };
 static WlShape wl_shape(const dmx_ctx* c) {
-    WlShape w = {false, false, false};
+    WlShape w = {false, false, false, false};
+    const char* dd = getenv("DMX_DEDUPE");   // 1 / 0 forces the uniform-block dedupe on / off (tests)
     const char* e = getenv("DMX_WORKLIST");
-    if (e && !strcmp(e, "list")) return WlShape{true, true, true};
-    if ((e && !strcmp(e, "plain")) || !c->whint) return w;
-    const uint32_t nb = c->whint[0];
-    if (!nb) return w;
-    w.loop1 = 2 * c->whint[1] < nb;
-    w.list2 = 2 * c->whint[2] < nb;
-    w.list4 = 2 * c->whint[3] < nb;
+    if (e && !strcmp(e, "list")) w = WlShape{true, true, true, false};
+    else if (!(e && !strcmp(e, "plain")) && c->whint && c->whint[0]) {
+        const uint32_t nb = c->whint[0];
+        w.loop1 = 2 * c->whint[1] < nb;
+        w.list2 = 2 * c->whint[2] < nb;
+        w.list4 = 2 * c->whint[3] < nb;
+        w.dedupe = 4 * c->whint[4] >= nb;   // a quarter of the blocks were full uniform blocks
+    }
+    if (dd) w.dedupe = atoi(dd) > 0;
     return w;
 }
 
@@ -4654,6 +4770,8 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
     const char* wle = getenv("DMX_WORKLIST");
     uint32_t* wl = ((o.flags & DMX_F_STORE_CHECK) && !(wle && !strcmp(wle, "0"))) ? c->wl : NULL;
     const WlShape wsh = wl_shape(c);
+    // the uniform-block dedupe's rep index per block (NULL: no dedupe in this encode)
+    const uint32_t* dupa = wl && wsh.dedupe && !(o.flags & DMX_F_SPLIT) ? wl_dup(wl, c->cap_blocks) : NULL;
     hipEvent_t* ev = NULL;
     if (c->timing) {
         const int j = (int)(c->ev_next++ % DMX_EV_RING);
@@ -4682,7 +4800,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                                (uint32_t*)d_out, out_cap, wl ? 1u : 0u);
         if (wl)
             hipLaunchKernelGGL(dmx_worklist_kernel, dim3(1), dim3(WLT), 0, s, (const dmx_blkinfo*)c->info, nblk, wl,
-                               (uint64_t)c->cap_blocks);
+                               (uint64_t)c->cap_blocks, (uint32_t)o.sw, dupa ? 1u : 0u);
         if (ev) (void)hipEventRecord(ev[1], s);
         const char* dstop = getenv("DMX_DEBUG_STOP");   // diagnostic only (dbg_stop)
         const uint32_t mfl = ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u) |
@@ -4717,7 +4835,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         else
             hipLaunchKernelGGL(dmx_huff_kernel, dim3(wl && wsh.list2 ? (nblk < 32 * c->ncu ? nblk : 32 * c->ncu) : nblk),
                                dim3(64), 0, s, c->hist, c->info, c->codes, c->hdr, c->sub, nblk, o.flags,
-                               wl && wsh.list2 ? wl : NULL, wl && wsh.list2 ? wl + WL_HDR + c->cap_blocks : NULL);
+                               wl && wsh.list2 ? wl : NULL, wl && wsh.list2 ? wl + WL_HDR + c->cap_blocks : NULL, dupa);
         if (ev) (void)hipEventRecord(ev[3], s);
     } else if (ev) {
         (void)hipEventRecord(ev[1], s);
@@ -4727,18 +4845,22 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
     const uint32_t ntile = (nblk + SCAN_TILE - 1) / SCAN_TILE;
     if (nblk)
         hipLaunchKernelGGL(dmx_scan_tile_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, n, (uint32_t)o.sw,
-                           c->tiles);
+                           c->tiles, dupa, c->sub);
     uint32_t* L4 = wl ? wl + WL_HDR + 2 * c->cap_blocks : NULL;
     hipLaunchKernelGGL(dmx_scan_kernel, dim3(1), dim3(ST), 0, s, c->tiles, nblk, n, o.flags, out_cap,
                        (uint32_t*)d_out, c->res, c->nfb);
     if (nblk)
         hipLaunchKernelGGL(dmx_scan_apply_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, o.flags, c->tiles,
-                           (uint32_t*)d_out, (const dmx_result*)c->res, wl, L4);
+                           (uint32_t*)d_out, (const dmx_result*)c->res, wl, L4, dupa);
     if (ev) (void)hipEventRecord(ev[4], s);
     if (nblk)
         hipLaunchKernelGGL(dmx_pack_kernel, dim3(wl && wsh.list4 ? (nblk < 16 * c->ncu ? nblk : 16 * c->ncu) : nblk),
                            dim3(PT), 0, s, (const uint8_t*)d_in, (uint32_t)o.sw, c->tok, c->codes, c->hdr, c->info, c->sub,
-                           nblk, o.flags, (uint32_t*)d_out, c->res, wl, wl && wsh.list4 ? L4 : NULL);
+                           nblk, o.flags, (uint32_t*)d_out, c->res, wl, wl && wsh.list4 ? L4 : NULL, dupa);
+    if (nblk && dupa)
+        hipLaunchKernelGGL(dmx_dup_copy_kernel, dim3(nblk < 4 * c->ncu ? nblk : 4 * c->ncu), dim3(256), 0, s,
+                           (const dmx_blkinfo*)c->info, (const uint32_t*)wl, (uint64_t)c->cap_blocks, (uint32_t*)d_out,
+                           (const dmx_result*)c->res);
     if (ev) (void)hipEventRecord(ev[5], s);
     HIPCHK(fault_hit(2) ? hipErrorLaunchFailure : hipGetLastError());
     c->last_nblk = nblk;

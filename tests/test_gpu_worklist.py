@@ -127,3 +127,57 @@ def test_worklist_inflate_gpu(enc):
     ix, n = enc.block_index()
     dec, st = D.inflate_gpu(out, len(data), ix, n)
     assert st == 0 and dec.cpu().numpy().tobytes() == data
+
+
+def _uniform_cases():
+    runs = b"".join(bytes([v]) * B for v in (0, 0, 7, 0, 255, 7, 7, 0))
+    return {
+        "zeros": bytes(10 * B),
+        "zeros_tail": bytes(6 * B + 12345),
+        "runs_of_bytes": runs + bytes([9]) * 500,
+        "uniform_in_noise": _noise(2 * B, 21) + bytes(4 * B) + _noise(B, 22) + bytes([65]) * (3 * B) + b"x",
+        "uniform_and_text": bytes(3 * B) + D.gen_text(2 * B, 23).tobytes() + bytes(3 * B) + D.gen_text(B, 24).tobytes(),
+    }
+
+
+@pytest.mark.parametrize("shape", ["list", "plain", None])
+@pytest.mark.parametrize("name", sorted(_uniform_cases()))
+def test_uniform_dedupe_matches_oracle(enc, shape, name):
+    """DMX_DEDUPE=1: full blocks of one byte value (block 1 .. nblk - 2) are coded once per byte
+    value and copied bit for bit to their offsets (dmx_dup_copy_kernel) -- the stream is the
+    oracle's; =0 the same stream without the dedupe."""
+    data = _uniform_cases()[name]
+    fl = D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | D.DMX_F_DEEP
+    want = O.compress(data, max_chain=7, lazy=True, store_check=True, deep=True)
+    old = os.environ.get("DMX_DEDUPE")
+    try:
+        for dd in ("1", "0"):
+            os.environ["DMX_DEDUPE"] = dd
+            z, r = _with_env(shape, lambda: enc.compress_bytes(data, max_chain=7, flags=fl))
+            assert r.status == 0
+            assert z == want, (name, shape, dd, len(z), len(want))
+    finally:
+        if old is None:
+            os.environ.pop("DMX_DEDUPE", None)
+        else:
+            os.environ["DMX_DEDUPE"] = old
+    assert zlib.decompress(z) == data
+
+
+def test_uniform_dedupe_inflate_and_split(enc):
+    data = _uniform_cases()["uniform_in_noise"]
+    old = os.environ.get("DMX_DEDUPE")
+    os.environ["DMX_DEDUPE"] = "1"
+    try:
+        t = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).cuda()
+        out, r = enc.compress_tensor(t, opts=D.Opts(B, 7, D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK, 0))
+        ix, n = enc.block_index()
+        dec, st = D.inflate_gpu(out, len(data), ix, n)
+        assert st == 0 and dec.cpu().numpy().tobytes() == data
+        z, _ = enc.compress_bytes(data, max_chain=7, flags=D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | D.DMX_F_SPLIT)
+        assert z == O.compress(data, max_chain=7, lazy=True, store_check=True, split=True)
+    finally:
+        if old is None:
+            os.environ.pop("DMX_DEDUPE", None)
+        else:
+            os.environ["DMX_DEDUPE"] = old
