@@ -1974,6 +1974,14 @@ __device__ __forceinline__ uint32_t uniform_parse(uint32_t bn, uint32_t c, uint3
 // take the representative's block record in the scan's tile pass and have its bits copied
 // to their offsets by dmx_dup_copy_kernel after K4.
 __host__ __device__ __forceinline__ const uint32_t* wl_dup(const uint32_t* wl, uint64_t cap) { return wl + WL_HDR + 4 * cap; }
+// K0's code per block (u16, after D; cap rounded up to 8): prestored in bits 1:0, bit 2 = a
+// full uniform block with 1 <= b <= nblk - 2 (a dedupe candidate), its byte value in 15:8
+__host__ __device__ __forceinline__ uint16_t* wl_codes(uint32_t* wl, uint64_t cap) {
+    return reinterpret_cast<uint16_t*>(wl + ((WL_HDR + 5 * cap + 3) & ~3ull));   // 16-byte aligned
+}
+__host__ __device__ __forceinline__ const uint16_t* wl_codes(const uint32_t* wl, uint64_t cap) {
+    return reinterpret_cast<const uint16_t*>(wl + ((WL_HDR + 5 * cap + 3) & ~3ull));
+}
 __device__ __forceinline__ void wl_hint_put(const uint32_t* __restrict__ wl, int k, uint32_t v) {
     uint32_t* h = reinterpret_cast<uint32_t*>((uint64_t)wl[WL_HINT] | ((uint64_t)wl[WL_HINT + 1] << 32));
     if (h) __hip_atomic_store(&h[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2020,7 +2028,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
                                                               dmx_blkinfo* __restrict__ info, uint32_t* __restrict__ tok_g,
                                                               uint32_t* __restrict__ hist_g, uint32_t uni_ok, uint32_t flags,
                                                               uint32_t* __restrict__ out32, uint64_t out_cap,
-                                                              uint32_t whole) {
+                                                              uint32_t whole, uint16_t* __restrict__ codes) {
     __shared__ uint32_t bm[1u << 12];   // the 17-bit presence bitmap (16 KB: 8 workgroups per CU)
     __shared__ uint32_t hist[256];
     __shared__ uint64_t red[10][SCT / 64];
@@ -2033,7 +2041,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
     const uint8_t* d = in + off;
     const uint32_t nblk = gridDim.x;
     if (bn < 4096) {
-        if (tid == 0) info[b].prestored = 0;
+        if (tid == 0) { info[b].prestored = 0; if (codes) codes[b] = 0; }
         return;
     }
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
@@ -2066,7 +2074,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
                 ok = ok && 8 * (dv < 0 ? -dv : dv) <= (int64_t)SC_PLANE;
             }
             pass_s = ok ? 1u : 0u;
-            if (!ok) info[b].prestored = 0;
+            if (!ok) { info[b].prestored = 0; if (codes) codes[b] = 0; }
         }
         __syncthreads();
         if (!pass_s) {
@@ -2098,6 +2106,8 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
                 info[b].adl_s = S;
                 info[b].adl_w = (uint64_t)bn * S - T;
                 info[b].prestored = 2;
+                if (codes)   // (a dedupe candidate: full, neither the first block nor the last)
+                    codes[b] = (uint16_t)(2u | ((bn == sw && b >= 1 && b + 2 <= nblk) ? 4u | (c << 8) : 0u));
             }
             __syncthreads();
             for (uint32_t k = tid; k < DMX_HIST; k += SCT) hist_g[(uint64_t)b * DMX_HIST + k] = H[k];
@@ -2205,6 +2215,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
         // the speculative copy (above) when the whole block fits the output at that offset
         const bool spec = sto && (spec_stored_bit(b, sw, flags) >> 3) + (uint64_t)bn + 16 <= out_cap;
         info[b].prestored = sto ? (spec ? 3u : 1u) : 0u;
+        if (codes) codes[b] = (uint16_t)(sto ? (spec ? 3u : 1u) : 0u);
         pass_s = spec ? 1u : 0u;
         if (sto) {
             info[b].ntok = 0;
@@ -2335,65 +2346,67 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
 // offset from a block scan + its count so far.  Also zeroes K1's claim counter and K4's list,
 // and (dedupe) picks each byte value's representative among the full uniform blocks.
 #define WLT 1024
-__device__ __forceinline__ bool wl_uniform_full(const dmx_blkinfo& bi, uint32_t b, uint32_t nblk, uint32_t sw) {
-    return bi.prestored == 2 && bi.n == sw && b >= 1 && b + 2 <= nblk;
-}
-__global__ __launch_bounds__(WLT) void dmx_worklist_kernel(const dmx_blkinfo* __restrict__ info, uint32_t nblk,
-                                                           uint32_t* __restrict__ wl, uint64_t cap, uint32_t sw,
+__global__ __launch_bounds__(WLT) void dmx_worklist_kernel(uint32_t nblk, uint32_t* __restrict__ wl, uint64_t cap,
                                                            uint32_t dedupe) {
     __shared__ uint32_t w1[WLT / 64], w2[WLT / 64], w5[WLT / 64], wm[WLT / 64], rep[256], nuni;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < 256) rep[tid] = 0xFFFFFFFFu;
     if (tid == 0) nuni = 0;
     __syncthreads();
-    uint32_t m = nblk;
-    for (uint32_t b0 = 0; b0 < nblk; b0 += 16 * WLT) {   // 16 loads in flight per thread
-        uint32_t ps[16];
+    // K0's code per block (wl_codes): thread t takes the C consecutive blocks [t C, t C + C),
+    // C a multiple of 8 (one 16-byte load per 8 codes)
+    const uint16_t* K = wl_codes(wl, cap);
+    const uint32_t C = ((nblk + WLT - 1) / WLT + 7) & ~7u;
+    const uint32_t b0 = tid * C, b1 = min(b0 + C, nblk);
+    auto code8 = [&](uint32_t b, uint32_t* k) {   // codes of blocks b .. b + 7 (b a multiple of 8)
+        const uint4 v = *reinterpret_cast<const uint4*>(K + b);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const uint32_t b = b0 + (uint32_t)j * WLT + tid;
-            ps[j] = b < nblk ? info[b].prestored : 3u;
-        }
+        for (int i = 0; i < 8; i++) k[i] = (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+    };
+    uint32_t m = nblk, nu = 0;
+    for (uint32_t b = b0; b < b1; b += 8) {
+        uint32_t k[8];
+        code8(b, k);
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const uint32_t b = b0 + (uint32_t)j * WLT + tid;
-            if (ps[j] != 3 && b < m) m = b;
-            if (dedupe && ps[j] == 2 && b < nblk) {   // the representative: the first block per byte value
-                const dmx_blkinfo bi = info[b];
-                if (wl_uniform_full(bi, b, nblk, sw)) {
-                    atomicMin(&rep[(uint32_t)(bi.adl_s / bi.n) & 0xFFu], b);
-                    atomicAdd(&nuni, 1u);
-                }
+        for (uint32_t i = 0; i < 8; i++) {
+            if (b + i >= b1) break;
+            if ((k[i] & 3u) != 3u) m = min(m, b + i);
+            if (k[i] & 4u) {
+                nu++;
+                if (dedupe) atomicMin(&rep[k[i] >> 8], b + i);
             }
         }
     }
+    if (nu) atomicAdd(&nuni, nu);
     __syncthreads();
     uint32_t* L1 = wl + WL_HDR;
     uint32_t* L2 = L1 + cap;
     uint32_t* L5 = L1 + 3 * cap;
     uint32_t* Dp = L1 + 4 * cap;
-    // per block: 1 = K1 parses it, 2 = K2 codes it, 4 = a dup (of D[b])
-    auto kind = [&](uint32_t b, uint32_t& r) -> uint32_t {
-        const uint32_t ps = info[b].prestored;
+    // per block: 1 = K1 parses it, 2 = K2 codes it, 4 = a dup (of r)
+    auto kind = [&](uint32_t k, uint32_t b, uint32_t& r) -> uint32_t {
         r = 0xFFFFFFFFu;
+        const uint32_t ps = k & 3u;
         if (ps == 0) return 3u;
         if (ps != 2) return 0u;
-        if (dedupe) {
-            const dmx_blkinfo bi = info[b];
-            if (wl_uniform_full(bi, b, nblk, sw)) {
-                const uint32_t rr = rep[(uint32_t)(bi.adl_s / bi.n) & 0xFFu];
-                if (rr != b) { r = rr; return 4u; }
-            }
+        if (dedupe && (k & 4u)) {
+            const uint32_t rr = rep[k >> 8];
+            if (rr != b) { r = rr; return 4u; }
         }
         return 2u;
     };
     uint32_t c1 = 0, c2 = 0, c5 = 0;
-    for (uint32_t b = tid; b < nblk; b += WLT) {
-        uint32_t r;
-        const uint32_t k = kind(b, r);
-        c1 += k & 1u;
-        c2 += (k >> 1) & 1u;
-        c5 += (k >> 2) & 1u;
+    for (uint32_t b = b0; b < b1; b += 8) {
+        uint32_t k[8];
+        code8(b, k);
+#pragma unroll
+        for (uint32_t i = 0; i < 8; i++) {
+            if (b + i >= b1) break;
+            uint32_t r;
+            const uint32_t t = kind(k[i], b + i, r);
+            c1 += t & 1u; c2 += (t >> 1) & 1u; c5 += (t >> 2) & 1u;
+        }
     }
     // exclusive block scans of the three counts, min of m
     const uint32_t i1 = wave_incl_scan(c1), i2 = wave_incl_scan(c2), i5 = wave_incl_scan(c5);
@@ -2411,13 +2424,19 @@ __global__ __launch_bounds__(WLT) void dmx_worklist_kernel(const dmx_blkinfo* __
         t5 += w5[w];
         M = min(M, wm[w]);
     }
-    for (uint32_t b = tid; b < nblk; b += WLT) {   // (the second read of the records: L2 hits)
-        uint32_t r;
-        const uint32_t k = kind(b, r);
-        if (k & 1u) L1[o1++] = b;
-        if (k & 2u) L2[o2++] = b;
-        if (k & 4u) L5[o5++] = b;
-        Dp[b] = r;
+    for (uint32_t b = b0; b < b1; b += 8) {   // (the codes again: L2 hits)
+        uint32_t k[8];
+        code8(b, k);
+#pragma unroll
+        for (uint32_t i = 0; i < 8; i++) {
+            if (b + i >= b1) break;
+            uint32_t r;
+            const uint32_t t = kind(k[i], b + i, r);
+            if (t & 1u) L1[o1++] = b + i;
+            if (t & 2u) L2[o2++] = b + i;
+            if (t & 4u) L5[o5++] = b + i;
+            Dp[b + i] = r;
+        }
     }
     if (tid == 0) {
         wl[WL_N1] = t1;
@@ -4605,7 +4624,7 @@ static int ctx_reserve(dmx_ctx* c, uint64_t nblk) {
     HIPCHK(dmx_malloc(&c->sub, cb * DMX_NSUB * sizeof(dmx_subinfo)));
     HIPCHK(dmx_malloc(&c->info, cb * sizeof(dmx_blkinfo)));
     HIPCHK(dmx_malloc(&c->tiles, (cb / SCAN_TILE + 1) * sizeof(ScanTile)));
-    HIPCHK(dmx_malloc(&c->wl, (WL_HDR + 5 * cb) * sizeof(uint32_t)));
+    HIPCHK(dmx_malloc(&c->wl, (WL_HDR + 5 * cb + 4 + (cb + 16) / 2) * sizeof(uint32_t)));
     {   // the hint's device address in the list header
         uint64_t hp = 0;
         void* dp = NULL;
@@ -4797,10 +4816,10 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         if (o.flags & DMX_F_STORE_CHECK)
             hipLaunchKernelGGL(dmx_store_check_kernel, dim3(nblk), dim3(SCT), 0, s, (const uint8_t*)d_in, n,
                                (uint32_t)o.sw, c->info, c->tok, c->hist, (o.flags & DMX_F_DICT) ? 0u : 1u, o.flags,
-                               (uint32_t*)d_out, out_cap, wl ? 1u : 0u);
+                               (uint32_t*)d_out, out_cap, wl ? 1u : 0u, wl ? wl_codes(wl, c->cap_blocks) : NULL);
         if (wl)
-            hipLaunchKernelGGL(dmx_worklist_kernel, dim3(1), dim3(WLT), 0, s, (const dmx_blkinfo*)c->info, nblk, wl,
-                               (uint64_t)c->cap_blocks, (uint32_t)o.sw, dupa ? 1u : 0u);
+            hipLaunchKernelGGL(dmx_worklist_kernel, dim3(1), dim3(WLT), 0, s, nblk, wl, (uint64_t)c->cap_blocks,
+                               dupa ? 1u : 0u);
         if (ev) (void)hipEventRecord(ev[1], s);
         const char* dstop = getenv("DMX_DEBUG_STOP");   // diagnostic only (dbg_stop)
         const uint32_t mfl = ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u) |
