@@ -1974,6 +1974,8 @@ __device__ __forceinline__ uint32_t uniform_parse(uint32_t bn, uint32_t c, uint3
 // take the representative's block record in the scan's tile pass and have its bits copied
 // to their offsets by dmx_dup_copy_kernel after K4.
 __host__ __device__ __forceinline__ const uint32_t* wl_dup(const uint32_t* wl, uint64_t cap) { return wl + WL_HDR + 4 * cap; }
+// block b is a dup (the worklist kernel set bit 3 of its code; its representative is in D)
+__device__ __forceinline__ bool is_dup(const uint16_t* codes, uint32_t b) { return codes && (codes[b] & 8u); }
 // K0's code per block (u16, after D; cap rounded up to 8): prestored in bits 1:0, bit 2 = a
 // full uniform block with 1 <= b <= nblk - 2 (a dedupe candidate), its byte value in 15:8
 __host__ __device__ __forceinline__ uint16_t* wl_codes(uint32_t* wl, uint64_t cap) {
@@ -2353,29 +2355,24 @@ __global__ __launch_bounds__(WLT) void dmx_worklist_kernel(uint32_t nblk, uint32
     if (tid < 256) rep[tid] = 0xFFFFFFFFu;
     if (tid == 0) nuni = 0;
     __syncthreads();
-    // K0's code per block (wl_codes): thread t takes the C consecutive blocks [t C, t C + C),
-    // C a multiple of 8 (one 16-byte load per 8 codes)
-    const uint16_t* K = wl_codes(wl, cap);
-    const uint32_t C = ((nblk + WLT - 1) / WLT + 7) & ~7u;
-    const uint32_t b0 = tid * C, b1 = min(b0 + C, nblk);
-    auto code8 = [&](uint32_t b, uint32_t* k) {   // codes of blocks b .. b + 7 (b a multiple of 8)
-        const uint4 v = *reinterpret_cast<const uint4*>(K + b);
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    // K0's code per block (wl_codes); thread t takes blocks t, t + WLT, ...: the codes of the
+    // first WLC x WLT blocks (1 GiB of 32 KiB blocks) are loaded together and kept in registers
+    uint16_t* K = wl_codes(wl, cap);
+    constexpr uint32_t WLC = 32;
+    uint32_t kc[WLC];
 #pragma unroll
-        for (int i = 0; i < 8; i++) k[i] = (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-    };
+    for (uint32_t j = 0; j < WLC; j++) {
+        const uint32_t b = j * WLT + tid;
+        kc[j] = b < nblk ? (uint32_t)K[b] : 3u;
+    }
+    auto code = [&](uint32_t j, uint32_t b) -> uint32_t { return j < WLC ? kc[j] : (uint32_t)K[b]; };
     uint32_t m = nblk, nu = 0;
-    for (uint32_t b = b0; b < b1; b += 8) {
-        uint32_t k[8];
-        code8(b, k);
-#pragma unroll
-        for (uint32_t i = 0; i < 8; i++) {
-            if (b + i >= b1) break;
-            if ((k[i] & 3u) != 3u) m = min(m, b + i);
-            if (k[i] & 4u) {
-                nu++;
-                if (dedupe) atomicMin(&rep[k[i] >> 8], b + i);
-            }
+    for (uint32_t j = 0, b = tid; b < nblk; j++, b += WLT) {
+        const uint32_t k = code(j, b);
+        if ((k & 3u) != 3u) m = min(m, b);
+        if (k & 4u) {
+            nu++;
+            if (dedupe) atomicMin(&rep[k >> 8], b);
         }
     }
     if (nu) atomicAdd(&nuni, nu);
@@ -2397,16 +2394,10 @@ __global__ __launch_bounds__(WLT) void dmx_worklist_kernel(uint32_t nblk, uint32
         return 2u;
     };
     uint32_t c1 = 0, c2 = 0, c5 = 0;
-    for (uint32_t b = b0; b < b1; b += 8) {
-        uint32_t k[8];
-        code8(b, k);
-#pragma unroll
-        for (uint32_t i = 0; i < 8; i++) {
-            if (b + i >= b1) break;
-            uint32_t r;
-            const uint32_t t = kind(k[i], b + i, r);
-            c1 += t & 1u; c2 += (t >> 1) & 1u; c5 += (t >> 2) & 1u;
-        }
+    for (uint32_t j = 0, b = tid; b < nblk; j++, b += WLT) {
+        uint32_t r;
+        const uint32_t t = kind(code(j, b), b, r);
+        c1 += t & 1u; c2 += (t >> 1) & 1u; c5 += (t >> 2) & 1u;
     }
     // exclusive block scans of the three counts, min of m
     const uint32_t i1 = wave_incl_scan(c1), i2 = wave_incl_scan(c2), i5 = wave_incl_scan(c5);
@@ -2424,18 +2415,15 @@ __global__ __launch_bounds__(WLT) void dmx_worklist_kernel(uint32_t nblk, uint32
         t5 += w5[w];
         M = min(M, wm[w]);
     }
-    for (uint32_t b = b0; b < b1; b += 8) {   // (the codes again: L2 hits)
-        uint32_t k[8];
-        code8(b, k);
-#pragma unroll
-        for (uint32_t i = 0; i < 8; i++) {
-            if (b + i >= b1) break;
-            uint32_t r;
-            const uint32_t t = kind(k[i], b + i, r);
-            if (t & 1u) L1[o1++] = b + i;
-            if (t & 2u) L2[o2++] = b + i;
-            if (t & 4u) L5[o5++] = b + i;
-            Dp[b + i] = r;
+    for (uint32_t j = 0, b = tid; b < nblk; j++, b += WLT) {
+        uint32_t r;
+        const uint32_t k = code(j, b), t = kind(k, b, r);
+        if (t & 1u) L1[o1++] = b;
+        if (t & 2u) L2[o2++] = b;
+        if (t & 4u) {   // a dup: its representative, and bit 3 of its code (what the kernels test)
+            L5[o5++] = b;
+            Dp[b] = r;
+            K[b] = (uint16_t)(k | 8u);
         }
     }
     if (tid == 0) {
@@ -3617,9 +3605,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void dm
                                                       uint32_t* __restrict__ codes_g, uint32_t* __restrict__ hdr_g,
                                                       dmx_subinfo* __restrict__ sub_g, uint32_t nblk, uint32_t flags,
                                                       const uint32_t* __restrict__ wl, const uint32_t* __restrict__ L2,
-                                                      const uint32_t* __restrict__ dup) {
+                                                      const uint16_t* __restrict__ codes) {
     if (!L2) {   // a workgroup per block; dups (uniform-block dedupe) take their representative's coding
-        if (dup && dup[blockIdx.x] != 0xFFFFFFFFu) return;
+        if (is_dup(codes, blockIdx.x)) return;
         huff_one(blockIdx.x, hist_g, info, codes_g, hdr_g, sub_g, nblk, flags);
         return;
     }
@@ -3931,6 +3919,7 @@ __device__ __forceinline__ Mono blk_elem(const dmx_blkinfo& bi) {
 
 __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_tile_kernel(dmx_blkinfo* __restrict__ info, uint32_t nblk,
                                                                  uint64_t n, uint32_t sw, ScanTile* __restrict__ tiles,
+                                                                 const uint16_t* __restrict__ codes,
                                                                  const uint32_t* __restrict__ dup,
                                                                  dmx_subinfo* __restrict__ sub_g) {
     __shared__ Mono wtot[SCAN_TILE / 64];
@@ -3941,8 +3930,8 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_tile_kernel(dmx_blkinfo* _
     uint64_t s1 = 0, s2 = 0, nt = 0, ns = 0, nf = 0;
     if (b < nblk) {
         dmx_blkinfo bi = info[b];
-        const uint32_t r = dup ? dup[b] : 0xFFFFFFFFu;
-        if (r != 0xFFFFFFFFu) {   // a dup (uniform-block dedupe): the representative's coding
+        if (is_dup(codes, b)) {   // a dup (uniform-block dedupe): the representative's coding
+            const uint32_t r = dup[b];
             const dmx_blkinfo ri = info[r];
             bi.btype = ri.btype;
             bi.hdr_bits = ri.hdr_bits;
@@ -4111,7 +4100,7 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply_kernel(dmx_blkinfo* 
                                                                   uint32_t* __restrict__ out32,
                                                                   const dmx_result* __restrict__ res,
                                                                   uint32_t* __restrict__ wl, uint32_t* __restrict__ L4,
-                                                                  const uint32_t* __restrict__ dup) {
+                                                                  const uint16_t* __restrict__ codes) {
     if (res->status) return;
     const uint32_t b = blockIdx.x * SCAN_TILE + threadIdx.x;
     if (b >= nblk) return;
@@ -4149,7 +4138,7 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply_kernel(dmx_blkinfo* 
     } else {
         out32[w1] = 0;
     }
-    if (dup && dup[b] != 0xFFFFFFFFu) return;   // packed by dmx_dup_copy_kernel
+    if (is_dup(codes, b)) return;   // packed by dmx_dup_copy_kernel
     L4[atomicAdd(&wl[WL_N4], 1u)] = b;
 }
 
@@ -4423,10 +4412,10 @@ __global__ __launch_bounds__(PT) void dmx_pack_kernel(const uint8_t* __restrict_
                                                       uint32_t nblk, uint32_t flags, uint32_t* __restrict__ out32,
                                                       dmx_result* __restrict__ res,
                                                       const uint32_t* __restrict__ wl, const uint32_t* __restrict__ L4,
-                                                      const uint32_t* __restrict__ dup) {
+                                                      const uint16_t* __restrict__ codes) {
     if (!L4) {   // a workgroup per block; with work lists, the whole-copy prefix returns at once
         if (wl && wl_skip(blockIdx.x, wl[WL_M], nblk)) return;
-        if (dup && dup[blockIdx.x] != 0xFFFFFFFFu) return;   // dmx_dup_copy_kernel's
+        if (is_dup(codes, blockIdx.x)) return;   // dmx_dup_copy_kernel's
         pack_one(blockIdx.x, in, sw, tok_g, codes_g, hdr_g, info, sub_g, nblk, flags, out32, res);
         if (wl && blockIdx.x == 0 && threadIdx.x == 0) wl_hint_put(wl, 3, wl[WL_N4]);
         return;
@@ -4790,7 +4779,9 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
     uint32_t* wl = ((o.flags & DMX_F_STORE_CHECK) && !(wle && !strcmp(wle, "0"))) ? c->wl : NULL;
     const WlShape wsh = wl_shape(c);
     // the uniform-block dedupe's rep index per block (NULL: no dedupe in this encode)
-    const uint32_t* dupa = wl && wsh.dedupe && !(o.flags & DMX_F_SPLIT) ? wl_dup(wl, c->cap_blocks) : NULL;
+    const bool dedupe = wl && wsh.dedupe && !(o.flags & DMX_F_SPLIT);
+    const uint16_t* dupk = dedupe ? wl_codes((const uint32_t*)wl, c->cap_blocks) : NULL;   // dup bits (bit 3)
+    const uint32_t* dupa = dedupe ? wl_dup(wl, c->cap_blocks) : NULL;                      // their representatives
     hipEvent_t* ev = NULL;
     if (c->timing) {
         const int j = (int)(c->ev_next++ % DMX_EV_RING);
@@ -4854,7 +4845,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         else
             hipLaunchKernelGGL(dmx_huff_kernel, dim3(wl && wsh.list2 ? (nblk < 32 * c->ncu ? nblk : 32 * c->ncu) : nblk),
                                dim3(64), 0, s, c->hist, c->info, c->codes, c->hdr, c->sub, nblk, o.flags,
-                               wl && wsh.list2 ? wl : NULL, wl && wsh.list2 ? wl + WL_HDR + c->cap_blocks : NULL, dupa);
+                               wl && wsh.list2 ? wl : NULL, wl && wsh.list2 ? wl + WL_HDR + c->cap_blocks : NULL, dupk);
         if (ev) (void)hipEventRecord(ev[3], s);
     } else if (ev) {
         (void)hipEventRecord(ev[1], s);
@@ -4864,18 +4855,18 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
     const uint32_t ntile = (nblk + SCAN_TILE - 1) / SCAN_TILE;
     if (nblk)
         hipLaunchKernelGGL(dmx_scan_tile_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, n, (uint32_t)o.sw,
-                           c->tiles, dupa, c->sub);
+                           c->tiles, dupk, dupa, c->sub);
     uint32_t* L4 = wl ? wl + WL_HDR + 2 * c->cap_blocks : NULL;
     hipLaunchKernelGGL(dmx_scan_kernel, dim3(1), dim3(ST), 0, s, c->tiles, nblk, n, o.flags, out_cap,
                        (uint32_t*)d_out, c->res, c->nfb);
     if (nblk)
         hipLaunchKernelGGL(dmx_scan_apply_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, o.flags, c->tiles,
-                           (uint32_t*)d_out, (const dmx_result*)c->res, wl, L4, dupa);
+                           (uint32_t*)d_out, (const dmx_result*)c->res, wl, L4, dupk);
     if (ev) (void)hipEventRecord(ev[4], s);
     if (nblk)
         hipLaunchKernelGGL(dmx_pack_kernel, dim3(wl && wsh.list4 ? (nblk < 16 * c->ncu ? nblk : 16 * c->ncu) : nblk),
                            dim3(PT), 0, s, (const uint8_t*)d_in, (uint32_t)o.sw, c->tok, c->codes, c->hdr, c->info, c->sub,
-                           nblk, o.flags, (uint32_t*)d_out, c->res, wl, wl && wsh.list4 ? L4 : NULL, dupa);
+                           nblk, o.flags, (uint32_t*)d_out, c->res, wl, wl && wsh.list4 ? L4 : NULL, dupk);
     if (nblk && dupa)
         hipLaunchKernelGGL(dmx_dup_copy_kernel, dim3(nblk < 4 * c->ncu ? nblk : 4 * c->ncu), dim3(256), 0, s,
                            (const dmx_blkinfo*)c->info, (const uint32_t*)wl, (uint64_t)c->cap_blocks, (uint32_t*)d_out,
