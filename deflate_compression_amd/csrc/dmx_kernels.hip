@@ -1976,8 +1976,9 @@ __device__ __forceinline__ uint32_t uniform_parse(uint32_t bn, uint32_t c, uint3
 __host__ __device__ __forceinline__ const uint32_t* wl_dup(const uint32_t* wl, uint64_t cap) { return wl + WL_HDR + 4 * cap; }
 // block b is a dup (the worklist kernel set bit 3 of its code; its representative is in D)
 __device__ __forceinline__ bool is_dup(const uint16_t* codes, uint32_t b) { return codes && (codes[b] & 8u); }
-// K0's code per block (u16, after D; cap rounded up to 8): prestored in bits 1:0, bit 2 = a
-// full uniform block with 1 <= b <= nblk - 2 (a dedupe candidate), its byte value in 15:8
+// The code per block (u16, after D; written by the worklist kernel from K0's prestored):
+// prestored in bits 1:0, bit 2 = a full uniform block with 1 <= b <= nblk - 2 (a dedupe
+// candidate), its byte value in 15:8, bit 3 = a dup
 __host__ __device__ __forceinline__ uint16_t* wl_codes(uint32_t* wl, uint64_t cap) {
     return reinterpret_cast<uint16_t*>(wl + ((WL_HDR + 5 * cap + 3) & ~3ull));   // 16-byte aligned
 }
@@ -2026,16 +2027,20 @@ __device__ __forceinline__ void stored_quads(uint64_t O, uint32_t bn, bool dal, 
         if (o0 >= 0 && (uint64_t)((o0 & ~3ll) + 20) <= bn) f(k, o0);
     }
 }
+// SPEC (work-list mode, when most blocks were stored in the previous encode): a full block's
+// eight chunks per thread are loaded before pass 0 decides anything, so the block's whole
+// input is in flight during pass 0's test and barriers; otherwise (text: pass 0 rejects the
+// block) they are loaded only for blocks that pass it.
+template <bool SPEC>
 __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
                                                               dmx_blkinfo* __restrict__ info, uint32_t* __restrict__ tok_g,
                                                               uint32_t* __restrict__ hist_g, uint32_t uni_ok, uint32_t flags,
                                                               uint32_t* __restrict__ out32, uint64_t out_cap,
-                                                              uint32_t whole, uint16_t* __restrict__ codes) {
+                                                              uint32_t unused_) {
     __shared__ uint32_t bm[1u << 12];   // the 17-bit presence bitmap (16 KB: 8 workgroups per CU)
     __shared__ uint32_t hist[256];
     __shared__ uint64_t red[10][SCT / 64];
     __shared__ uint32_t pass_s;
-    __shared__ uint32_t edge[32];   // the whole copy: the block's first and last 64 bytes (full blocks)
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t b = blockIdx.x;
     const uint64_t off = (uint64_t)b * sw;
@@ -2043,14 +2048,29 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
     const uint8_t* d = in + off;
     const uint32_t nblk = gridDim.x;
     if (bn < 4096) {
-        if (tid == 0) { info[b].prestored = 0; if (codes) codes[b] = 0; }
+        if (tid == 0) info[b].prestored = 0;
         return;
     }
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
+    const bool full = aligned16 && bn == SCT * 16 * 8;
+    uint4 v[8];
+    uint32_t nx[8];
+    if (SPEC && full) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t p = (tid + i * SCT) << 4;
+            v[i] = *reinterpret_cast<const uint4*>(d + p);
+            nx[i] = p + 16 < bn ? *reinterpret_cast<const uint32_t*>(d + p + 16) : 0u;
+        }
+    }
     // ---- pass 0: bit planes of the first 4096 bytes, one 16-byte load per thread ----
     {
         uint32_t w[5];
-        sc_load(d, tid << 4, bn, aligned16, w);
+        if (SPEC && full) {   // chunk tid is v[0]
+            w[0] = v[0].x; w[1] = v[0].y; w[2] = v[0].z; w[3] = v[0].w; w[4] = nx[0];
+        } else {
+            sc_load(d, tid << 4, bn, aligned16, w);
+        }
         uint32_t ones[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) {
@@ -2076,7 +2096,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
                 ok = ok && 8 * (dv < 0 ? -dv : dv) <= (int64_t)SC_PLANE;
             }
             pass_s = ok ? 1u : 0u;
-            if (!ok) { info[b].prestored = 0; if (codes) codes[b] = 0; }
+            if (!ok) info[b].prestored = 0;
         }
         __syncthreads();
         if (!pass_s) {
@@ -2107,9 +2127,9 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
                 info[b].n = bn;
                 info[b].adl_s = S;
                 info[b].adl_w = (uint64_t)bn * S - T;
-                info[b].prestored = 2;
-                if (codes)   // (a dedupe candidate: full, neither the first block nor the last)
-                    codes[b] = (uint16_t)(2u | ((bn == sw && b >= 1 && b + 2 <= nblk) ? 4u | (c << 8) : 0u));
+                // 2, and for a full block that is neither the first nor the last (a dedupe
+                // candidate, the work lists) bit 2 and its byte value in bits 15:8
+                info[b].prestored = 2u | ((bn == sw && b >= 1 && b + 2 <= nblk) ? 4u | (c << 8) : 0u);
             }
             __syncthreads();
             for (uint32_t k = tid; k < DMX_HIST; k += SCT) hist_g[(uint64_t)b * DMX_HIST + k] = H[k];
@@ -2130,24 +2150,21 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
     };
     // full 32 KiB block: all loads in flight at once, and the data stays in registers for
     // pass 2 (w4: the 4 bytes after each chunk, for the 4-grams that straddle it)
-    const bool full = aligned16 && bn == SCT * 16 * 8;
-    uint4 v[8];
-    uint32_t nx[8];
     if (full) {
+        if (!SPEC) {
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const uint32_t p = (tid + i * SCT) << 4;
-            v[i] = *reinterpret_cast<const uint4*>(d + p);
-            nx[i] = p + 16 < bn ? *reinterpret_cast<const uint32_t*>(d + p + 16) : 0u;
+            for (int i = 0; i < 8; i++) {
+                const uint32_t p = (tid + i * SCT) << 4;
+                v[i] = *reinterpret_cast<const uint4*>(d + p);
+                nx[i] = p + 16 < bn ? *reinterpret_cast<const uint32_t*>(d + p + 16) : 0u;
+            }
         }
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
             chunk1((tid + i * SCT) << 4, w);
         }
-        // the first 4 and the last 4 chunks for the whole copy (published by pass 2's barrier)
-        if (whole && tid < 4) reinterpret_cast<uint4*>(edge)[tid] = v[0];
-        if (whole && tid >= SCT - 4) reinterpret_cast<uint4*>(edge)[4 + tid - (SCT - 4)] = v[7];
+
     } else {
         for (uint32_t p = tid << 4; p < bn; p += SCT << 4) {
             uint32_t w[5];
@@ -2217,7 +2234,6 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
         // the speculative copy (above) when the whole block fits the output at that offset
         const bool spec = sto && (spec_stored_bit(b, sw, flags) >> 3) + (uint64_t)bn + 16 <= out_cap;
         info[b].prestored = sto ? (spec ? 3u : 1u) : 0u;
-        if (codes) codes[b] = (uint16_t)(sto ? (spec ? 3u : 1u) : 0u);
         pass_s = spec ? 1u : 0u;
         if (sto) {
             info[b].ntok = 0;
@@ -2285,62 +2301,6 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
             *reinterpret_cast<uint4*>(&out32[(O >> 5) + k]) = v;
         });
     }
-    if (pass_s && whole && b >= 1 && b + 1 < nblk) {
-        // the whole copy (work-list mode): every other byte of the block at its speculative
-        // offset too -- the header byte (BFINAL 0, BTYPE 00), LEN / NLEN, the words before and
-        // after the quads, any of the first two and last two quads that did not take the
-        // 20-byte fast path (as the pack kernel's stored path builds them); its two edge words
-        // by byte stores of its own bytes only (the neighbours' bytes share those words)
-        const uint64_t O = spec_stored_bit(b, sw, flags);
-        const uint32_t s0 = (uint32_t)(O & 31), P = (s0 + 3 + 7) & ~7u, B0 = (P + 32) >> 3;
-        const uint32_t nwords = (uint32_t)(((uint64_t)P + 32 + 8ull * bn + 31) >> 5);
-        const uint32_t ebyte = B0 + bn;   // the block's end, in bytes from word O >> 5
-        const uint64_t gw0 = O >> 5;
-        const bool dal = (reinterpret_cast<uintptr_t>(d) & 3) == 0;
-        const uint32_t ks = 4 - (uint32_t)(gw0 & 3);
-        const uint32_t nq = ((full || dal) && nwords > ks + 1) ? (nwords - 1 - ks) >> 2 : 0;
-        const uint32_t lenw = (bn & 0xFFFFu) | ((~bn & 0xFFFFu) << 16);
-        const uint8_t* e8 = reinterpret_cast<const uint8_t*>(edge);
-        auto gen_byte = [&](uint32_t q) -> uint32_t {
-            if (q >= B0) {   // (every byte the copy needs here is within 64 of an end)
-                const uint32_t i = q - B0;
-                if (i >= bn) return 0u;
-                if (full && i < 64) return e8[i];
-                if (full && i >= bn - 64) return e8[64 + i - (bn - 64)];
-                return (uint32_t)d[i];
-            }
-            if (q >= (P >> 3)) return (lenw >> (8 * (q - (P >> 3)))) & 0xFFu;
-            return 0u;   // the header byte (and the previous block's bytes below it: not written)
-        };
-        uint8_t* out8 = reinterpret_cast<uint8_t*>(out32 + gw0);
-        auto put_word = [&](uint32_t k) {
-            if (k == 0 || k == nwords - 1) {
-                for (uint32_t q = 4 * k; q < 4 * k + 4; q++)
-                    if (q >= (s0 >> 3) && q < ebyte) out8[q] = (uint8_t)gen_byte(q);
-            } else {
-                uint32_t v = 0;
-                for (uint32_t i = 0; i < 4; i++) v |= gen_byte(4 * k + i) << (8 * i);
-                out32[gw0 + k] = v;
-            }
-        };
-        auto fast = [&](uint32_t j) {
-            const int64_t o0 = (int64_t)(4 * (ks + 4 * j)) - (int64_t)B0;
-            return o0 >= 0 && (uint64_t)((o0 & ~3ll) + 20) <= bn;
-        };
-        const uint32_t kq = nq ? ks + 4 * nq : 0;
-        const uint32_t nrest = nq ? ks + (nwords - kq) : nwords;   // words outside the quads
-        for (uint32_t r = tid; r < nrest + 16; r += SCT) {
-            if (r < nrest) {
-                put_word(nq ? (r < ks ? r : kq + (r - ks)) : r);
-            } else {   // quads 0, 1, nq - 2, nq - 1 (each once) that are not fast
-                const uint32_t t = r - nrest, qi = t >> 2;
-                if (qi >= nq || (nq >= 4 ? false : qi >= nq)) continue;
-                const uint32_t j = qi < 2 ? qi : nq - 4 + qi;
-                if ((qi >= 2 && (nq < 4 || j < 2)) || fast(j)) continue;
-                put_word(ks + 4 * j + (t & 3));
-            }
-        }
-    }
 }
 
 // The work lists from K0's prestored values (one workgroup; thread t takes blocks t, t + WLT,
@@ -2348,31 +2308,35 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
 // offset from a block scan + its count so far.  Also zeroes K1's claim counter and K4's list,
 // and (dedupe) picks each byte value's representative among the full uniform blocks.
 #define WLT 1024
-__global__ __launch_bounds__(WLT) void dmx_worklist_kernel(uint32_t nblk, uint32_t* __restrict__ wl, uint64_t cap,
-                                                           uint32_t dedupe) {
+__global__ __launch_bounds__(WLT) void dmx_worklist_kernel(const dmx_blkinfo* __restrict__ info, uint32_t nblk,
+                                                           uint32_t* __restrict__ wl, uint64_t cap, uint32_t dedupe) {
     __shared__ uint32_t w1[WLT / 64], w2[WLT / 64], w5[WLT / 64], wm[WLT / 64], rep[256], nuni;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < 256) rep[tid] = 0xFFFFFFFFu;
     if (tid == 0) nuni = 0;
     __syncthreads();
-    // K0's code per block (wl_codes); thread t takes blocks t, t + WLT, ...: the codes of the
-    // first WLC x WLT blocks (1 GiB of 32 KiB blocks) are loaded together and kept in registers
+    // K0's prestored per block (its low 16 bits: the code); thread t takes blocks t, t + WLT,
+    // ...: the codes of the first WLC x WLT blocks (1 GiB of 32 KiB blocks) are loaded together
+    // and kept in registers
     uint16_t* K = wl_codes(wl, cap);
     constexpr uint32_t WLC = 32;
     uint32_t kc[WLC];
 #pragma unroll
     for (uint32_t j = 0; j < WLC; j++) {
         const uint32_t b = j * WLT + tid;
-        kc[j] = b < nblk ? (uint32_t)K[b] : 3u;
+        kc[j] = b < nblk ? info[b].prestored & 0xFFF7u : 3u;
     }
-    auto code = [&](uint32_t j, uint32_t b) -> uint32_t { return j < WLC ? kc[j] : (uint32_t)K[b]; };
-    uint32_t m = nblk, nu = 0;
+    auto code = [&](uint32_t j, uint32_t b) -> uint32_t { return j < WLC ? kc[j] : info[b].prestored & 0xFFF7u; };
+    uint32_t m = nblk, nu = 0, lastc = 0xFFFFFFFFu;
     for (uint32_t j = 0, b = tid; b < nblk; j++, b += WLT) {
         const uint32_t k = code(j, b);
         if ((k & 3u) != 3u) m = min(m, b);
         if (k & 4u) {
             nu++;
-            if (dedupe) atomicMin(&rep[k >> 8], b);
+            // this thread's blocks ascend: its first block of a byte value is its candidate
+            // (one LDS atomic per run of one value, not per block: 32 768 blocks of zeros)
+            if (dedupe && (k >> 8) != lastc) atomicMin(&rep[k >> 8], b);
+            lastc = k >> 8;
         }
     }
     if (nu) atomicAdd(&nuni, nu);
@@ -2423,8 +2387,8 @@ __global__ __launch_bounds__(WLT) void dmx_worklist_kernel(uint32_t nblk, uint32
         if (t & 4u) {   // a dup: its representative, and bit 3 of its code (what the kernels test)
             L5[o5++] = b;
             Dp[b] = r;
-            K[b] = (uint16_t)(k | 8u);
         }
+        K[b] = (uint16_t)(k | ((t & 4u) ? 8u : 0u));
     }
     if (tid == 0) {
         wl[WL_N1] = t1;
@@ -2440,37 +2404,86 @@ __global__ __launch_bounds__(WLT) void dmx_worklist_kernel(uint32_t nblk, uint32
     }
 }
 
-// After K4 (dedupe): every dup block gets its representative's bit string at its own offset,
-// one wave per dup: output word k of the dup holds the representative's bits shifted by the
-// two offsets' difference, masked to the dup's own bits (its two edge words, shared with its
-// neighbours and zeroed by the apply launch, by atomicOr).  The representative is complete:
-// K4 packed it in the previous launch.
-__global__ __launch_bounds__(256) void dmx_dup_copy_kernel(const dmx_blkinfo* __restrict__ info,
-                                                           const uint32_t* __restrict__ wl, uint64_t cap,
-                                                           uint32_t* __restrict__ out32, const dmx_result* __restrict__ res) {
+// After K4 (work-list mode), a wave per block, the blocks K4 skipped:
+//  * a dup (uniform-block dedupe) gets its representative's bit string: output word k of the
+//    dup holds the representative's bits shifted by the two offsets' difference, masked to
+//    the dup's own bits (its two edge words, shared with its neighbours and zeroed by the
+//    apply launch, by atomicOr).  The representative is complete: K4 packed it;
+//  * a block of the stored prefix (wl_skip) gets the bytes K0's speculative copy left out:
+//    the header byte (BFINAL 0, BTYPE 00), LEN / NLEN, the words before and after its 16-byte
+//    quads, any of the first two and last two quads that did not take the 20-byte fast path
+//    (as the pack kernel's stored path builds them); its two edge words by byte stores of its
+//    own bytes (the neighbours' bytes share those words and the apply launch left them).
+__global__ __launch_bounds__(256) void dmx_fill_kernel(const uint8_t* __restrict__ in, uint32_t sw, uint32_t flags,
+                                                       const dmx_blkinfo* __restrict__ info,
+                                                       const uint32_t* __restrict__ wl, uint64_t cap, uint32_t nblk,
+                                                       uint32_t* __restrict__ out32, const dmx_result* __restrict__ res,
+                                                       uint32_t dedupe) {
     if (res->status) return;
-    const uint32_t* L5 = wl + WL_HDR + 3 * cap;
-    const uint32_t* Dp = wl_dup(wl, cap);
-    const uint32_t cnt = wl[WL_N5];
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < cnt; i += nw) {
-        const uint32_t b = L5[i], r = Dp[b];
+    const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (b >= nblk) return;
+    if (dedupe && (wl_codes(wl, cap)[b] & 8u)) {   // a dup
+        const uint32_t r = wl_dup(wl, cap)[b];
         const uint64_t Ob = info[b].off_bits, Or = info[r].off_bits, Lb = info[b].len_bits;
         const uint64_t gw0 = Ob >> 5;
         const uint32_t nwords = (uint32_t)(((Ob & 31) + Lb + 31) >> 5);
         for (uint32_t k = lane; k < nwords; k += 64) {
-            const uint64_t lo = 32 * (gw0 + k), hi = lo + 32;               // the word's bits
+            const uint64_t lo = 32 * (gw0 + k), hi = lo + 32;                         // the word's bits
             const uint64_t a = lo > Ob ? lo : Ob, e = hi < Ob + Lb ? hi : Ob + Lb;   // its bits of the dup
-            const uint64_t q = a - Ob + Or;                                  // their source bit
+            const uint64_t q = a - Ob + Or;                                            // their source bit
             const uint64_t qw = q >> 5;
             const uint32_t sh = (uint32_t)(q & 31);
             const uint64_t src = (uint64_t)out32[qw] | ((uint64_t)out32[qw + 1] << 32);
             const uint32_t nb = (uint32_t)(e - a);
-            const uint64_t bits = (src >> sh) & (nb >= 64 ? ~0ull : ((1ull << nb) - 1ull));
+            const uint64_t bits = (src >> sh) & ((1ull << nb) - 1ull);
             const uint32_t v = (uint32_t)(bits << (a - lo));
             if (nb == 32) out32[gw0 + k] = v;
             else atomicOr(&out32[gw0 + k], v);
+        }
+        return;
+    }
+    if (!wl_skip(b, wl[WL_M], nblk)) return;
+    // a block of the stored prefix: full (not the last block), at its speculative offset
+    const uint8_t* d = in + (uint64_t)b * sw;
+    const uint32_t bn = sw;
+    const uint64_t O = spec_stored_bit(b, sw, flags);
+    const uint32_t s0 = (uint32_t)(O & 31), P = (s0 + 3 + 7) & ~7u, B0 = (P + 32) >> 3;
+    const uint32_t nwords = (uint32_t)(((uint64_t)P + 32 + 8ull * bn + 31) >> 5);
+    const uint32_t ebyte = B0 + bn;   // the block's end, in bytes from word O >> 5
+    const uint64_t gw0 = O >> 5;
+    const bool dal = (reinterpret_cast<uintptr_t>(d) & 3) == 0;
+    const uint32_t ks = 4 - (uint32_t)(gw0 & 3);
+    const uint32_t nq = (dal && nwords > ks + 1) ? (nwords - 1 - ks) >> 2 : 0;   // K0's quads (as its copy)
+    const uint32_t lenw = (bn & 0xFFFFu) | ((~bn & 0xFFFFu) << 16);
+    auto gen_byte = [&](uint32_t q) -> uint32_t {
+        if (q >= B0) return (q - B0) < bn ? (uint32_t)d[q - B0] : 0u;
+        if (q >= (P >> 3)) return (lenw >> (8 * (q - (P >> 3)))) & 0xFFu;
+        return 0u;   // the header byte (and the previous block's bytes below it: not written)
+    };
+    uint8_t* out8 = reinterpret_cast<uint8_t*>(out32 + gw0);
+    auto put_word = [&](uint32_t k) {
+        if (k == 0 || k == nwords - 1) {
+            for (uint32_t q = 4 * k; q < 4 * k + 4; q++)
+                if (q >= (s0 >> 3) && q < ebyte) out8[q] = (uint8_t)gen_byte(q);
+        } else {
+            uint32_t v = 0;
+            for (uint32_t i = 0; i < 4; i++) v |= gen_byte(4 * k + i) << (8 * i);
+            out32[gw0 + k] = v;
+        }
+    };
+    auto fast = [&](uint32_t j) {
+        const int64_t o0 = (int64_t)(4 * (ks + 4 * j)) - (int64_t)B0;
+        return o0 >= 0 && (uint64_t)((o0 & ~3ll) + 20) <= bn;
+    };
+    const uint32_t kq = nq ? ks + 4 * nq : 0;
+    const uint32_t nrest = nq ? ks + (nwords - kq) : nwords;   // words outside the quads
+    for (uint32_t r = lane; r < nrest + 16; r += 64) {
+        if (r < nrest) {
+            put_word(nq ? (r < ks ? r : kq + (r - ks)) : r);
+        } else if (nq >= 4) {   // quads 0, 1, nq - 2, nq - 1 that are not fast
+            const uint32_t t = r - nrest, qi = t >> 2;
+            const uint32_t j = qi < 2 ? qi : nq - 4 + qi;
+            if (!fast(j)) put_word(ks + 4 * j + (t & 3));
         }
     }
 }
@@ -4733,14 +4746,22 @@ static void ctx_collect_set(dmx_ctx* c, int j) {
 // the context's previous encode (WL_HINT) listed fewer than half of its blocks there, else a
 // workgroup per block.  DMX_WORKLIST=list / plain forces one shape (tests), =0 turns the
 // work lists off (one workgroup per block, no list builder, no whole copies in K0).
-struct WlShape { bool loop1, list2, list4, dedupe; };
+struct WlShape { bool loop1, list2, list4, dedupe; uint32_t n2, n4; };
+// a list kernel's grid: the previous encode's list length (a guess: the kernels stride over
+// the list whatever its length), within [lo, hi] and at most nblk
+static uint32_t list_grid(uint32_t nblk, uint32_t prev, uint32_t lo, uint32_t hi) {
+    uint32_t g = prev < lo ? lo : (prev > hi ? hi : prev);
+    return g < nblk ? g : nblk;
+}
 static WlShape wl_shape(const dmx_ctx* c) {
-    WlShape w = {false, false, false, false};
+    WlShape w = {false, false, false, false, ~0u, ~0u};
     const char* dd = getenv("DMX_DEDUPE");   // 1 / 0 forces the uniform-block dedupe on / off (tests)
     const char* e = getenv("DMX_WORKLIST");
-    if (e && !strcmp(e, "list")) w = WlShape{true, true, true, false};
+    if (e && !strcmp(e, "list")) w = WlShape{true, true, true, false, ~0u, ~0u};
     else if (!(e && !strcmp(e, "plain")) && c->whint && c->whint[0]) {
         const uint32_t nb = c->whint[0];
+        w.n2 = c->whint[2];   // the list grids are sized by the previous encode's lists
+        w.n4 = c->whint[3];
         w.loop1 = 2 * c->whint[1] < nb;
         w.list2 = 2 * c->whint[2] < nb;
         w.list4 = 2 * c->whint[3] < nb;
@@ -4805,12 +4826,13 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         }
         // stage 0 also holds K0, the noise check (DMX_F_STORE_CHECK)
         if (o.flags & DMX_F_STORE_CHECK)
-            hipLaunchKernelGGL(dmx_store_check_kernel, dim3(nblk), dim3(SCT), 0, s, (const uint8_t*)d_in, n,
+            hipLaunchKernelGGL(wl && wsh.loop1 ? dmx_store_check_kernel<true> : dmx_store_check_kernel<false>, dim3(nblk),
+                               dim3(SCT), 0, s, (const uint8_t*)d_in, n,
                                (uint32_t)o.sw, c->info, c->tok, c->hist, (o.flags & DMX_F_DICT) ? 0u : 1u, o.flags,
-                               (uint32_t*)d_out, out_cap, wl ? 1u : 0u, wl ? wl_codes(wl, c->cap_blocks) : NULL);
+                               (uint32_t*)d_out, out_cap, 0u);
         if (wl)
-            hipLaunchKernelGGL(dmx_worklist_kernel, dim3(1), dim3(WLT), 0, s, nblk, wl, (uint64_t)c->cap_blocks,
-                               dupa ? 1u : 0u);
+            hipLaunchKernelGGL(dmx_worklist_kernel, dim3(1), dim3(WLT), 0, s, (const dmx_blkinfo*)c->info, nblk, wl,
+                               (uint64_t)c->cap_blocks, dupa ? 1u : 0u);
         if (ev) (void)hipEventRecord(ev[1], s);
         const char* dstop = getenv("DMX_DEBUG_STOP");   // diagnostic only (dbg_stop)
         const uint32_t mfl = ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u) |
@@ -4843,7 +4865,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                                    c->info, c->codes, c->hdr, c->sub, nblk, o.flags);
             }
         else
-            hipLaunchKernelGGL(dmx_huff_kernel, dim3(wl && wsh.list2 ? (nblk < 32 * c->ncu ? nblk : 32 * c->ncu) : nblk),
+            hipLaunchKernelGGL(dmx_huff_kernel, dim3(wl && wsh.list2 ? list_grid(nblk, wsh.n2, 2 * c->ncu, 32 * c->ncu) : nblk),
                                dim3(64), 0, s, c->hist, c->info, c->codes, c->hdr, c->sub, nblk, o.flags,
                                wl && wsh.list2 ? wl : NULL, wl && wsh.list2 ? wl + WL_HDR + c->cap_blocks : NULL, dupk);
         if (ev) (void)hipEventRecord(ev[3], s);
@@ -4864,13 +4886,13 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                            (uint32_t*)d_out, (const dmx_result*)c->res, wl, L4, dupk);
     if (ev) (void)hipEventRecord(ev[4], s);
     if (nblk)
-        hipLaunchKernelGGL(dmx_pack_kernel, dim3(wl && wsh.list4 ? (nblk < 16 * c->ncu ? nblk : 16 * c->ncu) : nblk),
+        hipLaunchKernelGGL(dmx_pack_kernel, dim3(wl && wsh.list4 ? list_grid(nblk, wsh.n4, 2 * c->ncu, 16 * c->ncu) : nblk),
                            dim3(PT), 0, s, (const uint8_t*)d_in, (uint32_t)o.sw, c->tok, c->codes, c->hdr, c->info, c->sub,
                            nblk, o.flags, (uint32_t*)d_out, c->res, wl, wl && wsh.list4 ? L4 : NULL, dupk);
-    if (nblk && dupa)
-        hipLaunchKernelGGL(dmx_dup_copy_kernel, dim3(nblk < 4 * c->ncu ? nblk : 4 * c->ncu), dim3(256), 0, s,
-                           (const dmx_blkinfo*)c->info, (const uint32_t*)wl, (uint64_t)c->cap_blocks, (uint32_t*)d_out,
-                           (const dmx_result*)c->res);
+    if (nblk && wl)   // the blocks K4 skipped: dups and the stored prefix (a wave per block)
+        hipLaunchKernelGGL(dmx_fill_kernel, dim3((nblk + 3) / 4), dim3(256), 0, s, (const uint8_t*)d_in, (uint32_t)o.sw,
+                           o.flags, (const dmx_blkinfo*)c->info, (const uint32_t*)wl, (uint64_t)c->cap_blocks, nblk,
+                           (uint32_t*)d_out, (const dmx_result*)c->res, dupa ? 1u : 0u);
     if (ev) (void)hipEventRecord(ev[5], s);
     HIPCHK(fault_hit(2) ? hipErrorLaunchFailure : hipGetLastError());
     c->last_nblk = nblk;
