@@ -1976,7 +1976,8 @@ __device__ __forceinline__ uint32_t uniform_parse(uint32_t bn, uint32_t c, uint3
 __host__ __device__ __forceinline__ const uint32_t* wl_dup(const uint32_t* wl, uint64_t cap) { return wl + WL_HDR + 4 * cap; }
 // block b is a dup (the worklist kernel set bit 3 of its code; its representative is in D)
 __device__ __forceinline__ bool is_dup(const uint16_t* codes, uint32_t b) { return codes && (codes[b] & 8u); }
-// The code per block (u16, after D; written by the worklist kernel from K0's prestored):
+// The code per block (u16, after D; dmx_codes_kernel copies K0's prestored, the worklist kernel
+// adds the dup bit):
 // prestored in bits 1:0, bit 2 = a full uniform block with 1 <= b <= nblk - 2 (a dedupe
 // candidate), its byte value in 15:8, bit 3 = a dup
 __host__ __device__ __forceinline__ uint16_t* wl_codes(uint32_t* wl, uint64_t cap) {
@@ -2308,25 +2309,32 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
 // offset from a block scan + its count so far.  Also zeroes K1's claim counter and K4's list,
 // and (dedupe) picks each byte value's representative among the full uniform blocks.
 #define WLT 1024
-__global__ __launch_bounds__(WLT) void dmx_worklist_kernel(const dmx_blkinfo* __restrict__ info, uint32_t nblk,
-                                                           uint32_t* __restrict__ wl, uint64_t cap, uint32_t dedupe) {
+// K0's prestored per block (one 4-byte field of each 64-byte record) into the compact code
+// array, one thread per block over the whole chip: the list builder (one workgroup) then
+// reads 2 bytes per block, coalesced, instead of a cache line per block through one CU.
+__global__ __launch_bounds__(256) void dmx_codes_kernel(const dmx_blkinfo* __restrict__ info, uint32_t nblk,
+                                                        uint32_t* __restrict__ wl, uint64_t cap) {
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    if (b < nblk) wl_codes(wl, cap)[b] = (uint16_t)(info[b].prestored & 0xFFF7u);
+}
+__global__ __launch_bounds__(WLT) void dmx_worklist_kernel(uint32_t nblk, uint32_t* __restrict__ wl, uint64_t cap,
+                                                           uint32_t dedupe) {
     __shared__ uint32_t w1[WLT / 64], w2[WLT / 64], w5[WLT / 64], wm[WLT / 64], rep[256], nuni;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < 256) rep[tid] = 0xFFFFFFFFu;
     if (tid == 0) nuni = 0;
     __syncthreads();
-    // K0's prestored per block (its low 16 bits: the code); thread t takes blocks t, t + WLT,
-    // ...: the codes of the first WLC x WLT blocks (1 GiB of 32 KiB blocks) are loaded together
-    // and kept in registers
+    // the code per block (dmx_codes_kernel); thread t takes blocks t, t + WLT, ...: the codes of
+    // the first WLC x WLT blocks (1 GiB of 32 KiB blocks) are loaded together and kept in registers
     uint16_t* K = wl_codes(wl, cap);
     constexpr uint32_t WLC = 32;
     uint32_t kc[WLC];
 #pragma unroll
     for (uint32_t j = 0; j < WLC; j++) {
         const uint32_t b = j * WLT + tid;
-        kc[j] = b < nblk ? info[b].prestored & 0xFFF7u : 3u;
+        kc[j] = b < nblk ? (uint32_t)K[b] : 3u;
     }
-    auto code = [&](uint32_t j, uint32_t b) -> uint32_t { return j < WLC ? kc[j] : info[b].prestored & 0xFFF7u; };
+    auto code = [&](uint32_t j, uint32_t b) -> uint32_t { return j < WLC ? kc[j] : (uint32_t)K[b]; };
     uint32_t m = nblk, nu = 0, lastc = 0xFFFFFFFFu;
     for (uint32_t j = 0, b = tid; b < nblk; j++, b += WLT) {
         const uint32_t k = code(j, b);
@@ -4830,9 +4838,12 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                                dim3(SCT), 0, s, (const uint8_t*)d_in, n,
                                (uint32_t)o.sw, c->info, c->tok, c->hist, (o.flags & DMX_F_DICT) ? 0u : 1u, o.flags,
                                (uint32_t*)d_out, out_cap, 0u);
-        if (wl)
-            hipLaunchKernelGGL(dmx_worklist_kernel, dim3(1), dim3(WLT), 0, s, (const dmx_blkinfo*)c->info, nblk, wl,
-                               (uint64_t)c->cap_blocks, dupa ? 1u : 0u);
+        if (wl) {
+            hipLaunchKernelGGL(dmx_codes_kernel, dim3((nblk + 255) / 256), dim3(256), 0, s, (const dmx_blkinfo*)c->info,
+                               nblk, wl, (uint64_t)c->cap_blocks);
+            hipLaunchKernelGGL(dmx_worklist_kernel, dim3(1), dim3(WLT), 0, s, nblk, wl, (uint64_t)c->cap_blocks,
+                               dupa ? 1u : 0u);
+        }
         if (ev) (void)hipEventRecord(ev[1], s);
         const char* dstop = getenv("DMX_DEBUG_STOP");   // diagnostic only (dbg_stop)
         const uint32_t mfl = ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u) |
