@@ -2319,40 +2319,35 @@ __global__ __launch_bounds__(256) void dmx_codes_kernel(const dmx_blkinfo* __res
 }
 __global__ __launch_bounds__(WLT) void dmx_worklist_kernel(uint32_t nblk, uint32_t* __restrict__ wl, uint64_t cap,
                                                            uint32_t dedupe) {
-    __shared__ uint32_t w1[WLT / 64], w2[WLT / 64], w5[WLT / 64], wm[WLT / 64], rep[256], nuni;
+    constexpr uint32_t WLC = 16;   // blocks per thread and chunk: a chunk = WLC x WLT blocks (512 MiB of 32 KiB blocks)
+    __shared__ uint32_t cnt[3][WLC * (WLT / 64)];   // per (j, wave) of a chunk: list entries, then their offsets
+    __shared__ uint32_t wsum[WLT / 64], rep[256], nuni, mmin, tot[3];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t lt = (1ull << lane) - 1ull;
     if (tid < 256) rep[tid] = 0xFFFFFFFFu;
-    if (tid == 0) nuni = 0;
+    if (tid == 0) { nuni = 0; mmin = nblk; tot[0] = tot[1] = tot[2] = 0; }
     __syncthreads();
-    // the code per block (dmx_codes_kernel); thread t takes blocks t, t + WLT, ...: the codes of
-    // the first WLC x WLT blocks (1 GiB of 32 KiB blocks) are loaded together and kept in registers
     uint16_t* K = wl_codes(wl, cap);
-    constexpr uint32_t WLC = 32;
-    uint32_t kc[WLC];
-#pragma unroll
-    for (uint32_t j = 0; j < WLC; j++) {
-        const uint32_t b = j * WLT + tid;
-        kc[j] = b < nblk ? (uint32_t)K[b] : 3u;
-    }
-    auto code = [&](uint32_t j, uint32_t b) -> uint32_t { return j < WLC ? kc[j] : (uint32_t)K[b]; };
+    uint32_t* L1 = wl + WL_HDR;
+    uint32_t* L2 = L1 + cap;
+    uint32_t* L5 = L1 + 3 * cap;
+    uint32_t* Dp = L1 + 4 * cap;
+    // first sweep over every block: the first block that is not a stored prefix block
+    // (prestored != 3), the candidates' count and (dedupe) each byte value's representative
     uint32_t m = nblk, nu = 0, lastc = 0xFFFFFFFFu;
-    for (uint32_t j = 0, b = tid; b < nblk; j++, b += WLT) {
-        const uint32_t k = code(j, b);
+    for (uint32_t b = tid; b < nblk; b += WLT) {
+        const uint32_t k = K[b];
         if ((k & 3u) != 3u) m = min(m, b);
         if (k & 4u) {
             nu++;
             // this thread's blocks ascend: its first block of a byte value is its candidate
-            // (one LDS atomic per run of one value, not per block: 32 768 blocks of zeros)
             if (dedupe && (k >> 8) != lastc) atomicMin(&rep[k >> 8], b);
             lastc = k >> 8;
         }
     }
     if (nu) atomicAdd(&nuni, nu);
+    if (m < nblk) atomicMin(&mmin, m);
     __syncthreads();
-    uint32_t* L1 = wl + WL_HDR;
-    uint32_t* L2 = L1 + cap;
-    uint32_t* L5 = L1 + 3 * cap;
-    uint32_t* Dp = L1 + 4 * cap;
     // per block: 1 = K1 parses it, 2 = K2 codes it, 4 = a dup (of r)
     auto kind = [&](uint32_t k, uint32_t b, uint32_t& r) -> uint32_t {
         r = 0xFFFFFFFFu;
@@ -2365,54 +2360,76 @@ __global__ __launch_bounds__(WLT) void dmx_worklist_kernel(uint32_t nblk, uint32
         }
         return 2u;
     };
-    uint32_t c1 = 0, c2 = 0, c5 = 0;
-    for (uint32_t j = 0, b = tid; b < nblk; j++, b += WLT) {
-        uint32_t r;
-        const uint32_t t = kind(code(j, b), b, r);
-        c1 += t & 1u; c2 += (t >> 1) & 1u; c5 += (t >> 2) & 1u;
-    }
-    // exclusive block scans of the three counts, min of m
-    const uint32_t i1 = wave_incl_scan(c1), i2 = wave_incl_scan(c2), i5 = wave_incl_scan(c5);
-    uint32_t mm = m;
+    // the lists in block order, chunk by chunk: block b = c0 + j WLT + tid; a wave's entries
+    // of step j are contiguous (ballot ranks), steps and waves in order by a scan of the counts
+    for (uint32_t c0 = 0; c0 < nblk; c0 += WLC * WLT) {
+        uint32_t kc[WLC];   // code in bits 15:0, its kind (1 | 2 | 4) in bits 18:16
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) mm = min(mm, (uint32_t)__shfl_xor((int)mm, o));
-    if (lane == 63) { w1[wave] = i1; w2[wave] = i2; w5[wave] = i5; }
-    if (lane == 0) wm[wave] = mm;
-    __syncthreads();
-    uint32_t o1 = i1 - c1, o2 = i2 - c2, o5 = i5 - c5, t1 = 0, t2 = 0, t5 = 0, M = nblk;
-    for (uint32_t w = 0; w < WLT / 64; w++) {
-        if (w < wave) { o1 += w1[w]; o2 += w2[w]; o5 += w5[w]; }
-        t1 += w1[w];
-        t2 += w2[w];
-        t5 += w5[w];
-        M = min(M, wm[w]);
-    }
-    for (uint32_t j = 0, b = tid; b < nblk; j++, b += WLT) {
-        uint32_t r;
-        const uint32_t k = code(j, b), t = kind(k, b, r);
-        if (t & 1u) L1[o1++] = b;
-        if (t & 2u) L2[o2++] = b;
-        if (t & 4u) {   // a dup: its representative, and bit 3 of its code (what the kernels test)
-            L5[o5++] = b;
-            Dp[b] = r;
+        for (uint32_t j = 0; j < WLC; j++) {
+            const uint32_t b = c0 + j * WLT + tid;
+            kc[j] = b < nblk ? (uint32_t)K[b] : 3u;
         }
-        K[b] = (uint16_t)(k | ((t & 4u) ? 8u : 0u));
+#pragma unroll
+        for (uint32_t j = 0; j < WLC; j++) {
+            const uint32_t b = c0 + j * WLT + tid;
+            uint32_t r;
+            const uint32_t t = b < nblk ? kind(kc[j], b, r) : 0u;
+            kc[j] |= t << 16;
+            const uint64_t m1 = __ballot(t & 1u), m2 = __ballot(t & 2u), m5 = __ballot(t & 4u);
+            if (lane == 0) {
+                cnt[0][j * (WLT / 64) + wave] = (uint32_t)__popcll(m1);
+                cnt[1][j * (WLT / 64) + wave] = (uint32_t)__popcll(m2);
+                cnt[2][j * (WLT / 64) + wave] = (uint32_t)__popcll(m5);
+            }
+        }
+        __syncthreads();
+        // exclusive scans of the three count tables (WLC x 16 entries each, j-major), by
+        // threads 0 .. 3 x 64 - 1: a wave per table, WLC / 4 entries per lane
+        if (wave < 3) {
+            uint32_t* T = cnt[wave];
+            uint32_t v[WLC / 4], sum = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < WLC / 4; q++) { v[q] = T[lane * (WLC / 4) + q]; sum += v[q]; }
+            const uint32_t incl = wave_incl_scan(sum);
+            uint32_t run = tot[wave] + incl - sum;
+#pragma unroll
+            for (uint32_t q = 0; q < WLC / 4; q++) { T[lane * (WLC / 4) + q] = run; run += v[q]; }
+            if (lane == 63) wsum[wave] = incl;
+        }
+        __syncthreads();
+        if (tid < 3) tot[tid] += wsum[tid];
+#pragma unroll
+        for (uint32_t j = 0; j < WLC; j++) {
+            const uint32_t b = c0 + j * WLT + tid;
+            const uint32_t t = kc[j] >> 16;
+            const uint64_t m1 = __ballot(t & 1u), m2 = __ballot(t & 2u), m5 = __ballot(t & 4u);
+            if (t & 1u) L1[cnt[0][j * (WLT / 64) + wave] + (uint32_t)__popcll(m1 & lt)] = b;
+            if (t & 2u) L2[cnt[1][j * (WLT / 64) + wave] + (uint32_t)__popcll(m2 & lt)] = b;
+            if (t & 4u) {   // a dup: its representative, and bit 3 of its code (what the kernels test)
+                L5[cnt[2][j * (WLT / 64) + wave] + (uint32_t)__popcll(m5 & lt)] = b;
+                uint32_t r;
+                kind(kc[j] & 0xFFFFu, b, r);
+                Dp[b] = r;
+                K[b] = (uint16_t)((kc[j] & 0xFFFFu) | 8u);
+            }
+        }
+        __syncthreads();   // (cnt is rewritten by the next chunk; tot published)
     }
     if (tid == 0) {
-        wl[WL_N1] = t1;
+        wl[WL_N1] = tot[0];
         wl[WL_C1] = 0;
-        wl[WL_N2] = t2;
+        wl[WL_N2] = tot[1];
         wl[WL_N4] = 0;
-        wl[WL_M] = M;
-        wl[WL_N5] = t5;
+        wl[WL_M] = mmin;
+        wl[WL_N5] = tot[2];
         wl_hint_put(wl, 0, nblk);
-        wl_hint_put(wl, 1, t1);
-        wl_hint_put(wl, 2, t2);
+        wl_hint_put(wl, 1, tot[0]);
+        wl_hint_put(wl, 2, tot[1]);
         wl_hint_put(wl, 4, nuni);
     }
 }
 
-// After K4 (work-list mode), a wave per block, the blocks K4 skipped:
+// After K4 (work-list mode), the blocks K4 skipped (a wave per 4 blocks):
 //  * a dup (uniform-block dedupe) gets its representative's bit string: output word k of the
 //    dup holds the representative's bits shifted by the two offsets' difference, masked to
 //    the dup's own bits (its two edge words, shared with its neighbours and zeroed by the
@@ -2428,9 +2445,60 @@ __global__ __launch_bounds__(256) void dmx_fill_kernel(const uint8_t* __restrict
                                                        uint32_t* __restrict__ out32, const dmx_result* __restrict__ res,
                                                        uint32_t dedupe) {
     if (res->status) return;
-    const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (b >= nblk) return;
-    if (dedupe && (wl_codes(wl, cap)[b] & 8u)) {   // a dup
+    // a wave covers the 4 blocks b0 .. b0 + 3
+    const uint32_t lane = threadIdx.x & 63, b0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 4;
+    const uint32_t M = wl[WL_M];
+    {   // a block of the stored prefix (full: not the last block), at its speculative offset: 16 lanes
+        const uint32_t b = b0 + (lane >> 4), l16 = lane & 15;
+        if (b < nblk && wl_skip(b, M, nblk)) {
+            const uint8_t* d = in + (uint64_t)b * sw;
+            const uint32_t bn = sw;
+            const uint64_t O = spec_stored_bit(b, sw, flags);
+            const uint32_t s0 = (uint32_t)(O & 31), P = (s0 + 3 + 7) & ~7u, B0 = (P + 32) >> 3;
+            const uint32_t nwords = (uint32_t)(((uint64_t)P + 32 + 8ull * bn + 31) >> 5);
+            const uint32_t ebyte = B0 + bn;   // the block's end, in bytes from word O >> 5
+            const uint64_t gw0 = O >> 5;
+            const bool dal = (reinterpret_cast<uintptr_t>(d) & 3) == 0;
+            const uint32_t ks = 4 - (uint32_t)(gw0 & 3);
+            const uint32_t nq = (dal && nwords > ks + 1) ? (nwords - 1 - ks) >> 2 : 0;   // K0's quads (as its copy)
+            const uint32_t lenw = (bn & 0xFFFFu) | ((~bn & 0xFFFFu) << 16);
+            auto gen_byte = [&](uint32_t q) -> uint32_t {
+                if (q >= B0) return (q - B0) < bn ? (uint32_t)d[q - B0] : 0u;
+                if (q >= (P >> 3)) return (lenw >> (8 * (q - (P >> 3)))) & 0xFFu;
+                return 0u;   // the header byte (and the previous block's bytes below it: not written)
+            };
+            uint8_t* out8 = reinterpret_cast<uint8_t*>(out32 + gw0);
+            auto put_word = [&](uint32_t k) {
+                if (k == 0 || k == nwords - 1) {
+                    for (uint32_t q = 4 * k; q < 4 * k + 4; q++)
+                        if (q >= (s0 >> 3) && q < ebyte) out8[q] = (uint8_t)gen_byte(q);
+                } else {
+                    uint32_t v = 0;
+                    for (uint32_t i = 0; i < 4; i++) v |= gen_byte(4 * k + i) << (8 * i);
+                    out32[gw0 + k] = v;
+                }
+            };
+            auto fast = [&](uint32_t j) {
+                const int64_t o0 = (int64_t)(4 * (ks + 4 * j)) - (int64_t)B0;
+                return o0 >= 0 && (uint64_t)((o0 & ~3ll) + 20) <= bn;
+            };
+            const uint32_t kq = nq ? ks + 4 * nq : 0;
+            const uint32_t nrest = nq ? ks + (nwords - kq) : nwords;   // words outside the quads
+            for (uint32_t r = l16; r < nrest + 16; r += 16) {
+                if (r < nrest) {
+                    put_word(nq ? (r < ks ? r : kq + (r - ks)) : r);
+                } else if (nq >= 4) {   // quads 0, 1, nq - 2, nq - 1 that are not fast
+                    const uint32_t t = r - nrest, qi = t >> 2;
+                    const uint32_t j = qi < 2 ? qi : nq - 4 + qi;
+                    if (!fast(j)) put_word(ks + 4 * j + (t & 3));
+                }
+            }
+        }
+    }
+    if (!dedupe) return;
+    for (uint32_t i = 0; i < 4; i++) {   // dups: the whole wave per block
+        const uint32_t b = b0 + i;
+        if (b >= nblk || !(wl_codes(wl, cap)[b] & 8u)) continue;
         const uint32_t r = wl_dup(wl, cap)[b];
         const uint64_t Ob = info[b].off_bits, Or = info[r].off_bits, Lb = info[b].len_bits;
         const uint64_t gw0 = Ob >> 5;
@@ -2447,51 +2515,6 @@ __global__ __launch_bounds__(256) void dmx_fill_kernel(const uint8_t* __restrict
             const uint32_t v = (uint32_t)(bits << (a - lo));
             if (nb == 32) out32[gw0 + k] = v;
             else atomicOr(&out32[gw0 + k], v);
-        }
-        return;
-    }
-    if (!wl_skip(b, wl[WL_M], nblk)) return;
-    // a block of the stored prefix: full (not the last block), at its speculative offset
-    const uint8_t* d = in + (uint64_t)b * sw;
-    const uint32_t bn = sw;
-    const uint64_t O = spec_stored_bit(b, sw, flags);
-    const uint32_t s0 = (uint32_t)(O & 31), P = (s0 + 3 + 7) & ~7u, B0 = (P + 32) >> 3;
-    const uint32_t nwords = (uint32_t)(((uint64_t)P + 32 + 8ull * bn + 31) >> 5);
-    const uint32_t ebyte = B0 + bn;   // the block's end, in bytes from word O >> 5
-    const uint64_t gw0 = O >> 5;
-    const bool dal = (reinterpret_cast<uintptr_t>(d) & 3) == 0;
-    const uint32_t ks = 4 - (uint32_t)(gw0 & 3);
-    const uint32_t nq = (dal && nwords > ks + 1) ? (nwords - 1 - ks) >> 2 : 0;   // K0's quads (as its copy)
-    const uint32_t lenw = (bn & 0xFFFFu) | ((~bn & 0xFFFFu) << 16);
-    auto gen_byte = [&](uint32_t q) -> uint32_t {
-        if (q >= B0) return (q - B0) < bn ? (uint32_t)d[q - B0] : 0u;
-        if (q >= (P >> 3)) return (lenw >> (8 * (q - (P >> 3)))) & 0xFFu;
-        return 0u;   // the header byte (and the previous block's bytes below it: not written)
-    };
-    uint8_t* out8 = reinterpret_cast<uint8_t*>(out32 + gw0);
-    auto put_word = [&](uint32_t k) {
-        if (k == 0 || k == nwords - 1) {
-            for (uint32_t q = 4 * k; q < 4 * k + 4; q++)
-                if (q >= (s0 >> 3) && q < ebyte) out8[q] = (uint8_t)gen_byte(q);
-        } else {
-            uint32_t v = 0;
-            for (uint32_t i = 0; i < 4; i++) v |= gen_byte(4 * k + i) << (8 * i);
-            out32[gw0 + k] = v;
-        }
-    };
-    auto fast = [&](uint32_t j) {
-        const int64_t o0 = (int64_t)(4 * (ks + 4 * j)) - (int64_t)B0;
-        return o0 >= 0 && (uint64_t)((o0 & ~3ll) + 20) <= bn;
-    };
-    const uint32_t kq = nq ? ks + 4 * nq : 0;
-    const uint32_t nrest = nq ? ks + (nwords - kq) : nwords;   // words outside the quads
-    for (uint32_t r = lane; r < nrest + 16; r += 64) {
-        if (r < nrest) {
-            put_word(nq ? (r < ks ? r : kq + (r - ks)) : r);
-        } else if (nq >= 4) {   // quads 0, 1, nq - 2, nq - 1 that are not fast
-            const uint32_t t = r - nrest, qi = t >> 2;
-            const uint32_t j = qi < 2 ? qi : nq - 4 + qi;
-            if (!fast(j)) put_word(ks + 4 * j + (t & 3));
         }
     }
 }
@@ -4900,8 +4923,8 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         hipLaunchKernelGGL(dmx_pack_kernel, dim3(wl && wsh.list4 ? list_grid(nblk, wsh.n4, 2 * c->ncu, 16 * c->ncu) : nblk),
                            dim3(PT), 0, s, (const uint8_t*)d_in, (uint32_t)o.sw, c->tok, c->codes, c->hdr, c->info, c->sub,
                            nblk, o.flags, (uint32_t*)d_out, c->res, wl, wl && wsh.list4 ? L4 : NULL, dupk);
-    if (nblk && wl)   // the blocks K4 skipped: dups and the stored prefix (a wave per block)
-        hipLaunchKernelGGL(dmx_fill_kernel, dim3((nblk + 3) / 4), dim3(256), 0, s, (const uint8_t*)d_in, (uint32_t)o.sw,
+    if (nblk && wl)   // the blocks K4 skipped: dups and the stored prefix (a wave per 4 blocks)
+        hipLaunchKernelGGL(dmx_fill_kernel, dim3((nblk + 15) / 16), dim3(256), 0, s, (const uint8_t*)d_in, (uint32_t)o.sw,
                            o.flags, (const dmx_blkinfo*)c->info, (const uint32_t*)wl, (uint64_t)c->cap_blocks, nblk,
                            (uint32_t*)d_out, (const dmx_result*)c->res, dupa ? 1u : 0u);
     if (ev) (void)hipEventRecord(ev[5], s);
