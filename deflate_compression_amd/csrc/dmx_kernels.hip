@@ -1663,8 +1663,22 @@ __global__ __launch_bounds__(MT) void dmx_chain_kernel(const uint8_t* __restrict
     const uint32_t nv = len - 2;
     uint16_t* S = chs + (uint64_t)slot * DMX_BLK;
     uint16_t* E = che + (uint64_t)slot * DMX_NBUCKET;
+    // run-dominated blocks (a quarter of the 16-byte chunks one repeated byte, as K1 counts them)
+    // take the run-aware ranks; the others batch their rank atomics
+    __shared__ uint32_t nruns;
+    if (tid == 0) nruns = 0;
+    __syncthreads();
+    uint32_t runny = 0;
+    for (uint32_t k = tid; k < (len + 15) / 16; k += MT) {
+        const uint4 v = reinterpret_cast<const uint4*>(L.data)[k];
+        runny += (k * 16 + 16 <= len && v.x == v.y && v.y == v.z && v.z == v.w && v.x == (v.x & 0xFFu) * 0x01010101u) ? 1u : 0u;
+    }
+    if (runny) atomicAdd(&nruns, runny);
+    __syncthreads();
+    const bool runs = nruns * 4u >= (len + 15) / 16;
     for (uint32_t attempt = 0;; attempt++) {
-        if (attempt == 0) sort_positions<false>(L, len, 1, tid, false, tp0);
+        if (attempt == 0 && runs) sort_positions<false, true>(L, len, 1, tid, false, tp0);
+        else if (attempt == 0) sort_positions<false, false>(L, len, 1, tid, false, tp0);
         else sort_positions<true>(L, len, 1, tid, false, tp0);
         for (uint32_t k = tid; k < DMX_NBUCKET; k += MT) L.bstart[k] = 0;
         __syncthreads();
@@ -2332,17 +2346,27 @@ __global__ __launch_bounds__(WLT) void dmx_worklist_kernel(uint32_t nblk, uint32
     uint32_t* L2 = L1 + cap;
     uint32_t* L5 = L1 + 3 * cap;
     uint32_t* Dp = L1 + 4 * cap;
-    // first sweep over every block: the first block that is not a stored prefix block
-    // (prestored != 3), the candidates' count and (dedupe) each byte value's representative
+    // first sweep over every block (chunks of WLC loads in flight per thread): the first block
+    // that is not a stored prefix block (prestored != 3), the candidates' count and (dedupe)
+    // each byte value's representative
     uint32_t m = nblk, nu = 0, lastc = 0xFFFFFFFFu;
-    for (uint32_t b = tid; b < nblk; b += WLT) {
-        const uint32_t k = K[b];
-        if ((k & 3u) != 3u) m = min(m, b);
-        if (k & 4u) {
-            nu++;
-            // this thread's blocks ascend: its first block of a byte value is its candidate
-            if (dedupe && (k >> 8) != lastc) atomicMin(&rep[k >> 8], b);
-            lastc = k >> 8;
+    for (uint32_t c0 = 0; c0 < nblk; c0 += WLC * WLT) {
+        uint32_t kc[WLC];
+#pragma unroll
+        for (uint32_t j = 0; j < WLC; j++) {
+            const uint32_t b = c0 + j * WLT + tid;
+            kc[j] = b < nblk ? (uint32_t)K[b] : 3u;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < WLC; j++) {
+            const uint32_t b = c0 + j * WLT + tid, k = kc[j];
+            if ((k & 3u) != 3u) m = min(m, b);
+            if (k & 4u) {
+                nu++;
+                // this thread's blocks ascend: its first block of a byte value is its candidate
+                if (dedupe && (k >> 8) != lastc) atomicMin(&rep[k >> 8], b);
+                lastc = k >> 8;
+            }
         }
     }
     if (nu) atomicAdd(&nuni, nu);
