@@ -1990,8 +1990,8 @@ __device__ __forceinline__ uint32_t uniform_parse(uint32_t bn, uint32_t c, uint3
 __host__ __device__ __forceinline__ const uint32_t* wl_dup(const uint32_t* wl, uint64_t cap) { return wl + WL_HDR + 4 * cap; }
 // block b is a dup (the worklist kernel set bit 3 of its code; its representative is in D)
 __device__ __forceinline__ bool is_dup(const uint16_t* codes, uint32_t b) { return codes && (codes[b] & 8u); }
-// The code per block (u16, after D; dmx_codes_kernel copies K0's prestored, the worklist kernel
-// adds the dup bit):
+// The code per block (u16, after D; K0 writes its prestored there, the worklist kernel adds
+// the dup bit):
 // prestored in bits 1:0, bit 2 = a full uniform block with 1 <= b <= nblk - 2 (a dedupe
 // candidate), its byte value in 15:8, bit 3 = a dup
 __host__ __device__ __forceinline__ uint16_t* wl_codes(uint32_t* wl, uint64_t cap) {
@@ -2047,11 +2047,10 @@ __device__ __forceinline__ void stored_quads(uint64_t O, uint32_t bn, bool dal, 
 // input is in flight during pass 0's test and barriers; otherwise (text: pass 0 rejects the
 // block) they are loaded only for blocks that pass it.
 template <bool SPEC>
-__global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
-                                                              dmx_blkinfo* __restrict__ info, uint32_t* __restrict__ tok_g,
-                                                              uint32_t* __restrict__ hist_g, uint32_t uni_ok, uint32_t flags,
-                                                              uint32_t* __restrict__ out32, uint64_t out_cap,
-                                                              uint32_t unused_) {
+__device__ __forceinline__ uint32_t store_check_block(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
+                                                      dmx_blkinfo* __restrict__ info, uint32_t* __restrict__ tok_g,
+                                                      uint32_t* __restrict__ hist_g, uint32_t uni_ok, uint32_t flags,
+                                                      uint32_t* __restrict__ out32, uint64_t out_cap) {
     __shared__ uint32_t bm[1u << 12];   // the 17-bit presence bitmap (16 KB: 8 workgroups per CU)
     __shared__ uint32_t hist[256];
     __shared__ uint64_t red[10][SCT / 64];
@@ -2064,7 +2063,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
     const uint32_t nblk = gridDim.x;
     if (bn < 4096) {
         if (tid == 0) info[b].prestored = 0;
-        return;
+        return 0u;
     }
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
     const bool full = aligned16 && bn == SCT * 16 * 8;
@@ -2115,7 +2114,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
         }
         __syncthreads();
         if (!pass_s) {
-            if (!uni_ok || !uni4k) return;
+            if (!uni_ok || !uni4k) return 0u;
             // the first 4 KiB are one repeated byte: is the whole block?  Then its parse has
             // a closed form (as in K1's uniform path; no dictionary): a literal, distance-1
             // matches of min(258, bytes left) while >= 3 bytes are left, then literals.
@@ -2130,7 +2129,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
                     u = u && ((x[q] ^ c4) & m) == 0;
                 }
             }
-            if (!__syncthreads_and(u)) return;
+            if (!__syncthreads_and(u)) return 0u;
             uint32_t* H = bm;   // the 320-entry histogram (bm is free here)
             for (uint32_t k = tid; k < DMX_HIST; k += SCT) H[k] = 0;
             __syncthreads();
@@ -2148,7 +2147,7 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
             }
             __syncthreads();
             for (uint32_t k = tid; k < DMX_HIST; k += SCT) hist_g[(uint64_t)b * DMX_HIST + k] = H[k];
-            return;
+            return 2u | ((bn == sw && b >= 1 && b + 2 <= nblk) ? 4u | (c << 8) : 0u);
         }
     }
     // ---- pass 1: Adler sums (the block's data into registers for pass 2) ----
@@ -2316,6 +2315,20 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
             *reinterpret_cast<uint4*>(&out32[(O >> 5) + k]) = v;
         });
     }
+    return info[b].prestored;   // (the caller stores thread 0's)
+}
+
+// K0 (DMX_F_STORE_CHECK): the noise check of one block (store_check_block); with the work
+// lists, thread 0 also writes the block's code (its prestored) to the list builder's array --
+// in one place after the body, where its address costs no register through the body.
+template <bool SPEC>
+__global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
+                                                              dmx_blkinfo* __restrict__ info, uint32_t* __restrict__ tok_g,
+                                                              uint32_t* __restrict__ hist_g, uint32_t uni_ok, uint32_t flags,
+                                                              uint32_t* __restrict__ out32, uint64_t out_cap,
+                                                              uint16_t* __restrict__ codes) {
+    const uint32_t code = store_check_block<SPEC>(in, n, sw, info, tok_g, hist_g, uni_ok, flags, out32, out_cap);
+    if (codes && threadIdx.x == 0) codes[blockIdx.x] = (uint16_t)code;
 }
 
 // The work lists from K0's prestored values (one workgroup; thread t takes blocks t, t + WLT,
@@ -2323,14 +2336,6 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
 // offset from a block scan + its count so far.  Also zeroes K1's claim counter and K4's list,
 // and (dedupe) picks each byte value's representative among the full uniform blocks.
 #define WLT 1024
-// K0's prestored per block (one 4-byte field of each 64-byte record) into the compact code
-// array, one thread per block over the whole chip: the list builder (one workgroup) then
-// reads 2 bytes per block, coalesced, instead of a cache line per block through one CU.
-__global__ __launch_bounds__(256) void dmx_codes_kernel(const dmx_blkinfo* __restrict__ info, uint32_t nblk,
-                                                        uint32_t* __restrict__ wl, uint64_t cap) {
-    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-    if (b < nblk) wl_codes(wl, cap)[b] = (uint16_t)(info[b].prestored & 0xFFF7u);
-}
 __global__ __launch_bounds__(WLT) void dmx_worklist_kernel(uint32_t nblk, uint32_t* __restrict__ wl, uint64_t cap,
                                                            uint32_t dedupe) {
     constexpr uint32_t WLC = 16;   // blocks per thread and chunk: a chunk = WLC x WLT blocks (512 MiB of 32 KiB blocks)
@@ -4884,10 +4889,8 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
             hipLaunchKernelGGL(wl && wsh.loop1 ? dmx_store_check_kernel<true> : dmx_store_check_kernel<false>, dim3(nblk),
                                dim3(SCT), 0, s, (const uint8_t*)d_in, n,
                                (uint32_t)o.sw, c->info, c->tok, c->hist, (o.flags & DMX_F_DICT) ? 0u : 1u, o.flags,
-                               (uint32_t*)d_out, out_cap, 0u);
+                               (uint32_t*)d_out, out_cap, wl ? wl_codes(wl, c->cap_blocks) : NULL);
         if (wl) {
-            hipLaunchKernelGGL(dmx_codes_kernel, dim3((nblk + 255) / 256), dim3(256), 0, s, (const dmx_blkinfo*)c->info,
-                               nblk, wl, (uint64_t)c->cap_blocks);
             hipLaunchKernelGGL(dmx_worklist_kernel, dim3(1), dim3(WLT), 0, s, nblk, wl, (uint64_t)c->cap_blocks,
                                dupa ? 1u : 0u);
         }
