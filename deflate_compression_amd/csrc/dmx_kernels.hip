@@ -1970,9 +1970,11 @@ __device__ __forceinline__ uint32_t uniform_parse(uint32_t bn, uint32_t c, uint3
 // blocks took 0.11 ms, 32 768 blocks of zeros 0.79 ms -- same-address atomics from every
 // XCD serialise.)
 // The hint (words WL_HINT, WL_HINT + 1: a host-mapped pinned address, set at allocation):
-// {nblk, |L1|, |L2|, |L4|} of the latest encode, written by the list builder and K4, read
-// by the host at the next encode to choose the launch shapes (wl_shape).  Only the shape
-// depends on it -- every shape writes the same stream.
+// {nblk, |L1|, |L2|, |L4|, dedupe candidates} of the latest encode, written by the list
+// builder and K4 -- or, when that encode ran without the lists (every shape per block, no
+// dedupe: text), by the scan kernel from K0's block kinds -- read by the host at the next
+// encode to choose the launch shapes (wl_shape).  Only the shape depends on it -- every
+// shape writes the same stream.
 #define WL_N1 0
 #define WL_C1 1
 #define WL_N2 2
@@ -3980,7 +3982,8 @@ struct ScanTile {
     uint64_t a, c, s;                      // aggregate Mono (s: has a stored block)
     uint64_t ps, pa, pc;                   // exclusive prefix over the tiles before
     uint64_t adl_s1, adl_s2, ntok, nsto, nfix;
-    uint64_t pad_[5];
+    uint64_t kinds;   // K0's block kinds in the tile (16-bit fields: prestored 0, 2, 3, dedupe candidates)
+    uint64_t pad_[4];
 };
 
 __device__ __forceinline__ Mono blk_elem(const dmx_blkinfo& bi) {
@@ -3996,13 +3999,18 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_tile_kernel(dmx_blkinfo* _
                                                                  const uint32_t* __restrict__ dup,
                                                                  dmx_subinfo* __restrict__ sub_g) {
     __shared__ Mono wtot[SCAN_TILE / 64];
-    __shared__ uint64_t red[SCAN_TILE / 64][5];
+    __shared__ uint64_t red[SCAN_TILE / 64][6];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t b = blockIdx.x * SCAN_TILE + tid;
     Mono e = {0, 0, 0};
-    uint64_t s1 = 0, s2 = 0, nt = 0, ns = 0, nf = 0;
+    uint64_t s1 = 0, s2 = 0, nt = 0, ns = 0, nf = 0, kd = 0;
     if (b < nblk) {
         dmx_blkinfo bi = info[b];
+        {   // (the launch-shape hint: what K0 decided, DMX_F_STORE_CHECK)
+            const uint32_t ps = bi.prestored;
+            kd = (ps & 3u) == 0 ? 1ull : (ps & 3u) == 2 ? (1ull << 16) | ((ps & 4u) ? 1ull << 48 : 0ull)
+                                       : (ps & 3u) == 3 ? 1ull << 32 : 0ull;
+        }
         if (is_dup(codes, b)) {   // a dup (uniform-block dedupe): the representative's coding
             const uint32_t r = dup[b];
             const dmx_blkinfo ri = info[r];
@@ -4037,7 +4045,8 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_tile_kernel(dmx_blkinfo* _
     nt = wave_sum_u64(nt);
     ns = wave_sum_u64(ns);
     nf = wave_sum_u64(nf);
-    if (lane == 0) { red[wave][0] = s1; red[wave][1] = s2; red[wave][2] = nt; red[wave][3] = ns; red[wave][4] = nf; }
+    kd = wave_sum_u64(kd);
+    if (lane == 0) { red[wave][0] = s1; red[wave][1] = s2; red[wave][2] = nt; red[wave][3] = ns; red[wave][4] = nf; red[wave][5] = kd; }
     __syncthreads();
     Mono pre = {0, 0, 0};
     for (uint32_t w = 0; w < wave; w++) pre = mcompose(pre, wtot[w]);
@@ -4048,28 +4057,31 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_tile_kernel(dmx_blkinfo* _
     }
     if (tid == 0) {
         Mono agg = {0, 0, 0};
-        uint64_t a1 = 0, a2 = 0, t2 = 0, t3 = 0, t4 = 0;
+        uint64_t a1 = 0, a2 = 0, t2 = 0, t3 = 0, t4 = 0, t5 = 0;
         for (int w = 0; w < SCAN_TILE / 64; w++) {
             agg = mcompose(agg, wtot[w]);
-            a1 += red[w][0]; a2 += red[w][1]; t2 += red[w][2]; t3 += red[w][3]; t4 += red[w][4];
+            a1 += red[w][0]; a2 += red[w][1]; t2 += red[w][2]; t3 += red[w][3]; t4 += red[w][4]; t5 += red[w][5];
         }
         ScanTile& T = tiles[blockIdx.x];
         T.a = agg.a; T.c = agg.c; T.s = agg.s;
-        T.adl_s1 = a1 % ADL_MOD; T.adl_s2 = a2 % ADL_MOD; T.ntok = t2; T.nsto = t3; T.nfix = t4;
+        T.adl_s1 = a1 % ADL_MOD; T.adl_s2 = a2 % ADL_MOD; T.ntok = t2; T.nsto = t3; T.nfix = t4; T.kinds = t5;
     }
 }
 
 __global__ __launch_bounds__(ST) void dmx_scan_kernel(ScanTile* __restrict__ tiles, uint32_t nblk, uint64_t n,
                                                       uint32_t flags, uint64_t out_cap,
                                                       uint32_t* __restrict__ out32, dmx_result* __restrict__ res,
-                                                      uint32_t* __restrict__ nfallback) {
+                                                      uint32_t* __restrict__ nfallback, uint32_t* __restrict__ hint) {
     __shared__ Mono wtot[ST / 64];
+    __shared__ uint32_t kcnt[4];
     __shared__ Mono carry_s;
     __shared__ uint64_t red[ST / 64][5];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t start = (flags & DMX_F_HEADER) ? 16 : 0;
     const uint32_t ntile = (nblk + SCAN_TILE - 1) / SCAN_TILE;
     uint64_t adl_s1 = 0, adl_s2 = 0, ntok = 0, nsto = 0, nfix = 0;
+    uint32_t k0 = 0, k2 = 0, k3 = 0, ku = 0;
+    if (tid < 4) kcnt[tid] = 0;
     // thread t owns tiles [t C, t C + C)
     const uint32_t C = (ntile + ST - 1) / ST;
     const uint32_t t0 = tid * C < ntile ? tid * C : ntile, t1 = t0 + C < ntile ? t0 + C : ntile;
@@ -4084,6 +4096,10 @@ __global__ __launch_bounds__(ST) void dmx_scan_kernel(ScanTile* __restrict__ til
         ntok += T.ntok;
         nsto += T.nsto;
         nfix += T.nfix;
+        k0 += (uint32_t)(T.kinds & 0xFFFFu);
+        k2 += (uint32_t)((T.kinds >> 16) & 0xFFFFu);
+        k3 += (uint32_t)((T.kinds >> 32) & 0xFFFFu);
+        ku += (uint32_t)(T.kinds >> 48);
     }
     Mono x = agg;  // inclusive scan in the wave
 #pragma unroll
@@ -4092,7 +4108,13 @@ __global__ __launch_bounds__(ST) void dmx_scan_kernel(ScanTile* __restrict__ til
         if (lane >= (uint32_t)o) x = mcompose(y, x);
     }
     if (lane == 63) wtot[wave] = x;
-    __syncthreads();
+    __syncthreads();   // (kcnt zeroed)
+    if (hint) {   // the launch-shape hint of an encode without the work lists (wl_shape)
+        if (k0) atomicAdd(&kcnt[0], k0);
+        if (k2) atomicAdd(&kcnt[1], k2);
+        if (k3) atomicAdd(&kcnt[2], k3);
+        if (ku) atomicAdd(&kcnt[3], ku);
+    }
     if (tid == 0) {   // exclusive prefix over waves
         Mono acc = {0, 0, 0};
         for (int w = 0; w < ST / 64; w++) {
@@ -4150,6 +4172,13 @@ __global__ __launch_bounds__(ST) void dmx_scan_kernel(ScanTile* __restrict__ til
         nfallback[1] += nfallback[0];       // and the context's running total
         res->nsortfallback_total = nfallback[1];
         nfallback[0] = 0;
+        if (hint) {   // {nblk, |L1|, |L2|, |L4| (the blocks K4 would take), dedupe candidates}
+            __hip_atomic_store(&hint[0], nblk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&hint[1], kcnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&hint[2], kcnt[0] + kcnt[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&hint[3], nblk - kcnt[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&hint[4], kcnt[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         s_end = end;
         s_T = T;
         s_adler = adler;
@@ -4521,6 +4550,7 @@ struct dmx_ctx {
     ScanTile* tiles;  // cap_blocks / SCAN_TILE + 1: per-tile aggregates and prefixes (scan)
     uint32_t* wl;     // WL_HDR + 3 cap_blocks: the work lists of DMX_F_STORE_CHECK (WL_* comment)
     volatile uint32_t* whint;   // host-mapped pinned {nblk, |L1|, |L2|, |L4|, uniform full blocks} of the latest encode (WL_HINT)
+    uint32_t* whint_dev;        // its device address (the scan kernel writes it when an encode runs without the lists)
     uint32_t ncu;     // compute units (the persistent K1 grid of the work-list mode)
     dmx_result* res;
     uint32_t* nfb;        // [0] sort fallbacks of the encode in flight (kernels add, K3's scan reads and zeroes), [1] total
@@ -4718,6 +4748,8 @@ extern "C" int dmx_ctx_create(int device, uint64_t max_input, dmx_ctx** out) {
         if (hipHostMalloc(&hp, 32, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
             memset(hp, 0, 32);
             c->whint = (volatile uint32_t*)hp;
+            void* dp = NULL;
+            if (hipHostGetDevicePointer(&dp, hp, 0) == hipSuccess) c->whint_dev = (uint32_t*)dp;
         }
     }
     if (hip_fail(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate")) { c->stream = NULL; dmx_ctx_destroy(c); return -(int)E_DEVICE; }
@@ -4857,8 +4889,11 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     // DMX_F_STORE_CHECK: the work lists (WL_* above) and their launch shapes (wl_shape)
     const char* wle = getenv("DMX_WORKLIST");
-    uint32_t* wl = ((o.flags & DMX_F_STORE_CHECK) && !(wle && !strcmp(wle, "0"))) ? c->wl : NULL;
     const WlShape wsh = wl_shape(c);
+    // an encode whose shapes are all per block and without the dedupe runs without the lists
+    // (no list builder, no fill kernel); its scan kernel writes the hint instead
+    const bool anyl = wsh.loop1 || wsh.list2 || wsh.list4 || wsh.dedupe;
+    uint32_t* wl = ((o.flags & DMX_F_STORE_CHECK) && anyl && !(wle && !strcmp(wle, "0"))) ? c->wl : NULL;
     // the uniform-block dedupe's rep index per block (NULL: no dedupe in this encode)
     const bool dedupe = wl && wsh.dedupe && !(o.flags & DMX_F_SPLIT);
     const uint16_t* dupk = dedupe ? wl_codes((const uint32_t*)wl, c->cap_blocks) : NULL;   // dup bits (bit 3)
@@ -4941,7 +4976,8 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                            c->tiles, dupk, dupa, c->sub);
     uint32_t* L4 = wl ? wl + WL_HDR + 2 * c->cap_blocks : NULL;
     hipLaunchKernelGGL(dmx_scan_kernel, dim3(1), dim3(ST), 0, s, c->tiles, nblk, n, o.flags, out_cap,
-                       (uint32_t*)d_out, c->res, c->nfb);
+                       (uint32_t*)d_out, c->res, c->nfb,
+                       (!wl && (o.flags & DMX_F_STORE_CHECK)) ? c->whint_dev : NULL);
     if (nblk)
         hipLaunchKernelGGL(dmx_scan_apply_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, o.flags, c->tiles,
                            (uint32_t*)d_out, (const dmx_result*)c->res, wl, L4, dupk);
