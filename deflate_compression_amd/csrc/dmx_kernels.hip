@@ -2044,6 +2044,54 @@ __device__ __forceinline__ void stored_quads(uint64_t O, uint32_t bn, bool dal, 
         if (o0 >= 0 && (uint64_t)((o0 & ~3ll) + 20) <= bn) f(k, o0);
     }
 }
+// The rest of a stored block at its speculative offset O (bit, byte-aligned) beyond K0's
+// 16-byte quads (stored_quads): the header byte (BFINAL 0, BTYPE 00), LEN / NLEN, the words
+// before and after the quads, any of the first two and last two quads that did not take the
+// 20-byte fast path (as the pack kernel's stored path builds them); its two edge words by
+// byte stores of its own bytes (a neighbour's bytes share them).  Threads r0, r0 + rstep, ...
+__device__ __forceinline__ void stored_rest(const uint8_t* __restrict__ d, uint32_t bn, uint64_t O,
+                                            uint32_t r0, uint32_t rstep, uint32_t* __restrict__ out32) {
+    const uint32_t s0 = (uint32_t)(O & 31), P = (s0 + 3 + 7) & ~7u, B0 = (P + 32) >> 3;
+    const uint32_t nwords = (uint32_t)(((uint64_t)P + 32 + 8ull * bn + 31) >> 5);
+    const uint32_t ebyte = B0 + bn;   // the block's end, in bytes from word O >> 5
+    const uint64_t gw0 = O >> 5;
+    const bool dal = (reinterpret_cast<uintptr_t>(d) & 3) == 0;
+    const uint32_t ks = 4 - (uint32_t)(gw0 & 3);
+    const uint32_t nq = (dal && nwords > ks + 1) ? (nwords - 1 - ks) >> 2 : 0;   // K0's quads (as its copy)
+    const uint32_t lenw = (bn & 0xFFFFu) | ((~bn & 0xFFFFu) << 16);
+    auto gen_byte = [&](uint32_t q) -> uint32_t {
+        if (q >= B0) return (q - B0) < bn ? (uint32_t)d[q - B0] : 0u;
+        if (q >= (P >> 3)) return (lenw >> (8 * (q - (P >> 3)))) & 0xFFu;
+        return 0u;   // the header byte (and the previous block's bytes below it: not written)
+    };
+    uint8_t* out8 = reinterpret_cast<uint8_t*>(out32 + gw0);
+    auto put_word = [&](uint32_t k) {
+        if (k == 0 || k == nwords - 1) {
+            for (uint32_t q = 4 * k; q < 4 * k + 4; q++)
+                if (q >= (s0 >> 3) && q < ebyte) out8[q] = (uint8_t)gen_byte(q);
+        } else {
+            uint32_t v = 0;
+            for (uint32_t i = 0; i < 4; i++) v |= gen_byte(4 * k + i) << (8 * i);
+            out32[gw0 + k] = v;
+        }
+    };
+    auto fast = [&](uint32_t j) {
+        const int64_t o0 = (int64_t)(4 * (ks + 4 * j)) - (int64_t)B0;
+        return o0 >= 0 && (uint64_t)((o0 & ~3ll) + 20) <= bn;
+    };
+    const uint32_t kq = nq ? ks + 4 * nq : 0;
+    const uint32_t nrest = nq ? ks + (nwords - kq) : nwords;   // words outside the quads
+    for (uint32_t r = r0; r < nrest + 16; r += rstep) {
+        if (r < nrest) {
+            put_word(nq ? (r < ks ? r : kq + (r - ks)) : r);
+        } else if (nq >= 4) {   // quads 0, 1, nq - 2, nq - 1 that are not fast
+            const uint32_t t = r - nrest, qi = t >> 2;
+            const uint32_t j = qi < 2 ? qi : nq - 4 + qi;
+            if (!fast(j)) put_word(ks + 4 * j + (t & 3));
+        }
+    }
+}
+
 // SPEC (work-list mode, when most blocks were stored in the previous encode): a full block's
 // eight chunks per thread are loaded before pass 0 decides anything, so the block's whole
 // input is in flight during pass 0's test and barriers; otherwise (text: pass 0 rejects the
@@ -2201,6 +2249,8 @@ __device__ __forceinline__ uint32_t store_check_block(const uint8_t* __restrict_
     uint32_t qn = 0;   // sampled 4-grams of this thread
     // histogram stride s = 8 / 4 / 2 / 1 for blocks of >= 32768 / 16384 / 8192 / 4096 bytes
     const uint32_t smask = bn >= 32768 ? 7u : bn >= 16384 ? 3u : bn >= 8192 ? 1u : 0u;
+    // (a per-lane loop over only the sampled positions -- about 6 ds_or per chunk for the wave
+    // instead of 16 masked ones -- measured slower: 79 VGPRs, 510 -> 745 us on C4)
     auto chunk2 = [&](uint32_t p, const uint32_t* w) {   // 16 positions at block offset p (w[4]: next 4 bytes)
 #pragma unroll
         for (int j = 0; j < 16; j++) {
@@ -2215,11 +2265,13 @@ __device__ __forceinline__ uint32_t store_check_block(const uint8_t* __restrict_
         }
     };
     if (full) {
+#ifndef DMX_K0_NOPASS2   // (timing knockout, tools/build_var.sh)
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const uint32_t w[5] = {v[i].x, v[i].y, v[i].z, v[i].w, nx[i]};
             chunk2((tid + i * SCT) << 4, w);
         }
+#endif
     } else {
         for (uint32_t p = tid << 4; p < bn; p += SCT << 4) {
             uint32_t w[5];
@@ -2246,11 +2298,18 @@ __device__ __forceinline__ uint32_t store_check_block(const uint8_t* __restrict_
         }
         const uint64_t m = ((uint64_t)bn + smask) / (smask + 1), m2 = m * m;
         const uint64_t coll = Q - Dn;
+#ifdef DMX_K0_NOPASS2
+        const bool sto = (S2 | coll | m2 | 1) != 0;
+#else
         const bool sto = 256 * S2 <= m2 + (m2 >> 4) + 256 * m && 16 * Q >= (uint64_t)bn && 64 * coll <= 4 * Q;
+#endif
         // the speculative copy (above) when the whole block fits the output at that offset
         const bool spec = sto && (spec_stored_bit(b, sw, flags) >> 3) + (uint64_t)bn + 16 <= out_cap;
         info[b].prestored = sto ? (spec ? 3u : 1u) : 0u;
         pass_s = spec ? 1u : 0u;
+#ifdef DMX_K0_NOCOPY
+        pass_s = 0;
+#endif
         if (sto) {
             info[b].ntok = 0;
             info[b].n = bn;
@@ -2333,52 +2392,121 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
     if (codes && threadIdx.x == 0) codes[blockIdx.x] = (uint16_t)code;
 }
 
-// The work lists from K0's prestored values (one workgroup; thread t takes blocks t, t + WLT,
-// ...: every load of a round in flight).  Deterministic order: list position = the thread's
-// offset from a block scan + its count so far.  Also zeroes K1's claim counter and K4's list,
-// and (dedupe) picks each byte value's representative among the full uniform blocks.
+// The work lists from K0's prestored values: one launch, a workgroup per tile of WLC x WLT
+// blocks.  Deterministic block order without a chip-wide scan: the workgroup of tile t first
+// counts the kinds of every block before its tile (codes [0, t TS), u16 x 8 per load, at most
+// nblk codes -- 64 KB at 1 GiB -- all loads in flight), which gives its lists' offsets, then
+// writes its tile's entries in block order (ballot ranks per (step, wave), a scan of those
+// counts).  The last tile's workgroup has then seen every block: it writes the list header
+// (counts, M, K1's claim counter and K4's list zeroed) and the hint.  (Round 5's first builder
+// was one workgroup sweeping every block twice: 21 us at 32 768 blocks, latency-bound; this
+// one reads each code at most once per workgroup and its workgroups run side by side.)
+// Dedupe: each byte value's representative is its first full uniform block in the stream, so
+// for a tile it is either before the tile (the prefix sweep sees it) or inside it; the dups
+// before the tile number (candidates before it) - (byte values among them).
 #define WLT 1024
+#define WLC 4
 __global__ __launch_bounds__(WLT) void dmx_worklist_kernel(uint32_t nblk, uint32_t* __restrict__ wl, uint64_t cap,
                                                            uint32_t dedupe) {
-    constexpr uint32_t WLC = 16;   // blocks per thread and chunk: a chunk = WLC x WLT blocks (512 MiB of 32 KiB blocks)
-    __shared__ uint32_t cnt[3][WLC * (WLT / 64)];   // per (j, wave) of a chunk: list entries, then their offsets
-    __shared__ uint32_t wsum[WLT / 64], rep[256], nuni, mmin, tot[3];
+    constexpr uint32_t TS = WLC * WLT;
+    __shared__ uint32_t cnt[3][WLC * (WLT / 64)];   // per (j, wave) of the tile: list entries, then their offsets
+    __shared__ uint32_t wsum[3], rep[256], red[4], mmin, tot[3];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t lt = (1ull << lane) - 1ull;
+    const uint32_t t0 = blockIdx.x * TS;
+    const bool last = blockIdx.x + 1 == gridDim.x;
     if (tid < 256) rep[tid] = 0xFFFFFFFFu;
-    if (tid == 0) { nuni = 0; mmin = nblk; tot[0] = tot[1] = tot[2] = 0; }
+    if (tid < 4) red[tid] = 0;
+    if (tid == 0) mmin = nblk;
     __syncthreads();
     uint16_t* K = wl_codes(wl, cap);
     uint32_t* L1 = wl + WL_HDR;
     uint32_t* L2 = L1 + cap;
     uint32_t* L5 = L1 + 3 * cap;
     uint32_t* Dp = L1 + 4 * cap;
-    // first sweep over every block (chunks of WLC loads in flight per thread): the first block
-    // that is not a stored prefix block (prestored != 3), the candidates' count and (dedupe)
-    // each byte value's representative
-    uint32_t m = nblk, nu = 0, lastc = 0xFFFFFFFFu;
-    for (uint32_t c0 = 0; c0 < nblk; c0 += WLC * WLT) {
-        uint32_t kc[WLC];
-#pragma unroll
-        for (uint32_t j = 0; j < WLC; j++) {
-            const uint32_t b = c0 + j * WLT + tid;
-            kc[j] = b < nblk ? (uint32_t)K[b] : 3u;
+    // the prefix sweep (blocks [0, t0)): prestored-0 and -2 counts, candidates, their byte
+    // values (rep: the first candidate per value), the first block that is not prestored 3
+    uint32_t a0 = 0, a2 = 0, ac = 0, m = nblk, lastc = 0xFFFFFFFFu;
+    auto see = [&](uint32_t k, uint32_t b) {
+        const uint32_t ps = k & 3u;
+        a0 += ps == 0;
+        a2 += ps == 2;
+        if (ps != 3u) m = min(m, b);
+        if (k & 4u) {
+            ac++;
+            // a thread's blocks ascend: its first block of a byte value is its candidate
+            if (dedupe && (k >> 8) != lastc) atomicMin(&rep[k >> 8], b);
+            lastc = k >> 8;
         }
+    };
+    {
+        const uint4* K8 = reinterpret_cast<const uint4*>(K);   // (16-byte aligned, t0 a multiple of 8)
+        const uint32_t nq = t0 >> 3;
+        for (uint32_t q0 = 0; q0 < nq; q0 += 4 * WLT) {
+            uint4 v[4];
 #pragma unroll
-        for (uint32_t j = 0; j < WLC; j++) {
-            const uint32_t b = c0 + j * WLT + tid, k = kc[j];
-            if ((k & 3u) != 3u) m = min(m, b);
-            if (k & 4u) {
-                nu++;
-                // this thread's blocks ascend: its first block of a byte value is its candidate
-                if (dedupe && (k >> 8) != lastc) atomicMin(&rep[k >> 8], b);
-                lastc = k >> 8;
+            for (uint32_t i = 0; i < 4; i++) {
+                const uint32_t q = q0 + i * WLT + tid;
+                v[i] = q < nq ? K8[q] : make_uint4(0x00030003u, 0x00030003u, 0x00030003u, 0x00030003u);
+            }
+#pragma unroll
+            for (uint32_t i = 0; i < 4; i++) {
+                const uint32_t bb = (q0 + i * WLT + tid) << 3;
+                const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+                for (uint32_t e = 0; e < 4; e++) {   // two codes per word, counted in bit-parallel
+                    const uint32_t x = w[e] & 0x00070007u;
+                    const uint32_t z0 = ~(x | (x >> 1)) & 0x00010001u, z2 = (x >> 1) & ~x & 0x00010001u;
+                    const uint32_t n3 = ~(x & (x >> 1)) & 0x00010001u, zc = (x >> 2) & 0x00010001u;
+                    a0 += __builtin_popcount(z0);
+                    a2 += __builtin_popcount(z2);
+                    ac += __builtin_popcount(zc);
+                    if (n3 && m == nblk) m = bb + 2 * e + ((n3 & 1u) ? 0u : 1u);   // (this thread's blocks ascend)
+                    if (dedupe && zc) {
+#pragma unroll
+                        for (uint32_t h = 0; h < 2; h++) {
+                            const uint32_t k = (w[e] >> (16 * h)) & 0xFFFFu;
+                            if ((k & 4u) && (k >> 8) != lastc) atomicMin(&rep[k >> 8], bb + 2 * e + h);
+                            if (k & 4u) lastc = k >> 8;
+                        }
+                    }
+                }
             }
         }
     }
-    if (nu) atomicAdd(&nuni, nu);
-    if (m < nblk) atomicMin(&mmin, m);
+    const uint32_t p0 = a0, p2 = a2, pc = ac;   // this thread's prefix counts
+    // the tile's codes (block b = t0 + j WLT + tid): they add to rep and (last tile) the totals
+    uint32_t kc[WLC];   // code in bits 15:0, its kind (1 | 2 | 4) in bits 18:16
+#pragma unroll
+    for (uint32_t j = 0; j < WLC; j++) {
+        const uint32_t b = t0 + j * WLT + tid;
+        kc[j] = b < nblk ? (uint32_t)K[b] : 3u;
+    }
+    lastc = 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t j = 0; j < WLC; j++) see(kc[j], t0 + j * WLT + tid);
+    {
+        const uint32_t s0 = wave_sum_u32(p0), s2 = wave_sum_u32(p2), sc = wave_sum_u32(pc), sa = wave_sum_u32(ac);
+        if (lane == 0) {
+            if (s0) atomicAdd(&red[0], s0);
+            if (s2) atomicAdd(&red[1], s2);
+            if (sc) atomicAdd(&red[2], sc);
+            if (sa) atomicAdd(&red[3], sa);
+        }
+        if (m < nblk) atomicMin(&mmin, m);
+    }
     __syncthreads();
+    if (wave == 0) {   // the byte values with a candidate before the tile, and the list offsets
+        uint32_t dv = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) dv += (uint32_t)__popcll(__ballot(rep[q * 64 + lane] < t0));
+        if (lane == 0) {
+            const uint32_t dups = dedupe ? red[2] - dv : 0u;
+            tot[0] = red[0];
+            tot[1] = red[0] + red[1] - dups;
+            tot[2] = dups;
+        }
+    }
     // per block: 1 = K1 parses it, 2 = K2 codes it, 4 = a dup (of r)
     auto kind = [&](uint32_t k, uint32_t b, uint32_t& r) -> uint32_t {
         r = 0xFFFFFFFFu;
@@ -2391,85 +2519,72 @@ __global__ __launch_bounds__(WLT) void dmx_worklist_kernel(uint32_t nblk, uint32
         }
         return 2u;
     };
-    // the lists in block order, chunk by chunk: block b = c0 + j WLT + tid; a wave's entries
-    // of step j are contiguous (ballot ranks), steps and waves in order by a scan of the counts
-    for (uint32_t c0 = 0; c0 < nblk; c0 += WLC * WLT) {
-        uint32_t kc[WLC];   // code in bits 15:0, its kind (1 | 2 | 4) in bits 18:16
 #pragma unroll
-        for (uint32_t j = 0; j < WLC; j++) {
-            const uint32_t b = c0 + j * WLT + tid;
-            kc[j] = b < nblk ? (uint32_t)K[b] : 3u;
+    for (uint32_t j = 0; j < WLC; j++) {
+        const uint32_t b = t0 + j * WLT + tid;
+        uint32_t r;
+        const uint32_t t = b < nblk ? kind(kc[j], b, r) : 0u;
+        kc[j] |= t << 16;
+        const uint64_t m1 = __ballot(t & 1u), m2 = __ballot(t & 2u), m5 = __ballot(t & 4u);
+        if (lane == 0) {
+            cnt[0][j * (WLT / 64) + wave] = (uint32_t)__popcll(m1);
+            cnt[1][j * (WLT / 64) + wave] = (uint32_t)__popcll(m2);
+            cnt[2][j * (WLT / 64) + wave] = (uint32_t)__popcll(m5);
         }
-#pragma unroll
-        for (uint32_t j = 0; j < WLC; j++) {
-            const uint32_t b = c0 + j * WLT + tid;
-            uint32_t r;
-            const uint32_t t = b < nblk ? kind(kc[j], b, r) : 0u;
-            kc[j] |= t << 16;
-            const uint64_t m1 = __ballot(t & 1u), m2 = __ballot(t & 2u), m5 = __ballot(t & 4u);
-            if (lane == 0) {
-                cnt[0][j * (WLT / 64) + wave] = (uint32_t)__popcll(m1);
-                cnt[1][j * (WLT / 64) + wave] = (uint32_t)__popcll(m2);
-                cnt[2][j * (WLT / 64) + wave] = (uint32_t)__popcll(m5);
-            }
-        }
-        __syncthreads();
-        // exclusive scans of the three count tables (WLC x 16 entries each, j-major), by
-        // threads 0 .. 3 x 64 - 1: a wave per table, WLC / 4 entries per lane
-        if (wave < 3) {
-            uint32_t* T = cnt[wave];
-            uint32_t v[WLC / 4], sum = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < WLC / 4; q++) { v[q] = T[lane * (WLC / 4) + q]; sum += v[q]; }
-            const uint32_t incl = wave_incl_scan(sum);
-            uint32_t run = tot[wave] + incl - sum;
-#pragma unroll
-            for (uint32_t q = 0; q < WLC / 4; q++) { T[lane * (WLC / 4) + q] = run; run += v[q]; }
-            if (lane == 63) wsum[wave] = incl;
-        }
-        __syncthreads();
-        if (tid < 3) tot[tid] += wsum[tid];
-#pragma unroll
-        for (uint32_t j = 0; j < WLC; j++) {
-            const uint32_t b = c0 + j * WLT + tid;
-            const uint32_t t = kc[j] >> 16;
-            const uint64_t m1 = __ballot(t & 1u), m2 = __ballot(t & 2u), m5 = __ballot(t & 4u);
-            if (t & 1u) L1[cnt[0][j * (WLT / 64) + wave] + (uint32_t)__popcll(m1 & lt)] = b;
-            if (t & 2u) L2[cnt[1][j * (WLT / 64) + wave] + (uint32_t)__popcll(m2 & lt)] = b;
-            if (t & 4u) {   // a dup: its representative, and bit 3 of its code (what the kernels test)
-                L5[cnt[2][j * (WLT / 64) + wave] + (uint32_t)__popcll(m5 & lt)] = b;
-                uint32_t r;
-                kind(kc[j] & 0xFFFFu, b, r);
-                Dp[b] = r;
-                K[b] = (uint16_t)((kc[j] & 0xFFFFu) | 8u);
-            }
-        }
-        __syncthreads();   // (cnt is rewritten by the next chunk; tot published)
     }
-    if (tid == 0) {
-        wl[WL_N1] = tot[0];
+    __syncthreads();
+    // exclusive scans of the three count tables (WLC x 16 entries each, j-major), by waves
+    // 0 .. 2: WLC / 4 entries per lane
+    if (wave < 3) {
+        uint32_t* T = cnt[wave];
+        uint32_t v[WLC / 4], sum = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < WLC / 4; q++) { v[q] = T[lane * (WLC / 4) + q]; sum += v[q]; }
+        const uint32_t incl = wave_incl_scan(sum);
+        uint32_t run = tot[wave] + incl - sum;
+#pragma unroll
+        for (uint32_t q = 0; q < WLC / 4; q++) { T[lane * (WLC / 4) + q] = run; run += v[q]; }
+        if (lane == 63) wsum[wave] = tot[wave] + incl;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < WLC; j++) {
+        const uint32_t b = t0 + j * WLT + tid;
+        const uint32_t t = kc[j] >> 16;
+        const uint64_t m1 = __ballot(t & 1u), m2 = __ballot(t & 2u), m5 = __ballot(t & 4u);
+        if (t & 1u) L1[cnt[0][j * (WLT / 64) + wave] + (uint32_t)__popcll(m1 & lt)] = b;
+        if (t & 2u) L2[cnt[1][j * (WLT / 64) + wave] + (uint32_t)__popcll(m2 & lt)] = b;
+        if (t & 4u) {   // a dup: its representative, and bit 3 of its code (what the kernels test)
+            L5[cnt[2][j * (WLT / 64) + wave] + (uint32_t)__popcll(m5 & lt)] = b;
+            uint32_t r;
+            kind(kc[j] & 0xFFFFu, b, r);
+            Dp[b] = r;
+            K[b] = (uint16_t)((kc[j] & 0xFFFFu) | 8u);
+        }
+    }
+    if (last && tid == 0) {   // every block seen: the header and the hint
+        wl[WL_N1] = wsum[0];
         wl[WL_C1] = 0;
-        wl[WL_N2] = tot[1];
+        wl[WL_N2] = wsum[1];
         wl[WL_N4] = 0;
         wl[WL_M] = mmin;
-        wl[WL_N5] = tot[2];
+        wl[WL_N5] = wsum[2];
         wl_hint_put(wl, 0, nblk);
-        wl_hint_put(wl, 1, tot[0]);
-        wl_hint_put(wl, 2, tot[1]);
-        wl_hint_put(wl, 4, nuni);
+        wl_hint_put(wl, 1, wsum[0]);
+        wl_hint_put(wl, 2, wsum[1]);
+        wl_hint_put(wl, 4, red[3]);
     }
 }
 
 // After K4 (work-list mode), the blocks K4 skipped (a wave per 4 blocks):
+//  * a block of the stored prefix (wl_skip) gets the bytes K0's speculative copy left out
+//    (stored_rest).  (Measured elsewhere: in K0 itself the tail's dependent byte loads made
+//    every workgroup longer, 488 -> 530 us on C4; in K4's list grid, 4 blocks per 16 lanes in
+//    sequence, 27 us against this kernel's 11);
 //  * a dup (uniform-block dedupe) gets its representative's bit string: output word k of the
 //    dup holds the representative's bits shifted by the two offsets' difference, masked to
 //    the dup's own bits (its two edge words, shared with its neighbours and zeroed by the
-//    apply launch, by atomicOr).  The representative is complete: K4 packed it;
-//  * a block of the stored prefix (wl_skip) gets the bytes K0's speculative copy left out:
-//    the header byte (BFINAL 0, BTYPE 00), LEN / NLEN, the words before and after its 16-byte
-//    quads, any of the first two and last two quads that did not take the 20-byte fast path
-//    (as the pack kernel's stored path builds them); its two edge words by byte stores of its
-//    own bytes (the neighbours' bytes share those words and the apply launch left them).
+//    apply launch, by atomicOr).  The representative is complete: K4 packed it.
 __global__ __launch_bounds__(256) void dmx_fill_kernel(const uint8_t* __restrict__ in, uint32_t sw, uint32_t flags,
                                                        const dmx_blkinfo* __restrict__ info,
                                                        const uint32_t* __restrict__ wl, uint64_t cap, uint32_t nblk,
@@ -2478,53 +2593,10 @@ __global__ __launch_bounds__(256) void dmx_fill_kernel(const uint8_t* __restrict
     if (res->status) return;
     // a wave covers the 4 blocks b0 .. b0 + 3
     const uint32_t lane = threadIdx.x & 63, b0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 4;
-    const uint32_t M = wl[WL_M];
     {   // a block of the stored prefix (full: not the last block), at its speculative offset: 16 lanes
-        const uint32_t b = b0 + (lane >> 4), l16 = lane & 15;
-        if (b < nblk && wl_skip(b, M, nblk)) {
-            const uint8_t* d = in + (uint64_t)b * sw;
-            const uint32_t bn = sw;
-            const uint64_t O = spec_stored_bit(b, sw, flags);
-            const uint32_t s0 = (uint32_t)(O & 31), P = (s0 + 3 + 7) & ~7u, B0 = (P + 32) >> 3;
-            const uint32_t nwords = (uint32_t)(((uint64_t)P + 32 + 8ull * bn + 31) >> 5);
-            const uint32_t ebyte = B0 + bn;   // the block's end, in bytes from word O >> 5
-            const uint64_t gw0 = O >> 5;
-            const bool dal = (reinterpret_cast<uintptr_t>(d) & 3) == 0;
-            const uint32_t ks = 4 - (uint32_t)(gw0 & 3);
-            const uint32_t nq = (dal && nwords > ks + 1) ? (nwords - 1 - ks) >> 2 : 0;   // K0's quads (as its copy)
-            const uint32_t lenw = (bn & 0xFFFFu) | ((~bn & 0xFFFFu) << 16);
-            auto gen_byte = [&](uint32_t q) -> uint32_t {
-                if (q >= B0) return (q - B0) < bn ? (uint32_t)d[q - B0] : 0u;
-                if (q >= (P >> 3)) return (lenw >> (8 * (q - (P >> 3)))) & 0xFFu;
-                return 0u;   // the header byte (and the previous block's bytes below it: not written)
-            };
-            uint8_t* out8 = reinterpret_cast<uint8_t*>(out32 + gw0);
-            auto put_word = [&](uint32_t k) {
-                if (k == 0 || k == nwords - 1) {
-                    for (uint32_t q = 4 * k; q < 4 * k + 4; q++)
-                        if (q >= (s0 >> 3) && q < ebyte) out8[q] = (uint8_t)gen_byte(q);
-                } else {
-                    uint32_t v = 0;
-                    for (uint32_t i = 0; i < 4; i++) v |= gen_byte(4 * k + i) << (8 * i);
-                    out32[gw0 + k] = v;
-                }
-            };
-            auto fast = [&](uint32_t j) {
-                const int64_t o0 = (int64_t)(4 * (ks + 4 * j)) - (int64_t)B0;
-                return o0 >= 0 && (uint64_t)((o0 & ~3ll) + 20) <= bn;
-            };
-            const uint32_t kq = nq ? ks + 4 * nq : 0;
-            const uint32_t nrest = nq ? ks + (nwords - kq) : nwords;   // words outside the quads
-            for (uint32_t r = l16; r < nrest + 16; r += 16) {
-                if (r < nrest) {
-                    put_word(nq ? (r < ks ? r : kq + (r - ks)) : r);
-                } else if (nq >= 4) {   // quads 0, 1, nq - 2, nq - 1 that are not fast
-                    const uint32_t t = r - nrest, qi = t >> 2;
-                    const uint32_t j = qi < 2 ? qi : nq - 4 + qi;
-                    if (!fast(j)) put_word(ks + 4 * j + (t & 3));
-                }
-            }
-        }
+        const uint32_t b = b0 + (lane >> 4);
+        if (b < nblk && wl_skip(b, wl[WL_M], nblk))
+            stored_rest(in + (uint64_t)b * sw, sw, spec_stored_bit(b, sw, flags), lane & 15, 16, out32);
     }
     if (!dedupe) return;
     for (uint32_t i = 0; i < 4; i++) {   // dups: the whole wave per block
@@ -4222,8 +4294,8 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply_kernel(dmx_blkinfo* 
         out32[(o + l - 1) >> 5] = 0;  // shared with the block after (or the framing)
         return;
     }
-    // work lists: a block of the whole-copy prefix is complete already (K0) and K4 skips it;
-    // every other block zeroes its edge words -- only its own bytes where the neighbour is a
+    // work lists: a block of the whole-copy prefix has its quads from K0 and gets the rest of
+    // its bytes from the fill kernel (stored_rest, byte stores): nothing to zero; every other block zeroes its edge words -- only its own bytes where the neighbour is a
     // whole-copy block (that boundary is a byte boundary: both sides are stored blocks at their
     // speculative offsets) -- and goes on K4's list
     const uint32_t M = wl[WL_M];
@@ -4926,7 +4998,8 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                                (uint32_t)o.sw, c->info, c->tok, c->hist, (o.flags & DMX_F_DICT) ? 0u : 1u, o.flags,
                                (uint32_t*)d_out, out_cap, wl ? wl_codes(wl, c->cap_blocks) : NULL);
         if (wl) {
-            hipLaunchKernelGGL(dmx_worklist_kernel, dim3(1), dim3(WLT), 0, s, nblk, wl, (uint64_t)c->cap_blocks,
+            hipLaunchKernelGGL(dmx_worklist_kernel, dim3((nblk + WLC * WLT - 1) / (WLC * WLT)), dim3(WLT), 0, s, nblk, wl,
+                               (uint64_t)c->cap_blocks,
                                dupa ? 1u : 0u);
         }
         if (ev) (void)hipEventRecord(ev[1], s);

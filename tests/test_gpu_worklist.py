@@ -181,3 +181,55 @@ def test_uniform_dedupe_inflate_and_split(enc):
             os.environ.pop("DMX_DEDUPE", None)
         else:
             os.environ["DMX_DEDUPE"] = old
+
+
+def _multi_tile(sw):
+    """Over 3 worklist tiles (WLC x WLT = 4 096 blocks each) of sw-byte blocks: a noise prefix
+    that crosses the first tile, uniform runs of byte values that recur in later tiles (their
+    representatives in an earlier tile), text blocks, a short tail."""
+    rng = np.random.default_rng(31)
+    parts, seed = [], 40
+
+    def noise(k):
+        nonlocal seed
+        seed += 1
+        parts.append(_noise(k * sw, seed))
+
+    noise(5000)
+    parts.append(bytes(200 * sw))
+    noise(100)
+    parts.append(D.gen_text(40 * sw, 41).tobytes())
+    parts.append(bytes([7]) * (300 * sw))
+    noise(3000)
+    parts.append(bytes(100 * sw))
+    parts.append(bytes([7]) * (100 * sw) + bytes([200]) * (50 * sw))
+    parts.append(D.gen_text(20 * sw, 42).tobytes())
+    noise(4000)
+    parts.append(rng.integers(0, 256, 777, dtype=np.uint8).tobytes())
+    return b"".join(parts)
+
+
+@pytest.mark.parametrize("shape", ["list", None])
+def test_worklist_multi_tile(shape):
+    """The list builder's workgroups each count the blocks before their tile: lists, the stored
+    prefix M, the dups and their representatives across tiles (DMX_DEDUPE 1 and 0) -- the
+    oracle's stream byte for byte."""
+    sw = 4096
+    data = _multi_tile(sw)
+    fl = D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK
+    want = O.compress(data, sw=sw, max_chain=7, lazy=True, store_check=True)
+    e = D.Encoder(0, len(data), sw=sw)
+    old = os.environ.get("DMX_DEDUPE")
+    try:
+        for dd in ("1", "0"):
+            os.environ["DMX_DEDUPE"] = dd
+            for rep in range(2):
+                z, r = _with_env(shape, lambda: e.compress_bytes(data, sw=sw, max_chain=7, flags=fl))
+                assert r.status == 0
+                assert z == want, (shape, dd, rep, len(z), len(want))
+    finally:
+        e.close()
+        if old is None:
+            os.environ.pop("DMX_DEDUPE", None)
+        else:
+            os.environ["DMX_DEDUPE"] = old

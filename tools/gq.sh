@@ -41,6 +41,7 @@ PY
         tail -1 "$OUT/stage_time.txt" ;;
     ktrace) cd /tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ktrace_$nb" -o run -- python3 "$R/tools/stage_time.py" ${arg//,/ } >> "$OUT/ktrace.txt" 2>&1 || exit 3
            f=$(find "$OUT/ktrace_$nb" -name "*kernel_stats.csv" | head -1); cp "$f" "$OUT/kernel_stats_$nb.csv"; cut -d, -f1-4 "$OUT/kernel_stats_$nb.csv" | head -14; nb=$((nb + 1)); cd "$R" ;;
+    fdchunk) timeout -k 10 300 python3 "$R/tools/fd_chunk.py" ${arg//,/ } > "$OUT/fdchunk.txt" 2>&1 || exit 3; cat "$OUT/fdchunk.txt" ;;
     deep) timeout -k 10 300 python3 "$R/tools/deep_bench.py" 32 > "$OUT/deep.txt" 2>&1 || exit 3; cat "$OUT/deep.txt" ;;
     trace) cd /tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --cpu-budget 0 --exhaustive-steps 0 --tradeoff= --long-run 0 ${arg//,/ } > "$OUT/bench_trace.json" 2> "$OUT/trace.err" || exit 3
            find "$OUT/trace" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \; ; cut -d, -f1-8 "$OUT/kernel_stats.csv" | head -20; cd "$R" ;;
