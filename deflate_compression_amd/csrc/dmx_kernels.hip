@@ -2118,20 +2118,25 @@ __device__ __forceinline__ uint32_t store_check_block(const uint8_t* __restrict_
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
     const bool full = aligned16 && bn == SCT * 16 * 8;
     uint4 v[8];
-    uint32_t nx[8];
-    if (SPEC && full) {
+    // the 4 bytes after chunk i (for the 4-grams that straddle it) are the next lane's v[i].x
+    // (DPP), except on lane 63, whose eight are held by lanes 0 .. 7 of nx63 (7 VGPRs fewer)
+    uint32_t nx63 = 0;
+    auto load_full = [&]() {
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const uint32_t p = (tid + i * SCT) << 4;
-            v[i] = *reinterpret_cast<const uint4*>(d + p);
-            nx[i] = p + 16 < bn ? *reinterpret_cast<const uint32_t*>(d + p + 16) : 0u;
-        }
-    }
+        for (int i = 0; i < 8; i++) v[i] = *reinterpret_cast<const uint4*>(d + ((tid + i * SCT) << 4));
+        const uint32_t p63 = (((tid | 63u) + lane * SCT) << 4) + 16;
+        nx63 = lane < 8 && p63 < bn ? *reinterpret_cast<const uint32_t*>(d + p63) : 0u;
+    };
+    auto next4 = [&](int i) -> uint32_t {
+        const uint32_t nl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[i].x, 0x130, 0xF, 0xF, false);
+        return lane == 63 ? (uint32_t)__builtin_amdgcn_readlane((int)nx63, i) : nl;
+    };
+    if (SPEC && full) load_full();
     // ---- pass 0: bit planes of the first 4096 bytes, one 16-byte load per thread ----
     {
         uint32_t w[5];
         if (SPEC && full) {   // chunk tid is v[0]
-            w[0] = v[0].x; w[1] = v[0].y; w[2] = v[0].z; w[3] = v[0].w; w[4] = nx[0];
+            w[0] = v[0].x; w[1] = v[0].y; w[2] = v[0].z; w[3] = v[0].w; w[4] = 0;   // (w[4] unused here)
         } else {
             sc_load(d, tid << 4, bn, aligned16, w);
         }
@@ -2215,14 +2220,7 @@ __device__ __forceinline__ uint32_t store_check_block(const uint8_t* __restrict_
     // full 32 KiB block: all loads in flight at once, and the data stays in registers for
     // pass 2 (w4: the 4 bytes after each chunk, for the 4-grams that straddle it)
     if (full) {
-        if (!SPEC) {
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const uint32_t p = (tid + i * SCT) << 4;
-                v[i] = *reinterpret_cast<const uint4*>(d + p);
-                nx[i] = p + 16 < bn ? *reinterpret_cast<const uint32_t*>(d + p + 16) : 0u;
-            }
-        }
+        if (!SPEC) load_full();
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
@@ -2268,7 +2266,7 @@ __device__ __forceinline__ uint32_t store_check_block(const uint8_t* __restrict_
 #ifndef DMX_K0_NOPASS2   // (timing knockout, tools/build_var.sh)
 #pragma unroll
         for (int i = 0; i < 8; i++) {
-            const uint32_t w[5] = {v[i].x, v[i].y, v[i].z, v[i].w, nx[i]};
+            const uint32_t w[5] = {v[i].x, v[i].y, v[i].z, v[i].w, next4(i)};
             chunk2((tid + i * SCT) << 4, w);
         }
 #endif
@@ -2292,7 +2290,7 @@ __device__ __forceinline__ uint32_t store_check_block(const uint8_t* __restrict_
     __syncthreads();
     if (tid == 0) {
         uint64_t S = 0, T = 0, Dn = 0, S2 = 0, Q = 0;
-#pragma unroll
+#pragma unroll 1   // (one wave's partials at a time: all 20 u64 at once spilled at 64 VGPRs)
         for (int w = 0; w < SCT / 64; w++) {
             S += red[8][w]; T += red[9][w]; Dn += red[0][w]; S2 += red[1][w]; Q += red[2][w];
         }
