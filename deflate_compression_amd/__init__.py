@@ -449,8 +449,14 @@ class Encoder:
     def last_nblk(self) -> int:
         return int(self._L.dmx_last_blocks(self._ctx, None, None, None, 1 << 30))
 
-    def set_timing(self, on: bool) -> None:
-        self._L.dmx_ctx_set_timing(self._ctx, 1 if on else 0)
+    STAGES = ("pre", "match", "huff", "scan", "pack")
+
+    def set_timing(self, on: bool, stage: str | None = None) -> None:
+        """HIP-event stage times of the following encodes: every stage boundary, or with
+        `stage` only that stage's two events (a timed loop then pays two event records per
+        encode; the other stages read 0)."""
+        mode = 0 if not on else (1 if stage is None else 0x100 | self.STAGES.index(stage))
+        self._L.dmx_ctx_set_timing(self._ctx, mode)
 
     def stage_times(self):
         ms = (ctypes.c_double * 6)()

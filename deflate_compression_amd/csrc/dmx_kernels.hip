@@ -2049,18 +2049,19 @@ __device__ __forceinline__ void stored_quads(uint64_t O, uint32_t bn, bool dal, 
 // before and after the quads, any of the first two and last two quads that did not take the
 // 20-byte fast path (as the pack kernel's stored path builds them); its two edge words by
 // byte stores of its own bytes (a neighbour's bytes share them).  Threads r0, r0 + rstep, ...
-__device__ __forceinline__ void stored_rest(const uint8_t* __restrict__ d, uint32_t bn, uint64_t O,
+// src(j) = data byte j of the block.
+template <typename Src>
+__device__ __forceinline__ void stored_rest(Src src, bool dal, uint32_t bn, uint64_t O,
                                             uint32_t r0, uint32_t rstep, uint32_t* __restrict__ out32) {
     const uint32_t s0 = (uint32_t)(O & 31), P = (s0 + 3 + 7) & ~7u, B0 = (P + 32) >> 3;
     const uint32_t nwords = (uint32_t)(((uint64_t)P + 32 + 8ull * bn + 31) >> 5);
     const uint32_t ebyte = B0 + bn;   // the block's end, in bytes from word O >> 5
     const uint64_t gw0 = O >> 5;
-    const bool dal = (reinterpret_cast<uintptr_t>(d) & 3) == 0;
     const uint32_t ks = 4 - (uint32_t)(gw0 & 3);
     const uint32_t nq = (dal && nwords > ks + 1) ? (nwords - 1 - ks) >> 2 : 0;   // K0's quads (as its copy)
     const uint32_t lenw = (bn & 0xFFFFu) | ((~bn & 0xFFFFu) << 16);
     auto gen_byte = [&](uint32_t q) -> uint32_t {
-        if (q >= B0) return (q - B0) < bn ? (uint32_t)d[q - B0] : 0u;
+        if (q >= B0) return (q - B0) < bn ? src(q - B0) : 0u;
         if (q >= (P >> 3)) return (lenw >> (8 * (q - (P >> 3)))) & 0xFFu;
         return 0u;   // the header byte (and the previous block's bytes below it: not written)
     };
@@ -2092,6 +2093,11 @@ __device__ __forceinline__ void stored_rest(const uint8_t* __restrict__ d, uint3
     }
 }
 
+__device__ __forceinline__ void stored_rest(const uint8_t* __restrict__ d, uint32_t bn, uint64_t O,
+                                            uint32_t r0, uint32_t rstep, uint32_t* __restrict__ out32) {
+    stored_rest([&](uint32_t j) -> uint32_t { return d[j]; }, (reinterpret_cast<uintptr_t>(d) & 3) == 0, bn, O, r0,
+                rstep, out32);
+}
 // SPEC (work-list mode, when most blocks were stored in the previous encode): a full block's
 // eight chunks per thread are loaded before pass 0 decides anything, so the block's whole
 // input is in flight during pass 0's test and barriers; otherwise (text: pass 0 rejects the
@@ -2359,6 +2365,72 @@ __device__ __forceinline__ uint32_t store_check_block(const uint8_t* __restrict_
             o.w = sh ? __builtin_amdgcn_alignbyte(w[4], w[3], sh) : w[3];
             *reinterpret_cast<uint4*>(&out32[gw0 + ks + 4 * j]) = o;
         }
+        // The rest of the block (what stored_rest writes; then a block of the stored prefix
+        // is complete, and at any other offset the scan's edge zeroing and K4 overwrite it),
+        // from registers: wave 0 the words before the quads (header byte, LEN / NLEN, the first
+        // data bytes) and quads 0, 1 if not fast; the last wave quads nq - 2, nq - 1 if not fast
+        // and the words after them.  Source words by ds_bpermute from the wave's lanes (chunks
+        // base .. base + 63 in slot I).  (Staged through LDS after a barrier it cost 20 us on
+        // C4, with global byte loads 42 us; the fill kernel that did it took 10.5 us.)
+#ifndef DMX_K0_NOREST   // (A/B knockout: the fill kernel then writes the rest)
+        if (wave == 0 || wave == SCT / 64 - 1) {
+            const bool front = wave == 0;
+            const uint4 vv = front ? v[0] : v[7];
+            const int32_t base = (int32_t)(wave * 64 + (front ? 0 : 7) * SCT);
+            auto dword = [&](int32_t iw) -> uint32_t {   // input word iw, 0 outside the wave's chunks
+                const int32_t src = (iw >> 2) - base;
+                const bool ok = iw >= 0 && src >= 0 && src < 64 && 4 * iw < (int32_t)bn;
+                const int a = (ok ? src : 0) << 2;
+                const uint32_t x = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)vv.x);
+                const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)vv.y);
+                const uint32_t z = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)vv.z);
+                const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)vv.w);
+                const uint32_t c = (uint32_t)iw & 3u;
+                return ok ? (c == 0 ? x : c == 1 ? y : c == 2 ? z : w) : 0u;
+            };
+            auto fastq = [&](uint32_t jq) {
+                const int64_t q0 = (int64_t)(4 * (ks + 4 * jq)) - (int64_t)B0;
+                return q0 >= 0 && (uint64_t)((q0 & ~3ll) + 20) <= bn;
+            };
+            uint32_t k;
+            bool want;
+            if (front) {
+                k = lane;
+                want = lane < ks || (lane < ks + 8 && !fastq((lane - ks) >> 2));
+            } else {
+                k = ks + 4 * (nq - 2) + lane;
+                want = lane < 8 ? !fastq(nq - 2 + (lane >> 2)) : k < nwords;
+            }
+            const int32_t off = (int32_t)(4 * k) - (int32_t)B0;   // the word's first byte in the block's data
+            const int32_t iw = off >> 2;                           // (floor)
+            const uint32_t d0 = dword(iw), d1 = dword(iw + 1), sh2 = (uint32_t)off & 3u;
+            uint32_t val = sh2 ? __builtin_amdgcn_alignbyte(d1, d0, sh2) : d0;
+            const uint32_t lenw = (bn & 0xFFFFu) | ((~bn & 0xFFFFu) << 16);
+            if (off < 0) {   // bytes below B0: the header byte (0) and LEN / NLEN
+#pragma unroll
+                for (uint32_t i = 0; i < 4; i++) {
+                    const uint32_t q = 4 * k + i;
+                    if (q < B0) {
+                        const uint32_t hb = q >= (P >> 3) ? (lenw >> (8 * (q - (P >> 3)))) & 0xFFu : 0u;
+                        val = (val & ~(0xFFu << (8 * i))) | (hb << (8 * i));
+                    }
+                }
+            }
+            if (want && nq >= 4) {
+                if (k == 0 || k == nwords - 1) {   // edge words: this block's bytes only
+                    uint8_t* o8 = reinterpret_cast<uint8_t*>(out32 + gw0);
+                    const uint32_t ebyte = B0 + bn;
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; i++) {
+                        const uint32_t q = 4 * k + i;
+                        if (q >= (s0 >> 3) && q < ebyte) o8[q] = (uint8_t)(val >> (8 * i));
+                    }
+                } else {
+                    out32[gw0 + k] = val;
+                }
+            }
+        }
+#endif
     } else if (pass_s) {
         const uint64_t O = spec_stored_bit(b, sw, flags);
         const bool dal = (reinterpret_cast<uintptr_t>(d) & 3) == 0;
@@ -2574,11 +2646,10 @@ __global__ __launch_bounds__(WLT) void dmx_worklist_kernel(uint32_t nblk, uint32
     }
 }
 
-// After K4 (work-list mode), the blocks K4 skipped (a wave per 4 blocks):
-//  * a block of the stored prefix (wl_skip) gets the bytes K0's speculative copy left out
-//    (stored_rest).  (Measured elsewhere: in K0 itself the tail's dependent byte loads made
-//    every workgroup longer, 488 -> 530 us on C4; in K4's list grid, 4 blocks per 16 lanes in
-//    sequence, 27 us against this kernel's 11);
+// After K4 (work-list mode), the blocks K4 skipped (a wave per 4 blocks), launched only when
+// there are such blocks that K0 did not complete:
+//  * a block of the stored prefix (wl_skip) that is not a full 16-byte aligned block gets the
+//    bytes K0's speculative copy left out (stored_rest; K0 writes a full block's rest itself);
 //  * a dup (uniform-block dedupe) gets its representative's bit string: output word k of the
 //    dup holds the representative's bits shifted by the two offsets' difference, masked to
 //    the dup's own bits (its two edge words, shared with its neighbours and zeroed by the
@@ -2591,10 +2662,16 @@ __global__ __launch_bounds__(256) void dmx_fill_kernel(const uint8_t* __restrict
     if (res->status) return;
     // a wave covers the 4 blocks b0 .. b0 + 3
     const uint32_t lane = threadIdx.x & 63, b0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 4;
-    {   // a block of the stored prefix (full: not the last block), at its speculative offset: 16 lanes
+    {   // a block of the stored prefix that K0 did not complete (not a full 16-byte aligned
+        // block: K0 writes the rest of those itself), at its speculative offset: 16 lanes
         const uint32_t b = b0 + (lane >> 4);
+        const uint8_t* d = in + (uint64_t)b * sw;
+#ifdef DMX_K0_NOREST
         if (b < nblk && wl_skip(b, wl[WL_M], nblk))
-            stored_rest(in + (uint64_t)b * sw, sw, spec_stored_bit(b, sw, flags), lane & 15, 16, out32);
+#else
+        if (b < nblk && wl_skip(b, wl[WL_M], nblk) && !(sw == SCT * 16 * 8 && (reinterpret_cast<uintptr_t>(d) & 15) == 0))
+#endif
+            stored_rest(d, sw, spec_stored_bit(b, sw, flags), lane & 15, 16, out32);
     }
     if (!dedupe) return;
     for (uint32_t i = 0; i < 4; i++) {   // dups: the whole wave per block
@@ -4293,7 +4370,7 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply_kernel(dmx_blkinfo* 
         return;
     }
     // work lists: a block of the whole-copy prefix has its quads from K0 and gets the rest of
-    // its bytes from the fill kernel (stored_rest, byte stores): nothing to zero; every other block zeroes its edge words -- only its own bytes where the neighbour is a
+    // its bytes from K0 too (or the fill kernel: stored_rest, byte stores): nothing to zero; every other block zeroes its edge words -- only its own bytes where the neighbour is a
     // whole-copy block (that boundary is a byte boundary: both sides are stored blocks at their
     // speculative offsets) -- and goes on K4's list
     const uint32_t M = wl[WL_M];
@@ -4653,7 +4730,7 @@ struct dmx_ctx {
     uint64_t cap_split;
     uint32_t want;        // DMX_F_SPLIT / DMX_F_DICT: scratch kept reserved with the workspace
     // timing: a ring of event sets so timed encodes never block the host
-    int timing;
+    int timing;       // bit k: record event k (set_timing: 1 = all six, 0x100 | s = stage s's two)
     hipEvent_t ev[DMX_EV_RING][6];
     int ev_used[DMX_EV_RING];
     uint32_t ev_next;
@@ -4894,13 +4971,16 @@ extern "C" void dmx_ctx_destroy(dmx_ctx* c) {
 static void ctx_collect_set(dmx_ctx* c, int j) {
     if (!c->ev_used[j]) return;
     c->ev_used[j] = 0;
-    if (hipEventSynchronize(c->ev[j][5]) != hipSuccess) return;
+    const int m = c->timing;
+    int last = 5;
+    while (last > 0 && !((m >> last) & 1)) last--;
+    if (hipEventSynchronize(c->ev[j][last]) != hipSuccess) return;
     for (int k = 0; k < 5; k++) {
         float ms = 0.f;
-        if (hipEventElapsedTime(&ms, c->ev[j][k], c->ev[j][k + 1]) == hipSuccess) c->stage_ms[k] += ms;
+        if (((m >> k) & 3) == 3 && hipEventElapsedTime(&ms, c->ev[j][k], c->ev[j][k + 1]) == hipSuccess) c->stage_ms[k] += ms;
     }
     float tot = 0.f;
-    if (hipEventElapsedTime(&tot, c->ev[j][0], c->ev[j][5]) == hipSuccess) c->stage_ms[5] += tot;
+    if ((m & 0x21) == 0x21 && hipEventElapsedTime(&tot, c->ev[j][0], c->ev[j][5]) == hipSuccess) c->stage_ms[5] += tot;
     c->stage_n++;
 }
 
@@ -4974,7 +5054,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         ctx_collect_set(c, j);
         ev = c->ev[j];
         c->ev_used[j] = 1;
-        (void)hipEventRecord(ev[0], s);
+        if (c->timing & 1) (void)hipEventRecord(ev[0], s);
     }
     if (nblk) {
         // diagnostic phase stamps (DMX_STAMPS=1 when the context was reserved)
@@ -4995,12 +5075,12 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                                dim3(SCT), 0, s, (const uint8_t*)d_in, n,
                                (uint32_t)o.sw, c->info, c->tok, c->hist, (o.flags & DMX_F_DICT) ? 0u : 1u, o.flags,
                                (uint32_t*)d_out, out_cap, wl ? wl_codes(wl, c->cap_blocks) : NULL);
+        if (ev && ((c->timing >> 1) & 1)) (void)hipEventRecord(ev[1], s);   // (the list builder counts to "match")
         if (wl) {
             hipLaunchKernelGGL(dmx_worklist_kernel, dim3((nblk + WLC * WLT - 1) / (WLC * WLT)), dim3(WLT), 0, s, nblk, wl,
                                (uint64_t)c->cap_blocks,
                                dupa ? 1u : 0u);
         }
-        if (ev) (void)hipEventRecord(ev[1], s);
         const char* dstop = getenv("DMX_DEBUG_STOP");   // diagnostic only (dbg_stop)
         const uint32_t mfl = ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u) |
                              ((o.flags & DMX_F_STORE_CHECK) ? 4u : 0u) | ((o.flags & DMX_F_DEEP) ? 8u : 0u) | (dstop ? ((uint32_t)atoi(dstop) & 3u) << 8 : 0u) |
@@ -5021,7 +5101,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
             if (loop1) hipLaunchKernelGGL((dmx_match_kernel<false, 3, true>), g1, dim3(MT), 0, s, ma);
             else hipLaunchKernelGGL((dmx_match_kernel<false, 3, false>), g1, dim3(MT), 0, s, ma);
         }
-        if (ev) (void)hipEventRecord(ev[2], s);
+        if (ev && ((c->timing >> 2) & 1)) (void)hipEventRecord(ev[2], s);
         if (o.flags & DMX_F_SPLIT)
             {
                 hipLaunchKernelGGL(dmx_split_hist_kernel, dim3(nblk), dim3(SHT), 0, s, c->tok, c->info,
@@ -5035,11 +5115,10 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
             hipLaunchKernelGGL(dmx_huff_kernel, dim3(wl && wsh.list2 ? list_grid(nblk, wsh.n2, 2 * c->ncu, 32 * c->ncu) : nblk),
                                dim3(64), 0, s, c->hist, c->info, c->codes, c->hdr, c->sub, nblk, o.flags,
                                wl && wsh.list2 ? wl : NULL, wl && wsh.list2 ? wl + WL_HDR + c->cap_blocks : NULL, dupk);
-        if (ev) (void)hipEventRecord(ev[3], s);
+        if (ev && ((c->timing >> 3) & 1)) (void)hipEventRecord(ev[3], s);
     } else if (ev) {
-        (void)hipEventRecord(ev[1], s);
-        (void)hipEventRecord(ev[2], s);
-        (void)hipEventRecord(ev[3], s);
+        for (int k = 1; k <= 3; k++)
+            if ((c->timing >> k) & 1) (void)hipEventRecord(ev[k], s);
     }
     const uint32_t ntile = (nblk + SCAN_TILE - 1) / SCAN_TILE;
     if (nblk)
@@ -5052,16 +5131,23 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
     if (nblk)
         hipLaunchKernelGGL(dmx_scan_apply_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, o.flags, c->tiles,
                            (uint32_t*)d_out, (const dmx_result*)c->res, wl, L4, dupk);
-    if (ev) (void)hipEventRecord(ev[4], s);
+    if (ev && ((c->timing >> 4) & 1)) (void)hipEventRecord(ev[4], s);
     if (nblk)
         hipLaunchKernelGGL(dmx_pack_kernel, dim3(wl && wsh.list4 ? list_grid(nblk, wsh.n4, 2 * c->ncu, 16 * c->ncu) : nblk),
                            dim3(PT), 0, s, (const uint8_t*)d_in, (uint32_t)o.sw, c->tok, c->codes, c->hdr, c->info, c->sub,
                            nblk, o.flags, (uint32_t*)d_out, c->res, wl, wl && wsh.list4 ? L4 : NULL, dupk);
-    if (nblk && wl)   // the blocks K4 skipped: dups and the stored prefix (a wave per 4 blocks)
+    // the blocks K4 skipped that K0 did not complete: dups, and the stored prefix unless every
+    // block is a full 16-byte aligned one (a wave per 4 blocks)
+#ifdef DMX_K0_NOREST
+    const bool k0rest = false;
+#else
+    const bool k0rest = o.sw == SCT * 16 * 8 && (reinterpret_cast<uintptr_t>(d_in) & 15) == 0;
+#endif
+    if (nblk && wl && (dupa || !k0rest))
         hipLaunchKernelGGL(dmx_fill_kernel, dim3((nblk + 15) / 16), dim3(256), 0, s, (const uint8_t*)d_in, (uint32_t)o.sw,
                            o.flags, (const dmx_blkinfo*)c->info, (const uint32_t*)wl, (uint64_t)c->cap_blocks, nblk,
                            (uint32_t*)d_out, (const dmx_result*)c->res, dupa ? 1u : 0u);
-    if (ev) (void)hipEventRecord(ev[5], s);
+    if (ev && ((c->timing >> 5) & 1)) (void)hipEventRecord(ev[5], s);
     HIPCHK(fault_hit(2) ? hipErrorLaunchFailure : hipGetLastError());
     c->last_nblk = nblk;
     c->last_sw = (uint32_t)o.sw;
@@ -5087,7 +5173,9 @@ extern "C" int dmx_encode_result(dmx_ctx* c, dmx_result* r, void* stream) {
 extern "C" int dmx_ctx_set_timing(dmx_ctx* c, int enable) {
     (void)hipSetDevice(c->device);
     for (int j = 0; j < DMX_EV_RING; j++) c->ev_used[j] = 0;
-    c->timing = enable;
+    // 1: every stage boundary; 0x100 | s: only stage s's two events (s = 0 .. 4), so a timed
+    // loop pays two event records per encode (each one a gap of a few us between kernels)
+    c->timing = enable == 1 ? 0x3F : (enable & 0x100) ? 3 << (enable & 7) : 0;
     for (int k = 0; k < 6; k++) c->stage_ms[k] = 0;
     c->stage_n = 0;
     return 0;

@@ -233,3 +233,29 @@ def test_worklist_multi_tile(shape):
             os.environ.pop("DMX_DEDUPE", None)
         else:
             os.environ["DMX_DEDUPE"] = old
+
+
+def test_stage_timing_modes():
+    """set_timing: every stage boundary evented, or only one stage's two events (bench.py's
+    timed region); the stream is the same either way."""
+    data = _cases()["noise_prefix_then_text"]
+    fl = D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | D.DMX_F_DEEP
+    e = D.Encoder(0, len(data), max_chain=7, flags=fl)
+    try:
+        want = O.compress(data, max_chain=7, lazy=True, store_check=True, deep=True)
+        e.set_timing(True)
+        for _ in range(3):
+            z, _ = e.compress_bytes(data, max_chain=7, flags=fl)
+            assert z == want
+        st, cnt = e.stage_times()
+        assert cnt == 3 and all(st[k] > 0 for k in ("pre", "match", "huff", "scan", "pack", "total"))
+        for stage in D.Encoder.STAGES:
+            e.set_timing(True, stage=stage)
+            z, _ = e.compress_bytes(data, max_chain=7, flags=fl)
+            assert z == want
+            st, cnt = e.stage_times()
+            assert cnt == 1 and st[stage] > 0, (stage, st)
+            assert all(v == 0 for k, v in st.items() if k != stage), (stage, st)
+        e.set_timing(False)
+    finally:
+        e.close()

@@ -41,6 +41,10 @@ PY
         tail -1 "$OUT/stage_time.txt" ;;
     ktrace) cd /tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ktrace_$nb" -o run -- python3 "$R/tools/stage_time.py" ${arg//,/ } >> "$OUT/ktrace.txt" 2>&1 || exit 3
            f=$(find "$OUT/ktrace_$nb" -name "*kernel_stats.csv" | head -1); cp "$f" "$OUT/kernel_stats_$nb.csv"; cut -d, -f1-4 "$OUT/kernel_stats_$nb.csv" | head -14; nb=$((nb + 1)); cd "$R" ;;
+    pipe) a2=${arg//,/ }; lv=""   # pipe_time.py [libv=NAME] MB K FLAGS KIND STEPS
+        if [[ $a2 == libv=* ]]; then lv=${a2%% *}; lv=${lv#libv=}; a2=${a2#* }; fi
+        ( [ -n "$lv" ] && export DMX_LIBV="$R/build/var/libdmx_$lv.so"; timeout -k 10 300 python3 "$R/tools/pipe_time.py" $a2 ) >> "$OUT/pipe.txt" 2>&1 || exit 3
+        tail -1 "$OUT/pipe.txt" ;;
     fdchunk) timeout -k 10 300 python3 "$R/tools/fd_chunk.py" ${arg//,/ } > "$OUT/fdchunk.txt" 2>&1 || exit 3; cat "$OUT/fdchunk.txt" ;;
     deep) timeout -k 10 300 python3 "$R/tools/deep_bench.py" 32 > "$OUT/deep.txt" 2>&1 || exit 3; cat "$OUT/deep.txt" ;;
     trace) cd /tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --cpu-budget 0 --exhaustive-steps 0 --tradeoff= --long-run 0 ${arg//,/ } > "$OUT/bench_trace.json" 2> "$OUT/trace.err" || exit 3
