@@ -10,6 +10,9 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import deflate_compression_amd as D
 
+if os.environ.get("DMX_LIBV"):   # a variant built beside libdmx.so (tools/build_var.sh)
+    D.LIB_PATH = os.environ["DMX_LIBV"]
+
 
 def main():
     mb = float(sys.argv[1]) if len(sys.argv) > 1 else 100
@@ -36,7 +39,7 @@ def main():
                 assert rc == 0, rc
                 if best is None or t1 - t0 < best:
                     best, st = t1 - t0, D.fd_last_stats()
-            print(json.dumps({"chunk_mb": cm, "GBps": round(n / best / 1e9, 3), "ms": round(best * 1e3, 3),
+            print(json.dumps({"lib": os.path.basename(D.LIB_PATH), "chunk_mb": cm, "GBps": round(n / best / 1e9, 3), "ms": round(best * 1e3, 3),
                               "stages": st}), flush=True)
     finally:
         os.remove(fi)
