@@ -62,7 +62,7 @@ def parse_args(argv=None):
                          "fastest K inside the <= 2 %% size budget vs S_ref on every reference-held text "
                          "with --deep, profiles/r04_size/size_table.md)")
     ap.add_argument("--deep", type=int, default=int(os.environ.get("DMX_DEEP", "1")),
-                    help="1 = adaptive chain depth: small-alphabet blocks search 64 deep (DMX_F_DEEP)")
+                    help="1 = adaptive chain depth: small-alphabet blocks search 32 deep (DMX_F_DEEP, DMX_DEEP_CHAIN)")
     ap.add_argument("--lazy", type=int, default=int(os.environ.get("DMX_LAZY", "1")),
                     help="1 = lazy evaluation parse (DMX_F_LAZY, SURVEY §8 f2)")
     ap.add_argument("--split", type=int, default=int(os.environ.get("DMX_SPLIT", "0")),

@@ -194,7 +194,7 @@ int deflate_compress(int fd_in, int fd_out, int fd_stats, swi sw, int ops) {
     if (sc && atoi(sc) > 0 && fd_stats < 0) o.flags |= DMX_F_STORE_CHECK;
     const char* dp = getenv("DMX_DEEP");   /* 1 = adaptive chain depth (DMX_F_DEEP, bounded mode) */
     if (dp && atoi(dp) > 0) o.flags |= DMX_F_DEEP;
-    const char* dd = getenv("DMX_DEEP_CHAIN");   /* DMX_F_DEEP depth (0 / unset = 64) */
+    const char* dd = getenv("DMX_DEEP_CHAIN");   /* DMX_F_DEEP depth (0 / unset = DMX_DEEP_CHAIN, 32) */
     o.deep_chain = dd ? atoi(dd) : 0;
     o.dict = NULL;
     o.dict_len = 0;

@@ -156,9 +156,10 @@ struct compress_stats {
                             K < 64 -- a block whose trigrams are few (D distinct 13-bit
                             buckets among its positions p mod 2048 < 256, 4 D < samples:
                             small alphabets such as binary digits, hex, DNA) searches its
-                            own chains 64 deep instead of K (dmx_opts.deep_chain sets
-                            another depth).  Text never qualifies. */
-#define DMX_DEEP_CHAIN 64
+                            own chains 32 deep instead of K (dmx_opts.deep_chain sets
+                            another depth; 32 is the cheapest depth that keeps every
+                            reference-held text file within 2 % of the reference parse).  Text never qualifies. */
+#define DMX_DEEP_CHAIN 32
 
 typedef struct {
     int32_t sw;        /* block size 1..32768 (0 = 32768) */

@@ -90,7 +90,7 @@ def _lz(lazy: bool, deep: bool) -> int:
 
 
 def set_deep_chain(k: int) -> None:
-    """The depth DMX_F_DEEP gives small-alphabet blocks (0 = 64), as dmx_opts.deep_chain."""
+    """The depth DMX_F_DEEP gives small-alphabet blocks (0 = 32), as dmx_opts.deep_chain."""
     lib().dmx_oracle_set_deep_chain(int(k))
 
 

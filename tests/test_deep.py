@@ -8,7 +8,7 @@ import pytest
 from oracle import oracle as O
 from tests.deep_inputs import bitdump, inputs
 
-DEEP_K = 64
+DEEP_K = 32   # DMX_DEEP_CHAIN (round 5; 64 before)
 
 
 def rule(block: bytes, k: int) -> int:
@@ -54,8 +54,8 @@ def test_block_chain_edge_sizes(n):
 
 
 @pytest.mark.parametrize("lazy", [False, True])
-def test_deep_parse_equals_k64_on_deep_blocks(lazy):
-    """A deep block's parse is the K = 64 parse; a text block's is the K parse."""
+def test_deep_parse_equals_deep_k_on_deep_blocks(lazy):
+    """A deep block's parse is the K = DEEP_K parse; a text block's is the K parse."""
     d = inputs()
     for name in ("bitdump", "text"):
         blk = d[name][:32768]
@@ -83,14 +83,14 @@ def test_deep_streams_inflate_and_shrink():
 
 def test_oracle_deep_chain_setting():
     """dmx_oracle_set_deep_chain (the GPU's dmx_opts.deep_chain): a deep block gets that depth,
-    0 restores 64; K >= the depth is left alone."""
+    0 restores DEEP_K; K >= the depth is left alone."""
     from tests.deep_inputs import inputs
     blk = inputs()["bitdump"][:32768]
     try:
-        assert O.block_chain(blk, 7) == 64
+        assert O.block_chain(blk, 7) == DEEP_K
         O.set_deep_chain(24)
         assert O.block_chain(blk, 7) == 24
         assert O.block_chain(blk, 30) == 30
     finally:
         O.set_deep_chain(0)
-    assert O.block_chain(blk, 7) == 64
+    assert O.block_chain(blk, 7) == DEEP_K

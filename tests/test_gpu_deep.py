@@ -53,7 +53,7 @@ def test_deep_tokens_per_block(enc):
         blk = data[o:o + 32768]
         depths.add(O.block_chain(blk, 8))
         assert np.array_equal(enc.tokens(b), O.parse_block(blk, 8, lazy=True, deep=True)), b
-    assert depths == {8, 64}   # both kinds of block in one launch
+    assert depths == {8, 32}   # both kinds of block in one launch (DMX_DEEP_CHAIN = 32)
 
 
 @pytest.mark.parametrize("sw", [4096, 2049, 300])
@@ -86,14 +86,14 @@ def test_deep_with_block_options(enc, extra):
 
 
 def test_deep_off_for_exhaustive_and_long_chains(enc):
-    """max_chain 0 (the reference parse) and K >= 64 ignore the flag."""
+    """max_chain 0 (the reference parse) and K >= the depth (32) ignore the flag."""
     data = inputs()["bitdump"][:70000]
-    for k in (0, 64, 100):
+    for k in (0, 32, 64, 100):
         z, _ = enc.compress_bytes(data, max_chain=k, flags=D.DMX_ZLIB | D.DMX_F_DEEP)
         assert z == O.compress(data, max_chain=k), k
 
 
-@pytest.mark.parametrize("depth", [16, 24, 32])
+@pytest.mark.parametrize("depth", [16, 24, 48, 64])
 def test_deep_chain_depths(enc, depth):
     """dmx_opts.deep_chain: small-alphabet blocks search `depth` deep (the oracle at the same
     depth, dmx_oracle_set_deep_chain), at the headline parse."""

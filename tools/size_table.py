@@ -62,7 +62,7 @@ def main() -> None:
         f.write("# Bounded lazy parse vs S_ref on reference-held text (oracle, `tools/size_table.py`)\n\n")
         f.write("S_ref = the reference-semantics stream (exhaustive greedy, 32 KiB blocks). Columns: "
                 "stream size of the K-candidate lazy parse (store check on) relative to S_ref; \"deep\" = "
-                "with DMX_F_DEEP (small-alphabet blocks search 64 deep; the bench default is K=7 lazy deep). "
+                "with DMX_F_DEEP (small-alphabet blocks search DMX_DEEP_CHAIN deep, 32 since round 5; the bench default is K=7 lazy deep). "
                 "The reference's files are read as input bytes only.\n\n")
         hd = [f"K={k} lazy" + (" deep" if d else "") for k, d in COLS]
         f.write("| Input | Bytes | S_ref bytes | " + " | ".join(hd) + " |\n")
