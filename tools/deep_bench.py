@@ -14,6 +14,9 @@ import torch  # noqa: E402
 import deflate_compression_amd as D  # noqa: E402
 from tests.deep_inputs import bitdump  # noqa: E402
 
+if os.environ.get("DMX_LIBV"):   # a variant built beside libdmx.so (tools/build_var.sh)
+    D.LIB_PATH = os.environ["DMX_LIBV"]
+
 
 def main():
     mb = int(sys.argv[1]) if len(sys.argv) > 1 else 32

@@ -49,7 +49,9 @@ PY
         if [[ $a2 == libv=* ]]; then lv=${a2%% *}; lv=${lv#libv=}; a2=${a2#* }; fi
         ( [ -n "$lv" ] && export DMX_LIBV="$R/build/var/libdmx_$lv.so"; timeout -k 10 300 python3 "$R/tools/fd_chunk.py" $a2 ) >> "$OUT/fdchunk.txt" 2>&1 || exit 3
         grep chunk_mb "$OUT/fdchunk.txt" | tail -3 ;;
-    deep) timeout -k 10 300 python3 "$R/tools/deep_bench.py" 32 > "$OUT/deep.txt" 2>&1 || exit 3; cat "$OUT/deep.txt" ;;
+    deep) lv=${arg#libv=}   # deep[:libv=NAME]
+        ( [ -n "$arg" ] && export DMX_LIBV="$R/build/var/libdmx_$lv.so"; timeout -k 10 300 python3 "$R/tools/deep_bench.py" 32 ) >> "$OUT/deep.txt" 2>&1 || exit 3
+        grep -v amdgpu "$OUT/deep.txt" | tail -4 ;;
     trace) cd /tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --cpu-budget 0 --exhaustive-steps 0 --tradeoff= --long-run 0 ${arg//,/ } > "$OUT/bench_trace.json" 2> "$OUT/trace.err" || exit 3
            find "$OUT/trace" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \; ; cut -d, -f1-8 "$OUT/kernel_stats.csv" | head -20; cd "$R" ;;
     *) echo "unknown step $name"; exit 2 ;;

@@ -1,13 +1,18 @@
 """Diagnostic: per-phase cycle stamps of the match kernel (run with DMX_STAMPS=1)."""
 import os, sys, json
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.chdir(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ["DMX_STAMPS"] = "1"
 import numpy as np, torch
 import deflate_compression_amd as D
 if os.environ.get("DMX_LIBV"): D.LIB_PATH = os.environ["DMX_LIBV"]
 
 def run(kind, n, mc, flags=D.DMX_ZLIB | D.DMX_F_LAZY):
-    a = D.gen_text(n, 0xE5818) if kind == "text" else (D.gen_random(n, 1) if kind == "random" else np.zeros(n, np.uint8))
+    if kind == "bitdump":   # the small-alphabet input of tests/deep_inputs.py
+        from tests.deep_inputs import bitdump
+        a = np.frombuffer(bitdump(n, 1), dtype=np.uint8).copy()
+    else:
+        a = D.gen_text(n, 0xE5818) if kind == "text" else (D.gen_random(n, 1) if kind == "random" else np.zeros(n, np.uint8))
     t = torch.from_numpy(a).cuda()
     e = D.Encoder(0, n, max_chain=mc, flags=flags)
     for _ in range(2):
@@ -30,10 +35,12 @@ def run(kind, n, mc, flags=D.DMX_ZLIB | D.DMX_F_LAZY):
                       **({"hist_staged_kcyc": round(st[1:, 12].mean() / 1e3, 1), "hist_total_kcyc": round(st[1:, 13].mean() / 1e3, 1)}
                          if flags & D.DMX_F_DICT else {})}))
 
-# args: kind:max_chain[:opts]  (opts: d = with the cross-block dictionary, DMX_F_DICT; g = greedy, no lazy)
+# args: kind:max_chain[:opts]  (opts: d = with the cross-block dictionary, DMX_F_DICT; g = greedy, no lazy;
+# e = DMX_F_DEEP; kind text | random | zeros | bitdump)
 cfgs = [("text", 1, ""), ("text", 16, ""), ("text", 0, ""), ("random", 0, ""), ("zeros", 0, "")]
 if len(sys.argv) > 1:
     cfgs = [(a.split(":") + [""])[:3] for a in sys.argv[1:]]
 for kind, mc, opt in cfgs:
-    fl = D.DMX_ZLIB | (0 if "g" in opt else D.DMX_F_LAZY) | (D.DMX_F_DICT if "d" in opt else 0)
-    run(kind, 20_000_000 if kind == "text" else 64 << 20, int(mc), fl)
+    fl = D.DMX_ZLIB | (0 if "g" in opt else D.DMX_F_LAZY) | (D.DMX_F_DICT if "d" in opt else 0) | \
+        (D.DMX_F_DEEP if "e" in opt else 0)
+    run(kind, 20_000_000 if kind == "text" else (4 << 20 if kind == "bitdump" else 64 << 20), int(mc), fl)
