@@ -451,11 +451,13 @@ class Encoder:
 
     STAGES = ("pre", "match", "huff", "scan", "pack")
 
-    def set_timing(self, on: bool, stage: str | None = None) -> None:
+    def set_timing(self, on: bool, stage: str | None = None, every: int = 1) -> None:
         """HIP-event stage times of the following encodes: every stage boundary, or with
         `stage` only that stage's two events (a timed loop then pays two event records per
-        encode; the other stages read 0)."""
-        mode = 0 if not on else (1 if stage is None else 0x100 | self.STAGES.index(stage))
+        encode; the other stages read 0), on every `every`-th encode (1..255)."""
+        if not 1 <= every <= 255:
+            raise ValueError("every must be 1..255")
+        mode = 0 if not on else (1 if stage is None else 0x100 | self.STAGES.index(stage) | (every << 12))
         self._L.dmx_ctx_set_timing(self._ctx, mode)
 
     def stage_times(self):

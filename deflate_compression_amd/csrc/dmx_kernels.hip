@@ -4734,6 +4734,7 @@ struct dmx_ctx {
     hipEvent_t ev[DMX_EV_RING][6];
     int ev_used[DMX_EV_RING];
     uint32_t ev_next;
+    uint32_t ev_every, ev_count;   // with a one-stage mask: events on every ev_every-th encode only
     double stage_ms[6];
     uint32_t stage_n;
 };
@@ -5049,7 +5050,7 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
     const uint16_t* dupk = dedupe ? wl_codes((const uint32_t*)wl, c->cap_blocks) : NULL;   // dup bits (bit 3)
     const uint32_t* dupa = dedupe ? wl_dup(wl, c->cap_blocks) : NULL;                      // their representatives
     hipEvent_t* ev = NULL;
-    if (c->timing) {
+    if (c->timing && (c->ev_every <= 1 || c->ev_count++ % c->ev_every == 0)) {
         const int j = (int)(c->ev_next++ % DMX_EV_RING);
         ctx_collect_set(c, j);
         ev = c->ev[j];
@@ -5176,6 +5177,10 @@ extern "C" int dmx_ctx_set_timing(dmx_ctx* c, int enable) {
     // 1: every stage boundary; 0x100 | s: only stage s's two events (s = 0 .. 4), so a timed
     // loop pays two event records per encode (each one a gap of a few us between kernels)
     c->timing = enable == 1 ? 0x3F : (enable & 0x100) ? 3 << (enable & 7) : 0;
+    // 0x100 | s | every << 12: events on every `every`-th encode only (sampling the stage
+    // inside a timed loop at a fraction of the event records' idle)
+    c->ev_every = (enable & 0x100) ? ((uint32_t)enable >> 12) & 0xFFu : 0u;
+    c->ev_count = 0;
     for (int k = 0; k < 6; k++) c->stage_ms[k] = 0;
     c->stage_n = 0;
     return 0;

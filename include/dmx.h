@@ -324,8 +324,9 @@ int dmx_last_subblock(dmx_ctx* ctx, uint32_t blk, uint32_t sub, uint32_t* tok_ra
  * (bench): enable, then read the mean milliseconds per launch of each stage
  * {chain, match, huff, scan, pack} and of the whole encode, and the number of timed encodes.
  * enable: 0 off, 1 every stage boundary, 0x100 | s only stage s's two events (s = 0..4; the
- * other stages and the whole encode read 0).  Each event record costs a few microseconds of
- * idle between kernels. */
+ * other stages and the whole encode read 0), and with | every << 12 (every = 2..255) on
+ * every `every`-th encode only.  Each event record costs a few microseconds of idle
+ * between kernels. */
 int dmx_ctx_set_timing(dmx_ctx* ctx, int enable);
 int dmx_ctx_stage_times(dmx_ctx* ctx, double* ms6, uint32_t* count);
 

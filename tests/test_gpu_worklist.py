@@ -256,6 +256,12 @@ def test_stage_timing_modes():
             st, cnt = e.stage_times()
             assert cnt == 1 and st[stage] > 0, (stage, st)
             assert all(v == 0 for k, v in st.items() if k != stage), (stage, st)
+        e.set_timing(True, stage="match", every=3)   # events on encodes 0, 3, 6 of 7
+        for _ in range(7):
+            z, _ = e.compress_bytes(data, max_chain=7, flags=fl)
+            assert z == want
+        st, cnt = e.stage_times()
+        assert cnt == 3 and st["match"] > 0
         e.set_timing(False)
     finally:
         e.close()
