@@ -265,3 +265,21 @@ def test_stage_timing_modes():
         e.set_timing(False)
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("shift", [1, 4, 8])
+@pytest.mark.parametrize("shape", ["list", None])
+def test_worklist_unaligned_input(enc, shape, shift):
+    """A device input that is not 16-byte aligned: K0 takes its general path (no register
+    copy) and the fill kernel writes the rest of the stored prefix; the stream is the oracle's."""
+    data = _cases()["noise_prefix_then_text"]
+    fl = D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | D.DMX_F_DEEP
+    want = O.compress(data, max_chain=7, lazy=True, store_check=True, deep=True)
+    buf = torch.zeros(len(data) + 64, dtype=torch.uint8, device="cuda")
+    buf[shift:shift + len(data)] = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).cuda()
+    t = buf[shift:shift + len(data)]
+    assert t.data_ptr() % 16 == shift % 16
+    for rep in range(2):
+        z, r = _with_env(shape, lambda: enc.compress_tensor(t, opts=D.Opts(B, 7, fl, 0)))
+        assert r.status == 0
+        assert z.cpu().numpy().tobytes() == want, (shape, shift, rep)
