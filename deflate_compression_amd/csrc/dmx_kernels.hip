@@ -2471,6 +2471,9 @@ __global__ __launch_bounds__(SCT) void dmx_store_check_kernel(const uint8_t* __r
 // (counts, M, K1's claim counter and K4's list zeroed) and the hint.  (Round 5's first builder
 // was one workgroup sweeping every block twice: 21 us at 32 768 blocks, latency-bound; this
 // one reads each code at most once per workgroup and its workgroups run side by side.)
+// The prefix sweeps add up to ntile^2 / 2 x 8 KB of (L2 / MALL) reads: nothing at 1 GiB (8
+// tiles), 64 MB at 16 GiB (128 tiles), ~20 GB at 288 GB -- small against those encodes'
+// own traffic; the last tile's sweep is ~275 rounds of 4 x 16-byte loads per thread there.
 // Dedupe: each byte value's representative is its first full uniform block in the stream, so
 // for a tile it is either before the tile (the prefix sweep sees it) or inside it; the dups
 // before the tile number (candidates before it) - (byte values among them).
