@@ -5427,25 +5427,106 @@ static void* pread_job(void* a) {
     if (done < j->len) j->rc = -(int)E_NEXIST;   // the file shrank under us
     return NULL;
 }
+// The reader's pread helpers: FD_READERS - 1 threads started once per process (on the first
+// chunk read) and woken per chunk, instead of FD_READERS - 1 pthread_create / join per chunk.
+// Used by one reader at a time (dmx_encode_fd's, under g_mu).
+struct PreadPool {
+    pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+    pthread_cond_t work = PTHREAD_COND_INITIALIZER, done = PTHREAD_COND_INITIALIZER;
+    uint64_t gen = 0;
+    int pending = 0, nth = 0;
+    PreadJob* jobs = nullptr;
+    int njobs = 0;
+};
+static PreadPool g_pp;
+struct PreadWorker { int idx; };
+static PreadWorker g_ppw[FD_READERS];
+static void* pread_worker(void* a) {
+    const int idx = ((PreadWorker*)a)->idx;
+    uint64_t seen = 0;
+    for (;;) {
+        pthread_mutex_lock(&g_pp.mu);
+        while (g_pp.gen == seen) pthread_cond_wait(&g_pp.work, &g_pp.mu);
+        seen = g_pp.gen;
+        PreadJob* j = idx < g_pp.njobs ? &g_pp.jobs[idx] : nullptr;
+        pthread_mutex_unlock(&g_pp.mu);
+        if (j) pread_job(j);
+        pthread_mutex_lock(&g_pp.mu);
+        if (--g_pp.pending == 0) pthread_cond_signal(&g_pp.done);
+        pthread_mutex_unlock(&g_pp.mu);
+    }
+    return NULL;
+}
+// a forked child has none of the pool's threads: it starts its own on its first read
+static void pread_pool_atfork_child() {
+    pthread_mutex_init(&g_pp.mu, NULL);
+    pthread_cond_init(&g_pp.work, NULL);
+    pthread_cond_init(&g_pp.done, NULL);
+    g_pp.gen = 0;
+    g_pp.pending = 0;
+    g_pp.nth = 0;
+}
+// jobs[0] runs on the calling thread, jobs[1..nj) on the pool (inline where it has no thread)
+static void pread_run(PreadJob* jobs, int nj) {
+    static bool atfork = false;
+    if (!atfork) atfork = pthread_atfork(NULL, NULL, pread_pool_atfork_child) == 0;
+    if (g_pp.nth == 0) {   // start the pool (threads that fail to start leave their jobs inline)
+        for (int k = 1; k < FD_READERS; k++) {
+            g_ppw[k].idx = k;
+            pthread_t t;
+            pthread_attr_t at;
+            pthread_attr_init(&at);
+            pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
+            const bool ok = pthread_create(&t, &at, pread_worker, &g_ppw[k]) == 0;
+            pthread_attr_destroy(&at);
+            if (!ok) break;
+            g_pp.nth = k;
+        }
+        if (g_pp.nth == 0) g_pp.nth = -1;   // no threads: everything inline
+    }
+    const int nth = g_pp.nth > 0 ? g_pp.nth : 0;   // workers 1..nth
+    if (nth) {
+        pthread_mutex_lock(&g_pp.mu);
+        g_pp.jobs = jobs;
+        g_pp.njobs = nj < nth + 1 ? nj : nth + 1;
+        g_pp.pending = nth;
+        g_pp.gen++;
+        pthread_cond_broadcast(&g_pp.work);
+        pthread_mutex_unlock(&g_pp.mu);
+    }
+    if (nj > 0) pread_job(&jobs[0]);
+    for (int k = nth + 1; k < nj; k++) pread_job(&jobs[k]);   // jobs without a worker
+    if (nth) {
+        pthread_mutex_lock(&g_pp.mu);
+        while (g_pp.pending > 0) pthread_cond_wait(&g_pp.done, &g_pp.mu);
+        pthread_mutex_unlock(&g_pp.mu);
+    }
+}
+
 static int64_t fd_read_chunk(FdReader* R, uint8_t* b, uint64_t chunk) {
     if (R->seekable) {
         const uint64_t left = R->size - R->off, len = left < chunk ? left : chunk;
         const uint64_t piece = ((len + FD_READERS - 1) / FD_READERS + 4095) & ~4095ull;
         PreadJob jobs[FD_READERS];
+        int nj = 0;
+        for (uint64_t o = 0; o < len; o += piece, nj++)
+            jobs[nj] = {R->fd, b + o, R->off + o, (len - o) < piece ? (len - o) : piece, 0};
+#ifdef DMX_FD_SPAWN   // (A/B build: a thread per piece per chunk, as before round 5)
         pthread_t th[FD_READERS];
         bool started[FD_READERS] = {};
-        int nj = 0;
-        for (uint64_t o = 0; o < len; o += piece, nj++) {
-            jobs[nj] = {R->fd, b + o, R->off + o, (len - o) < piece ? (len - o) : piece, 0};
-            if (nj > 0 && pthread_create(&th[nj], NULL, pread_job, &jobs[nj]) == 0) started[nj] = true;
-            else if (nj > 0) pread_job(&jobs[nj]);
+        for (int k = 1; k < nj; k++) {
+            if (pthread_create(&th[k], NULL, pread_job, &jobs[k]) == 0) started[k] = true;
+            else pread_job(&jobs[k]);
         }
         if (nj > 0) pread_job(&jobs[0]);
-        int rc = 0;
-        for (int k = 0; k < nj; k++) {
+        for (int k = 1; k < nj; k++)
             if (started[k]) pthread_join(th[k], NULL);
+#else
+        pread_run(jobs, nj);
+#endif
+        int rc = 0;
+        for (int k = 0; k < nj; k++)
             if (jobs[k].rc) rc = jobs[k].rc;
-        }
         if (rc) return rc;
         R->off += len;
         R->eof = R->off >= R->size;
