@@ -432,3 +432,39 @@ def test_uniform_blocks_closed_form(enc, check, k, lazy):
     z, _ = enc.compress_bytes(data, max_chain=k, flags=fl)
     assert z == O.compress(data, max_chain=k, lazy=lazy, store_check=check)
     assert zlib.decompress(z) == data
+
+
+@pytest.mark.parametrize("n", [5000, (9 << 20) + 123])
+def test_fd_api_output_offset_and_append(tmp_path, n):
+    """fd_out is written from its current offset (positioned parallel writes on a regular file)
+    and left at the stream's end, as write() would; an O_APPEND fd takes write() and appends."""
+    import os
+    text = D.gen_text(n, 93).tobytes()
+    fi = tmp_path / "in"
+    fi.write_bytes(text)
+    env = {"DMX_CHUNK_MB": "4", "DMX_MAX_CHAIN": "7", "DMX_LAZY": "1"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        fo = tmp_path / "out"
+        with open(fi, "rb") as a:
+            b = os.open(fo, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+            os.write(b, b"HDR")
+            assert D.deflate_compress(a.fileno(), b, -1, 32768, 0) == 0
+            end = os.lseek(b, 0, os.SEEK_CUR)
+            os.write(b, b"END")
+            os.close(b)
+        got = fo.read_bytes()
+        assert got[:3] == b"HDR" and got[-3:] == b"END" and end == len(got) - 3
+        z = got[3:-3]
+        assert zlib.decompress(z) == text
+        fa = tmp_path / "app"
+        fa.write_bytes(b"PRE")
+        with open(fi, "rb") as a:
+            b = os.open(fa, os.O_WRONLY | os.O_APPEND)
+            assert D.deflate_compress(a.fileno(), b, -1, 32768, 0) == 0
+            os.close(b)
+        assert fa.read_bytes() == b"PRE" + z
+    finally:
+        for k, v in old.items():
+            os.environ.pop(k, None) if v is None else os.environ.__setitem__(k, v)

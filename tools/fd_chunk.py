@@ -1,5 +1,6 @@
-"""Diagnostic: the drop-in fd path into /dev/null (bench.py's end_to_end sink_devnull leg) at
-several DMX_CHUNK_MB values, with the bench's parse settings; best of 5 per chunk size.
+"""Diagnostic: the drop-in fd path into /dev/null (bench.py's end_to_end sink_devnull leg; with
+FD_SINK_FILE=1 into a file next to the input) at several DMX_CHUNK_MB values, with the bench's
+parse settings; best of 5 per chunk size.
     python tools/fd_chunk.py [MB] [chunk_mb ...]"""
 import json
 import os
@@ -30,7 +31,8 @@ def main():
             best, st = None, None
             for _ in range(5):
                 a = os.open(fi, os.O_RDONLY)
-                b = os.open(os.devnull, os.O_WRONLY)
+                b = os.open(os.devnull, os.O_WRONLY) if not os.environ.get("FD_SINK_FILE") else \
+                    os.open(os.path.join(td, "out"), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
                 t0 = time.perf_counter()
                 rc = D.deflate_compress(a, b, -1, 32768, 0)
                 t1 = time.perf_counter()
@@ -42,7 +44,8 @@ def main():
             print(json.dumps({"lib": os.path.basename(D.LIB_PATH), "chunk_mb": cm, "GBps": round(n / best / 1e9, 3), "ms": round(best * 1e3, 3),
                               "stages": st}), flush=True)
     finally:
-        os.remove(fi)
+        for f in os.listdir(td):
+            os.remove(os.path.join(td, f))
         os.rmdir(td)
 
 
