@@ -4394,6 +4394,147 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply_kernel(dmx_blkinfo* 
     L4[atomicAdd(&wl[WL_N4], 1u)] = b;
 }
 
+// K3 in two launches when the stream has at most SA1_MAXT tiles (8 GiB of 32 KiB blocks):
+// dmx_scan_tile_kernel as above, then this kernel, a workgroup per tile, which composes the
+// tile aggregates itself (at most 4 per thread) -- its tile's prefix and the stream's total,
+// hence the status every workgroup needs before it writes -- instead of a one-workgroup
+// dmx_scan_kernel launch between the two.  The last tile's workgroup also does what that
+// launch did once: Adler-32, the dmx_result record, the fallback counters, the hint and the
+// words past the last block.  Then each block: as dmx_scan_apply_kernel.
+#define SA1_MAXT (4 * SCAN_TILE)
+__global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply1_kernel(dmx_blkinfo* __restrict__ info, uint32_t nblk, uint64_t n,
+                                                                   uint32_t flags, uint64_t out_cap,
+                                                                   const ScanTile* __restrict__ tiles,
+                                                                   uint32_t* __restrict__ out32, dmx_result* __restrict__ res,
+                                                                   uint32_t* __restrict__ nfallback, uint32_t* __restrict__ hint,
+                                                                   uint32_t* __restrict__ wl, uint32_t* __restrict__ L4,
+                                                                   const uint16_t* __restrict__ codes) {
+    __shared__ Mono wt[SCAN_TILE / 64];
+    __shared__ Mono s_pre;
+    __shared__ uint64_t red[SCAN_TILE / 64][9];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t ntile = (nblk + SCAN_TILE - 1) / SCAN_TILE, tt = blockIdx.x;
+    const bool lastwg = tt + 1 == ntile;
+    const uint64_t start = (flags & DMX_F_HEADER) ? 16 : 0;
+    // thread i composes tiles [i C, i C + C) in order; the one holding tile tt notes the part before it
+    const uint32_t C = (ntile + SCAN_TILE - 1) / SCAN_TILE;
+    const uint32_t t0 = tid * C < ntile ? tid * C : ntile, t1 = t0 + C < ntile ? t0 + C : ntile;
+    Mono agg = {0, 0, 0}, part = {0, 0, 0};
+    bool mine = false;
+    uint64_t s1 = 0, s2 = 0, nt = 0, ns = 0, nf = 0, k0 = 0, k2 = 0, k3 = 0, ku = 0;
+    for (uint32_t u = t0; u < t1; u++) {
+        const ScanTile T = tiles[u];
+        if (u == tt) { part = agg; mine = true; }
+        Mono e;
+        e.s = (uint32_t)T.s; e.a = T.a; e.c = T.c;
+        agg = mcompose(agg, e);
+        if (lastwg) {
+            s1 = (s1 + T.adl_s1) % ADL_MOD;
+            s2 = (s2 + T.adl_s2) % ADL_MOD;
+            nt += T.ntok; ns += T.nsto; nf += T.nfix;
+            k0 += T.kinds & 0xFFFFu; k2 += (T.kinds >> 16) & 0xFFFFu; k3 += (T.kinds >> 32) & 0xFFFFu; ku += T.kinds >> 48;
+        }
+    }
+    Mono x = agg;   // inclusive scan over the threads' ranges
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const Mono y = mshfl_up(x, o);
+        if (lane >= (uint32_t)o) x = mcompose(y, x);
+    }
+    const Mono before = mshfl_up(x, 1);
+    if (lane == 63) wt[wave] = x;
+    if (lastwg) {
+        s1 = wave_sum_u64(s1); s2 = wave_sum_u64(s2); nt = wave_sum_u64(nt);
+        ns = wave_sum_u64(ns); nf = wave_sum_u64(nf);
+        k0 = wave_sum_u64(k0); k2 = wave_sum_u64(k2); k3 = wave_sum_u64(k3); ku = wave_sum_u64(ku);
+        if (lane == 0) {
+            red[wave][0] = s1; red[wave][1] = s2; red[wave][2] = nt; red[wave][3] = ns; red[wave][4] = nf;
+            red[wave][5] = k0; red[wave][6] = k2; red[wave][7] = k3; red[wave][8] = ku;
+        }
+    }
+    __syncthreads();
+    Mono tot = {0, 0, 0}, wpre = {0, 0, 0};
+#pragma unroll
+    for (int w = 0; w < SCAN_TILE / 64; w++) {
+        if (w == (int)wave) wpre = tot;
+        tot = mcompose(tot, wt[w]);
+    }
+    if (mine) s_pre = mcompose(lane ? mcompose(wpre, before) : wpre, part);
+    // the stream's end and status (every workgroup: nothing is written past out_cap)
+    const uint64_t T = mapply(tot, start);
+    const uint64_t end = (flags & DMX_F_FINAL) ? align8(T) : align8(T + 3) + 32;
+    const uint64_t out_len = end / 8 + ((flags & DMX_F_TRAILER) ? 4 : 0);
+    const int32_t status = (((out_len + 3) & ~3ull) > out_cap) ? -(int32_t)E_SZ : 0;
+    if (lastwg && tid == 0) {
+        uint64_t a1 = 0, a2 = 0, ntk = 0, nst = 0, nfx = 0, q0 = 0, q2 = 0, q3 = 0, qu = 0;
+        for (int w = 0; w < SCAN_TILE / 64; w++) {
+            a1 += red[w][0]; a2 += red[w][1]; ntk += red[w][2]; nst += red[w][3]; nfx += red[w][4];
+            q0 += red[w][5]; q2 += red[w][6]; q3 += red[w][7]; qu += red[w][8];
+        }
+        a1 = (1 + a1) % ADL_MOD;
+        a2 = (n % ADL_MOD + a2) % ADL_MOD;
+        res->out_len = out_len;
+        res->end_bits = T;
+        res->n = n;
+        res->ntokens = ntk;
+        res->adler = (uint32_t)((a2 << 16) | a1);
+        res->status = status;
+        res->nblocks = nblk;
+        res->nstored = (uint32_t)nst;
+        res->nfixed = (uint32_t)nfx;
+        res->ndynamic = nblk - (uint32_t)nst - (uint32_t)nfx;
+        res->nsortfallback = nfallback[0];
+        nfallback[1] += nfallback[0];
+        res->nsortfallback_total = nfallback[1];
+        nfallback[0] = 0;
+        if (hint) {   // as dmx_scan_kernel
+            __hip_atomic_store(&hint[0], nblk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&hint[1], (uint32_t)q0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&hint[2], (uint32_t)(q0 + q2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&hint[3], nblk - (uint32_t)q3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&hint[4], (uint32_t)qu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    if (status) return;
+    if (lastwg) {   // zero the words past the last block (the framing goes there)
+        const uint64_t tail_end = end + ((flags & DMX_F_TRAILER) ? 32 : 0);
+        for (uint64_t w = (T >> 5) + tid; w < ((tail_end + 31) >> 5); w += SCAN_TILE) out32[w] = 0;
+    }
+    __syncthreads();   // (s_pre)
+    const uint32_t b = tt * SCAN_TILE + tid;
+    if (b >= nblk) return;
+    const Mono tp = s_pre;
+    Mono lp;
+    const dmx_blkinfo bi = info[b];
+    lp.c = bi.off_bits; lp.s = (uint32_t)(bi.len_bits >> 32); lp.a = bi.len_bits & 0xFFFFFFFFu;
+    const Mono pre = mcompose(tp, lp);
+    const uint64_t o = mapply(pre, start);
+    const uint64_t l = mapply(blk_elem(bi), o) - o;
+    info[b].off_bits = o;
+    info[b].len_bits = l;
+    if (!wl) {
+        out32[o >> 5] = 0;
+        out32[(o + l - 1) >> 5] = 0;
+        return;
+    }
+    const uint32_t M = wl[WL_M];
+    if (wl_skip(b, M, nblk)) return;
+    uint8_t* o8 = reinterpret_cast<uint8_t*>(out32);
+    const uint64_t e = o + l, w0 = o >> 5, w1 = (e - 1) >> 5;
+    if (b >= 1 && wl_skip(b - 1, M, nblk)) {
+        for (uint64_t q = o >> 3; q < 4 * w0 + 4 && q < ((e + 7) >> 3); q++) o8[q] = 0;
+    } else {
+        out32[w0] = 0;
+    }
+    if (wl_skip(b + 1, M, nblk)) {
+        for (uint64_t q = 4 * w1 > (o >> 3) ? 4 * w1 : (o >> 3); q < (e >> 3); q++) o8[q] = 0;
+    } else {
+        out32[w1] = 0;
+    }
+    if (is_dup(codes, b)) return;
+    L4[atomicAdd(&wl[WL_N4], 1u)] = b;
+}
+
 // ------------------------------------------------------------------------------------
 // K4: bit packing
 // ------------------------------------------------------------------------------------
@@ -5129,12 +5270,18 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
         hipLaunchKernelGGL(dmx_scan_tile_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, n, (uint32_t)o.sw,
                            c->tiles, dupk, dupa, c->sub);
     uint32_t* L4 = wl ? wl + WL_HDR + 2 * c->cap_blocks : NULL;
-    hipLaunchKernelGGL(dmx_scan_kernel, dim3(1), dim3(ST), 0, s, c->tiles, nblk, n, o.flags, out_cap,
-                       (uint32_t*)d_out, c->res, c->nfb,
-                       (!wl && (o.flags & DMX_F_STORE_CHECK)) ? c->whint_dev : NULL);
-    if (nblk)
-        hipLaunchKernelGGL(dmx_scan_apply_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, o.flags, c->tiles,
-                           (uint32_t*)d_out, (const dmx_result*)c->res, wl, L4, dupk);
+    uint32_t* hintp = (!wl && (o.flags & DMX_F_STORE_CHECK)) ? c->whint_dev : NULL;
+    const char* s3 = getenv("DMX_SCAN3");   // 1: the three-launch scan at any size (tests)
+    if (nblk && ntile <= SA1_MAXT && !(s3 && !strcmp(s3, "1"))) {
+        hipLaunchKernelGGL(dmx_scan_apply1_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, n, o.flags, out_cap,
+                           (const ScanTile*)c->tiles, (uint32_t*)d_out, c->res, c->nfb, hintp, wl, L4, dupk);
+    } else {
+        hipLaunchKernelGGL(dmx_scan_kernel, dim3(1), dim3(ST), 0, s, c->tiles, nblk, n, o.flags, out_cap,
+                           (uint32_t*)d_out, c->res, c->nfb, hintp);
+        if (nblk)
+            hipLaunchKernelGGL(dmx_scan_apply_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, o.flags, c->tiles,
+                               (uint32_t*)d_out, (const dmx_result*)c->res, wl, L4, dupk);
+    }
     if (ev && ((c->timing >> 4) & 1)) (void)hipEventRecord(ev[4], s);
     if (nblk)
         hipLaunchKernelGGL(dmx_pack_kernel, dim3(wl && wsh.list4 ? list_grid(nblk, wsh.n4, 2 * c->ncu, 16 * c->ncu) : nblk),

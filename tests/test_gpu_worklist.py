@@ -283,3 +283,25 @@ def test_worklist_unaligned_input(enc, shape, shift):
         z, r = _with_env(shape, lambda: enc.compress_tensor(t, opts=D.Opts(B, 7, fl, 0)))
         assert r.status == 0
         assert z.cpu().numpy().tobytes() == want, (shape, shift, rep)
+
+
+@pytest.mark.parametrize("name", ["noise_prefix_then_text", "text_only", "noise_zeros_text"])
+def test_scan_paths_agree(enc, name):
+    """K3's fused scan + apply launch (up to 1 024 tiles) and the three-launch scan
+    (DMX_SCAN3=1, every size above that) write the same stream -- the oracle's."""
+    data = _cases()[name]
+    fl = D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | D.DMX_F_DEEP
+    want = O.compress(data, max_chain=7, lazy=True, store_check=True, deep=True)
+    old = os.environ.get("DMX_SCAN3")
+    try:
+        for v in ("1", "0"):
+            os.environ["DMX_SCAN3"] = v
+            for rep in range(2):
+                z, r = enc.compress_bytes(data, max_chain=7, flags=fl)
+                assert r.status == 0 and z == want, (name, v, rep)
+                assert r.nblocks == (len(data) + B - 1) // B and r.adler == zlib.adler32(data)
+    finally:
+        if old is None:
+            os.environ.pop("DMX_SCAN3", None)
+        else:
+            os.environ["DMX_SCAN3"] = old
