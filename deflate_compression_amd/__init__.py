@@ -126,6 +126,7 @@ def lib() -> ctypes.CDLL:
         "dmx_last_code_lengths": ([vp, u32, u8p], ctypes.c_int),
         "dmx_last_subblock": ([vp, u32, u32, u32p, u32p, u32p, u8p], ctypes.c_int),
         "dmx_ctx_set_timing": ([vp, ctypes.c_int], ctypes.c_int),
+        "dmx_ctx_set_hook": ([vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "dmx_ctx_stage_times": ([vp, ctypes.POINTER(ctypes.c_double), u32p], ctypes.c_int),
         "dmx_adler32_combine": ([u32, u32, u64], u32),
         "dmx_debug_stamps": ([vp, ctypes.POINTER(u64), u32], ctypes.c_int),
@@ -450,6 +451,21 @@ class Encoder:
         return int(self._L.dmx_last_blocks(self._ctx, None, None, None, 1 << 30))
 
     STAGES = ("pre", "match", "huff", "scan", "pack")
+
+    HOOKS = {"worklist": 1, "dedupe": 2, "scan3": 3}   # DMX_HOOK_* (include/dmx.h)
+    WORKLIST = {None: -1, "0": 0, "list": 1, "plain": 2}
+
+    def set_hook(self, name: str, value) -> None:
+        """Test hooks of this context (dmx_ctx_set_hook): "worklist" None (adaptive) / "0" /
+        "list" / "plain"; "dedupe" None / 0 / 1; "scan3" 0 / 1.  Every setting must give the
+        same stream; they pick launch shapes only."""
+        if name == "worklist":
+            v = self.WORKLIST[value]
+        elif name == "dedupe":
+            v = -1 if value is None else int(value)
+        else:
+            v = int(value)
+        _check(self._L.dmx_ctx_set_hook(self._ctx, self.HOOKS[name], v), "dmx_ctx_set_hook")
 
     def set_timing(self, on: bool, stage: str | None = None, every: int = 1) -> None:
         """HIP-event stage times of the following encodes: every stage boundary, or with

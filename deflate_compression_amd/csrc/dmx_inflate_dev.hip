@@ -948,8 +948,8 @@ extern "C" int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_ibl
     if (zbytes > 0xFFFFFFF0ull) return -(int)E_RANGE;   // reader word indices are 32-bit
     hipStream_t s = (hipStream_t)stream;
     if (hipMemsetAsync(d_status, 0, sizeof(dmx_inflate_status), s) != hipSuccess) return -(int)E_DEVICE;
-    // the workgroups' first-level tables: scratch cached per (device, stream) and grown
-    // stream-ordered, so a steady stream of decodes allocates nothing
+    // the workgroups' first-level tables: scratch from the per-device stream-ordered pool
+    // (hipMallocFromPoolAsync here, hipFreeAsync on the same stream after the launch)
     const uint64_t tb = (uint64_t)(d_index ? nblk : 1) * ITAB_WORDS * 4;
     uint32_t* gtab = itab_scratch(s, tb);
     if (!gtab) return -(int)E_MALLOC;

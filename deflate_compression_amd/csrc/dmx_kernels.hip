@@ -2010,6 +2010,25 @@ __device__ __forceinline__ void wl_hint_put(const uint32_t* __restrict__ wl, int
 __device__ __forceinline__ bool wl_skip(uint32_t x, uint32_t M, uint32_t nblk) {
     return x >= 1 && x < M && x + 1 < nblk;
 }
+// The bytes [A, P) of the stream that the skipped blocks 1 .. R - 1 (R = min(M, nblk - 1))
+// occupy, at their speculative offsets (the true ones inside the stored prefix); empty when
+// there are none.  Nothing after K0 may write there: the apply launch zeroes the words the
+// other blocks share around that range byte by byte (zero_word_keep).
+__device__ __forceinline__ uint64_t spec_stored_bit(uint32_t b, uint32_t sw, uint32_t flags);
+__device__ __forceinline__ void wl_prefix_bytes(uint32_t M, uint32_t nblk, uint32_t sw, uint32_t flags,
+                                                uint64_t& A, uint64_t& P) {
+    const uint32_t R = M < nblk - 1 ? M : nblk - 1;
+    A = P = 0;
+    if (nblk >= 1 && R >= 2) { A = spec_stored_bit(1, sw, flags) >> 3; P = spec_stored_bit(R, sw, flags) >> 3; }
+}
+// zero output word w except its bytes in [A, P)
+__device__ __forceinline__ void zero_word_keep(uint32_t* out32, uint64_t w, uint64_t A, uint64_t P) {
+    const uint64_t q0 = 4 * w;
+    if (q0 + 4 <= A || q0 >= P) { out32[w] = 0; return; }
+    uint8_t* o8 = reinterpret_cast<uint8_t*>(out32);
+    for (uint32_t i = 0; i < 4; i++)
+        if (q0 + i < A || q0 + i >= P) o8[q0 + i] = 0;
+}
 
 // prestored: 0 = parse in K1; 1 = stored by the noise check; 2 = a block of one repeated
 // byte, parsed here in closed form (K1 skips it, the Huffman kernels code it); 3 = stored,
@@ -2700,7 +2719,7 @@ __global__ __launch_bounds__(256) void dmx_fill_kernel(const uint8_t* __restrict
     }
 }
 
-// Diagnostic (DMX_DEBUG_STOP=1|2|3, never in a product run): end the block after P0 (sort),
+// Diagnostic (a library variant built with -DDMX_DEBUG_STOP=1|2|3, never the product library): end the block after P0 (sort),
 // P1 (search) or P2 (walk), recording it as an empty block, so that SQ counters of the
 // truncated kernel give the instruction count of each phase by difference.  The stream
 // of such an encode is not the input's.
@@ -4339,7 +4358,10 @@ __global__ __launch_bounds__(ST) void dmx_scan_kernel(ScanTile* __restrict__ til
     // zero the words past the last block (the framing goes there)
     const uint64_t T = s_T, end = s_end;
     const uint64_t tail_end = end + ((flags & DMX_F_TRAILER) ? 32 : 0);
-    for (uint64_t w = (T >> 5) + tid; w < ((tail_end + 31) >> 5); w += ST) out32[w] = 0;
+    // (word T >> 5, when the last block ends inside it, is that block's last word: the apply
+    // launch zeroes it, keeping any bytes of the whole-copy prefix it holds)
+    const uint64_t tw0 = nblk ? (T + 31) >> 5 : T >> 5;
+    for (uint64_t w = tw0 + tid; w < ((tail_end + 31) >> 5); w += ST) out32[w] = 0;
     if (nblk == 0) {   // no pack launch: the whole stream is written here
         if (tid == 0 && start) out32[0] = 0;
         __syncthreads();
@@ -4348,7 +4370,7 @@ __global__ __launch_bounds__(ST) void dmx_scan_kernel(ScanTile* __restrict__ til
 }
 
 __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply_kernel(dmx_blkinfo* __restrict__ info, uint32_t nblk,
-                                                                  uint32_t flags, const ScanTile* __restrict__ tiles,
+                                                                  uint32_t flags, uint32_t sw, const ScanTile* __restrict__ tiles,
                                                                   uint32_t* __restrict__ out32,
                                                                   const dmx_result* __restrict__ res,
                                                                   uint32_t* __restrict__ wl, uint32_t* __restrict__ L4,
@@ -4378,18 +4400,11 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply_kernel(dmx_blkinfo* 
     // speculative offsets) -- and goes on K4's list
     const uint32_t M = wl[WL_M];
     if (wl_skip(b, M, nblk)) return;
-    uint8_t* o8 = reinterpret_cast<uint8_t*>(out32);
-    const uint64_t e = o + l, w0 = o >> 5, w1 = (e - 1) >> 5;
-    if (b >= 1 && wl_skip(b - 1, M, nblk)) {
-        for (uint64_t q = o >> 3; q < 4 * w0 + 4 && q < ((e + 7) >> 3); q++) o8[q] = 0;
-    } else {
-        out32[w0] = 0;
-    }
-    if (wl_skip(b + 1, M, nblk)) {
-        for (uint64_t q = 4 * w1 > (o >> 3) ? 4 * w1 : (o >> 3); q < (e >> 3); q++) o8[q] = 0;
-    } else {
-        out32[w1] = 0;
-    }
+    uint64_t A, P;
+    wl_prefix_bytes(M, nblk, sw, flags, A, P);
+    const uint64_t w0 = o >> 5, w1 = (o + l - 1) >> 5;
+    zero_word_keep(out32, w0, A, P);
+    if (w1 != w0) zero_word_keep(out32, w1, A, P);
     if (is_dup(codes, b)) return;   // packed by dmx_dup_copy_kernel
     L4[atomicAdd(&wl[WL_N4], 1u)] = b;
 }
@@ -4403,7 +4418,7 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply_kernel(dmx_blkinfo* 
 // words past the last block.  Then each block: as dmx_scan_apply_kernel.
 #define SA1_MAXT (4 * SCAN_TILE)
 __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply1_kernel(dmx_blkinfo* __restrict__ info, uint32_t nblk, uint64_t n,
-                                                                   uint32_t flags, uint64_t out_cap,
+                                                                   uint32_t flags, uint64_t out_cap, uint32_t sw,
                                                                    const ScanTile* __restrict__ tiles,
                                                                    uint32_t* __restrict__ out32, dmx_result* __restrict__ res,
                                                                    uint32_t* __restrict__ nfallback, uint32_t* __restrict__ hint,
@@ -4498,7 +4513,7 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply1_kernel(dmx_blkinfo*
     if (status) return;
     if (lastwg) {   // zero the words past the last block (the framing goes there)
         const uint64_t tail_end = end + ((flags & DMX_F_TRAILER) ? 32 : 0);
-        for (uint64_t w = (T >> 5) + tid; w < ((tail_end + 31) >> 5); w += SCAN_TILE) out32[w] = 0;
+        for (uint64_t w = ((T + 31) >> 5) + tid; w < ((tail_end + 31) >> 5); w += SCAN_TILE) out32[w] = 0;   // (as dmx_scan_kernel)
     }
     __syncthreads();   // (s_pre)
     const uint32_t b = tt * SCAN_TILE + tid;
@@ -4519,18 +4534,11 @@ __global__ __launch_bounds__(SCAN_TILE) void dmx_scan_apply1_kernel(dmx_blkinfo*
     }
     const uint32_t M = wl[WL_M];
     if (wl_skip(b, M, nblk)) return;
-    uint8_t* o8 = reinterpret_cast<uint8_t*>(out32);
-    const uint64_t e = o + l, w0 = o >> 5, w1 = (e - 1) >> 5;
-    if (b >= 1 && wl_skip(b - 1, M, nblk)) {
-        for (uint64_t q = o >> 3; q < 4 * w0 + 4 && q < ((e + 7) >> 3); q++) o8[q] = 0;
-    } else {
-        out32[w0] = 0;
-    }
-    if (wl_skip(b + 1, M, nblk)) {
-        for (uint64_t q = 4 * w1 > (o >> 3) ? 4 * w1 : (o >> 3); q < (e >> 3); q++) o8[q] = 0;
-    } else {
-        out32[w1] = 0;
-    }
+    uint64_t A, P;
+    wl_prefix_bytes(M, nblk, sw, flags, A, P);
+    const uint64_t w0 = o >> 5, w1 = (o + l - 1) >> 5;
+    zero_word_keep(out32, w0, A, P);
+    if (w1 != w0) zero_word_keep(out32, w1, A, P);
     if (is_dup(codes, b)) return;
     L4[atomicAdd(&wl[WL_N4], 1u)] = b;
 }
@@ -4881,6 +4889,10 @@ struct dmx_ctx {
     uint32_t ev_every, ev_count;   // with a one-stage mask: events on every ev_every-th encode only
     double stage_ms[6];
     uint32_t stage_n;
+    // test hooks (dmx_ctx_set_hook; defaults from the environment, read once at creation):
+    int hk_wl;       // -1 adaptive launch shapes, 0 no work lists, 1 list shapes, 2 per-block shapes (DMX_WORKLIST)
+    int hk_dedupe;   // -1 adaptive, 0 / 1 the uniform-block dedupe forced off / on (DMX_DEDUPE)
+    int hk_scan3;    // 1: K3 in three launches at any size (DMX_SCAN3)
 };
 
 struct FdPipe;
@@ -5032,6 +5044,14 @@ extern "C" int dmx_ctx_create(int device, uint64_t max_input, dmx_ctx** out) {
     dmx_ctx* c = (dmx_ctx*)calloc(1, sizeof(dmx_ctx));
     if (!c) return -(int)E_MALLOC;
     c->device = device;
+    {   // the test hooks' defaults: the environment, once per context (never per encode)
+        const char* e = getenv("DMX_WORKLIST");
+        c->hk_wl = !e ? -1 : !strcmp(e, "0") ? 0 : !strcmp(e, "list") ? 1 : !strcmp(e, "plain") ? 2 : -1;
+        const char* dd = getenv("DMX_DEDUPE");
+        c->hk_dedupe = dd ? (atoi(dd) > 0 ? 1 : 0) : -1;
+        const char* s3 = getenv("DMX_SCAN3");
+        c->hk_scan3 = s3 && !strcmp(s3, "1");
+    }
     int ncu = 0;
     c->ncu = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0
                  ? (uint32_t)ncu : 256u;
@@ -5142,10 +5162,8 @@ static uint32_t list_grid(uint32_t nblk, uint32_t prev, uint32_t lo, uint32_t hi
 }
 static WlShape wl_shape(const dmx_ctx* c) {
     WlShape w = {false, false, false, false, ~0u, ~0u};
-    const char* dd = getenv("DMX_DEDUPE");   // 1 / 0 forces the uniform-block dedupe on / off (tests)
-    const char* e = getenv("DMX_WORKLIST");
-    if (e && !strcmp(e, "list")) w = WlShape{true, true, true, false, ~0u, ~0u};
-    else if (!(e && !strcmp(e, "plain")) && c->whint && c->whint[0]) {
+    if (c->hk_wl == 1) w = WlShape{true, true, true, false, ~0u, ~0u};
+    else if (c->hk_wl != 2 && c->whint && c->whint[0]) {
         const uint32_t nb = c->whint[0];
         w.n2 = c->whint[2];   // the list grids are sized by the previous encode's lists
         w.n4 = c->whint[3];
@@ -5154,8 +5172,28 @@ static WlShape wl_shape(const dmx_ctx* c) {
         w.list4 = 2 * c->whint[3] < nb;
         w.dedupe = 4 * c->whint[4] >= nb;   // a quarter of the blocks were full uniform blocks
     }
-    if (dd) w.dedupe = atoi(dd) > 0;
+    if (c->hk_dedupe >= 0) w.dedupe = c->hk_dedupe > 0;
     return w;
+}
+
+extern "C" int dmx_ctx_set_hook(dmx_ctx* c, int hook, int value) {
+    if (!c) return -(int)E_INVAL;
+    switch (hook) {
+        case DMX_HOOK_WORKLIST:
+            if (value < -1 || value > 2) return -(int)E_RANGE;
+            c->hk_wl = value;
+            return 0;
+        case DMX_HOOK_DEDUPE:
+            if (value < -1 || value > 1) return -(int)E_RANGE;
+            c->hk_dedupe = value;
+            return 0;
+        case DMX_HOOK_SCAN3:
+            if (value < 0 || value > 1) return -(int)E_RANGE;
+            c->hk_scan3 = value;
+            return 0;
+        default:
+            return -(int)E_INVAL;
+    }
 }
 
 extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* d_out, uint64_t out_cap,
@@ -5183,12 +5221,11 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
     if ((o.flags & DMX_F_DICT) && c->cap_chain < (uint64_t)nblk + 1) return -(int)E_SZ;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     // DMX_F_STORE_CHECK: the work lists (WL_* above) and their launch shapes (wl_shape)
-    const char* wle = getenv("DMX_WORKLIST");
     const WlShape wsh = wl_shape(c);
     // an encode whose shapes are all per block and without the dedupe runs without the lists
     // (no list builder, no fill kernel); its scan kernel writes the hint instead
     const bool anyl = wsh.loop1 || wsh.list2 || wsh.list4 || wsh.dedupe;
-    uint32_t* wl = ((o.flags & DMX_F_STORE_CHECK) && anyl && !(wle && !strcmp(wle, "0"))) ? c->wl : NULL;
+    uint32_t* wl = ((o.flags & DMX_F_STORE_CHECK) && anyl && c->hk_wl != 0) ? c->wl : NULL;
     // the uniform-block dedupe's rep index per block (NULL: no dedupe in this encode)
     const bool dedupe = wl && wsh.dedupe && !(o.flags & DMX_F_SPLIT);
     const uint16_t* dupk = dedupe ? wl_codes((const uint32_t*)wl, c->cap_blocks) : NULL;   // dup bits (bit 3)
@@ -5226,9 +5263,13 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                                (uint64_t)c->cap_blocks,
                                dupa ? 1u : 0u);
         }
-        const char* dstop = getenv("DMX_DEBUG_STOP");   // diagnostic only (dbg_stop)
+#ifdef DMX_DEBUG_STOP   // diagnostic library variants only (tools/build_var.sh NAME -DDMX_DEBUG_STOP=1|2|3, dbg_stop)
+        const uint32_t dstop = (uint32_t)(DMX_DEBUG_STOP) & 3u;
+#else
+        const uint32_t dstop = 0;
+#endif
         const uint32_t mfl = ((o.flags & DMX_F_LAZY) ? 1u : 0u) | ((o.flags & DMX_F_EXACT_SORT) ? 2u : 0u) |
-                             ((o.flags & DMX_F_STORE_CHECK) ? 4u : 0u) | ((o.flags & DMX_F_DEEP) ? 8u : 0u) | (dstop ? ((uint32_t)atoi(dstop) & 3u) << 8 : 0u) |
+                             ((o.flags & DMX_F_STORE_CHECK) ? 4u : 0u) | ((o.flags & DMX_F_DEEP) ? 8u : 0u) | (dstop << 8) |
                              ((uint32_t)o.deep_chain << 16);   // DMX_F_DEEP depth (0 = DMX_DEEP_CHAIN)
         // work lists: the persistent K1 over L1 when the previous encode left most blocks
         // stored (wl_shape), else a workgroup per block
@@ -5271,15 +5312,14 @@ extern "C" int dmx_encode_async(dmx_ctx* c, const void* d_in, uint64_t n, void* 
                            c->tiles, dupk, dupa, c->sub);
     uint32_t* L4 = wl ? wl + WL_HDR + 2 * c->cap_blocks : NULL;
     uint32_t* hintp = (!wl && (o.flags & DMX_F_STORE_CHECK)) ? c->whint_dev : NULL;
-    const char* s3 = getenv("DMX_SCAN3");   // 1: the three-launch scan at any size (tests)
-    if (nblk && ntile <= SA1_MAXT && !(s3 && !strcmp(s3, "1"))) {
+    if (nblk && ntile <= SA1_MAXT && !c->hk_scan3) {   // (hk_scan3: the three-launch scan at any size, tests)
         hipLaunchKernelGGL(dmx_scan_apply1_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, n, o.flags, out_cap,
-                           (const ScanTile*)c->tiles, (uint32_t*)d_out, c->res, c->nfb, hintp, wl, L4, dupk);
+                           (uint32_t)o.sw, (const ScanTile*)c->tiles, (uint32_t*)d_out, c->res, c->nfb, hintp, wl, L4, dupk);
     } else {
         hipLaunchKernelGGL(dmx_scan_kernel, dim3(1), dim3(ST), 0, s, c->tiles, nblk, n, o.flags, out_cap,
                            (uint32_t*)d_out, c->res, c->nfb, hintp);
         if (nblk)
-            hipLaunchKernelGGL(dmx_scan_apply_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, o.flags, c->tiles,
+            hipLaunchKernelGGL(dmx_scan_apply_kernel, dim3(ntile), dim3(SCAN_TILE), 0, s, c->info, nblk, o.flags, (uint32_t)o.sw, c->tiles,
                                (uint32_t*)d_out, (const dmx_result*)c->res, wl, L4, dupk);
     }
     if (ev && ((c->timing >> 4) & 1)) (void)hipEventRecord(ev[4], s);

@@ -165,8 +165,9 @@ typedef struct {
     int32_t sw;        /* block size 1..32768 (0 = 32768) */
     int32_t max_chain; /* 0 = exhaustive (reference semantics); K > 0 = the K newest chain entries */
     uint32_t flags;    /* DMX_F_* */
-    int32_t deep_chain; /* DMX_F_DEEP: the chain depth of a small-alphabet block, K < depth <=
-                           255 (0 = DMX_DEEP_CHAIN); other values return -E_RANGE.  (This
+    int32_t deep_chain; /* DMX_F_DEEP: the chain depth of a small-alphabet block, 0..255
+                           (0 = DMX_DEEP_CHAIN); values outside 0..255 return -E_RANGE, and a
+                           depth <= max_chain has no effect (the block keeps K).  (This
                            field was `reserved`, always 0, before round 5.) */
     const void* dict;  /* DMX_F_DICT: the bytes just before the input (device memory for
                           dmx_encode_async, host memory for dmx_encode_host), history of
@@ -264,6 +265,18 @@ int dmx_encode_fd_multi(int fd_in, int fd_out, const dmx_opts* opts, uint64_t ch
  * that its context does not own.  Returns 0, or -E_INVAL / -E_RANGE for a bad spec. */
 int dmx_fault_set(const char* spec);
 
+/* Test hooks of one context: launch shapes that every encode must turn into the same stream
+ * (DESIGN.md §3.3).  Their defaults come from the environment, read once when the context is
+ * created (DMX_WORKLIST = 0 | list | plain, DMX_DEDUPE = 0 | 1, DMX_SCAN3 = 1); an encode
+ * never reads the environment.  Values: DMX_HOOK_WORKLIST -1 adaptive (default), 0 no work
+ * lists, 1 the list shapes, 2 a workgroup per block; DMX_HOOK_DEDUPE -1 adaptive, 0 off,
+ * 1 on; DMX_HOOK_SCAN3 0 / 1 (K3 in three launches at any size).  Set them between encodes
+ * on the context's own thread.  Returns 0, -E_INVAL (unknown hook) or -E_RANGE. */
+#define DMX_HOOK_WORKLIST 1
+#define DMX_HOOK_DEDUPE 2
+#define DMX_HOOK_SCAN3 3
+int dmx_ctx_set_hook(dmx_ctx* ctx, int hook, int value);
+
 /* ---- GPU inflate, csrc/dmx_inflate_dev.hip ---- */
 /* One entry per independently decodable DEFLATE block: start bit in the stream, output
  * offset and length.  Blocks of a dmx stream never reference earlier blocks. */
@@ -283,10 +296,10 @@ int dmx_block_index(dmx_ctx* ctx, dmx_iblock* d_index, uint32_t cap, void* strea
 /* Inflate on the GPU.  d_index != NULL: decode the nblk listed blocks in parallel (one
  * wave each) into d_out + out_off.  d_index == NULL: decode the whole zlib stream d_z
  * (header, blocks until BFINAL, Adler-32 check) in one workgroup.  Status in the device
- * record d_status.  The first-level tables live in device scratch cached per (device,
- * stream) and grown stream-ordered: the first call on a stream (or a larger one) allocates.
- * Returns 0 or -E_*: -E_MALLOC when that scratch cannot be allocated, -E_DEVICE for
- * launch errors. */
+ * record d_status.  The first-level tables live in device scratch taken from a per-device
+ * stream-ordered pool on every call (hipMallocFromPoolAsync before the launch, hipFreeAsync
+ * after it on the same stream).  Returns 0 or -E_*: -E_MALLOC when that scratch cannot be
+ * allocated, -E_DEVICE for launch errors. */
 int dmx_inflate_async(const void* d_z, uint64_t zbytes, const dmx_iblock* d_index, uint32_t nblk, void* d_out,
                       uint64_t out_cap, dmx_inflate_status* d_status, void* stream);
 

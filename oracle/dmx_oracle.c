@@ -182,7 +182,7 @@ static int orc_search_hist(const orc_hist* H, const uint8_t* d, int n, int i, in
  * have long chains of real matches that K = 8 cuts short; text never qualifies
  * (D / samples >= 0.32 on the reference-held text, profiles/r04_size). */
 static int ORC_DEEP_K = 32;   /* dmx_opts.deep_chain's default (DMX_DEEP_CHAIN) */
-/* the depth of small-alphabet blocks (0 = 64): the GPU's dmx_opts.deep_chain */
+/* the depth of small-alphabet blocks (0 = 32): the GPU's dmx_opts.deep_chain */
 void dmx_oracle_set_deep_chain(int k) { ORC_DEEP_K = k > 0 ? k : 32; }
 int dmx_oracle_block_chain(const uint8_t* d, int n, int max_chain) {
     if (max_chain <= 0 || max_chain >= ORC_DEEP_K) return max_chain;

@@ -10,6 +10,9 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
+    if os.environ.get("DMX_LIBV"):   # a diagnostic library variant (tools/build_var.sh), e.g. the claim guard
+        import deflate_compression_amd as D
+        D.LIB_PATH = os.path.abspath(os.environ["DMX_LIBV"])
     config.addinivalue_line("markers", "slow: long-running")
 
 

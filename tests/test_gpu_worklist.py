@@ -6,7 +6,6 @@ lists) must write the oracle's stream byte for byte, and the adaptive choice (th
 encode's hint) too, whatever it picks.
 
 Bar: bit-exact against the oracle (store_check=True), zlib inflates."""
-import os
 import zlib
 
 import numpy as np
@@ -36,6 +35,12 @@ def _cases():
         "noise_zeros_text": _noise(2 * B, 6) + z + text[:2 * B] + _noise(B + 100, 7),
         "text_only": text,
         "noise_short_tail": _noise(4 * B + 5000, 8),
+        # a 1- / 2- / 3-byte last block after a stored prefix: its fixed-Huffman bits share a
+        # word with the prefix's last bytes (the apply launch and the tail zeroing
+        # must keep those bytes)
+        "noise_1byte_tail": _noise(3 * B + 1, 16),
+        "noise_2byte_tail": _noise(5 * B + 2, 17),
+        "noise_3byte_tail": _noise(2 * B + 3, 18),
         "one_block_noise": _noise(B, 9),
         "two_blocks_noise": _noise(2 * B, 10),
     }
@@ -48,19 +53,21 @@ def enc():
     e.close()
 
 
-def _with_env(val, fn):
-    old = os.environ.get("DMX_WORKLIST")
-    if val is None:
-        os.environ.pop("DMX_WORKLIST", None)
-    else:
-        os.environ["DMX_WORKLIST"] = val
+def _with_shape(e, val, fn):
+    """fn() with the context's launch shapes forced (dmx_ctx_set_hook; None = adaptive)."""
+    e.set_hook("worklist", val)
     try:
         return fn()
     finally:
-        if old is None:
-            os.environ.pop("DMX_WORKLIST", None)
-        else:
-            os.environ["DMX_WORKLIST"] = old
+        e.set_hook("worklist", None)
+
+
+def _with_hook(e, name, val, fn):
+    e.set_hook(name, val)
+    try:
+        return fn()
+    finally:
+        e.set_hook(name, None if name == "dedupe" else 0)
 
 
 @pytest.mark.parametrize("shape", ["list", "plain", "0", None])
@@ -70,7 +77,7 @@ def test_worklist_shapes_match_oracle(enc, shape, name):
     fl = D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | D.DMX_F_DEEP
     want = O.compress(data, max_chain=7, lazy=True, store_check=True, deep=True)
     for rep in range(2):   # the second encode on the context follows the first one's hint
-        z, r = _with_env(shape, lambda: enc.compress_bytes(data, max_chain=7, flags=fl))
+        z, r = _with_shape(enc, shape, lambda: enc.compress_bytes(data, max_chain=7, flags=fl))
         assert r.status == 0
         assert z == want, (name, shape, rep, len(z), len(want))
     assert zlib.decompress(z) == data
@@ -80,7 +87,7 @@ def test_worklist_shapes_match_oracle(enc, shape, name):
 @pytest.mark.parametrize("k", [0, 8])
 def test_worklist_exhaustive_and_greedy(enc, shape, k):
     data = _cases()["noise_prefix_then_text"]
-    z, _ = _with_env(shape, lambda: enc.compress_bytes(data, max_chain=k, flags=D.DMX_ZLIB | D.DMX_F_STORE_CHECK))
+    z, _ = _with_shape(enc, shape, lambda: enc.compress_bytes(data, max_chain=k, flags=D.DMX_ZLIB | D.DMX_F_STORE_CHECK))
     assert z == O.compress(data, max_chain=k, store_check=True)
 
 
@@ -89,7 +96,7 @@ def test_worklist_exhaustive_and_greedy(enc, shape, k):
 def test_worklist_small_windows(enc, shape, sw):
     data = _noise(6 * sw, 11) + D.gen_text(3 * sw, 12).tobytes() + _noise(2 * sw + 9, 13)
     fl = D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK
-    z, _ = _with_env(shape, lambda: enc.compress_bytes(data, sw=sw, max_chain=6, flags=fl))
+    z, _ = _with_shape(enc, shape, lambda: enc.compress_bytes(data, sw=sw, max_chain=6, flags=fl))
     assert z == O.compress(data, sw=sw, max_chain=6, lazy=True, store_check=True)
 
 
@@ -102,7 +109,7 @@ def test_worklist_shard_framing(enc, shape):
         fl = D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | S.shard_flags(r, 3)
         piece = data[lo:hi]
         t = torch.from_numpy(piece.copy()).cuda()
-        z, _ = _with_env(shape, lambda: enc.compress_tensor(t, opts=D.Opts(B, 7, fl, 0)))
+        z, _ = _with_shape(enc, shape, lambda: enc.compress_tensor(t, opts=D.Opts(B, 7, fl, 0)))
         assert z.cpu().numpy().tobytes() == O.compress(piece, max_chain=7, lazy=True, store_check=True,
                                                         flags=S.shard_flags(r, 3)), (shape, r)
 
@@ -110,10 +117,10 @@ def test_worklist_shard_framing(enc, shape):
 def test_worklist_with_dict_and_split(enc):
     data = _cases()["noise_prefix_then_text"]
     for shape in ("list", "plain"):
-        z, _ = _with_env(shape, lambda: enc.compress_bytes(
+        z, _ = _with_shape(enc, shape, lambda: enc.compress_bytes(
             data, max_chain=7, flags=D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | D.DMX_F_DICT))
         assert z == O.compress(data, max_chain=7, lazy=True, store_check=True, dict=True), shape
-        z, _ = _with_env(shape, lambda: enc.compress_bytes(
+        z, _ = _with_shape(enc, shape, lambda: enc.compress_bytes(
             data, max_chain=7, flags=D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | D.DMX_F_SPLIT))
         assert z == O.compress(data, max_chain=7, lazy=True, store_check=True, split=True), shape
 
@@ -122,7 +129,7 @@ def test_worklist_inflate_gpu(enc):
     """The indexed GPU inflate of a stream whose noise prefix K0 wrote whole."""
     data = _cases()["noise_prefix_then_text"]
     t = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).cuda()
-    out, r = _with_env("list", lambda: enc.compress_tensor(
+    out, r = _with_shape(enc, "list", lambda: enc.compress_tensor(
         t, opts=D.Opts(B, 7, D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK, 0)))
     ix, n = enc.block_index()
     dec, st = D.inflate_gpu(out, len(data), ix, n)
@@ -149,25 +156,17 @@ def test_uniform_dedupe_matches_oracle(enc, shape, name):
     data = _uniform_cases()[name]
     fl = D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | D.DMX_F_DEEP
     want = O.compress(data, max_chain=7, lazy=True, store_check=True, deep=True)
-    old = os.environ.get("DMX_DEDUPE")
-    try:
-        for dd in ("1", "0"):
-            os.environ["DMX_DEDUPE"] = dd
-            z, r = _with_env(shape, lambda: enc.compress_bytes(data, max_chain=7, flags=fl))
-            assert r.status == 0
-            assert z == want, (name, shape, dd, len(z), len(want))
-    finally:
-        if old is None:
-            os.environ.pop("DMX_DEDUPE", None)
-        else:
-            os.environ["DMX_DEDUPE"] = old
+    for dd in (1, 0):
+        z, r = _with_hook(enc, "dedupe", dd,
+                          lambda: _with_shape(enc, shape, lambda: enc.compress_bytes(data, max_chain=7, flags=fl)))
+        assert r.status == 0
+        assert z == want, (name, shape, dd, len(z), len(want))
     assert zlib.decompress(z) == data
 
 
 def test_uniform_dedupe_inflate_and_split(enc):
     data = _uniform_cases()["uniform_in_noise"]
-    old = os.environ.get("DMX_DEDUPE")
-    os.environ["DMX_DEDUPE"] = "1"
+    enc.set_hook("dedupe", 1)
     try:
         t = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).cuda()
         out, r = enc.compress_tensor(t, opts=D.Opts(B, 7, D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK, 0))
@@ -177,10 +176,7 @@ def test_uniform_dedupe_inflate_and_split(enc):
         z, _ = enc.compress_bytes(data, max_chain=7, flags=D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | D.DMX_F_SPLIT)
         assert z == O.compress(data, max_chain=7, lazy=True, store_check=True, split=True)
     finally:
-        if old is None:
-            os.environ.pop("DMX_DEDUPE", None)
-        else:
-            os.environ["DMX_DEDUPE"] = old
+        enc.set_hook("dedupe", None)
 
 
 def _multi_tile(sw):
@@ -219,20 +215,16 @@ def test_worklist_multi_tile(shape):
     fl = D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK
     want = O.compress(data, sw=sw, max_chain=7, lazy=True, store_check=True)
     e = D.Encoder(0, len(data), sw=sw)
-    old = os.environ.get("DMX_DEDUPE")
     try:
-        for dd in ("1", "0"):
-            os.environ["DMX_DEDUPE"] = dd
+        e.set_hook("worklist", shape)
+        for dd in (1, 0):
+            e.set_hook("dedupe", dd)
             for rep in range(2):
-                z, r = _with_env(shape, lambda: e.compress_bytes(data, sw=sw, max_chain=7, flags=fl))
+                z, r = e.compress_bytes(data, sw=sw, max_chain=7, flags=fl)
                 assert r.status == 0
                 assert z == want, (shape, dd, rep, len(z), len(want))
     finally:
         e.close()
-        if old is None:
-            os.environ.pop("DMX_DEDUPE", None)
-        else:
-            os.environ["DMX_DEDUPE"] = old
 
 
 def test_stage_timing_modes():
@@ -280,7 +272,7 @@ def test_worklist_unaligned_input(enc, shape, shift):
     t = buf[shift:shift + len(data)]
     assert t.data_ptr() % 16 == shift % 16
     for rep in range(2):
-        z, r = _with_env(shape, lambda: enc.compress_tensor(t, opts=D.Opts(B, 7, fl, 0)))
+        z, r = _with_shape(enc, shape, lambda: enc.compress_tensor(t, opts=D.Opts(B, 7, fl, 0)))
         assert r.status == 0
         assert z.cpu().numpy().tobytes() == want, (shape, shift, rep)
 
@@ -292,16 +284,66 @@ def test_scan_paths_agree(enc, name):
     data = _cases()[name]
     fl = D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | D.DMX_F_DEEP
     want = O.compress(data, max_chain=7, lazy=True, store_check=True, deep=True)
-    old = os.environ.get("DMX_SCAN3")
     try:
-        for v in ("1", "0"):
-            os.environ["DMX_SCAN3"] = v
+        for v in (1, 0):
+            enc.set_hook("scan3", v)
             for rep in range(2):
                 z, r = enc.compress_bytes(data, max_chain=7, flags=fl)
                 assert r.status == 0 and z == want, (name, v, rep)
                 assert r.nblocks == (len(data) + B - 1) // B and r.adler == zlib.adler32(data)
     finally:
-        if old is None:
-            os.environ.pop("DMX_SCAN3", None)
+        enc.set_hook("scan3", 0)
+
+
+def _many_blocks(nblk, sw, seed):
+    """nblk blocks of sw bytes, mostly zeros (cheap for the oracle), with text and noise
+    runs spread over every scan tile, and a ragged tail."""
+    rng = np.random.default_rng(seed)
+    a = np.zeros(nblk * sw - sw // 3, dtype=np.uint8)
+    text = D.gen_text(64 * sw, seed)
+    for s in range(0, nblk - 64, 331):
+        k = int(rng.integers(1, 32))
+        if rng.integers(0, 2):
+            a[s * sw:(s + k) * sw] = text[:k * sw]
         else:
-            os.environ["DMX_SCAN3"] = old
+            a[s * sw:(s + k) * sw] = rng.integers(0, 256, k * sw, dtype=np.uint8)
+    return a
+
+
+@pytest.mark.parametrize("sw,ntile", [(4096, 257), (1024, 1025)])
+def test_scan_many_tiles(sw, ntile):
+    """K3 above 65 536 blocks: the fused launch's threads compose C = 2 tile aggregates each
+    (257 tiles), and just past its 1 024-tile limit the three-launch path takes over (1 025
+    tiles) -- both the oracle's stream, with DMX_SCAN3 forced and not."""
+    nblk = ntile * 256 - 100
+    a = _many_blocks(nblk, sw, 5 + ntile)
+    assert (a.size + sw - 1) // sw == nblk and (nblk + 255) // 256 == ntile
+    fl = D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK
+    want = O.compress_par(a, sw=sw, max_chain=4, lazy=True, store_check=True, threads=16)
+    e = D.Encoder(0, a.size, sw=sw)
+    try:
+        t = torch.from_numpy(a).cuda()
+        for v in (1, 0):
+            e.set_hook("scan3", v)
+            for rep in range(2):
+                z, r = e.compress_tensor(t, opts=D.Opts(sw, 4, fl, 0))
+                assert r.status == 0 and r.nblocks == nblk
+                assert z.cpu().numpy().tobytes() == want, (sw, ntile, v, rep)
+    finally:
+        e.close()
+
+
+def test_debug_stop_env_is_ignored(monkeypatch):
+    """the phase knockout is a compile-time variant; with DMX_DEBUG_STOP exported
+    the product library still writes the oracle's stream."""
+    monkeypatch.setenv("DMX_DEBUG_STOP", "1")
+    data = _cases()["noise_prefix_then_text"]
+    fl = D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK | D.DMX_F_DEEP
+    e = D.Encoder(0, len(data))
+    try:
+        for k in (7, 0):
+            z, r = e.compress_bytes(data, max_chain=k, flags=fl)
+            assert r.status == 0
+            assert z == O.compress(data, max_chain=k, lazy=True, store_check=True, deep=True), k
+    finally:
+        e.close()

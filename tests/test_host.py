@@ -171,3 +171,16 @@ def test_product_does_not_reference_oracle():
                 assert "oracle" not in txt.lower().replace("oracle_", ""), f
     out = subprocess.check_output(["nm", "-D", D.LIB_PATH], text=True)
     assert "dmx_oracle" not in out
+
+
+def test_product_library_has_no_debug_knockout():
+    """the phase knockout that ends every block after P0 / P1 / P2 (wrong streams)
+    exists only in diagnostic variants built with -DDMX_DEBUG_STOP (tools/build_var.sh): the
+    product library never reads such a switch from the environment, and an encode reads no
+    environment variable at all (test hooks are per-context, dmx_ctx_set_hook)."""
+    blob = open(D.LIB_PATH, "rb").read()
+    assert b"DMX_DEBUG_STOP" not in blob
+    src = open(os.path.join(REPO, "deflate_compression_amd", "csrc", "dmx_kernels.hip")).read()
+    body = src[src.index('extern "C" int dmx_encode_async('):]
+    body = body[:body.index("\n}\n")]
+    assert "getenv" not in body

@@ -1,6 +1,6 @@
 """Diagnostic: one text encode on cuda:0 for per-phase SQ counters of the match kernel.
-Run under rocprofv3 --pmc with DMX_DEBUG_STOP=1|2|3 (end blocks after P0 / P1 / P2; the
-stream is then not the input's) or unset (the whole kernel).  usage: phase_run.py [MB] [K] [lazy] [dict]"""
+Run under rocprofv3 --pmc with DMX_LIBV = a -DDMX_DEBUG_STOP=1|2|3 library variant (end
+blocks after P0 / P1 / P2; the stream is then not the input's) or unset (the whole kernel).  usage: phase_run.py [MB] [K] [lazy] [dict]"""
 import os
 import sys
 
@@ -8,6 +8,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
 import deflate_compression_amd as D
+
+if os.environ.get("DMX_LIBV"):
+    D.LIB_PATH = os.environ["DMX_LIBV"]
 
 mb = float(sys.argv[1]) if len(sys.argv) > 1 else 20
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 6
@@ -19,5 +22,5 @@ e = D.Encoder(0, n, max_chain=k, flags=D.DMX_ZLIB | (D.DMX_F_LAZY if lazy else 0
 for _ in range(2):
     out, r = e.compress_tensor(t)
 torch.cuda.synchronize()
-print(f"stop={os.environ.get('DMX_DEBUG_STOP', '-')} blocks={r.nblocks} out={r.out_len}")
+print(f"lib={os.path.basename(D.LIB_PATH)} blocks={r.nblocks} out={r.out_len}")
 e.close()
