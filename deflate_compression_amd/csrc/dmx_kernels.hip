@@ -838,6 +838,151 @@ __device__ __forceinline__ uint32_t search_pairs(MatchLDS& L, uint32_t bn, uint3
     return iters;
 }
 
+// ---- Short chains K = 6..8, four entries per lane (round 6) --------------------------------
+// Lane l holds the consecutive entries E_r = 4l' + r (r = 0..3, l' = l - HQ) of S; the HQ = 2
+// lanes below the owned ones are the halo (8 entries: K <= 8).  Candidate j of E_r is E_r' of
+// lane l - s with 4s + r - r' = j: s = 0 (r' < r: the same lane, no move), s = 1 (every stream
+// moved down one lane) and s = 2 (the streams r' >= 8 - K moved a second lane).  Per chunk
+// 4 (64 - HQ) = 248 entries: half the stream moves per compare of the two-entry path (one DPP
+// move per two compares), and the chunk's bookkeeping (claim, loads, sort check, limits, queue)
+// spread over twice the entries.  Same keys, queue and results as search_pairs.
+#define HQ 2
+template <int KK, int S, int R, int RP, bool GEN, bool GUARD, bool CLAMP>
+__device__ __forceinline__ void qcmp(const uint32_t (&e)[8], const uint32_t (&c)[8], uint32_t (&key)[4],
+                                     const uint32_t (&nc)[4], const uint32_t (&lim)[4]) {
+    constexpr int J = 4 * S + R - RP;
+    if constexpr (J >= 1 && J <= KK) {
+        uint32_t t;
+        if constexpr (GEN) t = pkey_g<GUARD, CLAMP>(e[2 * R], e[2 * R + 1], c[2 * RP], c[2 * RP + 1], J, nc[R], lim[R]);
+        else t = pkey<8 - J>(e[2 * R], e[2 * R + 1], c[2 * RP], c[2 * RP + 1]);
+        key[R] = max(key[R], t);
+    }
+}
+template <int KK, int S, int I, bool GEN, bool GUARD, bool CLAMP>
+__device__ __forceinline__ void qrow(const uint32_t (&e)[8], const uint32_t (&c)[8], uint32_t (&key)[4],
+                                     const uint32_t (&nc)[4], const uint32_t (&lim)[4]) {
+    if constexpr (I < 16) {
+        qcmp<KK, S, I / 4, I % 4, GEN, GUARD, CLAMP>(e, c, key, nc, lim);
+        qrow<KK, S, I + 1, GEN, GUARD, CLAMP>(e, c, key, nc, lim);
+    }
+}
+template <int KK, bool GEN, bool GUARD, bool CLAMP>
+__device__ __forceinline__ void quad_steps(const uint32_t (&e)[8], uint32_t (&key)[4], const uint32_t (&nc)[4],
+                                           const uint32_t (&lim)[4]) {
+    qrow<KK, 0, 0, GEN, GUARD, CLAMP>(e, e, key, nc, lim);   // s = 0: the lane's own earlier entries
+    uint32_t c[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) c[q] = PSHR(e[q]);
+    qrow<KK, 1, 0, GEN, GUARD, CLAMP>(e, c, key, nc, lim);
+#pragma unroll
+    for (int q = 2 * (8 - KK); q < 8; q++) c[q] = PSHR(c[q]);   // (streams r' < 8 - K are not used at s = 2)
+    qrow<KK, 2, 0, GEN, GUARD, CLAMP>(e, c, key, nc, lim);
+}
+template <bool DICT, int KK>
+__device__ __forceinline__ uint32_t search_quads(MatchLDS& L, uint32_t bn, uint32_t tid, bool stamp, uint64_t& tdef,
+                                                 const uint32_t* __restrict__ hbk) {
+    static_assert(KK >= 5 && KK <= 8, "four entries per lane with a halo of two lanes: K = 5..8");
+    constexpr uint32_t OWN = 4 * (64 - HQ);
+    const uint32_t lane = tid & 63, wave = wave_of(tid);
+    const uint32_t nvalid = bn > 2 ? bn - 2 : 0;
+    uint32_t* Qw = L.tsm + (wave << 6);   // the extension queue (P2 arrays are free during the search)
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t qn = 0, iters = 0;
+    uint32_t cnext = wave_claim(&L.ntok);   // chunks from the workgroup counter, one ahead (search_pairs)
+    for (;;) {
+        const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnext) * OWN;
+        const bool more = base < nvalid;   // wave-uniform
+        if (more) cnext = wave_claim(&L.ntok);
+        const int ea = (int)base + 4 * ((int)lane - (int)HQ);
+        const uint32_t k0 = (uint32_t)ea;
+        const bool own = lane >= HQ;
+        bool act[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) act[r] = more && own && k0 + (uint32_t)r < nvalid;
+        uint32_t key[4] = {0, 0, 0, 0}, lim[4] = {0, 0, 0, 0}, pos[4] = {0, 0, 0, 0};
+        if (more) {
+            uint32_t e[8];
+            {   // the four positions in one aligned 8-byte LDS word, then their first 8 bytes
+                uint2 pr = make_uint2(0, 0);
+                if (ea >= 0 && k0 < nvalid) pr = reinterpret_cast<const uint2*>(L.sorted)[k0 >> 2];
+                pos[0] = pr.x & 0xFFFFu; pos[1] = pr.x >> 16; pos[2] = pr.y & 0xFFFFu; pos[3] = pr.y >> 16;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    if (!(k0 + (uint32_t)r < nvalid)) pos[r] = 0;   // (past the last entry: never a candidate)
+                    const uint64_t v = ld8(L.data, pos[r]);
+                    e[2 * r] = (uint32_t)v;
+                    e[2 * r + 1] = (uint32_t)(v >> 32);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                if (act[r]) lim[r] = (bn - pos[r]) < MAXLEN ? (bn - pos[r]) : MAXLEN;
+            iters += 4 * KK;
+            {   // sort check: E_0 after E_3 of the lane below, E_r after E_(r-1)
+                uint32_t sk[4];
+#pragma unroll
+                for (int r = 0; r < 4; r++) sk[r] = sort_key(e[2 * r], pos[r]);
+                const uint32_t pk = PSHR(sk[3]);
+                bool bad = act[0] && k0 >= 1 && pk > sk[0];
+#pragma unroll
+                for (int r = 1; r < 4; r++) bad = bad || (act[r] && sk[r - 1] > sk[r]);
+                if (__ballot(bad)) L.sortbad = 1;
+            }
+            if (base == 0) {
+                uint32_t nc[4];
+#pragma unroll
+                for (int r = 0; r < 4; r++) nc[r] = min(k0 + (uint32_t)r, (uint32_t)KK);
+                quad_steps<KK, true, true, true>(e, key, nc, lim);
+            } else if (__ballot((act[0] && lim[0] < CBS) || (act[1] && lim[1] < CBS) || (act[2] && lim[2] < CBS) ||
+                                (act[3] && lim[3] < CBS))) {
+                const uint32_t nc[4] = {KK, KK, KK, KK};
+                quad_steps<KK, true, false, true>(e, key, nc, lim);
+            } else {
+                const uint32_t nc[4] = {0, 0, 0, 0};
+                quad_steps<KK, false, false, false>(e, key, nc, lim);
+            }
+        }
+        // a candidate equal in all CBS bytes (key >= 64): the entry is queued for the LDS
+        // extension (unless the block end caps it there); E_0's items, then E_1's, ...
+        bool push[4];
+        uint64_t pmv[4];
+        uint32_t pbits = 0, jbits = 0;   // per slot r: push flag (bit r), the key's 8 - j (bits 3r + 2 .. 3r)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            push[r] = act[r] && key[r] >= (CBS << 3) && lim[r] > CBS;
+            pmv[r] = __ballot(push[r]);
+            pbits |= push[r] ? 1u << r : 0u;
+            jbits |= (key[r] & 7u) << (3 * r);
+        }
+        const uint32_t npt = (uint32_t)(__popcll(pmv[0]) + __popcll(pmv[1]) + __popcll(pmv[2]) + __popcll(pmv[3]));
+        if (npt || (!more && qn)) {
+#pragma nounroll
+            for (uint32_t h = 0; h < 4; h++) {   // (one call site of ext_queue)
+                const uint64_t pm = h == 0 ? pmv[0] : h == 1 ? pmv[1] : h == 2 ? pmv[2] : pmv[3];   // (scalar selects)
+                const uint32_t npx = (uint32_t)__popcll(pm);
+                if (qn + npx > 64 || (!more && qn)) {
+                    const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
+                    ext_queue<DICT, false>(L, bn, KK, Qw, qn, lane, hbk);
+                    if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
+                    qn = 0;
+                }
+                if (!more) break;
+                if ((pbits >> h) & 1u)
+                    lds_st(&Qw[qn + (uint32_t)__popcll(pm & lt)], (k0 + h) | ((8u - ((jbits >> (3 * h)) & 7u)) << 15));
+                qn += npx;
+            }
+        }
+        if (!more) break;
+        uint32_t nib = 0;
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+            if (act[r] && !push[r])
+                nib |= short_result<DICT>(L, k0 + (uint32_t)r, pos[r], key[r], hbk) << (((k0 + (uint32_t)r) & 7u) << 2);
+        if (nib) atomicOr(&nib_words(L)[k0 >> 3], nib);
+    }
+    return iters;
+}
+
 template <bool DICT, bool RUNS, int NB = 3>
 __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, int32_t max_chain, uint16_t* __restrict__ pg,
                                      uint32_t tid, bool stamp, uint64_t& tdef, const uint32_t* __restrict__ hbk,
@@ -849,10 +994,16 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
     uint32_t iters = 0;
     if (RUNS) build_chg(L, bn, tid);
 #ifndef DMX_NO_PAIRS
-    if (!RUNS && NB == 3 && K >= 6 && K <= 8) {   // two entries per lane (search_pairs)
+    if (!RUNS && NB == 3 && K >= 6 && K <= 8) {
+#ifdef DMX_QUADS   // four entries per lane (search_quads)
+        iters = K == 8 ? search_quads<DICT, 8>(L, bn, tid, stamp, tdef, hbk)
+              : K == 7 ? search_quads<DICT, 7>(L, bn, tid, stamp, tdef, hbk)
+                       : search_quads<DICT, 6>(L, bn, tid, stamp, tdef, hbk);
+#else   // two entries per lane (search_pairs)
         iters = K == 8 ? search_pairs<DICT, 8>(L, bn, tid, stamp, tdef, hbk)
               : K == 7 ? search_pairs<DICT, 7>(L, bn, tid, stamp, tdef, hbk)
                        : search_pairs<DICT, 6>(L, bn, tid, stamp, tdef, hbk);
+#endif
     } else
 #endif
     if (K <= KE) {
@@ -1242,6 +1393,20 @@ __device__ __forceinline__ void count_sort_positions(MatchLDS& L, uint32_t bn, i
     const uint4 z4 = make_uint4(0, 0, 0, 0);
     reinterpret_cast<uint4*>(T)[tid] = z4;
     reinterpret_cast<uint4*>(T)[tid + MT] = z4;
+#ifdef DMX_SORT_G4
+    // four groups of four waves: groups 2 and 3 count in the first half of S (free until the
+    // scatter), four ordered rounds of four waves instead of eight of two
+    uint32_t* T2 = reinterpret_cast<uint32_t*>(L.sorted);
+    reinterpret_cast<uint4*>(T2)[tid] = z4;
+    reinterpret_cast<uint4*>(T2)[tid + MT] = z4;
+    constexpr uint32_t NR = 4;
+    uint32_t* Tg = (wave >> 3) ? T2 : T;
+    const uint32_t sh = ((wave >> 2) & 1) << 4;   // this wave's group field
+#else
+    constexpr uint32_t NR = 8;
+    uint32_t* Tg = T;
+    const uint32_t sh = (wave >> 3) << 4;   // this wave's group field
+#endif
     __syncthreads();   // (also: the staged block, for callers without a barrier after staging)
     const uint64_t lt = (1ull << lane) - 1ull;
     uint32_t x0l = (wave << 11) + lane, nvl = nvalid;
@@ -1256,19 +1421,18 @@ __device__ __forceinline__ void count_sort_positions(MatchLDS& L, uint32_t bn, i
         if ((st & 7) == 6) __builtin_amdgcn_sched_barrier(0);   // 8 loads in flight per group
     }
     if (stamp && tid == 0) tp0[0] = __builtin_amdgcn_s_memtime();
-    const uint32_t sh = (wave >> 3) << 4;   // this wave's group field
     uint32_t rk[16];                        // rank of each entry, two per register
 #pragma unroll
     for (int j = 0; j < 16; j++) rk[j] = 0;
-    for (uint32_t r = 0; r < 8; r++) {
-        if (r == (wave & 7)) {
+    for (uint32_t r = 0; r < NR; r++) {
+        if (r == (wave & (NR - 1))) {
             asm volatile("" : "+v"(x0l), "+v"(nvl));
             if (RUNCHK) {
 #pragma unroll
                 for (int st = 0; st < 32; st++) {
                     const uint32_t x = x0l + ((uint32_t)st << 6);
                     const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
-                    const uint32_t rr = atomic_rank16<true>(T, h, x < nvl, lt, sh);
+                    const uint32_t rr = atomic_rank16<true>(Tg, h, x < nvl, lt, sh);
                     rk[st >> 1] |= rr << (16 * (st & 1));
                 }
             } else {
@@ -1282,7 +1446,7 @@ __device__ __forceinline__ void count_sort_positions(MatchLDS& L, uint32_t bn, i
                         const int st = hb + q;
                         const uint32_t x = x0l + ((uint32_t)st << 6);
                         const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
-                        old[q] = atomicAdd(&T[h], x < nvl ? 1u << sh : 0u);
+                        old[q] = atomicAdd(&Tg[h], x < nvl ? 1u << sh : 0u);
                     }
 #pragma unroll
                     for (int q = 0; q < 16; q++) {
@@ -1298,26 +1462,60 @@ __device__ __forceinline__ void count_sort_positions(MatchLDS& L, uint32_t bn, i
     {   // bucket starts: thread t scans buckets 8t .. 8t + 7
         const uint4 a = reinterpret_cast<const uint4*>(T)[2 * tid], c = reinterpret_cast<const uint4*>(T)[2 * tid + 1];
         uint32_t w[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w}, pre[8], s = 0;
+#ifdef DMX_SORT_G4
+        const uint4 a2 = reinterpret_cast<const uint4*>(T2)[2 * tid], c2 = reinterpret_cast<const uint4*>(T2)[2 * tid + 1];
+        uint32_t w2[8] = {a2.x, a2.y, a2.z, a2.w, c2.x, c2.y, c2.z, c2.w};
+#endif
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             pre[j] = s;
             s += (w[j] & 0xFFFFu) + (w[j] >> 16);
+#ifdef DMX_SORT_G4
+            s += (w2[j] & 0xFFFFu) + (w2[j] >> 16);
+#endif
         }
         const uint32_t base = block_excl_scan(L, s, tid);
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const uint32_t st0 = base + pre[j];
             pre[j] = st0;
+#ifdef DMX_SORT_G4
+            const uint32_t s1 = st0 + (w[j] & 0xFFFFu), s2 = s1 + (w[j] >> 16);
+            w[j] = st0 | (s1 << 16);
+            w2[j] = s2 | ((s2 + (w2[j] & 0xFFFFu)) << 16);
+#else
             w[j] = st0 | ((st0 + (w[j] & 0xFFFFu)) << 16);
+#endif
         }
         reinterpret_cast<uint4*>(T)[2 * tid] = make_uint4(w[0], w[1], w[2], w[3]);
         reinterpret_cast<uint4*>(T)[2 * tid + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+#ifdef DMX_SORT_G4
+        reinterpret_cast<uint4*>(T2)[2 * tid] = make_uint4(w2[0], w2[1], w2[2], w2[3]);
+        reinterpret_cast<uint4*>(T2)[2 * tid + 1] = make_uint4(w2[4], w2[5], w2[6], w2[7]);
+#endif
         if (need_starts)
             reinterpret_cast<uint4*>(L.bstart)[tid] = make_uint4(pre[0] | (pre[1] << 16), pre[2] | (pre[3] << 16),
                                                                  pre[4] | (pre[5] << 16), pre[6] | (pre[7] << 16));
     }
     __syncthreads();
     asm volatile("" : "+v"(x0l), "+v"(nvl));
+#ifdef DMX_SORT_G4
+    // the destinations first (groups 2 and 3 read theirs from S's first half), then the stores
+#pragma unroll
+    for (int st = 0; st < 32; st++) {
+        const uint32_t h = (hh[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
+        const uint32_t rr = (rk[st >> 1] >> (16 * (st & 1))) & 0xFFFFu;
+        const uint32_t dst = ((Tg[h] >> sh) & 0xFFFFu) + rr;
+        rk[st >> 1] = (rk[st >> 1] & (0xFFFF0000u >> (16 * (st & 1)))) | ((dst & 0xFFFFu) << (16 * (st & 1)));
+        if ((st & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < 32; st++) {
+        const uint32_t x = x0l + ((uint32_t)st << 6);
+        if (x < nvl) L.sorted[(rk[st >> 1] >> (16 * (st & 1))) & 0xFFFFu] = (uint16_t)x;
+    }
+#else
 #pragma unroll
     for (int st = 0; st < 32; st++) {
         const uint32_t x = x0l + ((uint32_t)st << 6);
@@ -1326,6 +1524,7 @@ __device__ __forceinline__ void count_sort_positions(MatchLDS& L, uint32_t bn, i
         if (x < nvl) L.sorted[((T[h] >> sh) & 0xFFFFu) + rr] = (uint16_t)x;
         if ((st & 7) == 7) __builtin_amdgcn_sched_barrier(0);
     }
+#endif
     __syncthreads();
     if (stamp && tid == 0) tp0[2] = __builtin_amdgcn_s_memtime();
 }
@@ -2805,6 +3004,16 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
     for (uint32_t k = tid; k < DMX_HIST; k += MT) L.hist[k] = 0;
     for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) L.lit[k] = 0;
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
+#ifdef DMX_PF
+    // L2 prefetch of the block DMX_PF blocks ahead (the one that takes this CU's slot next when
+    // the blocks take about the same time; same XCD: DMX_PF is a multiple of 8): one dword per
+    // 128-byte line, its value consumed after P0 so the load never stalls the staging
+    uint32_t pfv = 0;
+    if (!LOOP && tid < 256) {
+        const uint64_t po = (uint64_t)(b + DMX_PF) * sw + (uint64_t)tid * 128;
+        if (po < n) pfv = *reinterpret_cast<const uint32_t*>(in + (po & ~3ull));
+    }
+#endif
     uint32_t runny = 0;   // 16-byte chunks of one repeated byte (run-dominated blocks)
     const uint32_t c4 = bn ? (uint32_t)d[0] * 0x01010101u : 0u;
     bool uni = true;      // every byte of the block equals byte 0
@@ -2886,6 +3095,9 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
     }
 
     if (dbg_stop(mflags, 1, info, hist_g, b, bn, tid)) return;
+#ifdef DMX_PF
+    asm volatile("" ::"v"(pfv));
+#endif
     {   // Adler-32 partial sums of this block
         uint64_t s = 0, t = 0;
         const uint32_t lo = tid << 5;   // 32 bytes per thread, read as two 16-byte vectors
@@ -3062,9 +3274,11 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
             const uint32_t dw[4] = {dv[j].x, dv[j].y, dv[j].z, dv[j].w}, pw[4] = {pv[j].x, pv[j].y, pv[j].z, pv[j].w};
 #pragma unroll
             for (int e = 0; e < 8; e++) {
+                // only matches (distance > 0): P3 reads S[p] for match tokens alone, so a
+                // literal position keeps whatever the slot held
                 const uint32_t kk = (tid + (uint32_t)j * MT) * 8 + (uint32_t)e;
-                if (kk < nvalid)
-                    L.sorted[(pw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu] = (uint16_t)(dw[e >> 1] >> (16 * (e & 1)));
+                const uint32_t d16 = (dw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+                if (kk < nvalid && d16 != 0) L.sorted[(pw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu] = (uint16_t)d16;
             }
         }
     }

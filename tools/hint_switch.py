@@ -31,7 +31,7 @@ def run(sizes):
     cap = D.max_compressed(n)
     out = torch.empty(cap, dtype=torch.uint8, device="cuda")
     e = D.Encoder(0, n, max_chain=7, flags=fl)
-    s = torch.cuda.current_stream()
+    s = torch.cuda.Stream()   # (a stream of its own: handle 0 would mean the context's stream to the encoder)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 
     def once(t):
