@@ -995,7 +995,7 @@ __device__ __forceinline__ uint32_t search_positions(MatchLDS& L, uint32_t bn, i
     if (RUNS) build_chg(L, bn, tid);
 #ifndef DMX_NO_PAIRS
     if (!RUNS && NB == 3 && K >= 6 && K <= 8) {
-#ifdef DMX_QUADS   // four entries per lane (search_quads)
+#ifndef DMX_PAIRS   // four entries per lane (search_quads; DMX_PAIRS: the round-5 two-entry path)
         iters = K == 8 ? search_quads<DICT, 8>(L, bn, tid, stamp, tdef, hbk)
               : K == 7 ? search_quads<DICT, 7>(L, bn, tid, stamp, tdef, hbk)
                        : search_quads<DICT, 6>(L, bn, tid, stamp, tdef, hbk);
@@ -1260,10 +1260,33 @@ __device__ __forceinline__ uint32_t resolve_word(const MatchLDS& L, uint32_t lo,
     if (e >= lo + 32 || e >= bn) { nm_out = 0; return e; }
     uint32_t nm = 0, p = e;
     while (p < lo + 32 && p < bn) {
+#ifndef DMX_WALK_STEP
+        // a run of literals in one step (their bits in lw, up to the segment end or bn): every
+        // position of it is a token start; no LDS read
+        const uint32_t sh = p - lo;
+        const uint32_t run = min(ffbl_hw(~(lw >> sh)), min(lo + 32u, bn) - p);   // (lit bits past bn may be set by P1b)
+        if (run) {
+            const uint32_t rm = (run >= 32u ? ~0u : ((1u << run) - 1u)) << sh;
+            if (m & rm) {
+                const uint32_t bb = ffbl_hw(m & rm), below = (1u << bb) - 1u;   // the first shared position
+                nm_out = nm | (rm & below) | (m & ~below);
+                merged = true;
+                return x;
+            }
+            nm |= rm;
+            p += run;
+            continue;
+        }
+        const uint32_t bit = 1u << sh;
+        if (m & bit) { nm_out = nm | (m & ~(bit - 1u)); merged = true; return x; }
+        nm |= bit;
+        p += (uint32_t)L.len8[p] + 3u;
+#else
         const uint32_t bit = 1u << (p - lo);
         if (m & bit) { nm_out = nm | (m & ~(bit - 1u)); merged = true; return x; }
         nm |= bit;
         p += ((lw >> (p - lo)) & 1u) ? 1u : (uint32_t)L.len8[p] + 3u;
+#endif
     }
     nm_out = nm;
     return p;
@@ -1368,18 +1391,22 @@ __device__ __forceinline__ uint32_t atomic_rank16(uint32_t* T, uint32_t v, bool 
 
 // Bucket-sorted positions S (stable by position inside a bucket) by ONE counting pass over
 // the 13-bit bucket (round 5; the two-pass LSD sort below stays as the checked fallback).
-// The block's positions form two groups (g = 0: [0, 16384), g = 1: the rest); T[h] holds
-// group 0's count of bucket h in its low 16 bits and group 1's in its high 16 bits.
+// The block's positions form four groups of 8192 (g = w >> 2 for wave w; round 6: two groups
+// of 16384 until round 5, -DDMX_SORT_G2); T[h] (in len8) holds the counts of bucket h of groups
+// 0 and 1 in its low and high 16 bits, T2[h] (in S's first half, free until the scatter)
+// those of groups 2 and 3.
 //  1. every wave hashes its 2048 positions [2048w, 2048w + 2048) into registers;
-//  2. eight rounds, one wave of each group per round (wave w in round w & 7, its group
-//     w >> 3), separated by barriers: the wave adds 1 << 16g to T[h] for its 32 steps of
-//     64 positions and keeps the old field as the entry's rank.  Inside a round a wave's LDS
-//     instructions execute in order and same-address lanes of one instruction in lane
-//     order; the rounds run in position order, so the rank of every entry is the number of
-//     earlier positions of its bucket in its group -- the stable order;
-//  3. one scan over the 8192 buckets: T[h] := start(h) | (start(h) + count0(h)) << 16, the
-//     first slot of each group's run (and start(h) is the bucket start the long chains need);
-//  4. every wave stores its entries at T[h]'s field + rank, no atomics.
+//  2. four rounds, one wave of each group per round (wave w in round w & 3), separated by
+//     barriers: the wave adds 1 << 16 (g & 1) to its group's word of bucket h for its 32
+//     steps of 64 positions and keeps the old field as the entry's rank.  Inside a round a
+//     wave's LDS instructions execute in order and same-address lanes of one instruction in
+//     lane order; the rounds run in position order, so the rank of every entry is the number
+//     of earlier positions of its bucket in its group -- the stable order (four waves at a
+//     time: half the rounds and barriers of two groups, the same atomics);
+//  3. one scan over the 8192 buckets: each group's field := the first slot of its run
+//     (start(h), + count0, + count1, + count2; start(h) is the bucket start long chains need);
+//  4. every wave reads its entries' destinations (field + rank), a barrier (S's first half
+//     held counters), then stores them, no atomics.
 // One rank atomic per entry instead of the LSD sort's two (plus its second count), and the
 // scatter is plain stores.  The search checks every adjacent pair of S (sortbad), so a lane
 // order violation can never go unnoticed: the block then re-sorts with the match-any path.
@@ -1393,7 +1420,7 @@ __device__ __forceinline__ void count_sort_positions(MatchLDS& L, uint32_t bn, i
     const uint4 z4 = make_uint4(0, 0, 0, 0);
     reinterpret_cast<uint4*>(T)[tid] = z4;
     reinterpret_cast<uint4*>(T)[tid + MT] = z4;
-#ifdef DMX_SORT_G4
+#ifndef DMX_SORT_G2
     // four groups of four waves: groups 2 and 3 count in the first half of S (free until the
     // scatter), four ordered rounds of four waves instead of eight of two
     uint32_t* T2 = reinterpret_cast<uint32_t*>(L.sorted);
@@ -1462,7 +1489,7 @@ __device__ __forceinline__ void count_sort_positions(MatchLDS& L, uint32_t bn, i
     {   // bucket starts: thread t scans buckets 8t .. 8t + 7
         const uint4 a = reinterpret_cast<const uint4*>(T)[2 * tid], c = reinterpret_cast<const uint4*>(T)[2 * tid + 1];
         uint32_t w[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w}, pre[8], s = 0;
-#ifdef DMX_SORT_G4
+#ifndef DMX_SORT_G2
         const uint4 a2 = reinterpret_cast<const uint4*>(T2)[2 * tid], c2 = reinterpret_cast<const uint4*>(T2)[2 * tid + 1];
         uint32_t w2[8] = {a2.x, a2.y, a2.z, a2.w, c2.x, c2.y, c2.z, c2.w};
 #endif
@@ -1470,7 +1497,7 @@ __device__ __forceinline__ void count_sort_positions(MatchLDS& L, uint32_t bn, i
         for (int j = 0; j < 8; j++) {
             pre[j] = s;
             s += (w[j] & 0xFFFFu) + (w[j] >> 16);
-#ifdef DMX_SORT_G4
+#ifndef DMX_SORT_G2
             s += (w2[j] & 0xFFFFu) + (w2[j] >> 16);
 #endif
         }
@@ -1479,7 +1506,7 @@ __device__ __forceinline__ void count_sort_positions(MatchLDS& L, uint32_t bn, i
         for (int j = 0; j < 8; j++) {
             const uint32_t st0 = base + pre[j];
             pre[j] = st0;
-#ifdef DMX_SORT_G4
+#ifndef DMX_SORT_G2
             const uint32_t s1 = st0 + (w[j] & 0xFFFFu), s2 = s1 + (w[j] >> 16);
             w[j] = st0 | (s1 << 16);
             w2[j] = s2 | ((s2 + (w2[j] & 0xFFFFu)) << 16);
@@ -1489,7 +1516,7 @@ __device__ __forceinline__ void count_sort_positions(MatchLDS& L, uint32_t bn, i
         }
         reinterpret_cast<uint4*>(T)[2 * tid] = make_uint4(w[0], w[1], w[2], w[3]);
         reinterpret_cast<uint4*>(T)[2 * tid + 1] = make_uint4(w[4], w[5], w[6], w[7]);
-#ifdef DMX_SORT_G4
+#ifndef DMX_SORT_G2
         reinterpret_cast<uint4*>(T2)[2 * tid] = make_uint4(w2[0], w2[1], w2[2], w2[3]);
         reinterpret_cast<uint4*>(T2)[2 * tid + 1] = make_uint4(w2[4], w2[5], w2[6], w2[7]);
 #endif
@@ -1499,7 +1526,7 @@ __device__ __forceinline__ void count_sort_positions(MatchLDS& L, uint32_t bn, i
     }
     __syncthreads();
     asm volatile("" : "+v"(x0l), "+v"(nvl));
-#ifdef DMX_SORT_G4
+#ifndef DMX_SORT_G2
     // the destinations first (groups 2 and 3 read theirs from S's first half), then the stores
 #pragma unroll
     for (int st = 0; st < 32; st++) {
@@ -3225,8 +3252,21 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
         const uint32_t lo = tid << 5, lw = L.lit[tid];   // the segment's literal bits: one read
         uint32_t m = 0, p = lo;
         while (p < lo + 32 && p < bn) {
+#ifndef DMX_WALK_STEP
+            // a run of literals in one step (resolve_word); a match reads its length
+            const uint32_t sh = p - lo;
+            const uint32_t run = min(ffbl_hw(~(lw >> sh)), min(lo + 32u, bn) - p);   // (lit bits past bn may be set by P1b)
+            if (run) {
+                m |= (run >= 32u ? ~0u : ((1u << run) - 1u)) << sh;
+                p += run;
+                continue;
+            }
+            m |= 1u << sh;
+            p += (uint32_t)L.len8[p] + 3u;
+#else
             m |= 1u << (p - lo);
             p += ((lw >> (p - lo)) & 1u) ? 1u : (uint32_t)L.len8[p] + 3u;
+#endif
         }
         L.tsm[tid] = m;
         L.exitp[tid] = p;
@@ -3407,6 +3447,7 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
                 if (kk >= r0) TP[kk - r0] = (uint16_t)((tid << 5) + (uint32_t)__builtin_ctz(mm));
             __syncthreads();
             if (dbg && tid == 0 && r0 == 0) st_p3a = __builtin_amdgcn_s_memtime() - t1;   // first list built
+#ifndef DMX_P3_BATCH   // (the batched loads measured slower at K = 7: 48.8 -> 50.1 K cycles to P3's end, round 6)
             for (uint32_t t = r0 + tid; t < r1; t += MT) {
                 const uint32_t p = TP[t - r0];
                 uint32_t tk;
@@ -3424,6 +3465,44 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
                 }
                 tb[t] = tk;
             }
+#else
+            // DMX_P3_BATCH: P3B tokens per thread at a time, their LDS reads issued together (token position,
+            // literal word, then byte, length and distance of each, whichever it is): three
+            // rounds of latency for the batch instead of three per token
+            constexpr uint32_t P3B = 8;
+            for (uint32_t t0 = r0 + tid; t0 < r1; t0 += P3B * MT) {
+                uint32_t pp[P3B], lw8[P3B], cb[P3B], l8[P3B], ds[P3B];
+#pragma unroll
+                for (uint32_t j = 0; j < P3B; j++) pp[j] = t0 + j * MT < r1 ? (uint32_t)TP[t0 + j * MT - r0] : 0u;
+#pragma unroll
+                for (uint32_t j = 0; j < P3B; j++) lw8[j] = L.lit[pp[j] >> 5];
+#pragma unroll
+                for (uint32_t j = 0; j < P3B; j++) {
+                    cb[j] = D8[pp[j]];
+                    l8[j] = L.len8[pp[j]];
+                    ds[j] = L.sorted[pp[j]];
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < P3B; j++) {
+                    const uint32_t t = t0 + j * MT;
+                    if (t >= r1) break;
+                    uint32_t tk;
+                    if ((lw8[j] >> (pp[j] & 31)) & 1u) {
+                        tk = cb[j];
+                        atomicAdd(&hl[tk], 1u);
+                    } else {
+                        const uint32_t len = l8[j] + 3u, dist = ds[j];
+                        tk = (dist << 9) | len;
+                        uint32_t sy, eb, ev;
+                        len_sym(len, sy, eb, ev);
+                        atomicAdd(&hl[sy], 1u);
+                        dist_sym(dist, sy, eb, ev);
+                        atomicAdd(&hl[DMX_DIST0 + sy], 1u);
+                    }
+                    tb[t] = tk;
+                }
+            }
+#endif
         }
         __syncthreads();
         for (uint32_t q = tid; q < DMX_HIST; q += MT) L.hist[q] += HS[q] + HS[HSTR + q] + HS[2 * HSTR + q] + HS[3 * HSTR + q];

@@ -6,6 +6,7 @@ lists) must write the oracle's stream byte for byte, and the adaptive choice (th
 encode's hint) too, whatever it picks.
 
 Bar: bit-exact against the oracle (store_check=True), zlib inflates."""
+import os
 import zlib
 
 import numpy as np
@@ -315,11 +316,21 @@ def test_scan_many_tiles(sw, ntile):
     """K3 above 65 536 blocks: the fused launch's threads compose C = 2 tile aggregates each
     (257 tiles), and just past its 1 024-tile limit the three-launch path takes over (1 025
     tiles) -- both the oracle's stream, with DMX_SCAN3 forced and not."""
+    import time
+    hb = os.environ.get("DMX_TEST_HEARTBEAT")   # progress for a watchdog (each step names itself)
+
+    def beat(msg):
+        if hb:
+            with open(hb, "a") as h:
+                h.write(f"scan_many_tiles sw={sw} ntile={ntile}: {msg} {time.time():.1f}\n")
+
     nblk = ntile * 256 - 100
     a = _many_blocks(nblk, sw, 5 + ntile)
     assert (a.size + sw - 1) // sw == nblk and (nblk + 255) // 256 == ntile
     fl = D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_STORE_CHECK
-    want = O.compress_par(a, sw=sw, max_chain=4, lazy=True, store_check=True, threads=16)
+    beat("input")
+    want = O.compress_par(a, sw=sw, max_chain=4, lazy=True, store_check=True, threads=8)
+    beat("oracle")
     e = D.Encoder(0, a.size, sw=sw)
     try:
         t = torch.from_numpy(a).cuda()
@@ -327,6 +338,7 @@ def test_scan_many_tiles(sw, ntile):
             e.set_hook("scan3", v)
             for rep in range(2):
                 z, r = e.compress_tensor(t, opts=D.Opts(sw, 4, fl, 0))
+                beat(f"encode scan3={v} rep={rep}")
                 assert r.status == 0 and r.nblocks == nblk
                 assert z.cpu().numpy().tobytes() == want, (sw, ntile, v, rep)
     finally:
