@@ -890,7 +890,19 @@ long long dmx_oracle_compress_par(const uint8_t* in, size_t n, int sw, int max_c
     long long r = -1;
     if (!bad) {
         orc_bw w = orc_start(out, cap, nblk, flags);
-        for (size_t b = 0; b < nblk; b++) orc_put_bits(&w, bb + b * bcap, bits[b]);
+        for (size_t b = 0; b < nblk; b++) {
+            const uint8_t* buf = bb + b * bcap;
+            if ((buf[0] & 6u) == 0 && bits[b] >= 8) {
+                /* a stored block (BTYPE 00, never split): its padding to the byte boundary was
+                 * taken at bit 3 of its own buffer; in the stream it pads from wherever the
+                 * block starts (RFC 1951 3.2.4), as the serial writer does */
+                orc_put(&w, buf[0] & 7u, 3);
+                orc_align(&w);
+                orc_put_bits(&w, buf + 1, bits[b] - 8);
+            } else {
+                orc_put_bits(&w, buf, bits[b]);
+            }
+        }
         r = orc_finish(&w, out, cap, nblk, flags, (flags & ORC_F_TRAILER) ? dmx_oracle_adler32(in, n) : 0u);
     }
     free(bb);

@@ -340,7 +340,8 @@ def test_scan_many_tiles(sw, ntile):
                 z, r = e.compress_tensor(t, opts=D.Opts(sw, 4, fl, 0))
                 beat(f"encode scan3={v} rep={rep}")
                 assert r.status == 0 and r.nblocks == nblk
-                assert z.cpu().numpy().tobytes() == want, (sw, ntile, v, rep)
+                same = z.cpu().numpy().tobytes() == want   # (no assertion diff of 11 MB streams)
+                assert same, (sw, ntile, v, rep, int(r.out_len), len(want))
     finally:
         e.close()
 
