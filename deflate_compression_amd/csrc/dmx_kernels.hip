@@ -638,10 +638,11 @@ __device__ __forceinline__ void store_short(MatchLDS& L, uint32_t k, uint32_t i,
 // CBS bytes only for the rare survivors.  Then the entry's result is stored.
 template <bool DICT, bool RUNS>
 __device__ __forceinline__ void ext_queue(MatchLDS& L, uint32_t bn, uint32_t K, uint32_t* Qw, uint32_t qn,
-                                          uint32_t lane, const uint32_t* __restrict__ hbk) {
+                                          uint32_t lane, const uint32_t* __restrict__ hbk, uint32_t head = 0,
+                                          uint32_t qmask = 63) {
     __builtin_amdgcn_wave_barrier();
     if (lane < qn) {
-        const uint32_t it = lds_ld(&Qw[lane]);
+        const uint32_t it = lds_ld(&Qw[(head + lane) & qmask]);   // (items head .. head + qn - 1 of a ring)
         const uint32_t k = it & 0x7FFFu, nc = min(k, K);
         uint32_t bj = it >> 15;
         const uint32_t i = L.sorted[k];
@@ -885,7 +886,14 @@ __device__ __forceinline__ uint32_t search_quads(MatchLDS& L, uint32_t bn, uint3
     constexpr uint32_t OWN = 4 * (64 - HQ);
     const uint32_t lane = tid & 63, wave = wave_of(tid);
     const uint32_t nvalid = bn > 2 ? bn - 2 : 0;
+#ifndef DMX_QSLOTS
+    // the extension queue: a ring of 128 items per wave over tsm + exitp (both free during the
+    // search, adjacent in MatchLDS): a chunk's items go in at once, batches of 64 come out
+    uint32_t* Qw = L.tsm + (wave << 7);
+    uint32_t qh = 0;   // ring head (wave-uniform)
+#else
     uint32_t* Qw = L.tsm + (wave << 6);   // the extension queue (P2 arrays are free during the search)
+#endif
     const uint64_t lt = (1ull << lane) - 1ull;
     uint32_t qn = 0, iters = 0;
     uint32_t cnext = wave_claim(&L.ntok);   // chunks from the workgroup counter, one ahead (search_pairs)
@@ -948,6 +956,54 @@ __device__ __forceinline__ uint32_t search_quads(MatchLDS& L, uint32_t bn, uint3
         }
         // a candidate equal in all CBS bytes (key >= 64): the entry is queued for the LDS
         // extension (unless the block end caps it there); E_0's items, then E_1's, ...
+#ifndef DMX_QSLOTS
+        bool push[4];
+        uint64_t pmv[4];
+        uint32_t npr[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+#ifdef DMX_KO_QUEUE   // timing knockout (wrong output): no queued extension
+            push[r] = false;
+#else
+            push[r] = act[r] && key[r] >= (CBS << 3) && lim[r] > CBS;
+#endif
+            pmv[r] = __ballot(push[r]);
+            npr[r] = (uint32_t)__popcll(pmv[r]);
+        }
+        const uint32_t npt = npr[0] + npr[1] + npr[2] + npr[3];
+        // appends: all four slots at once when they fit the ring (the usual case), else one slot
+        // at a time; batches of 64 leave whenever 64 are in (all of them at the end).  One call
+        // site of ext_queue (code size, registers)
+        uint32_t rs = (qn + npt <= 128u) ? 4u : 0u;   // next append: slot rs, 4 = all, 5 = done
+        if (npt || (!more && qn)) {
+#pragma nounroll
+            for (;;) {
+                const uint32_t want = rs == 4u ? npt : rs < 4u ? (rs == 0 ? npr[0] : rs == 1 ? npr[1] : rs == 2 ? npr[2] : npr[3]) : 0u;
+                if (qn >= 64u || (qn && (!more || qn + want > 128u))) {
+                    const uint32_t nq = qn < 64u ? qn : 64u;
+                    const uint64_t td0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
+                    ext_queue<DICT, false>(L, bn, KK, Qw, nq, lane, hbk, qh, 127u);
+                    if (stamp) tdef += __builtin_amdgcn_s_memtime() - td0;
+                    qh += nq;
+                    qn -= nq;
+                    continue;
+                }
+                if (!more || rs == 5u) break;
+                uint32_t off = 0;
+#pragma unroll
+                for (uint32_t r = 0; r < 4; r++) {
+                    if (rs == 4u || rs == r) {
+                        if (push[r])
+                            lds_st(&Qw[(qh + qn + off + (uint32_t)__popcll(pmv[r] & lt)) & 127u],
+                                   (k0 + r) | ((8u - (key[r] & 7u)) << 15));
+                        off += npr[r];
+                    }
+                }
+                qn += want;
+                rs = rs >= 3u ? 5u : rs + 1u;
+            }
+        }
+#else
         bool push[4];
         uint64_t pmv[4];
         uint32_t pbits = 0, jbits = 0;   // per slot r: push flag (bit r), the key's 8 - j (bits 3r + 2 .. 3r)
@@ -980,6 +1036,7 @@ __device__ __forceinline__ uint32_t search_quads(MatchLDS& L, uint32_t bn, uint3
                 qn += npx;
             }
         }
+#endif
         if (!more) break;
         uint32_t nib = 0;
 #pragma unroll
@@ -3455,7 +3512,12 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
                 if (kk >= r0) TP[kk - r0] = (uint16_t)((tid << 5) + (uint32_t)__builtin_ctz(mm));
             __syncthreads();
             if (dbg && tid == 0 && r0 == 0) st_p3a = __builtin_amdgcn_s_memtime() - t1;   // first list built
-#ifndef DMX_P3_BATCH   // (the batched loads measured slower at K = 7: 48.8 -> 50.1 K cycles to P3's end, round 6)
+#ifdef DMX_P3_BATCH
+            constexpr bool p3batch = true;
+#else
+            constexpr bool p3batch = h4;   // (batched loads: the exhaustive parse +0.6 %; K = 7 48.8 -> 50.1 K cycles to P3's end, round 6)
+#endif
+            if constexpr (!p3batch) {
             for (uint32_t t = r0 + tid; t < r1; t += MT) {
                 const uint32_t p = TP[t - r0];
                 uint32_t tk;
@@ -3473,8 +3535,8 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
                 }
                 tb[t] = tk;
             }
-#else
-            // DMX_P3_BATCH: P3B tokens per thread at a time, their LDS reads issued together (token position,
+            } else {
+            // DMX_P3_BATCH (and the exhaustive parse): P3B tokens per thread at a time, their LDS reads issued together (token position,
             // literal word, then byte, length and distance of each, whichever it is): three
             // rounds of latency for the batch instead of three per token
             constexpr uint32_t P3B = 8;
@@ -3510,7 +3572,7 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
                     tb[t] = tk;
                 }
             }
-#endif
+            }
         }
         __syncthreads();
         for (uint32_t q = tid; q < DMX_HIST; q += MT) L.hist[q] += HS[q] + HS[HSTR + q] + HS[2 * HSTR + q] + HS[3 * HSTR + q];
