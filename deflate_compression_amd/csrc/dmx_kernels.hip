@@ -3067,6 +3067,14 @@ __device__ __forceinline__ int32_t block_chain(MatchLDS& L, uint32_t bn, int32_t
 #ifndef DMX_NBX
 #define DMX_NBX 4   // the exhaustive parse's chain length in bytes (4; 5 measured slower: a second gram pass and sort)
 #endif
+// 16 bytes of a block from HBM for the staging (bytes past bn are zero)
+__device__ __forceinline__ uint4 stage16(const uint8_t* __restrict__ d, uint32_t p, uint32_t bn, bool aligned16) {
+    if (aligned16 && p + 16 <= bn) return *reinterpret_cast<const uint4*>(d + p);
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (uint32_t j = 0; j < 16; j++)
+        if (p + j < bn) w[j >> 2] |= (uint32_t)d[p + j] << (8 * (j & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
 template <bool DICT, int NBX, bool LOOP = false>
 __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __restrict__ in, uint64_t n, uint32_t sw,
                                             int32_t max_chain, uint32_t mflags, uint16_t* __restrict__ dist_g,
@@ -3082,10 +3090,25 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
     // across the whole block
     if (LOOP) asm volatile("" : "+v"(tid));
     const uint32_t lane = tid & 63, wave = wave_of(tid);
-    if ((mflags & 4u) && info[b].prestored) return;   // stored by the noise check (K0)
     const uint64_t off = (uint64_t)b * sw;
     const uint32_t bn = (uint32_t)((n - off) < sw ? (n - off) : sw);
     const uint8_t* d = in + off;
+    const bool aligned16 = ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
+    // a workgroup per block: the block's bytes (the 2 MT chunks below DMX_BLK) are requested
+    // right after the noise check's record, so the two HBM latencies overlap (a stored
+    // block's are wasted: such blocks take the work-list loop when they are most of the input)
+    const uint32_t pst = info[b].prestored;   // (read unconditionally: a conditional read is waited for at once)
+#ifndef DMX_LATE_STAGE   // (A/B build: the loads after the check, in the staging loop)
+    constexpr bool early = !LOOP;
+#else
+    constexpr bool early = false;
+#endif
+    uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0;
+    if (early) {
+        v0 = stage16(d, tid << 4, bn, aligned16);
+        v1 = stage16(d, (tid + MT) << 4, bn, aligned16);
+    }
+    if ((mflags & 4u) && pst) return;   // stored by the noise check (K0)
     uint16_t* pg = dist_g + (uint64_t)b * DMX_BLK;   // best distances, bucket order (staging)
     uint8_t* D8 = reinterpret_cast<uint8_t*>(L.data);
 
@@ -3095,7 +3118,6 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
     if (dbg && tid == 0) { st_search = 0; st_iters = 0; st_def = 0; st_p3a = 0; }
     for (uint32_t k = tid; k < DMX_HIST; k += MT) L.hist[k] = 0;
     for (uint32_t k = tid; k < DMX_BLK / 32; k += MT) L.lit[k] = 0;
-    const bool aligned16 = ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
 #ifdef DMX_PF
     // L2 prefetch of the block DMX_PF blocks ahead (the one that takes this CU's slot next when
     // the blocks take about the same time; same XCD: DMX_PF is a multiple of 8): one dword per
@@ -3107,28 +3129,29 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
     }
 #endif
     uint32_t runny = 0;   // 16-byte chunks of one repeated byte (run-dominated blocks)
-    const uint32_t c4 = bn ? (uint32_t)d[0] * 0x01010101u : 0u;
-    bool uni = true;      // every byte of the block equals byte 0
+    // a block of one repeated byte: every chunk of this thread is one repeated byte, the same
+    // byte cb in all of them (0x100: none yet), and (below, after the barrier) cb is byte 0
+    // -- no separate load of byte 0
+    bool uni = true;
+    uint32_t cb = 0x100u;
     for (uint32_t k = tid; k < DATA_WORDS / 4; k += MT) {   // 16-byte chunks
         const uint32_t p = k << 4;
         uint4 v;
-        if (aligned16 && p + 16 <= bn) {
-            v = *reinterpret_cast<const uint4*>(d + p);
-        } else {
-            uint32_t w[4] = {0, 0, 0, 0};
-            for (uint32_t j = 0; j < 16; j++)
-                if (p + j < bn) w[j >> 2] |= (uint32_t)d[p + j] << (8 * (j & 3));
-            v = make_uint4(w[0], w[1], w[2], w[3]);
-        }
+        if (early && k < 2 * MT) v = k < MT ? v0 : v1;
+        else v = stage16(d, p, bn, aligned16);
         *reinterpret_cast<uint4*>(&L.data[k << 2]) = v;
         // run-dominated blocks take the run_len search (search_positions<.., true>): count the
         // 16-byte chunks that are one repeated byte
-        runny += (p < bn && v.x == v.y && v.y == v.z && v.z == v.w && v.x == (v.x & 0xFFu) * 0x01010101u) ? 1u : 0u;
+        const bool rep = v.x == v.y && v.y == v.z && v.z == v.w && v.x == (v.x & 0xFFu) * 0x01010101u;
+        runny += (p < bn && rep) ? 1u : 0u;
         if (p + 16 <= bn) {
-            uni = uni && v.x == c4 && v.y == c4 && v.z == c4 && v.w == c4;
+            uni = uni && rep && (cb == 0x100u || cb == (v.x & 0xFFu));
+            cb = v.x & 0xFFu;
         } else if (p < bn) {   // the tail chunk: its bytes below bn
             const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-            for (uint32_t j = 0; j < bn - p; j++) uni = uni && ((w4[j >> 2] >> (8 * (j & 3))) & 0xFFu) == (c4 & 0xFFu);
+            const uint32_t c0 = cb == 0x100u ? (v.x & 0xFFu) : cb;
+            for (uint32_t j = 0; j < bn - p; j++) uni = uni && ((w4[j >> 2] >> (8 * (j & 3))) & 0xFFu) == c0;
+            cb = c0;
         }
     }
     runny = wave_sum_u32(runny);
@@ -3160,8 +3183,8 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
         // (position i's nearest candidate is i - 1, matching to the block's end; lazy
         // evaluation never defers: i + 1 is never longer).  Tokens, histograms and the
         // block record are written directly.
-        if (__syncthreads_and(uni)) {   // (also publishes the waves' run counts)
-            const uint32_t c = c4 & 0xFFu;
+        if (__syncthreads_and(uni) && __syncthreads_and(cb == 0x100u || cb == (uint32_t)D8[0])) {   // (also publishes the waves' run counts)
+            const uint32_t c = D8[0];
             const uint32_t nt = uniform_parse(bn, c, tok_g + (uint64_t)b * DMX_BLK, L.hist, tid, MT);
             if (tid == 0) {
                 const uint64_t S = (uint64_t)c * bn, T = (uint64_t)c * ((uint64_t)bn * (bn - 1) / 2);
@@ -3476,7 +3499,6 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
     }
     if (dbg && tid == 0) st_w23 = __builtin_amdgcn_s_memtime() - t1;
     if (dbg_stop(mflags, 3, info, hist_g, b, bn, tid)) return;
-
     // ---- P3: compaction + histograms ----
     {
         const uint32_t m = L.tsm[tid];

@@ -14,7 +14,7 @@ for v in $VARS; do
   ( cd /tmp && DMX_LIBV=$lib timeout -k 10 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/sq_$v" -o sq \
       -- python3 "$R/tools/phase_run.py" 20 7 1 > "$OUT/sq_$v.log" 2>&1 ) || exit $?
   echo "== $v" >> "$OUT/var_sq.txt"
-  python3 "$R/tools/pmc.py" "$OUT/sq_$v" | grep match_kernel >> "$OUT/var_sq.txt"
+  python3 "$R/tools/pmc.py" "$OUT/sq_$v" | grep -E "match_(pf_)?kernel" >> "$OUT/var_sq.txt"
   DMX_LIBV=$lib timeout -k 10 120 python3 "$R/tools/stamps.py" text:7 text:0:g >> "$OUT/var_sq.txt" 2>&1 || exit $?
 done
 cat "$OUT/var_sq.txt"
