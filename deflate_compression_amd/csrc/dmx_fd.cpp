@@ -639,9 +639,13 @@ static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts,
         pthread_mutex_unlock(&S.mu);
         if (r) break;
         // H2D into device input kd: encode i - FDP_NDIN read it, encode i - FDP_NDIN + 1 its tail
-        // (history); the latter is ordered after the former on the encode stream
+        // (history); the latter is ordered after the former on the encode stream, and the host
+        // has already waited for it (finish(i - 2) ran in the previous iteration, or earlier with
+        // a callback), so the copy stream needs no wait packet before the copy
+#ifdef DMX_FD_WAIT   // (A/B build: the stream wait as before)
         if (i >= FDP_NDIN - 1 && hip_fail(hipStreamWaitEvent(P->sh, P->eve[(i - (FDP_NDIN - 1)) & 1], 0), "wait"))
             r = -(int)E_DEVICE;
+#endif
         if (!r && hip_fail(hipEventRecord(P->th[ki], P->sh), "hipEventRecord")) r = -(int)E_DEVICE;
         if (!r && len && hip_fail(hipMemcpyAsync(P->din[kd], P->hin[ki], (size_t)len, hipMemcpyHostToDevice, P->sh), "H2D"))
             r = -(int)E_DEVICE;
@@ -652,7 +656,9 @@ static int encode_fd_on(int device, int fd_in, int fd_out, const dmx_opts* opts,
         pthread_mutex_unlock(&S.mu);
         // the encode: after its H2D, and after the D2H that last read device output k2
         if (!r && hip_fail(hipStreamWaitEvent(s, P->evh[ki], 0), "wait")) r = -(int)E_DEVICE;
-        if (!r && i >= 2 && hip_fail(hipStreamWaitEvent(s, P->evd[k2], 0), "wait")) r = -(int)E_DEVICE;
+        if (!r && i >= 2 && hipEventQuery(P->evd[k2]) != hipSuccess &&   // (no wait packet when the D2H is done)
+            hip_fail(hipStreamWaitEvent(s, P->evd[k2], 0), "wait"))
+            r = -(int)E_DEVICE;
         dmx_opts oc = o;
         oc.flags = pflags | (i == 0 ? DMX_F_HEADER : 0u) | (last ? DMX_F_FINAL : 0u);
         oc.dict = NULL;

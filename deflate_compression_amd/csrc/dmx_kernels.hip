@@ -3881,14 +3881,17 @@ __device__ void huff_lengths(K2LDS& S, const F* f, int n, int maxbits, uint8_t* 
             uu[r] = j < nn ? S.up[u[r]] : 0u;
         }
         wsync();
+        bool open = false;   // a node whose ancestor is not the root yet
 #pragma unroll
         for (int r = 0; r < 5; r++) {
             const int j = r * 64 + (int)lane;
             d[r] += du[r];
             u[r] = uu[r];
             if (j < nn) { S.dd[j] = (uint16_t)d[r]; S.up[j] = (uint16_t)u[r]; }
+            open = open || (j < nn && u[r] != (uint32_t)root);
         }
         wsync();
+        if (!__ballot(open)) break;   // every node points at the root: the depths are final (text: 5 of 9 rounds)
     }
     // leaf depths -> leaves per length
     uint32_t maxd = 0;

@@ -6,5 +6,5 @@ set -euo pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; shift
 make -s -C "$R/deflate_compression_amd/csrc" OUT="$R/build/var/libdmx_$NAME.so" BUILD="$R/build/var/$NAME" \
-    HIPFLAGS="-O3 -fPIC --offload-arch=gfx950 -std=c++17 -Wall -Wno-unused-function $*"
+    DEFS="$*"
 echo "built build/var/libdmx_$NAME.so"
