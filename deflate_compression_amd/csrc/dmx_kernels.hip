@@ -3751,13 +3751,13 @@ __constant__ uint8_t c_clorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 1
 // (dmx_k2_stamps): 0 rank sort, 1 two-queue merge, 2 depths + lengths, 3 canonical codes,
 // 4 run-length coding, 5 header emission, 6 the rest, 7 blocks.
 #ifdef DMX_K2_STAMPS
-__device__ unsigned long long dmx_k2_st[8];
+__device__ unsigned long long dmx_k2_st[16];
 #define K2T() __builtin_amdgcn_s_memtime()
 #define K2ST(k, t0) do { const uint64_t t1_ = K2T(); if ((threadIdx.x & 63) == 0) atomicAdd(&dmx_k2_st[k], (unsigned long long)(t1_ - (t0))); t0 = t1_; } while (0)
 extern "C" int dmx_k2_stamps(unsigned long long* host, int reset) {
-    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(dmx_k2_st), sizeof(unsigned long long) * 8, 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(dmx_k2_st), sizeof(unsigned long long) * 16, 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long z[16] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(dmx_k2_st), z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess) return -1;
     }
     return 0;
@@ -3842,11 +3842,46 @@ __device__ void huff_lengths(K2LDS& S, const F* f, int n, int maxbits, uint8_t* 
             S.sym[rk[r]] = (uint16_t)(ck[r] & 511u);
         }
     if (lane < 32) S.blc[lane] = 0;
+#ifndef DMX_MERGE_BRANCHY
+    // sentinels for the merge: no leaf past the last (two reads ahead), no node not yet made
+    // (a weight is at most 32 770, so 0xFFFF is above every real one)
+    if (lane < 2) S.fs[m + lane] = 0xFFFFu;
+#pragma unroll
+    for (int r = 0; r < 5; r++)
+        if (r * 64 + (int)lane < 288) S.nodew[r * 64 + lane] = 0xFFFFu;
+#endif
     wsync();
     K2ST(0, kt);
     const int mm = (int)m, nn = mm - 1, root = nn - 1;
     if (lane == 0) {   // two-queue merge
         int li = 0, ni = 0;
+#ifndef DMX_MERGE_BRANCHY
+        // branch-free (the sentinels stand for an empty queue: of two items left at least one
+        // is real, so a sentinel never wins a compare it should lose): four unconditional
+        // reads, selects for the picks and the two parent slots -- no exec-mask changes in
+        // the loop, about half the instructions of the branchy form (K2 is half VALU-bound)
+        uint16_t* const H = reinterpret_cast<uint16_t*>(&S);   // the parent slots as one u16 space
+        constexpr uint32_t OL = offsetof(K2LDS, lpar) / 2, OU = offsetof(K2LDS, up) / 2;
+        uint32_t ul = 0, un = 0;
+        for (uint32_t k = 0; k < (uint32_t)nn; k++) {
+            uint32_t a0 = S.fs[ul], a1 = S.fs[ul + 1], b0 = S.nodew[un], b1 = S.nodew[un + 1];
+            asm volatile("" : "+v"(a0), "+v"(a1), "+v"(b0), "+v"(b1));   // (all four read, none sunk into a branch)
+            const bool l1 = a0 <= b0;
+            const uint32_t q1 = l1 ? OL + ul : OU + un;
+            const uint32_t w1 = l1 ? a0 : b0, A = l1 ? a1 : a0, B = l1 ? b0 : b1;
+            ul += l1 ? 1u : 0u;
+            un += l1 ? 0u : 1u;
+            const bool l2 = A <= B;
+            const uint32_t q2 = l2 ? OL + ul : OU + un;
+            ul += l2 ? 1u : 0u;
+            un += l2 ? 0u : 1u;
+            H[q1] = (uint16_t)k;
+            H[q2] = (uint16_t)k;
+            S.nodew[k] = (uint16_t)(w1 + (l2 ? A : B));
+        }
+        (void)li;
+        (void)ni;
+#else
         for (int k = 0; k < nn; k++) {
             const uint32_t a0 = li < mm ? S.fs[li] : 0xFFFFFFFFu, a1 = li + 1 < mm ? S.fs[li + 1] : 0xFFFFFFFFu;
             const uint32_t b0 = ni < k ? S.nodew[ni] : 0xFFFFFFFFu, b1 = ni + 1 < k ? S.nodew[ni + 1] : 0xFFFFFFFFu;
@@ -3858,6 +3893,7 @@ __device__ void huff_lengths(K2LDS& S, const F* f, int n, int maxbits, uint8_t* 
             else { w += B; S.up[ni++] = (uint16_t)k; }
             S.nodew[k] = (uint16_t)w;
         }
+#endif
         S.up[root] = (uint16_t)root;
     }
     wsync();
@@ -3924,6 +3960,11 @@ __device__ void huff_lengths(K2LDS& S, const F* f, int n, int maxbits, uint8_t* 
         for (int e = maxbits; e >= 1; e--) { S.lstart[e] = k; k += S.blc[e]; }
     }
     wsync();
+    // sorted index i gets the first length e (from maxbits down) whose range ends past i, i.e.
+    // maxbits minus the lengths 2..maxbits whose range ends at or before i: the range ends
+    // from one LDS read per lane, then broadcasts (the loop over e was a chain of dependent
+    // LDS reads per symbol register)
+#ifdef DMX_LEN_LOOP   // (A/B build: the loop over e per symbol register)
 #pragma unroll
     for (int r = 0; r < 5; r++) {
         const int i = r * 64 + (int)lane;
@@ -3933,6 +3974,21 @@ __device__ void huff_lengths(K2LDS& S, const F* f, int n, int maxbits, uint8_t* 
             len[S.sym[i]] = (uint8_t)e;
         }
     }
+#else
+    const int32_t endv = (lane >= 2 && (int)lane <= maxbits) ? S.lstart[lane] + S.blc[lane] : 0x7FFFFFFF;
+    int32_t cnt[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int e = 2; e <= 15; e++) {
+        const int32_t x = __builtin_amdgcn_readlane(endv, e);
+#pragma unroll
+        for (int r = 0; r < 5; r++) cnt[r] += (r * 64 + (int)lane) >= x ? 1 : 0;
+    }
+#pragma unroll
+    for (int r = 0; r < 5; r++) {
+        const int i = r * 64 + (int)lane;
+        if (i < mm) len[S.sym[i]] = (uint8_t)(maxbits - cnt[r]);
+    }
+#endif
     wsync();
     K2ST(2, kt);
 }
@@ -4188,13 +4244,6 @@ __device__ uint32_t huff_emit(K2LDS& S, uint32_t final_bit, uint32_t bt, uint32_
     return carry;
 }
 
-__device__ HuffRes huff_block(K2LDS& S, uint32_t bn, uint32_t final_bit, bool allow_stored, uint32_t lane,
-                              uint32_t* __restrict__ codes_out) {
-    HuffRes h = huff_plan(S, bn, allow_stored, lane);
-    h.hbits = huff_emit(S, final_bit, h.bt, lane, codes_out);
-    return h;
-}
-
 __device__ __forceinline__ void huff_one(const uint32_t b, const uint32_t* __restrict__ hist_g, dmx_blkinfo* __restrict__ info,
                                          uint32_t* __restrict__ codes_g, uint32_t* __restrict__ hdr_g,
                                          dmx_subinfo* __restrict__ sub_g, uint32_t nblk, uint32_t flags) {
@@ -4209,8 +4258,13 @@ __device__ __forceinline__ void huff_one(const uint32_t b, const uint32_t* __res
     for (int s = (int)lane; s < 288; s += 64) S.fll[s] = s < 286 ? (s == 256 ? 1u : hg[s]) : 0u;   // + end of block
     for (int s = (int)lane; s < 32; s += 64) S.fd[s] = s < 30 ? hg[DMX_DIST0 + s] : 0u;
     wsync();
+    [[maybe_unused]] uint64_t kt1 = kt0;
+    K2ST(8, kt1);
     uint32_t* cg = codes_g + (uint64_t)b * DMX_NSUB * DMX_HIST;
-    const HuffRes h = huff_block(S, bn, final_bit, true, lane, cg);
+    HuffRes h = huff_plan(S, bn, true, lane);
+    K2ST(9, kt1);
+    h.hbits = huff_emit(S, final_bit, h.bt, lane, cg);
+    K2ST(10, kt1);
 #ifdef DMX_K2_STAMPS
     if (lane == 0) { atomicAdd(&dmx_k2_st[6], (unsigned long long)(K2T() - kt0)); atomicAdd(&dmx_k2_st[7], 1ull); }
 #endif
@@ -4981,6 +5035,12 @@ __device__ __forceinline__ void pack_one(const uint32_t b, const uint8_t* __rest
                                          dmx_result* __restrict__ res) {
     __shared__ uint32_t stage[PK_RING];
     __shared__ uint32_t code[DMX_HIST];
+#ifndef DMX_PACK_OLD
+    // one entry per first piece of a token, value | bits << 24: literals 0..255, then the
+    // lengths 3..258 with their extra bits appended (the length symbol, its code and its extra
+    // bits in one read instead of len_sym arithmetic and a branch per token)
+    __shared__ uint32_t ptab[512];
+#endif
     __shared__ uint32_t wsum[PT / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const dmx_blkinfo bi = info[b];   // in flight with the status load (a stored block's WG is
@@ -5091,6 +5151,25 @@ __device__ __forceinline__ void pack_one(const uint32_t b, const uint8_t* __rest
     for (uint32_t k = tid; k < PK_RING; k += PT) stage[k] = 0;
     for (uint32_t k = tid; k < 316; k += PT) code[k] = codes_g[(uint64_t)b * DMX_NSUB * DMX_HIST + k];
     __syncthreads();
+#ifndef DMX_PACK_OLD
+    auto build_ptab = [&]() {   // (after code[] is complete; a barrier follows)
+        for (uint32_t k = tid; k < 512; k += PT) {
+            uint32_t e;
+            if (k < 256) {
+                const uint32_t cw = code[k];
+                e = (cw & 0xFFFFu) | ((cw >> 16) << 24);
+            } else {
+                uint32_t sy, eb, ev;
+                len_sym(k - 253, sy, eb, ev);   // length k - 256 + 3
+                const uint32_t cw = code[sy];
+                e = ((cw & 0xFFFFu) | (ev << (cw >> 16))) | (((cw >> 16) + eb) << 24);
+            }
+            ptab[k] = e;
+        }
+    };
+    build_ptab();
+    __syncthreads();
+#endif
     {   // (stored blocks left above)
         // one or more DEFLATE blocks (f3 split): header, tokens [t0, t1), end of block
         uint32_t pos = s0;   // block bit position
@@ -5103,6 +5182,10 @@ __device__ __forceinline__ void pack_one(const uint32_t b, const uint8_t* __rest
 #pragma unroll
                 for (int t = 0; t < TPT; t++) nxt[t] = tb[min(si.t0 + tid * TPT + (uint32_t)t, (uint32_t)DMX_BLK - 1)];
                 __syncthreads();
+#ifndef DMX_PACK_OLD
+                build_ptab();
+                __syncthreads();
+#endif
             }
             flush(pos);
             const uint32_t* hg = hdr_g + slot * DMX_HDR_WORDS;
@@ -5133,6 +5216,19 @@ __device__ __forceinline__ void pack_one(const uint32_t b, const uint8_t* __rest
                     pv[2 * t] = pb[2 * t] = pv[2 * t + 1] = pb[2 * t + 1] = 0;
                     if (j0 + t < si.t1) {
                         const uint32_t tk = cur[t];
+#ifndef DMX_PACK_OLD
+                        // both pieces without a branch: the first from ptab, the distance's
+                        // computed for every token and dropped for a literal
+                        const bool lit = (tk >> 9) == 0;
+                        const uint32_t e1 = ptab[lit ? tk : 253u + (tk & 0x1FFu)];
+                        pv[2 * t] = e1 & 0xFFFFFFu;
+                        pb[2 * t] = e1 >> 24;
+                        uint32_t sy, eb, ev;
+                        dist_sym(lit ? 1u : tk >> 9, sy, eb, ev);
+                        const uint32_t cw = code[DMX_DIST0 + sy];
+                        pv[2 * t + 1] = lit ? 0u : (cw & 0xFFFFu) | (ev << (cw >> 16));
+                        pb[2 * t + 1] = lit ? 0u : (cw >> 16) + eb;
+#else
                         if ((tk >> 9) == 0) {
                             const uint32_t cw = code[tk];
                             pv[2 * t] = cw & 0xFFFFu;
@@ -5148,6 +5244,7 @@ __device__ __forceinline__ void pack_one(const uint32_t b, const uint8_t* __rest
                             pv[2 * t + 1] = (cw & 0xFFFFu) | (ev << (cw >> 16));
                             pb[2 * t + 1] = (cw >> 16) + eb;
                         }
+#endif
                         mybits += pb[2 * t] + pb[2 * t + 1];
                     }
                 }

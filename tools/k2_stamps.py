@@ -17,7 +17,7 @@ def main():
     t = torch.from_numpy(D.gen_text(n, 0xE5818)).cuda()
     e = D.Encoder(0, n, max_chain=8, flags=D.DMX_ZLIB | D.DMX_F_LAZY | D.DMX_F_DEEP)
     e.compress_tensor(t)
-    st = (ctypes.c_ulonglong * 8)()
+    st = (ctypes.c_ulonglong * 16)()
     L = D.lib()
     L.dmx_k2_stamps(st, 1)
     e.compress_tensor(t)
@@ -26,8 +26,8 @@ def main():
     e.close()
     v = list(st)
     nb = max(v[7], 1)
-    names = ["rank", "merge", "depth+len", "canon", "rle", "header", "total"]
-    print({k: round(v[i] / nb / 1e3, 1) for i, k in enumerate(names)}, "K cycles per block over", nb, "blocks")
+    names = ["rank", "merge", "depth+len", "canon", "rle", "header", "total", None, "load", "plan", "emit"]
+    print({k: round(v[i] / nb / 1e3, 1) for i, k in enumerate(names) if k}, "K cycles per block over", nb, "blocks")
 
 
 if __name__ == "__main__":
