@@ -3832,7 +3832,7 @@ __device__ void huff_lengths(K2LDS& S, const F* f, int n, int maxbits, uint8_t* 
             const uint32_t k2 = __builtin_amdgcn_readlane(ck[r2], (int)l2);
 #pragma unroll
             for (int r = 0; r < NR; r++)
-                if ((uint32_t)r < nru) rk[r] += k2 < ck[r] ? 1u : 0u;
+                rk[r] += k2 < ck[r] ? 1u : 0u;   // (registers past nru hold 0xFFFFFFFF: counted, never scattered)
         }
     }
 #pragma unroll
@@ -5213,22 +5213,31 @@ __device__ __forceinline__ void pack_one(const uint32_t b, const uint8_t* __rest
                 uint32_t mybits = 0;
     #pragma unroll
                 for (int t = 0; t < TPT; t++) {
+#ifndef DMX_PACK_OLD
+                    {   // both pieces without a branch: the first from ptab, the distance's computed
+                        // for every token and dropped for a literal; slots past the sub-block's
+                        // last token (the last round) get no bits
+                        const uint32_t tk = cur[t];
+                        const bool ok = j0 + t < si.t1, lit = (tk >> 9) == 0;
+                        const uint32_t e1 = ptab[lit ? tk : min(253u + (tk & 0x1FFu), 511u)];
+                        // RFC 1951 3.2.5 distance symbol of x = distance - 1 without a branch:
+                        // e = floor(log2(x | 2)), the symbol 2e + the bit below the top one
+                        // (x < 2: the symbol is x; both have no extra bits)
+                        const uint32_t x = lit ? 0u : (tk >> 9) - 1u;
+                        const uint32_t e = 31u - __clz(x | 2u), eb = e - 1u;
+                        const uint32_t sy = min(x < 2u ? x : 2u * e + ((x >> eb) & 1u), 29u);
+                        const uint32_t cw = code[DMX_DIST0 + sy];
+                        const bool dd = ok && !lit;
+                        pv[2 * t] = ok ? (e1 & 0xFFFFFFu) : 0u;
+                        pb[2 * t] = ok ? e1 >> 24 : 0u;
+                        pv[2 * t + 1] = dd ? (cw & 0xFFFFu) | ((x & ((1u << eb) - 1u)) << (cw >> 16)) : 0u;
+                        pb[2 * t + 1] = dd ? (cw >> 16) + eb : 0u;
+                        mybits += pb[2 * t] + pb[2 * t + 1];
+                    }
+#else
                     pv[2 * t] = pb[2 * t] = pv[2 * t + 1] = pb[2 * t + 1] = 0;
                     if (j0 + t < si.t1) {
                         const uint32_t tk = cur[t];
-#ifndef DMX_PACK_OLD
-                        // both pieces without a branch: the first from ptab, the distance's
-                        // computed for every token and dropped for a literal
-                        const bool lit = (tk >> 9) == 0;
-                        const uint32_t e1 = ptab[lit ? tk : 253u + (tk & 0x1FFu)];
-                        pv[2 * t] = e1 & 0xFFFFFFu;
-                        pb[2 * t] = e1 >> 24;
-                        uint32_t sy, eb, ev;
-                        dist_sym(lit ? 1u : tk >> 9, sy, eb, ev);
-                        const uint32_t cw = code[DMX_DIST0 + sy];
-                        pv[2 * t + 1] = lit ? 0u : (cw & 0xFFFFu) | (ev << (cw >> 16));
-                        pb[2 * t + 1] = lit ? 0u : (cw >> 16) + eb;
-#else
                         if ((tk >> 9) == 0) {
                             const uint32_t cw = code[tk];
                             pv[2 * t] = cw & 0xFFFFu;
@@ -5244,9 +5253,9 @@ __device__ __forceinline__ void pack_one(const uint32_t b, const uint8_t* __rest
                             pv[2 * t + 1] = (cw & 0xFFFFu) | (ev << (cw >> 16));
                             pb[2 * t + 1] = (cw >> 16) + eb;
                         }
-#endif
                         mybits += pb[2 * t] + pb[2 * t + 1];
                     }
+#endif
                 }
                 // exclusive scan of the threads' bit counts over the workgroup
                 const uint32_t incl = wave_incl_scan(mybits);
