@@ -3540,6 +3540,25 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
             constexpr bool p3batch = h4;   // (batched loads: the exhaustive parse +0.6 %; K = 7 48.8 -> 50.1 K cycles to P3's end, round 6)
 #endif
             if constexpr (!p3batch) {
+#ifndef DMX_P3_BRANCHY
+            for (uint32_t t = r0 + tid; t < r1; t += MT) {
+                // one path for both token kinds: the byte, length and distance slots are read
+                // together, the lit/len symbol is the byte or the length's (RFC 1951 3.2.5 by
+                // formula: l = len - 3, e = max(floor(log2 l), 2) - 2, 257 + 4e + (l >> e), 258
+                // -> 285), and only a match adds its distance symbol
+                const uint32_t p = TP[t - r0];
+                const bool lit = (L.lit[p >> 5] >> (p & 31)) & 1u;
+                const uint32_t c = D8[p], len = (uint32_t)L.len8[p] + 3u, dist = L.sorted[p];
+                const uint32_t l = len - 3u, e = max(31u - __clz(l | 1u), 2u) - 2u;
+                const uint32_t sl = len == 258u ? 285u : 257u + 4u * e + (l >> e);
+                atomicAdd(&hl[lit ? c : sl], 1u);
+                if (!lit) {
+                    const uint32_t x = dist - 1u, ed = 31u - __clz(x | 2u);
+                    atomicAdd(&hl[DMX_DIST0 + (x < 2u ? x : 2u * ed + ((x >> (ed - 1u)) & 1u))], 1u);
+                }
+                tb[t] = lit ? c : (dist << 9) | len;
+            }
+#else
             for (uint32_t t = r0 + tid; t < r1; t += MT) {
                 const uint32_t p = TP[t - r0];
                 uint32_t tk;
@@ -3557,6 +3576,7 @@ __device__ __forceinline__ void match_block(const uint32_t b, const uint8_t* __r
                 }
                 tb[t] = tk;
             }
+#endif
             } else {
             // DMX_P3_BATCH (and the exhaustive parse): P3B tokens per thread at a time, their LDS reads issued together (token position,
             // literal word, then byte, length and distance of each, whichever it is): three
@@ -3899,9 +3919,9 @@ __device__ void huff_lengths(K2LDS& S, const F* f, int n, int maxbits, uint8_t* 
     wsync();
     K2ST(1, kt);
     // node depths by pointer jumping: dd = distance to up, up = an ancestor, doubling
-    uint32_t u[5], d[5];
+    uint32_t u[NR], d[NR];   // (nodes < NR x 64: n <= 64 NR)
 #pragma unroll
-    for (int r = 0; r < 5; r++) {
+    for (int r = 0; r < NR; r++) {
         const int j = r * 64 + (int)lane;
         u[r] = j < nn ? S.up[j] : 0u;
         d[r] = (j < nn && j != root) ? 1u : 0u;
@@ -3909,9 +3929,9 @@ __device__ void huff_lengths(K2LDS& S, const F* f, int n, int maxbits, uint8_t* 
     }
     wsync();
     for (int round = 0; round < 9; round++) {   // 2^9 > 320 nodes
-        uint32_t du[5], uu[5];
+        uint32_t du[NR], uu[NR];
 #pragma unroll
-        for (int r = 0; r < 5; r++) {
+        for (int r = 0; r < NR; r++) {
             const int j = r * 64 + (int)lane;
             du[r] = j < nn ? S.dd[u[r]] : 0u;
             uu[r] = j < nn ? S.up[u[r]] : 0u;
@@ -3919,7 +3939,7 @@ __device__ void huff_lengths(K2LDS& S, const F* f, int n, int maxbits, uint8_t* 
         wsync();
         bool open = false;   // a node whose ancestor is not the root yet
 #pragma unroll
-        for (int r = 0; r < 5; r++) {
+        for (int r = 0; r < NR; r++) {
             const int j = r * 64 + (int)lane;
             d[r] += du[r];
             u[r] = uu[r];
@@ -3932,7 +3952,7 @@ __device__ void huff_lengths(K2LDS& S, const F* f, int n, int maxbits, uint8_t* 
     // leaf depths -> leaves per length
     uint32_t maxd = 0;
 #pragma unroll
-    for (int r = 0; r < 5; r++) {
+    for (int r = 0; r < NR; r++) {
         const int i = r * 64 + (int)lane;
         if (i < mm) {
             const uint32_t dl = S.dd[S.lpar[i]] + 1u;
@@ -3976,15 +3996,15 @@ __device__ void huff_lengths(K2LDS& S, const F* f, int n, int maxbits, uint8_t* 
     }
 #else
     const int32_t endv = (lane >= 2 && (int)lane <= maxbits) ? S.lstart[lane] + S.blc[lane] : 0x7FFFFFFF;
-    int32_t cnt[5] = {0, 0, 0, 0, 0};
+    int32_t cnt[NR] = {};
 #pragma unroll
     for (int e = 2; e <= 15; e++) {
         const int32_t x = __builtin_amdgcn_readlane(endv, e);
 #pragma unroll
-        for (int r = 0; r < 5; r++) cnt[r] += (r * 64 + (int)lane) >= x ? 1 : 0;
+        for (int r = 0; r < NR; r++) cnt[r] += (r * 64 + (int)lane) >= x ? 1 : 0;
     }
 #pragma unroll
-    for (int r = 0; r < 5; r++) {
+    for (int r = 0; r < NR; r++) {
         const int i = r * 64 + (int)lane;
         if (i < mm) len[S.sym[i]] = (uint8_t)(maxbits - cnt[r]);
     }

@@ -5,8 +5,8 @@
 set -uo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/${1:-r06_q}
-STAMPS=${STAMPS:-k2s k2old}
-VARS=${VARS:-lenloop}
+STAMPS=${STAMPS-k2s k2old}
+VARS=${VARS-lenloop}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 for v in $STAMPS; do
