@@ -3882,19 +3882,18 @@ __device__ void huff_lengths(K2LDS& S, const F* f, int n, int maxbits, uint8_t* 
         // the loop, about half the instructions of the branchy form (K2 is half VALU-bound)
         uint16_t* const H = reinterpret_cast<uint16_t*>(&S);   // the parent slots as one u16 space
         constexpr uint32_t OL = offsetof(K2LDS, lpar) / 2, OU = offsetof(K2LDS, up) / 2;
-        uint32_t ul = 0, un = 0;
+        uint32_t ul = 0;   // leaves taken; nodes taken = 2k - ul (a node takes two items)
         for (uint32_t k = 0; k < (uint32_t)nn; k++) {
+            const uint32_t un = 2 * k - ul;
             uint32_t a0 = S.fs[ul], a1 = S.fs[ul + 1], b0 = S.nodew[un], b1 = S.nodew[un + 1];
             asm volatile("" : "+v"(a0), "+v"(a1), "+v"(b0), "+v"(b1));   // (all four read, none sunk into a branch)
-            const bool l1 = a0 <= b0;
+            const uint32_t l1 = a0 <= b0 ? 1u : 0u;
             const uint32_t q1 = l1 ? OL + ul : OU + un;
             const uint32_t w1 = l1 ? a0 : b0, A = l1 ? a1 : a0, B = l1 ? b0 : b1;
-            ul += l1 ? 1u : 0u;
-            un += l1 ? 0u : 1u;
-            const bool l2 = A <= B;
-            const uint32_t q2 = l2 ? OL + ul : OU + un;
-            ul += l2 ? 1u : 0u;
-            un += l2 ? 0u : 1u;
+            const uint32_t ul1 = ul + l1;
+            const uint32_t l2 = A <= B ? 1u : 0u;
+            const uint32_t q2 = l2 ? OL + ul1 : OU + (2 * k + 1 - ul1);
+            ul = ul1 + l2;
             H[q1] = (uint16_t)k;
             H[q2] = (uint16_t)k;
             S.nodew[k] = (uint16_t)(w1 + (l2 ? A : B));
